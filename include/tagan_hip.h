@@ -1,0 +1,159 @@
+/*
+ * tagan_hip.h — C-ABI of libtagan_hip.so, the MI355X (gfx950) hot path of TAGAN.
+ *
+ * The reference (MaLoskins/Temporal-Asymmetric-Graph-Attention-Network @ 2025-04-18)
+ * is pure PyTorch; it has no FFI.  Each entry point below replaces the ATen op
+ * sequence of one reference function (cited per function).  The Python host
+ * package binds these with ctypes (INTEGRATION.md shows the stub).
+ *
+ * Conventions
+ *   - Plain pointers + sizes, no torch/HIP types.  `stream` is a hipStream_t
+ *     passed as void* (NULL = default stream).  All launches are asynchronous.
+ *   - The library never allocates or frees device memory.  Callers pass outputs
+ *     and workspaces (sized by the *_workspace() queries).
+ *   - Return 0 (TAGAN_OK) or a negative tagan_status; tagan_last_error() gives a
+ *     thread-local message for the last failure on the calling thread.
+ *   - Device arrays are row-major.  "ld" arguments are row strides in elements.
+ *   - dtype: TAGAN_F32 (fp32 storage, fp32 math).  Other values -> TAGAN_ERR_UNSUPPORTED.
+ *   - Dropout masks are counter-based: keep(u) with u = tagan_uniform(seed, index),
+ *     index layouts documented per kernel, so tests can regenerate them.
+ */
+#ifndef TAGAN_HIP_H
+#define TAGAN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum tagan_status {
+    TAGAN_OK = 0,
+    TAGAN_ERR_ARG = -1,          /* bad pointer / size / stride */
+    TAGAN_ERR_UNSUPPORTED = -2,  /* dtype / metric / shape not implemented */
+    TAGAN_ERR_LAUNCH = -3,       /* hipGetLastError after launch */
+    TAGAN_ERR_WORKSPACE = -4     /* workspace too small */
+};
+
+enum tagan_dtype { TAGAN_F32 = 0 };
+
+/* Distance metrics of DistanceMetric.get_metric (geometric_attention.py:196-225).
+ * Scores are similarities: distance metrics are negated as in
+ * _get_attention_weights (geometric_attention.py:378-401). */
+enum tagan_metric {
+    TAGAN_METRIC_EUCLIDEAN = 0,
+    TAGAN_METRIC_SQUARED_EUCLIDEAN = 1,
+    TAGAN_METRIC_MANHATTAN = 2,
+    TAGAN_METRIC_COSINE_SIMILARITY = 3,
+    TAGAN_METRIC_COSINE_DISTANCE = 4,
+    TAGAN_METRIC_DOT_PRODUCT = 5,
+    TAGAN_METRIC_SCALED_DOT_PRODUCT = 6,
+    TAGAN_METRIC_GAUSSIAN_KERNEL = 7,   /* sigma = metric_param[h] or 1.0 if NULL */
+    TAGAN_METRIC_RBF_KERNEL = 8         /* gamma = metric_param[h] or 1.0 if NULL */
+};
+
+const char* tagan_last_error(void);
+int tagan_version(void);
+int tagan_device_arch(char* buf, int len);   /* e.g. "gfx950"; needs a device */
+
+/* Counter-based uniform in [0,1) used by every dropout mask (splitmix64 finaliser). */
+float tagan_uniform(uint64_t seed, uint64_t index);
+
+/* ---------------------------------------------------------------------------
+ * Snapshot CSR builder.  Replaces graph_attention.py:96-105
+ *   adj = zeros(N,N); adj[edge_index[0], edge_index[1]] = 1; adj += eye(N)
+ * for a BATCH of G snapshots laid out block-diagonally: snapshot g owns global
+ * nodes [node_ptr[g], node_ptr[g+1]) and edges [edge_ptr[g], edge_ptr[g+1]) of
+ * edge_index ([2, ld_ei] int64, local indices; negative indices wrap like torch
+ * indexing).  Output = the set {(src,dst)} ∪ {(i,i)} (duplicates collapsed):
+ *   CSR by src (query row):  rowptr[n_nodes+1], col[nnz]
+ *   CSC by dst:               csc_ptr[n_nodes+1], csc_row[nnz], csc_eid[nnz]
+ *                             (csc_eid = CSR position of the same pair)
+ * Capacity of col/csc_* must be >= n_edges + n_nodes.  *nnz_out and *err_out
+ * are device int64/int32 scalars; *err_out != 0 if any index was out of range
+ * (those edges are dropped; the reference raises IndexError).
+ * n_nodes < 2^31.
+ * ------------------------------------------------------------------------- */
+size_t tagan_csr_build_workspace(int64_t n_edges, int64_t n_nodes);
+int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges,
+                    const int64_t* edge_ptr, const int64_t* node_ptr, int32_t n_graphs,
+                    int64_t n_nodes,
+                    int32_t* rowptr, int32_t* col,
+                    int32_t* csc_ptr, int32_t* csc_row, int32_t* csc_eid,
+                    int64_t* nnz_out, int32_t* err_out,
+                    void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Geometric (edge-softmax) attention.  Replaces geometric_attention.py:332-516
+ * (_get_attention_weights: metric scores -> masked_fill(-inf) -> softmax ->
+ * attn_dropout) and :579-583 (context = A·V) for query rows = CSR rows.
+ *   q,k,v: [n_nodes, heads*head_dim] with row stride ld_qkv (may alias one
+ *          fused [n,3H] buffer).  out: [n_nodes, H] (ld = H).
+ *   lse:   [n_nodes, heads] log-sum-exp of the row's scores (saved for bwd).
+ *   edge_alpha (optional): [nnz, heads] post-dropout attention weights.
+ * Dropout index layout: edge e (CSR position), head h -> index e*heads + h.
+ * A row with no entries yields NaN (softmax over all -inf, as the reference).
+ * ------------------------------------------------------------------------- */
+int tagan_geo_attn_fwd(int dtype, int metric, int64_t n_nodes, int32_t heads, int32_t head_dim,
+                       const int32_t* rowptr, const int32_t* col,
+                       const void* q, const void* k, const void* v, int64_t ld_qkv,
+                       const float* metric_param, float p_drop, uint64_t seed,
+                       void* out, float* lse, float* edge_alpha, void* stream);
+
+/* Backward of tagan_geo_attn_fwd: row pass over CSR (dq, delta = rowsum(dO∘O))
+ * then column pass over CSC (dk, dv).  Atomic-free and deterministic.
+ * dq/dk/dv: [n_nodes, H] with row stride ld_dqkv (may alias one [n,3H] buffer).
+ * dmetric_param: [heads] (gaussian/rbf learnable parameter) or NULL. */
+size_t tagan_geo_attn_bwd_workspace(int64_t n_nodes, int32_t heads);
+int tagan_geo_attn_bwd(int dtype, int metric, int64_t n_nodes, int32_t heads, int32_t head_dim,
+                       const int32_t* rowptr, const int32_t* col,
+                       const int32_t* csc_ptr, const int32_t* csc_row, const int32_t* csc_eid,
+                       const void* q, const void* k, const void* v, int64_t ld_qkv,
+                       const float* metric_param, float p_drop, uint64_t seed,
+                       const void* out, const float* lse, const void* dout,
+                       void* dq, void* dk, void* dv, int64_t ld_dqkv,
+                       float* dmetric_param, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Per-row temporal attention.  Replaces temporal_attention.py:1006-1183
+ * (QKᵀ/√d + relative-position bias + asymmetric-kernel bias [+ dense bias]
+ * -> masks -> softmax -> attn_dropout -> A·V) for `rows` independent rows
+ * (nodes) of T snapshots each.
+ *   q,k,v: element (row r, time t, feature f) at ptr[r*s_row + t*s_t + f]
+ *   bias_table (optional): [heads, 2T-1]; entry [h][i-j+T-1] added to score(i,j).
+ *   bias_dense (optional): [*, heads, T, T] fp32, row stride bias_bstride (0 = shared).
+ *   mask (optional): uint8 keep-mask, element (r,h,i,j) at
+ *        mask[r*mask_bstride + h*mask_hstride + i*T + j]; causal != 0 adds j<=i.
+ *   out: element (r,t,f) at out[r*o_row + t*o_t + f];  lse: [rows, heads, T].
+ *   attn (optional): [rows, heads, T, T] post-dropout weights.
+ * Dropout index layout: ((r*heads + h)*T + i)*T + j.
+ * ------------------------------------------------------------------------- */
+int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim,
+                            const void* q, const void* k, const void* v, int64_t s_row, int64_t s_t,
+                            const float* bias_table, const float* bias_dense, int64_t bias_bstride,
+                            const uint8_t* mask, int64_t mask_bstride, int64_t mask_hstride, int causal,
+                            float p_drop, uint64_t seed,
+                            void* out, int64_t o_row, int64_t o_t,
+                            float* lse, float* attn, void* stream);
+
+/* Backward.  dbias_table: [heads, 2T-1] (reduced over rows, deterministic) or NULL.
+ * dbias_dense: [rows, heads, T, T] per-row score gradients (caller reduces a
+ * shared bias) or NULL.  dq/dk/dv element (r,t,f) at d*[r*d_row + t*d_t + f]. */
+size_t tagan_temporal_attn_bwd_workspace(int64_t rows, int32_t T, int32_t heads);
+int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim,
+                            const void* q, const void* k, const void* v, int64_t s_row, int64_t s_t,
+                            const float* bias_table, const float* bias_dense, int64_t bias_bstride,
+                            const uint8_t* mask, int64_t mask_bstride, int64_t mask_hstride, int causal,
+                            float p_drop, uint64_t seed,
+                            const void* out, int64_t o_row, int64_t o_t, const float* lse,
+                            const void* dout, int64_t do_row, int64_t do_t,
+                            void* dq, void* dk, void* dv, int64_t d_row, int64_t d_t,
+                            float* dbias_table, float* dbias_dense,
+                            void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TAGAN_HIP_H */

@@ -1,0 +1,94 @@
+"""ctypes binding of libtagan_hip.so (C-ABI declared in include/tagan_hip.h).
+
+There is no fallback: if the shared object is missing or a call fails, a
+RuntimeError is raised.  The .so is built in-tree by ``__graft_entry__.build()``
+(``make -C temporal-asymmetric-graph-attention-network_amd/csrc``).
+"""
+import ctypes
+import os
+import re
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtagan_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tagan_hip.h")
+
+TAGAN_F32 = 0
+METRIC_IDS = {
+    "euclidean": 0, "squared_euclidean": 1, "manhattan": 2, "cosine_similarity": 3,
+    "cosine_distance": 4, "dot_product": 5, "scaled_dot_product": 6, "gaussian_kernel": 7,
+    "rbf_kernel": 8,
+}
+
+_c = ctypes
+_p = _c.c_void_p
+_i32, _i64, _u64, _f32, _sz = _c.c_int32, _c.c_int64, _c.c_uint64, _c.c_float, _c.c_size_t
+
+_SIGNATURES = {
+    "tagan_last_error": (_c.c_char_p, []),
+    "tagan_version": (_c.c_int, []),
+    "tagan_device_arch": (_c.c_int, [_c.c_char_p, _c.c_int]),
+    "tagan_uniform": (_f32, [_u64, _u64]),
+    "tagan_csr_build_workspace": (_sz, [_i64, _i64]),
+    "tagan_csr_build": (_c.c_int, [_p, _i64, _i64, _p, _p, _i32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
+    "tagan_geo_attn_fwd": (_c.c_int, [_c.c_int, _c.c_int, _i64, _i32, _i32, _p, _p, _p, _p, _p, _i64, _p, _f32,
+                                      _u64, _p, _p, _p, _p]),
+    "tagan_geo_attn_bwd_workspace": (_sz, [_i64, _i32]),
+    "tagan_geo_attn_bwd": (_c.c_int, [_c.c_int, _c.c_int, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p,
+                                      _i64, _p, _f32, _u64, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _sz, _p]),
+    "tagan_temporal_attn_fwd": (_c.c_int, [_c.c_int, _i64, _i32, _i32, _i32, _p, _p, _p, _i64, _i64, _p, _p,
+                                           _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,
+                                           _p]),
+    "tagan_temporal_attn_bwd_workspace": (_sz, [_i64, _i32, _i32]),
+    "tagan_temporal_attn_bwd": (_c.c_int, [_c.c_int, _i64, _i32, _i32, _i32, _p, _p, _p, _i64, _i64, _p, _p,
+                                           _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,
+                                           _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p, _sz, _p]),
+}
+
+_lib = None
+
+
+def header_symbols():
+    """Function names declared in include/tagan_hip.h (for the ABI export test)."""
+    with open(HEADER_PATH) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(tagan_[a-z_0-9]+)\s*\(", src, re.M)))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libtagan_hip.so is not built (%s); run __graft_entry__.build() or "
+                               "make -C temporal-asymmetric-graph-attention-network_amd/csrc" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(L, name, None)
+            if fn is None:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().tagan_last_error().decode(errors="replace")
+        raise RuntimeError("%s failed (status %d): %s" % (what, rc, msg))
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_hip(*tensors):
+    for t in tensors:
+        if t is not None and (not t.is_cuda or torch.version.hip is None):
+            raise RuntimeError("tagan_amd runs on a HIP device only (got a tensor on %s); there is no CPU path"
+                               % (t.device,))

@@ -1,0 +1,223 @@
+// Snapshot CSR/CSC builder: the sparse form of graph_attention.py:96-105
+//   adj = zeros(N,N); adj[edge_index[0], edge_index[1]] = 1; adj += eye(N)
+// for a block-diagonal batch of snapshots.  Integer/byte work: HBM-bound,
+// no MFMA.  Keys (src<<32 | dst) are radix-sorted with rocPRIM, de-duplicated,
+// scattered into CSR; the CSC (with CSR edge ids) is a second key-value sort.
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include "common.cuh"
+
+namespace tagan {
+namespace {
+
+constexpr int BLK = 256;
+
+// Graph of edge e: binary search in edge_ptr[0..G] (G small; edge_ptr in L2/scalar cache).
+__device__ __forceinline__ int find_graph(const int64_t* __restrict__ edge_ptr, int G, int64_t e) {
+    int lo = 0, hi = G - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (edge_ptr[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(BLK) k_make_keys(const int64_t* __restrict__ ei, int64_t ld_ei, int64_t E,
+                                                   const int64_t* __restrict__ edge_ptr,
+                                                   const int64_t* __restrict__ node_ptr, int G,
+                                                   int64_t N, uint64_t* __restrict__ keys,
+                                                   int32_t* __restrict__ err) {
+    const uint64_t sentinel = (uint64_t)N << 32;
+    for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < E + N; p += (int64_t)gridDim.x * BLK) {
+        uint64_t key;
+        if (p < E) {
+            const int g = find_graph(edge_ptr, G, p);
+            const int64_t base = node_ptr[g];
+            const int64_t n = node_ptr[g + 1] - base;
+            int64_t s = ei[p], d = ei[ld_ei + p];
+            s += (s < 0) ? n : 0;                 // torch advanced indexing wraps negatives
+            d += (d < 0) ? n : 0;
+            if (s < 0 || s >= n || d < 0 || d >= n) {
+                atomicOr(err, 1);
+                key = sentinel;
+            } else {
+                key = ((uint64_t)(base + s) << 32) | (uint64_t)(base + d);
+            }
+        } else {
+            const uint64_t i = (uint64_t)(p - E);   // self-loop of global node i (the "+ eye")
+            key = (i << 32) | i;
+        }
+        keys[p] = key;
+    }
+}
+
+__global__ void __launch_bounds__(BLK) k_unique_flags(const uint64_t* __restrict__ keys, int64_t M, int64_t N,
+                                                      int32_t* __restrict__ flags) {
+    const uint64_t sentinel = (uint64_t)N << 32;
+    for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
+        const uint64_t k = keys[p];
+        flags[p] = (k < sentinel && (p == 0 || keys[p - 1] != k)) ? 1 : 0;
+    }
+}
+
+// Scatter unique keys into CSR; emit CSC keys (dst<<32 | src) with value = CSR position.
+__global__ void __launch_bounds__(BLK) k_scatter_csr(const uint64_t* __restrict__ keys,
+                                                     const int32_t* __restrict__ flags,
+                                                     const int32_t* __restrict__ pos, int64_t M, int64_t N,
+                                                     int32_t* __restrict__ rowptr, int32_t* __restrict__ col,
+                                                     uint64_t* __restrict__ ckeys, int32_t* __restrict__ cvals,
+                                                     int64_t* __restrict__ nnz_out) {
+    for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
+        if (p == M - 1) {
+            const int64_t nnz = (int64_t)pos[p] + flags[p];
+            *nnz_out = nnz;
+            rowptr[N] = (int32_t)nnz;
+        }
+        if (!flags[p]) continue;
+        const uint64_t k = keys[p];
+        const int32_t r = (int32_t)(k >> 32), c = (int32_t)(k & 0xffffffffu);
+        const int32_t q = pos[p];
+        col[q] = c;
+        if (p == 0 || (int32_t)(keys[p - 1] >> 32) != r) rowptr[r] = q;   // every row has its self-loop
+        ckeys[q] = ((uint64_t)c << 32) | (uint64_t)r;
+        cvals[q] = q;
+    }
+}
+
+__global__ void __launch_bounds__(BLK) k_fill_tail(uint64_t* __restrict__ ckeys, int32_t* __restrict__ cvals,
+                                                   const int64_t* __restrict__ nnz_p, int64_t M, int64_t N) {
+    const int64_t nnz = *nnz_p;
+    const uint64_t sentinel = (uint64_t)N << 32;
+    for (int64_t p = nnz + blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
+        ckeys[p] = sentinel;
+        cvals[p] = -1;
+    }
+}
+
+__global__ void __launch_bounds__(BLK) k_scatter_csc(const uint64_t* __restrict__ ckeys,
+                                                     const int32_t* __restrict__ cvals,
+                                                     const int64_t* __restrict__ nnz_p, int64_t N,
+                                                     int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_row,
+                                                     int32_t* __restrict__ csc_eid) {
+    const int64_t nnz = *nnz_p;
+    for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * BLK) {
+        const uint64_t k = ckeys[p];
+        const int32_t c = (int32_t)(k >> 32);
+        csc_row[p] = (int32_t)(k & 0xffffffffu);
+        csc_eid[p] = cvals[p];
+        if (p == 0 || (int32_t)(ckeys[p - 1] >> 32) != c) csc_ptr[c] = (int32_t)p;
+        if (p == nnz - 1) csc_ptr[N] = (int32_t)nnz;
+    }
+}
+
+int key_bits(int64_t N) {
+    int b = 1;
+    while (b < 32 && ((int64_t)1 << b) <= N) ++b;   // values 0..N inclusive (sentinel = N)
+    return b;
+}
+
+struct CsrWs {
+    size_t keys_a, keys_b, ckeys_b, cvals_b, flags, pos, temp, total;
+    size_t temp_bytes;
+};
+
+CsrWs plan(int64_t E, int64_t N) {
+    const int64_t M = E + N;
+    CsrWs w{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
+    w.keys_a = take(M * 8);
+    w.keys_b = take(M * 8);
+    w.ckeys_b = take(M * 8);
+    w.cvals_b = take(M * 4);
+    w.flags = take(M * 4);
+    w.pos = take(M * 4);
+    const int bits = key_bits(N);
+    size_t t1 = 0, t2 = 0, t3 = 0;
+    (void)rocprim::radix_sort_keys(nullptr, t1, (uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)M, 0, 32 + bits);
+    (void)rocprim::radix_sort_pairs(nullptr, t2, (uint64_t*)nullptr, (uint64_t*)nullptr, (int32_t*)nullptr,
+                              (int32_t*)nullptr, (size_t)M, 0, 32 + bits);
+    (void)rocprim::exclusive_scan(nullptr, t3, (int32_t*)nullptr, (int32_t*)nullptr, 0, (size_t)M,
+                            rocprim::plus<int32_t>());
+    w.temp_bytes = std::max(t1, std::max(t2, t3));
+    w.temp = take(w.temp_bytes);
+    w.total = off;
+    return w;
+}
+
+int grid_for(int64_t n) {
+    int64_t g = (n + BLK - 1) / BLK;
+    if (g > 256 * 16) g = 256 * 16;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+}  // namespace tagan
+
+extern "C" {
+
+size_t tagan_csr_build_workspace(int64_t n_edges, int64_t n_nodes) {
+    if (n_edges < 0 || n_nodes <= 0) return 0;
+    return tagan::plan(n_edges, n_nodes).total;
+}
+
+int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, const int64_t* edge_ptr,
+                    const int64_t* node_ptr, int32_t n_graphs, int64_t n_nodes, int32_t* rowptr, int32_t* col,
+                    int32_t* csc_ptr, int32_t* csc_row, int32_t* csc_eid, int64_t* nnz_out, int32_t* err_out,
+                    void* workspace, size_t workspace_bytes, void* stream) {
+    using namespace tagan;
+    TAGAN_REQUIRE(n_nodes > 0 && n_nodes < (int64_t)INT32_MAX - 1, TAGAN_ERR_ARG,
+                  "tagan_csr_build: n_nodes=%lld out of range", (long long)n_nodes);
+    TAGAN_REQUIRE(n_edges >= 0 && (n_edges == 0 || (edge_index && ld_ei >= n_edges)), TAGAN_ERR_ARG,
+                  "tagan_csr_build: bad edge_index (E=%lld ld=%lld)", (long long)n_edges, (long long)ld_ei);
+    TAGAN_REQUIRE(n_edges + n_nodes < (int64_t)INT32_MAX, TAGAN_ERR_ARG, "tagan_csr_build: too many edges");
+    TAGAN_REQUIRE(n_graphs >= 1 && edge_ptr && node_ptr, TAGAN_ERR_ARG, "tagan_csr_build: bad graph pointers");
+    TAGAN_REQUIRE(rowptr && col && csc_ptr && csc_row && csc_eid && nnz_out && err_out, TAGAN_ERR_ARG,
+                  "tagan_csr_build: null output");
+    const CsrWs w = plan(n_edges, n_nodes);
+    TAGAN_REQUIRE(workspace && workspace_bytes >= w.total, TAGAN_ERR_WORKSPACE,
+                  "tagan_csr_build: workspace %zu < %zu", workspace_bytes, w.total);
+    hipStream_t s = as_stream(stream);
+    char* ws = (char*)workspace;
+    uint64_t* keys_a = (uint64_t*)(ws + w.keys_a);
+    uint64_t* keys_b = (uint64_t*)(ws + w.keys_b);
+    uint64_t* ckeys_b = (uint64_t*)(ws + w.ckeys_b);
+    int32_t* cvals_b = (int32_t*)(ws + w.cvals_b);
+    int32_t* flags = (int32_t*)(ws + w.flags);
+    int32_t* pos = (int32_t*)(ws + w.pos);
+    void* temp = ws + w.temp;
+    const int64_t M = n_edges + n_nodes;
+    const int bits = key_bits(n_nodes);
+
+    TAGAN_CHECK_HIP(hipMemsetAsync(err_out, 0, sizeof(int32_t), s), "csr_build memset");
+    k_make_keys<<<grid_for(M), BLK, 0, s>>>(edge_index, ld_ei, n_edges, edge_ptr, node_ptr, n_graphs, n_nodes,
+                                            keys_a, err_out);
+    TAGAN_CHECK_LAUNCH("csr_build.make_keys");
+    size_t tb = w.temp_bytes;
+    TAGAN_CHECK_HIP(rocprim::radix_sort_keys(temp, tb, keys_a, keys_b, (size_t)M, 0, 32 + bits, s),
+                    "csr_build radix_sort_keys");
+    k_unique_flags<<<grid_for(M), BLK, 0, s>>>(keys_b, M, n_nodes, flags);
+    TAGAN_CHECK_LAUNCH("csr_build.unique_flags");
+    tb = w.temp_bytes;
+    TAGAN_CHECK_HIP(rocprim::exclusive_scan(temp, tb, flags, pos, 0, (size_t)M, rocprim::plus<int32_t>(), s),
+                    "csr_build exclusive_scan");
+    // keys_a is free now: reuse it as the unsorted CSC key buffer; cvals via csc_eid scratch? use csc_row.
+    uint64_t* ckeys_a = keys_a;
+    int32_t* cvals_a = csc_row;   // staging only; overwritten by the final CSC scatter
+    k_scatter_csr<<<grid_for(M), BLK, 0, s>>>(keys_b, flags, pos, M, n_nodes, rowptr, col, ckeys_a, cvals_a,
+                                              nnz_out);
+    TAGAN_CHECK_LAUNCH("csr_build.scatter_csr");
+    k_fill_tail<<<grid_for(M), BLK, 0, s>>>(ckeys_a, cvals_a, nnz_out, M, n_nodes);
+    TAGAN_CHECK_LAUNCH("csr_build.fill_tail");
+    tb = w.temp_bytes;
+    TAGAN_CHECK_HIP(rocprim::radix_sort_pairs(temp, tb, ckeys_a, ckeys_b, cvals_a, cvals_b, (size_t)M, 0,
+                                              32 + bits, s),
+                    "csr_build radix_sort_pairs");
+    k_scatter_csc<<<grid_for(M), BLK, 0, s>>>(ckeys_b, cvals_b, nnz_out, n_nodes, csc_ptr, csc_row, csc_eid);
+    TAGAN_CHECK_LAUNCH("csr_build.scatter_csc");
+    return TAGAN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,257 @@
+"""Device-side building blocks of the hot path, each a thin wrapper of the C-ABI.
+
+* ``SnapshotGraph`` / ``build_graph`` — block-diagonal CSR (+CSC) of a batch of
+  snapshots: the sparse equivalent of graph_attention.py:96-105.
+* ``GeoAttnFn``      — autograd Function over ``tagan_geo_attn_fwd/bwd``
+  (geometric_attention.py:332-516 + :579-583).
+* ``TemporalAttnFn`` — autograd Function over ``tagan_temporal_attn_fwd/bwd``
+  (temporal_attention.py:1006-1205 minus the projections).
+
+Every output and workspace is allocated here from PyTorch's caching allocator;
+kernels are launched on the current HIP stream.
+"""
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, require_hip, stream_of
+
+
+def new_seed() -> int:
+    """Dropout seed drawn from torch's default CPU generator (reproducible under manual_seed, no device sync)."""
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+
+
+# ----------------------------------------------------------------------------- graph
+@dataclass
+class SnapshotGraph:
+    """CSR by source (query) row and CSC by destination, int32, device-resident."""
+    num_nodes: int
+    rowptr: torch.Tensor
+    col: torch.Tensor
+    csc_ptr: torch.Tensor
+    csc_row: torch.Tensor
+    csc_eid: torch.Tensor
+    nnz: torch.Tensor              # int64[1] on device
+    node_counts: Sequence[int]
+
+    def nnz_host(self) -> int:
+        return int(self.nnz.item())
+
+
+def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], validate: bool = True) -> SnapshotGraph:
+    """CSR/CSC of the block-diagonal union of snapshot adjacencies (+ self-loops, de-duplicated).
+
+    ``edge_indices[g]`` is snapshot g's [2, E_g] edge_index with local node ids.
+    With ``validate`` an out-of-range index raises IndexError like the reference's
+    ``adj[edge_index[0], edge_index[1]] = 1`` (costs one device sync).
+    """
+    dev = edge_indices[0].device
+    require_hip(*edge_indices)
+    eis = [e.to(torch.int64) for e in edge_indices]
+    ei = torch.cat(eis, dim=1) if len(eis) > 1 else eis[0]
+    ei = ei.contiguous()
+    E = int(ei.shape[1])
+    N = int(sum(node_counts))
+    e_ptr = [0]
+    for e in eis:
+        e_ptr.append(e_ptr[-1] + int(e.shape[1]))
+    n_ptr = [0]
+    for n in node_counts:
+        n_ptr.append(n_ptr[-1] + int(n))
+    meta = torch.tensor(e_ptr + n_ptr, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+    edge_ptr, node_ptr = meta[:len(e_ptr)], meta[len(e_ptr):]
+    cap = E + N
+    i32 = dict(dtype=torch.int32, device=dev)
+    rowptr = torch.empty(N + 1, **i32)
+    col = torch.empty(cap, **i32)
+    csc_ptr = torch.empty(N + 1, **i32)
+    csc_row = torch.empty(cap, **i32)
+    csc_eid = torch.empty(cap, **i32)
+    scal = torch.empty(2, dtype=torch.int64, device=dev)
+    nnz = scal[0:1]
+    err = scal[1:2].view(torch.int32)[:1]
+    L = lib()
+    ws_bytes = L.tagan_csr_build_workspace(E, N)
+    ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=dev)
+    check(L.tagan_csr_build(ptr(ei), E, E, ptr(edge_ptr), ptr(node_ptr), len(eis), N, ptr(rowptr), ptr(col),
+                            ptr(csc_ptr), ptr(csc_row), ptr(csc_eid), ptr(nnz), ptr(err), ptr(ws), ws_bytes,
+                            stream_of(ei)), "tagan_csr_build")
+    if validate and int(err.item()) != 0:
+        raise IndexError("edge_index contains an index out of range for its snapshot's node count")
+    return SnapshotGraph(N, rowptr, col, csc_ptr, csc_row, csc_eid, nnz, list(node_counts))
+
+
+def graph_from_dense_mask(mask: torch.Tensor) -> SnapshotGraph:
+    """CSR/CSC of a dense [B,S,S] (or [S,S]) attention mask (nonzero = attend), block-diagonal over B."""
+    if mask.dim() == 2:
+        mask = mask.unsqueeze(0)
+    B, S, _ = mask.shape
+    b, i, j = (mask != 0).nonzero(as_tuple=True)
+    src = (b * S + i).to(torch.int64)
+    dst = (b * S + j).to(torch.int64)
+    return _graph_from_pairs(src, dst, B * S, [S] * B)
+
+
+def _graph_from_pairs(src, dst, N, node_counts):
+    """CSR/CSC from already-unique (src,dst) pairs sorted by (src,dst) (torch.nonzero order); no self-loops added."""
+    dev = src.device
+    nnz = int(src.numel())
+    counts = torch.bincount(src, minlength=N)
+    rowptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+    rowptr[1:] = torch.cumsum(counts, 0)
+    order = torch.argsort(dst * N + src)
+    ccounts = torch.bincount(dst, minlength=N)
+    cptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+    cptr[1:] = torch.cumsum(ccounts, 0)
+    i32 = torch.int32
+    return SnapshotGraph(N, rowptr.to(i32), dst.to(i32), cptr.to(i32), src[order].to(i32), order.to(i32),
+                         torch.tensor([nnz], dtype=torch.int64, device=dev), list(node_counts))
+
+
+# ----------------------------------------------------------------------------- geometric attention
+class GeoAttnFn(torch.autograd.Function):
+    """ctx = edge-softmax attention over ``graph`` for qkv = [N, 3H] (q | k | v)."""
+
+    @staticmethod
+    def forward(ctx, qkv, param, graph: SnapshotGraph, metric: int, heads: int, p_drop: float, seed: int):
+        require_hip(qkv)
+        assert qkv.dim() == 2 and qkv.is_contiguous() and qkv.dtype == torch.float32
+        N, H3 = qkv.shape
+        H = H3 // 3
+        d = H // heads
+        out = torch.empty(N, H, device=qkv.device, dtype=torch.float32)
+        lse = torch.empty(N, heads, device=qkv.device, dtype=torch.float32)
+        base = qkv.data_ptr()
+        es = qkv.element_size()
+        prm = param.detach().contiguous() if param is not None else None
+        check(lib().tagan_geo_attn_fwd(_lib.TAGAN_F32, metric, N, heads, d, ptr(graph.rowptr), ptr(graph.col),
+                                       base, base + H * es, base + 2 * H * es, H3, ptr(prm), float(p_drop),
+                                       seed, ptr(out), ptr(lse), None, stream_of(qkv)), "tagan_geo_attn_fwd")
+        ctx.save_for_backward(qkv, out, lse, prm)
+        ctx.graph, ctx.metric, ctx.heads, ctx.p_drop, ctx.seed = graph, metric, heads, p_drop, seed
+        ctx.has_param = param is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse, prm = ctx.saved_tensors
+        g = ctx.graph
+        N, H3 = qkv.shape
+        H = H3 // 3
+        heads = ctx.heads
+        d = H // heads
+        dout = dout.contiguous()
+        dqkv = torch.empty_like(qkv)
+        L = lib()
+        ws_bytes = L.tagan_geo_attn_bwd_workspace(N, heads)
+        ws = torch.empty(int(ws_bytes), dtype=torch.uint8, device=qkv.device)
+        dprm = torch.empty(heads, device=qkv.device, dtype=torch.float32) if ctx.has_param and \
+            ctx.needs_input_grad[1] else None
+        base, es = qkv.data_ptr(), qkv.element_size()
+        dbase = dqkv.data_ptr()
+        check(L.tagan_geo_attn_bwd(_lib.TAGAN_F32, ctx.metric, N, heads, d, ptr(g.rowptr), ptr(g.col),
+                                   ptr(g.csc_ptr), ptr(g.csc_row), ptr(g.csc_eid), base, base + H * es,
+                                   base + 2 * H * es, H3, ptr(prm), float(ctx.p_drop), ctx.seed, ptr(out),
+                                   ptr(lse), ptr(dout), dbase, dbase + H * es, dbase + 2 * H * es, H3, ptr(dprm),
+                                   ptr(ws), ws_bytes, stream_of(qkv)), "tagan_geo_attn_bwd")
+        return dqkv, dprm, None, None, None, None, None
+
+
+def geo_edge_alpha(qkv, graph: SnapshotGraph, metric: int, heads: int, param=None, p_drop=0.0, seed=0):
+    """Per-edge post-dropout attention weights [nnz, heads] (no autograd; inspection only)."""
+    N, H3 = qkv.shape
+    H = H3 // 3
+    out = torch.empty(N, H, device=qkv.device)
+    lse = torch.empty(N, heads, device=qkv.device)
+    alpha = torch.empty(int(graph.col.numel()), heads, device=qkv.device)
+    base, es = qkv.data_ptr(), qkv.element_size()
+    prm = param.detach().contiguous() if param is not None else None
+    check(lib().tagan_geo_attn_fwd(_lib.TAGAN_F32, metric, N, heads, H // heads, ptr(graph.rowptr),
+                                   ptr(graph.col), base, base + H * es, base + 2 * H * es, H3, ptr(prm),
+                                   float(p_drop), seed, ptr(out), ptr(lse), ptr(alpha), stream_of(qkv)),
+          "tagan_geo_attn_fwd(alpha)")
+    return alpha[:graph.nnz_host()]
+
+
+# ----------------------------------------------------------------------------- temporal attention
+@dataclass
+class TemporalMask:
+    """Effective keep-mask for the temporal kernel (broadcast over rows/heads via zero strides)."""
+    causal: bool = False
+    keep: Optional[torch.Tensor] = None     # uint8, contiguous, last two dims [T, T]
+    bstride: int = 0
+    hstride: int = 0
+
+
+class TemporalAttnFn(torch.autograd.Function):
+    """Per-row attention over T steps.  ``qkv`` is [R, T, 3H] (row-major) or [T, R, 3H] (time_major)."""
+
+    @staticmethod
+    def forward(ctx, qkv, bias_table, bias_dense, time_major: bool, heads: int, mask: TemporalMask,
+                p_drop: float, seed: int, want_attn: bool):
+        require_hip(qkv)
+        assert qkv.dim() == 3 and qkv.is_contiguous() and qkv.dtype == torch.float32
+        A0, A1, H3 = qkv.shape
+        H = H3 // 3
+        d = H // heads
+        R, T = (A1, A0) if time_major else (A0, A1)
+        s_row, s_t = (H3, R * H3) if time_major else (T * H3, H3)
+        o_row, o_t = (H, R * H) if time_major else (T * H, H)
+        out = torch.empty(A0, A1, H, device=qkv.device, dtype=torch.float32)
+        lse = torch.empty(R, heads, T, device=qkv.device, dtype=torch.float32)
+        attn = torch.empty(R, heads, T, T, device=qkv.device, dtype=torch.float32) if want_attn else None
+        bt = bias_table.detach().contiguous() if bias_table is not None else None
+        bd = bias_dense.detach().contiguous() if bias_dense is not None else None
+        bd_stride = (0 if bd.shape[0] == 1 else heads * T * T) if bd is not None else 0
+        base, es = qkv.data_ptr(), qkv.element_size()
+        check(lib().tagan_temporal_attn_fwd(_lib.TAGAN_F32, R, T, heads, d, base, base + H * es,
+                                            base + 2 * H * es, s_row, s_t, ptr(bt), ptr(bd), bd_stride,
+                                            ptr(mask.keep), mask.bstride, mask.hstride, int(mask.causal),
+                                            float(p_drop), seed, ptr(out), o_row, o_t, ptr(lse), ptr(attn),
+                                            stream_of(qkv)), "tagan_temporal_attn_fwd")
+        ctx.save_for_backward(qkv, out, lse, bt, bd)
+        ctx.cfg = (time_major, heads, mask, p_drop, seed, bd_stride)
+        ctx.need_bt = bias_table is not None
+        ctx.need_bd = bias_dense is not None
+        if attn is not None:
+            ctx.mark_non_differentiable(attn)
+        return out, attn
+
+    @staticmethod
+    def backward(ctx, dout, _dattn):
+        qkv, out, lse, bt, bd = ctx.saved_tensors
+        time_major, heads, mask, p_drop, seed, bd_stride = ctx.cfg
+        A0, A1, H3 = qkv.shape
+        H = H3 // 3
+        d = H // heads
+        R, T = (A1, A0) if time_major else (A0, A1)
+        s_row, s_t = (H3, R * H3) if time_major else (T * H3, H3)
+        o_row, o_t = (H, R * H) if time_major else (T * H, H)
+        dout = dout.contiguous()
+        dqkv = torch.empty_like(qkv)
+        L = lib()
+        dbt = torch.empty(heads, 2 * T - 1, device=qkv.device) if (ctx.need_bt and ctx.needs_input_grad[1]) else None
+        dbd = torch.empty(R, heads, T, T, device=qkv.device) if (ctx.need_bd and ctx.needs_input_grad[2]) else None
+        ws_bytes = L.tagan_temporal_attn_bwd_workspace(R, T, heads)
+        ws = torch.empty(int(ws_bytes), dtype=torch.uint8, device=qkv.device)
+        base, es = qkv.data_ptr(), qkv.element_size()
+        dbase = dqkv.data_ptr()
+        check(L.tagan_temporal_attn_bwd(_lib.TAGAN_F32, R, T, heads, d, base, base + H * es, base + 2 * H * es,
+                                        s_row, s_t, ptr(bt), ptr(bd), bd_stride, ptr(mask.keep), mask.bstride,
+                                        mask.hstride, int(mask.causal), float(p_drop), seed, ptr(out), o_row, o_t,
+                                        ptr(lse), ptr(dout), o_row, o_t, dbase, dbase + H * es, dbase + 2 * H * es,
+                                        s_row, s_t, ptr(dbt), ptr(dbd), ptr(ws), ws_bytes, stream_of(qkv)),
+              "tagan_temporal_attn_bwd")
+        if dbd is not None and bd is not None and bd.shape[0] == 1:
+            dbd = dbd.sum(0, keepdim=True)
+        return dqkv, dbt, dbd, None, None, None, None, None, None
+
+
+def fused_qkv(x, q_lin, k_lin, v_lin):
+    """One GEMM for the three projections (hipBLASLt via torch): [.., H] -> [.., 3H] = q | k | v."""
+    w = torch.cat([q_lin.weight, k_lin.weight, v_lin.weight], 0)
+    b = torch.cat([q_lin.bias, k_lin.bias, v_lin.bias], 0)
+    return torch.nn.functional.linear(x, w, b)

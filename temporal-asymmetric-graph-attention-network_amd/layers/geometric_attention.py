@@ -1,0 +1,163 @@
+"""Geometric attention on MI355X (drop-in for src/tagan/layers/geometric_attention.py).
+
+``GeometricAttention`` keeps the reference constructor, parameter names/shapes,
+initialisation order and forward signature (geometric_attention.py:228-607), so
+reference ``state_dict``s load unchanged and ``torch.manual_seed(s)`` yields the
+same initial weights.  The forward runs:
+
+  LN1 (torch) -> one fused QKV GEMM (hipBLASLt) -> ``tagan_geo_attn_fwd``
+  (metric score, edge-softmax, attn-dropout, A·V over the mask's CSR; HIP)
+  -> out-proj GEMM -> dropout -> residual -> LN2
+
+Dense masks become CSR (``graph_from_dense_mask``); TAGANGraphAttention hands in
+a prebuilt snapshot CSR through ``forward_graph``.  There is no CPU path.
+"""
+import math
+from typing import Callable, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _lib
+from ..kernels import GeoAttnFn, SnapshotGraph, fused_qkv, graph_from_dense_mask, new_seed
+
+
+class DistanceMetric:
+    """Distance metrics of geometric_attention.py:15-225 (plain torch utilities, any device)."""
+
+    @staticmethod
+    def euclidean(x, y):
+        return torch.sqrt(torch.sum((x - y) ** 2, dim=-1) + 1e-8)
+
+    @staticmethod
+    def squared_euclidean(x, y):
+        return torch.sum((x - y) ** 2, dim=-1)
+
+    @staticmethod
+    def manhattan(x, y):
+        return torch.sum(torch.abs(x - y), dim=-1)
+
+    @staticmethod
+    def cosine_similarity(x, y):
+        xn = torch.norm(x, p=2, dim=-1, keepdim=True)
+        yn = torch.norm(y, p=2, dim=-1, keepdim=True)
+        xn = torch.where(xn == 0, torch.ones_like(xn) * 1e-8, xn)
+        yn = torch.where(yn == 0, torch.ones_like(yn) * 1e-8, yn)
+        return torch.clamp(torch.sum(x * y, dim=-1) / (xn * yn).squeeze(-1), -1.0, 1.0)
+
+    @staticmethod
+    def cosine_distance(x, y):
+        return 1.0 - DistanceMetric.cosine_similarity(x, y)
+
+    @staticmethod
+    def dot_product(x, y):
+        return torch.sum(x * y, dim=-1)
+
+    @staticmethod
+    def scaled_dot_product(x, y):
+        return torch.sum(x * y, dim=-1) / math.sqrt(x.size(-1))
+
+    @staticmethod
+    def mahalanobis(x, y, cov_inv):
+        diff = x - y
+        shape = diff.shape
+        d2 = diff.reshape(-1, shape[-1])
+        return torch.sqrt(torch.sum(d2 @ cov_inv * d2, dim=-1).view(*shape[:-1]) + 1e-8)
+
+    @staticmethod
+    def gaussian_kernel(x, y, sigma=1.0):
+        return torch.exp(-DistanceMetric.squared_euclidean(x, y) / (2 * sigma ** 2))
+
+    @staticmethod
+    def rbf_kernel(x, y, gamma=1.0):
+        return torch.exp(-gamma * DistanceMetric.squared_euclidean(x, y))
+
+    @staticmethod
+    def get_metric(metric_name: str) -> Callable:
+        # Same accepted names as geometric_attention.py:196-225 ("mahalanobis" is not one of them).
+        if metric_name in _lib.METRIC_IDS:
+            return getattr(DistanceMetric, metric_name)
+        raise ValueError(f"Unknown distance metric: {metric_name}")
+
+
+class GeometricAttention(nn.Module):
+    def __init__(self, hidden_dim: int, num_heads: int = 8, dropout: float = 0.1,
+                 distance_metric: str = "scaled_dot_product", use_layer_norm: bool = True,
+                 learnable_distance: bool = False):
+        super().__init__()
+        self.hidden_dim = hidden_dim
+        self.num_heads = num_heads
+        self.dropout_prob = dropout
+        self.distance_metric = distance_metric
+        self.use_layer_norm = use_layer_norm
+        self.learnable_distance = learnable_distance
+        assert hidden_dim % num_heads == 0, "Hidden dimension must be divisible by number of heads"
+        self.head_dim = hidden_dim // num_heads
+        self.q_linear = nn.Linear(hidden_dim, hidden_dim)
+        self.k_linear = nn.Linear(hidden_dim, hidden_dim)
+        self.v_linear = nn.Linear(hidden_dim, hidden_dim)
+        self.output_proj = nn.Linear(hidden_dim, hidden_dim)
+        if use_layer_norm:
+            self.layer_norm1 = nn.LayerNorm(hidden_dim)
+            self.layer_norm2 = nn.LayerNorm(hidden_dim)
+        self.attn_dropout = nn.Dropout(dropout)
+        self.output_dropout = nn.Dropout(dropout)
+        if learnable_distance:
+            if distance_metric in ("gaussian_kernel", "rbf_kernel"):
+                self.distance_param = nn.Parameter(torch.ones(num_heads))
+            elif distance_metric == "mahalanobis":
+                rank = min(16, hidden_dim // 4)
+                self.cov_factors = nn.Parameter(torch.zeros(num_heads, rank, self.head_dim))
+                nn.init.xavier_uniform_(self.cov_factors)
+        self.distance_fn = DistanceMetric.get_metric(distance_metric)
+        self.metric_id = _lib.METRIC_IDS[distance_metric]
+        self._init_parameters()
+
+    def _init_parameters(self):
+        for lin in (self.q_linear, self.k_linear, self.v_linear, self.output_proj):
+            nn.init.xavier_uniform_(lin.weight)
+        for lin in (self.q_linear, self.k_linear, self.v_linear, self.output_proj):
+            nn.init.zeros_(lin.bias)
+        if self.learnable_distance and self.distance_metric in ("gaussian_kernel", "rbf_kernel"):
+            nn.init.constant_(self.distance_param, 1.0 if self.distance_metric == "gaussian_kernel" else 0.1)
+
+    def _metric_param(self):
+        if self.learnable_distance and self.distance_metric in ("gaussian_kernel", "rbf_kernel"):
+            return self.distance_param
+        return None
+
+    def forward_graph(self, x: torch.Tensor, graph: SnapshotGraph) -> torch.Tensor:
+        """Hot path: x [N, H] (N = all nodes of a snapshot batch), graph = their CSR/CSC."""
+        identity = x
+        h = self.layer_norm1(x) if self.use_layer_norm else x
+        qkv = fused_qkv(h, self.q_linear, self.k_linear, self.v_linear).contiguous()
+        p = self.attn_dropout.p if self.training else 0.0
+        ctx = GeoAttnFn.apply(qkv, self._metric_param(), graph, self.metric_id, self.num_heads, p,
+                              new_seed() if p > 0 else 0)
+        out = self.output_dropout(self.output_proj(ctx)) + identity
+        if self.use_layer_norm:
+            out = self.layer_norm2(out)
+        return out
+
+    def forward(self, x: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
+                geometric_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x [B,S,H]; mask [B,S,S] (0 = masked) or None (dense); see geometric_attention.py:518-598."""
+        B, S, H = x.shape
+        if geometric_bias is not None:
+            raise NotImplementedError("geometric_bias (post-softmax re-normalisation, geometric_attention.py:567-575) "
+                                      "is not implemented on the HIP path yet")
+        if attention_mask is None or attention_mask.shape[-2:] != (S, S):
+            mask = torch.ones(B, S, S, device=x.device)       # mismatched masks -> full attention (:482-498)
+        else:
+            mask = attention_mask.expand(B, S, S) if attention_mask.dim() == 3 else attention_mask
+        graph = graph_from_dense_mask(mask)
+        return self.forward_graph(x.reshape(B * S, H), graph).view(B, S, H)
+
+    def extra_repr(self) -> str:
+        return (f"hidden_dim={self.hidden_dim}, num_heads={self.num_heads}, "
+                f"distance_metric={self.distance_metric}, learnable_distance={self.learnable_distance}, "
+                f"use_layer_norm={self.use_layer_norm}, dropout={self.dropout_prob}")
+
+
+GeometricAttentionLayer = GeometricAttention

@@ -1,0 +1,75 @@
+"""CPU checks of the C-ABI library: it loads without a GPU, exports every symbol of
+include/tagan_hip.h, and its host-side helpers / argument validation behave."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import tagan_amd
+from tagan_amd import _lib
+
+
+def test_library_loads_and_exports_header_symbols():
+    L = _lib.lib()
+    syms = _lib.header_symbols()
+    assert len(syms) >= 12
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert L.tagan_version() >= 1
+
+
+def _splitmix_uniform(seed, idx):
+    """numpy restatement of tagan::uniform01 (common.cuh) used to regenerate dropout masks in tests."""
+    m = np.uint64(0xFFFFFFFFFFFFFFFF)
+    with np.errstate(over="ignore"):
+        z = (np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * (np.asarray(idx, dtype=np.uint64) + np.uint64(1))) & m
+        z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & m
+        z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & m
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(40)).astype(np.float64) / 16777216.0
+
+
+def test_uniform_matches_numpy_restatement():
+    L = _lib.lib()
+    for seed in (0, 1, 123456789, 2 ** 62 - 1):
+        idx = np.array([0, 1, 2, 1000, 2 ** 40 + 3], dtype=np.uint64)
+        want = _splitmix_uniform(seed, idx)
+        got = np.array([L.tagan_uniform(seed, int(i)) for i in idx])
+        np.testing.assert_array_equal(got.astype(np.float32), want.astype(np.float32))
+        assert ((got >= 0) & (got < 1)).all()
+
+
+def test_workspace_queries_are_host_only():
+    L = _lib.lib()
+    assert L.tagan_geo_attn_bwd_workspace(1000, 8) >= 1000 * 8 * 4
+    assert L.tagan_temporal_attn_bwd_workspace(100, 32, 8) >= 8 * 63 * 4
+    assert L.tagan_geo_attn_bwd_workspace(0, 8) == 0
+
+
+def test_argument_validation_reports_errors():
+    L = _lib.lib()
+    rc = L.tagan_geo_attn_fwd(0, 99, 10, 4, 16, None, None, None, None, None, 64, None, 0.0, 0, None, None, None,
+                              None)
+    assert rc == -2
+    assert b"metric" in L.tagan_last_error()
+    rc = L.tagan_temporal_attn_fwd(1, 10, 4, 2, 8, None, None, None, 0, 0, None, None, 0, None, 0, 0, 0, 0.0, 0,
+                                   None, 0, 0, None, None, None)
+    assert rc == -2
+    rc = L.tagan_geo_attn_fwd(0, 0, 10, 4, 16, None, None, None, None, None, 64, None, 1.5, 0, None, None, None,
+                              None)
+    assert rc == -1
+
+
+def test_no_cpu_path():
+    from tagan_amd.kernels import GeoAttnFn, SnapshotGraph
+    x = torch.zeros(4, 12)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        GeoAttnFn.apply(x, None, None, 0, 1, 0.0, 0)
+
+
+def test_metric_table_matches_header():
+    with open(_lib.HEADER_PATH) as f:
+        src = f.read()
+    for name, mid in _lib.METRIC_IDS.items():
+        assert ("TAGAN_METRIC_%s = %d" % (name.upper(), mid)) in src

@@ -1,0 +1,232 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden vectors
+and against the CPU oracle.  Tolerance: 1e-4 fp32 (north_star), written per check.
+
+Run on an MI355X:  python -m pytest tests -m gpu -q
+"""
+import pytest
+import torch
+
+import golden_io as G
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+OUT_ATOL, OUT_RTOL = 1e-4, 1e-4      # forward values
+GRAD_ATOL, GRAD_RTOL = 1e-4, 1e-3    # gradients (longer fp32 reduction chains)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import tagan_amd  # noqa: F401
+    return torch.device("cuda:0")
+
+
+def _load(module, sd, dev):
+    module.load_state_dict({k: v for k, v in sd.items()}, strict=True)
+    return module.to(dev).train()
+
+
+# ----------------------------------------------------------------------------- CSR builder
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_csr_build_matches_oracle(dev, seed):
+    from tagan_amd.kernels import build_graph
+    g = torch.Generator().manual_seed(seed)
+    counts = [1, 7, 50, 3, 200]
+    eis = []
+    for n in counts:
+        E = int(torch.randint(0, 4 * n + 1, (1,), generator=g))
+        ei = torch.randint(-n, n, (2, E), generator=g)      # negatives wrap like torch indexing
+        eis.append(ei)
+    graph = build_graph([e.to(dev) for e in eis], counts)
+    nnz = graph.nnz_host()
+    rows, cols, off = [], [], 0
+    rp_all = [0]
+    for n, ei in zip(counts, eis):
+        rp, c = oracle.csr_from_edge_index(ei, n)
+        cols.append(c + off)
+        rp_all.extend((rp[1:] + rp_all[-1]).tolist())
+        off += n
+    want_col = torch.cat(cols)
+    assert nnz == want_col.numel()
+    assert graph.rowptr.cpu().tolist() == rp_all
+    assert torch.equal(graph.col[:nnz].cpu().long(), want_col)
+    # CSC is the transpose with edge ids pointing back into the CSR
+    src = torch.repeat_interleave(torch.arange(off), torch.tensor(rp_all).diff())
+    eid = graph.csc_eid[:nnz].cpu().long()
+    crow = graph.csc_row[:nnz].cpu().long()
+    assert torch.equal(src[eid], crow)
+    cptr = graph.csc_ptr.cpu().long()
+    for j in range(off):
+        seg = eid[cptr[j]:cptr[j + 1]]
+        assert torch.all(want_col[seg] == j)
+        assert torch.all(crow[cptr[j]:cptr[j + 1]].diff() > 0)
+
+
+def test_csr_build_rejects_out_of_range(dev):
+    from tagan_amd.kernels import build_graph
+    with pytest.raises(IndexError):
+        build_graph([torch.tensor([[0, 1], [1, 5]], device=dev)], [5])
+
+
+# ----------------------------------------------------------------------------- layer units vs goldens
+@pytest.mark.parametrize("case", G.case_names("gat_"))
+def test_graph_attention_golden(dev, case):
+    from tagan_amd.layers import TAGANGraphAttention
+    meta, t = G.load(case)
+    torch.manual_seed(0)
+    layer = _load(TAGANGraphAttention(meta["H"], meta["heads"], 0.0, meta["metric"], True,
+                                      meta["learnable_distance"]), G.state_dict(t), dev)
+    x = t["in.x"].to(dev).requires_grad_(True)
+    out = layer(x, t["in.edge_index"].to(dev))
+    G.assert_close("out", out, t["out"], OUT_ATOL, OUT_RTOL)
+    (out * t["in.grad_out"].to(dev)).sum().backward()
+    G.assert_close("grad x", x.grad, t["grad.x"], GRAD_ATOL, GRAD_RTOL)
+    params = dict(layer.named_parameters())
+    for name, g in G.grads(t).items():
+        G.assert_close("grad " + name, params[name].grad, g, GRAD_ATOL, GRAD_RTOL)
+
+
+@pytest.mark.parametrize("case", [c for c in G.case_names("geo_") if "bias" not in c])
+def test_geometric_attention_golden(dev, case):
+    from tagan_amd.layers import GeometricAttention
+    meta, t = G.load(case)
+    mod = _load(GeometricAttention(meta["H"], meta["heads"], 0.0, meta["metric"], True), G.state_dict(t), dev)
+    x = t["in.x"].to(dev).requires_grad_(True)
+    mask = t.get("in.mask")
+    out = mod(x, mask.to(dev) if mask is not None else None)
+    G.assert_close("out", out, t["out"], OUT_ATOL, OUT_RTOL)
+    (out * t["in.grad_out"].to(dev)).sum().backward()
+    G.assert_close("grad x", x.grad, t["grad.x"], GRAD_ATOL, GRAD_RTOL)
+    params = dict(mod.named_parameters())
+    for name, g in G.grads(t).items():
+        G.assert_close("grad " + name, params[name].grad, g, GRAD_ATOL, GRAD_RTOL)
+
+
+@pytest.mark.parametrize("case", G.case_names("tatt_"))
+def test_temporal_attention_golden(dev, case):
+    from tagan_amd.layers import AsymmetricTemporalAttention, TemporalAttention
+    meta, t = G.load(case)
+    cls = AsymmetricTemporalAttention if meta["cls"] == "AsymmetricTemporalAttention" else TemporalAttention
+    mod = _load(cls(**meta["ctor"]), G.state_dict(t), dev)
+    if meta.get("eval"):
+        mod.eval()
+    if meta["x_kind"] == "list":
+        xs = [t["in.x.%d" % i].to(dev).requires_grad_(True) for i in range(meta["T"])]
+        x_in = xs
+    else:
+        xs = [t["in.x"].to(dev).requires_grad_(True)]
+        x_in = xs[0]
+    kw = {}
+    if "in.mask" in t:
+        kw["attention_mask"] = t["in.mask"].to(dev)
+    if "in.time_stamps" in t:
+        kw["time_stamps"] = t["in.time_stamps"].to(dev)
+    if meta["with_attn"]:
+        kw["return_attention_weights"] = True
+    res = mod(x_in, **kw)
+    out, attn = res if meta["with_attn"] else (res, None)
+    G.assert_close("out", out, t["out"], OUT_ATOL, OUT_RTOL)
+    if attn is not None:
+        G.assert_close("attn", attn, t["out.attn"], OUT_ATOL, OUT_RTOL)
+    (out * t["in.grad_out"].to(dev)).sum().backward()
+    for i, xi in enumerate(xs):
+        key = "grad.x.%d" % i if meta["x_kind"] == "list" else "grad.x"
+        G.assert_close(key, xi.grad, t[key], GRAD_ATOL, GRAD_RTOL)
+    params = dict(mod.named_parameters())
+    for name, g in G.grads(t).items():
+        G.assert_close("grad " + name, params[name].grad, g, GRAD_ATOL, GRAD_RTOL)
+
+
+# ----------------------------------------------------------------------------- end to end vs goldens
+@pytest.mark.parametrize("case", G.case_names("e2e_"))
+def test_tagan_golden(dev, case):
+    from tagan_amd import TAGAN, TAGANConfig
+    meta, t = G.load(case)
+    cfg = TAGANConfig(**dict(meta["config"], device="cuda"))
+    model = _load(TAGAN(cfg), G.state_dict(t), dev)
+    if meta.get("eval"):
+        model.eval()
+    seq = G.sequence(meta, t, dev)
+    seq = [(x.requires_grad_(True), ei, ea, ids) for x, ei, ea, ids in seq]
+    labels = G.labels(meta, t, dev)
+    with torch.set_grad_enabled(not meta.get("eval", False)):
+        out = model(seq, labels=labels, return_attention_weights=meta.get("return_attention_weights", False))
+    G.assert_close("logits", out["logits"], t["out.logits"], OUT_ATOL, OUT_RTOL)
+    G.assert_close("predictions", out["predictions"], t["out.predictions"], OUT_ATOL, OUT_RTOL)
+    if meta.get("return_attention_weights"):
+        G.assert_close("tattn", out["temporal_attention_weights"], t["out.temporal_attention_weights"],
+                       OUT_ATOL, OUT_RTOL)
+        assert out["geometric_attention_weights"] == [{"node_attention": None}] * meta["n_geo_attn_weights"]
+    if "out.loss" not in t:
+        assert out["loss"] is None
+        return
+    G.assert_close("loss", out["loss"].reshape(1), t["out.loss"], OUT_ATOL, OUT_RTOL)
+    out["loss"].backward()
+    want = G.grads(t)
+    for name, p in model.named_parameters():
+        if name in want:
+            G.assert_close("grad " + name, p.grad, want[name], GRAD_ATOL, GRAD_RTOL)
+        else:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, name
+    for i, (x, _, _, _) in enumerate(seq):
+        G.assert_close("grad x.%d" % i, x.grad, t["grad.x.%d" % i], GRAD_ATOL, GRAD_RTOL)
+
+
+# ----------------------------------------------------------------------------- larger shapes vs oracle
+def _rand_seq(counts, F, De, epn, seed):
+    g = torch.Generator().manual_seed(seed)
+    seq = []
+    for n in counts:
+        seq.append((torch.randn(n, F, generator=g), torch.randint(0, n, (2, epn * n), generator=g),
+                    torch.randn(epn * n, De, generator=g), list(range(n))))
+    return seq
+
+
+@pytest.mark.parametrize("learnable,H,heads,counts", [
+    (False, 128, 8, [700, 650, 720, 690, 700, 710]),       # C2 architecture (euclidean), ragged N
+    (True, 128, 8, [600] * 8),                              # scaled-dot metric
+    (False, 256, 16, [300] * 16),                           # C5 head geometry (d=16, T=heads -> causal)
+    (False, 128, 4, [400] * 5),                             # C4 head geometry (d=32)
+])
+def test_tagan_vs_oracle_medium(dev, learnable, H, heads, counts):
+    from tagan_amd import TAGAN, TAGANConfig
+    F_, De = 27, 2
+    cfg = TAGANConfig(hidden_dim=H, num_heads=heads, node_feature_dim=F_, edge_feature_dim=De,
+                      use_edge_features=True, output_dim=1, loss_type="bce", dropout=0.0,
+                      learnable_distance=learnable, device="cuda")
+    torch.manual_seed(3)
+    model = TAGAN(cfg).to(dev).train()
+    seq = _rand_seq(counts, F_, De, 10, 4)
+    labels = torch.tensor([1.0])
+    out = model([(x.to(dev), ei.to(dev), ea.to(dev), ids) for x, ei, ea, ids in seq], labels=labels.to(dev))
+    out["loss"].backward()
+    P = {k: v.detach().cpu().double().requires_grad_(v.is_floating_point())
+         for k, v in model.state_dict().items()}
+    seq64 = [(x.double(), ei, ea.double(), ids) for x, ei, ea, ids in seq]
+    ref = oracle.tagan_forward(P, cfg.to_dict(), seq64, labels.double())
+    G.assert_close("logits", out["logits"], ref["logits"], OUT_ATOL, OUT_RTOL)
+    G.assert_close("loss", out["loss"].reshape(1), ref["loss"].reshape(1), OUT_ATOL, OUT_RTOL)
+    ref["loss"].backward()
+    for name, p in model.named_parameters():
+        if P[name].grad is not None:
+            G.assert_close("grad " + name, p.grad, P[name].grad, GRAD_ATOL, GRAD_RTOL)
+
+
+# ----------------------------------------------------------------------------- determinism / dropout
+def test_deterministic_with_dropout(dev):
+    from tagan_amd import TAGAN, TAGANConfig
+    cfg = TAGANConfig(hidden_dim=128, num_heads=8, node_feature_dim=27, edge_feature_dim=2, use_edge_features=True,
+                      output_dim=1, loss_type="bce", dropout=0.1, device="cuda")
+    seq = [(x.to(dev), ei.to(dev), ea.to(dev), ids) for x, ei, ea, ids in _rand_seq([500] * 6, 27, 2, 10, 9)]
+    grads = []
+    for _ in range(2):
+        torch.manual_seed(11)
+        model = TAGAN(cfg).to(dev).train()
+        torch.manual_seed(12)
+        out = model(seq, labels=torch.tensor([1.0], device=dev))
+        out["loss"].backward()
+        grads.append(torch.cat([p.grad.flatten() for p in model.parameters() if p.grad is not None]))
+    assert torch.equal(grads[0], grads[1]), "backward is not bitwise reproducible"
+    assert torch.isfinite(grads[0]).all()
