@@ -85,6 +85,53 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges,
                     void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Work decomposition for skewed (power-law) graphs: every CSR row / CSC column
+ * ("segment") is split into chunks of at most `chunk` entries.  A segment
+ * with more than one chunk is "multi"; its chunks write partial results to a
+ * workspace slot chunk_part[c] (>= 0; -1 for single-chunk segments) and a merge
+ * pass combines them in chunk order (deterministic).
+ *   chunk_ptr[n+1]: chunks of segment s are [chunk_ptr[s], chunk_ptr[s+1])
+ *   chunk_seg[c], chunk_beg[c]: segment and first entry of chunk c
+ *   multi_seg[k]: k-th multi segment;  counts = {n_chunks, n_multi, n_parts} (device int32[3])
+ * Capacities: chunk arrays >= tagan_chunk_capacity(n, nnz_cap, chunk),
+ * multi_seg / parts >= tagan_part_capacity(nnz_cap, chunk).
+ * ------------------------------------------------------------------------- */
+int64_t tagan_chunk_capacity(int64_t n_segments, int64_t nnz_cap, int32_t chunk);
+int64_t tagan_part_capacity(int64_t nnz_cap, int32_t chunk);
+size_t tagan_graph_chunks_workspace(int64_t n_segments);
+int tagan_graph_chunks(const int32_t* seg_ptr, int64_t n_segments, int32_t chunk,
+                       int32_t* chunk_ptr, int32_t* chunk_seg, int32_t* chunk_beg, int32_t* chunk_part,
+                       int32_t* multi_seg, int32_t* counts,
+                       void* workspace, size_t workspace_bytes, void* stream);
+
+/* A built snapshot-batch graph (all device pointers).  Filled by the host from
+ * tagan_csr_build + two tagan_graph_chunks calls (rows over the CSR, columns
+ * over the CSC). */
+typedef struct tagan_graph {
+    int64_t n_nodes;
+    const int32_t* rowptr;      /* [n+1] */
+    const int32_t* col;         /* [nnz] */
+    const int32_t* csc_ptr;     /* [n+1] */
+    const int32_t* csc_row;     /* [nnz] */
+    const int32_t* csc_eid;     /* [nnz] CSR position of each CSC entry */
+    int32_t chunk;              /* max entries per chunk */
+    int64_t chunk_cap;          /* capacity of the chunk arrays (launch bound) */
+    int64_t part_cap;           /* capacity of partial slots / multi segments */
+    const int32_t* row_chunk_ptr;
+    const int32_t* row_chunk_seg;
+    const int32_t* row_chunk_beg;
+    const int32_t* row_chunk_part;
+    const int32_t* row_multi;
+    const int32_t* row_counts;  /* {n_chunks, n_multi, n_parts} */
+    const int32_t* col_chunk_ptr;
+    const int32_t* col_chunk_seg;
+    const int32_t* col_chunk_beg;
+    const int32_t* col_chunk_part;
+    const int32_t* col_multi;
+    const int32_t* col_counts;
+} tagan_graph;
+
+/* ---------------------------------------------------------------------------
  * Geometric (edge-softmax) attention.  Replaces geometric_attention.py:332-516
  * (_get_attention_weights: metric scores -> masked_fill(-inf) -> softmax ->
  * attn_dropout) and :579-583 (context = A·V) for query rows = CSR rows.
@@ -95,20 +142,19 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges,
  * Dropout index layout: edge e (CSR position), head h -> index e*heads + h.
  * A row with no entries yields NaN (softmax over all -inf, as the reference).
  * ------------------------------------------------------------------------- */
-int tagan_geo_attn_fwd(int dtype, int metric, int64_t n_nodes, int32_t heads, int32_t head_dim,
-                       const int32_t* rowptr, const int32_t* col,
+size_t tagan_geo_attn_fwd_workspace(const tagan_graph* g, int32_t heads, int32_t head_dim);
+int tagan_geo_attn_fwd(int dtype, int metric, const tagan_graph* g, int32_t heads, int32_t head_dim,
                        const void* q, const void* k, const void* v, int64_t ld_qkv,
                        const float* metric_param, float p_drop, uint64_t seed,
-                       void* out, float* lse, float* edge_alpha, void* stream);
+                       void* out, float* lse, float* edge_alpha,
+                       void* workspace, size_t workspace_bytes, void* stream);
 
 /* Backward of tagan_geo_attn_fwd: row pass over CSR (dq, delta = rowsum(dO∘O))
  * then column pass over CSC (dk, dv).  Atomic-free and deterministic.
  * dq/dk/dv: [n_nodes, H] with row stride ld_dqkv (may alias one [n,3H] buffer).
  * dmetric_param: [heads] (gaussian/rbf learnable parameter) or NULL. */
-size_t tagan_geo_attn_bwd_workspace(int64_t n_nodes, int32_t heads);
-int tagan_geo_attn_bwd(int dtype, int metric, int64_t n_nodes, int32_t heads, int32_t head_dim,
-                       const int32_t* rowptr, const int32_t* col,
-                       const int32_t* csc_ptr, const int32_t* csc_row, const int32_t* csc_eid,
+size_t tagan_geo_attn_bwd_workspace(const tagan_graph* g, int32_t heads, int32_t head_dim);
+int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t heads, int32_t head_dim,
                        const void* q, const void* k, const void* v, int64_t ld_qkv,
                        const float* metric_param, float p_drop, uint64_t seed,
                        const void* out, const float* lse, const void* dout,

@@ -32,11 +32,16 @@ _SIGNATURES = {
     "tagan_uniform": (_f32, [_u64, _u64]),
     "tagan_csr_build_workspace": (_sz, [_i64, _i64]),
     "tagan_csr_build": (_c.c_int, [_p, _i64, _i64, _p, _p, _i32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
-    "tagan_geo_attn_fwd": (_c.c_int, [_c.c_int, _c.c_int, _i64, _i32, _i32, _p, _p, _p, _p, _p, _i64, _p, _f32,
-                                      _u64, _p, _p, _p, _p]),
-    "tagan_geo_attn_bwd_workspace": (_sz, [_i64, _i32]),
-    "tagan_geo_attn_bwd": (_c.c_int, [_c.c_int, _c.c_int, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p,
-                                      _i64, _p, _f32, _u64, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _sz, _p]),
+    "tagan_chunk_capacity": (_i64, [_i64, _i64, _i32]),
+    "tagan_part_capacity": (_i64, [_i64, _i32]),
+    "tagan_graph_chunks_workspace": (_sz, [_i64]),
+    "tagan_graph_chunks": (_c.c_int, [_p, _i64, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
+    "tagan_geo_attn_fwd_workspace": (_sz, [_p, _i32, _i32]),
+    "tagan_geo_attn_fwd": (_c.c_int, [_c.c_int, _c.c_int, _p, _i32, _i32, _p, _p, _p, _i64, _p, _f32,
+                                      _u64, _p, _p, _p, _p, _sz, _p]),
+    "tagan_geo_attn_bwd_workspace": (_sz, [_p, _i32, _i32]),
+    "tagan_geo_attn_bwd": (_c.c_int, [_c.c_int, _c.c_int, _p, _i32, _i32, _p, _p, _p, _i64, _p, _f32, _u64,
+                                      _p, _p, _p, _p, _p, _p, _i64, _p, _p, _sz, _p]),
     "tagan_temporal_attn_fwd": (_c.c_int, [_c.c_int, _i64, _i32, _i32, _i32, _p, _p, _p, _i64, _i64, _p, _p,
                                            _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,
                                            _p]),
@@ -45,6 +50,18 @@ _SIGNATURES = {
                                            _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,
                                            _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p, _sz, _p]),
 }
+
+
+
+class TaganGraph(ctypes.Structure):
+    """Mirror of ``struct tagan_graph`` (include/tagan_hip.h)."""
+    _fields_ = [("n_nodes", _i64), ("rowptr", _p), ("col", _p), ("csc_ptr", _p), ("csc_row", _p),
+                ("csc_eid", _p), ("chunk", _i32), ("chunk_cap", _i64), ("part_cap", _i64),
+                ("row_chunk_ptr", _p), ("row_chunk_seg", _p), ("row_chunk_beg", _p), ("row_chunk_part", _p),
+                ("row_multi", _p), ("row_counts", _p),
+                ("col_chunk_ptr", _p), ("col_chunk_seg", _p), ("col_chunk_beg", _p), ("col_chunk_part", _p),
+                ("col_multi", _p), ("col_counts", _p)]
+
 
 _lib = None
 

@@ -4,15 +4,18 @@
 // masked_fill(-inf) with the dense adjacency of graph_attention.py:96-105,
 // softmax, attn_dropout) and :579-583 (A·V), for rows = CSR rows = src = query.
 //
-// Layout: one wave64 per query row, all heads at once.  Lane l owns features
-// [l*VEC, l*VEC+VEC) of the H = heads*d row, so a head is an aligned group of
-// LPH = d/VEC lanes and per-head reductions are XOR butterflies inside the
-// group.  K/V rows of neighbours are gathered as whole coalesced rows
-// (64 lanes x VEC floats); the neighbour index is read once per 64 edges with a
-// coalesced load and broadcast with v_readlane (scalar base address).  Softmax
-// is online (running max / sum per head), so scores are never stored; the row's
-// log-sum-exp is saved for the backward pass.  HBM-bound: algorithmic bytes per
-// (layer, snapshot) in DESIGN.md §4.
+// Work decomposition (fast path): rows are split into chunks of <= `chunk`
+// CSR entries (tagan_graph_chunks) so power-law hubs do not serialise on one
+// wave; multi-chunk rows merge their partial (max, sum, acc) states in chunk
+// order (deterministic).  A group of LPR = H/4 lanes owns one chunk: lane l of
+// the group holds features [4l, 4l+4) (float4 gathers of whole K/V rows), a
+// head is an aligned sub-group of LPH = d/4 lanes (per-head reductions are XOR
+// butterflies), and a wave runs 64/LPR chunks side by side (more independent
+// gathers in flight).  Softmax is online (running max / sum per head), so
+// scores are never stored; the row's log-sum-exp is saved for the backward
+// pass.  HBM-bound: algorithmic bytes per (layer, snapshot) in DESIGN.md §4.
+// Shapes outside the fast path (H not in {32..256}, d % 4 != 0) use the
+// one-wave-per-row and one-thread-per-(row, head) fallbacks below.
 //
 // Backward (atomic-free, bitwise deterministic):
 //   row pass (CSR):    delta_i = Σ_f dO_i·O_i per head, dq_i = Σ_j ds_ij ∂s/∂q_i
@@ -159,13 +162,9 @@ __device__ __forceinline__ void store_vec(float* __restrict__ p, const float (&r
 }
 
 struct GeoArgs {
+    tagan_graph g;
     int64_t N;
     int heads, d, lph, H;
-    const int32_t* rowptr;
-    const int32_t* col;
-    const int32_t* csc_ptr;
-    const int32_t* csc_row;
-    const int32_t* csc_eid;
     const float* q;
     const float* k;
     const float* v;
@@ -184,247 +183,346 @@ struct GeoArgs {
     int64_t ldd;
     float* delta;
     float* prm_partial;
+    float* part_m;      // [part_cap, heads]
+    float* part_l;      // [part_cap, heads]
+    float* part_v;      // [part_cap, H]  (fwd acc / bwd dq)
+    float* part_v2;     // [part_cap, 2H] (bwd col: dk | dv)
     float inv_sqrt_d;
 };
 
 constexpr int UNROLL = 4;
 
-// ------------------------------------------------------------------ forward
-template <int METRIC, int VEC>
-__global__ void __launch_bounds__(BLK) k_geo_fwd(GeoArgs A) {
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int64_t row = xcd_remap(blockIdx.x, gridDim.x) * ROWS_PER_BLK + (threadIdx.x >> 6);
-    if (row >= A.N) return;
-    const int f0 = lane * VEC;
-    const bool active = f0 < A.H;
-    const int fo = active ? f0 : 0;
-    const int h = fo / A.d;
-    float qv[VEC];
-    load_vec<VEC>(A.q + row * A.ld + fo, qv);
-    float qq = 0.f;
-    if constexpr (MetricTraits<METRIC>::fam == FAM_COS) {
-#pragma unroll
-        for (int c = 0; c < VEC; ++c) qq = fmaf(qv[c], qv[c], qq);
-        qq = grp_sum(active ? qq : 0.f, A.lph);
-    }
-    const float prm = A.mparam ? A.mparam[h] : 1.f;
-    float m = -INFINITY, l = 0.f, acc[VEC];
-#pragma unroll
-    for (int c = 0; c < VEC; ++c) acc[c] = 0.f;
-    const int e0 = A.rowptr[row], e1 = A.rowptr[row + 1];
-    for (int base = e0; base < e1; base += WAVE) {
-        const int cnt = min(WAVE, e1 - base);
-        const int mycol = (lane < cnt) ? A.col[base + lane] : 0;
-        for (int jj = 0; jj < cnt; jj += UNROLL) {
-            float kv[UNROLL][VEC], vv[UNROLL][VEC];
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const int src_lane = min(jj + u, cnt - 1);
-                const int j = __builtin_amdgcn_readlane(mycol, src_lane);
-                load_vec<VEC>(A.k + (int64_t)j * A.ld + fo, kv[u]);
-                load_vec<VEC>(A.v + (int64_t)j * A.ld + fo, vv[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                if (jj + u >= cnt) break;
-                float a, b;
-                pair_partial<METRIC, VEC>(qv, kv[u], a, b);
-                a = grp_sum(a, A.lph);
-                if constexpr (MetricTraits<METRIC>::fam == FAM_COS) b = grp_sum(b, A.lph);
-                const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
-                const float mn = fmaxf(m, s);
-                const float corr = __expf(m - mn);
-                const float p = __expf(s - mn);
-                l = fmaf(l, corr, p);
-                float pw = p;
-                if (A.p_drop > 0.f) {
-                    const uint64_t idx = (uint64_t)(base + jj + u) * (uint64_t)A.heads + (uint64_t)h;
-                    pw = (uniform01(A.seed, idx) >= A.p_drop) ? p * A.inv_keep : 0.f;
-                }
-#pragma unroll
-                for (int c = 0; c < VEC; ++c) acc[c] = fmaf(acc[c], corr, pw * vv[u][c]);
-                m = mn;
-            }
-        }
-    }
-    if (!active) return;
-    const float inv_l = 1.f / l;   // l == 0 (no entries) -> NaN output, as softmax over all -inf
-    float r[VEC];
-#pragma unroll
-    for (int c = 0; c < VEC; ++c) r[c] = (l > 0.f) ? acc[c] * inv_l : NAN;
-    store_vec<VEC>(A.out + row * (int64_t)A.H + f0, r);
-    if ((lane % A.lph) == 0) A.lse[row * A.heads + h] = m + __logf(l);
+__device__ __forceinline__ float sgnf(float x) { return (x > 0.f) ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float f4(const float4& v, int c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
+
+template <int METRIC>
+__device__ __forceinline__ void partial4(const float4& q, const float4& k, float& a, float& b) {
+    float qa[4] = {q.x, q.y, q.z, q.w}, ka[4] = {k.x, k.y, k.z, k.w};
+    pair_partial<METRIC, 4>(qa, ka, a, b);
 }
 
-// ------------------------------------------------------------------ backward, row pass
-template <int METRIC, int VEC>
-__global__ void __launch_bounds__(BLK) k_geo_bwd_row(GeoArgs A) {
-    __shared__ float red[ROWS_PER_BLK][64];
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int wid = threadIdx.x >> 6;
-    const int64_t blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int64_t row = blk * ROWS_PER_BLK + wid;
-    const int f0 = lane * VEC;
-    const bool active = f0 < A.H;
-    const int fo = active ? f0 : 0;
-    const int h = fo / A.d;
-    float prm_acc = 0.f;
-    if (row < A.N) {
-        float qv[VEC], ov[VEC], dov[VEC];
-        load_vec<VEC>(A.q + row * A.ld + fo, qv);
-        load_vec<VEC>(A.o + row * (int64_t)A.H + fo, ov);
-        load_vec<VEC>(A.dout + row * (int64_t)A.H + fo, dov);
-        float D = 0.f;
+// =================================================================== fast path: chunked kernels
+// Lane geometry shared by the chunk kernels.
+template <int LPR>
+struct Lanes {
+    static constexpr int RPW = WAVE / LPR;   // chunks per wave
+    int lane, sub, sl, base;                  // base = first lane of this chunk's group
+    int64_t chunk;                            // global chunk id of this group
+    __device__ __forceinline__ Lanes() {
+        lane = threadIdx.x & (WAVE - 1);
+        sub = lane / LPR;
+        sl = lane % LPR;
+        base = sub * LPR;
+        const int64_t wave = xcd_remap(blockIdx.x, gridDim.x) * (BLK / WAVE) + (threadIdx.x >> 6);
+        chunk = wave * RPW + sub;
+    }
+};
+
+// ------------------------------------------------------------------ forward
+template <int METRIC, int LPR>
+__global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
+    Lanes<LPR> L;
+    const int nchunks = A.g.row_counts[0];
+    const bool valid = L.chunk < nchunks;
+    int row = 0, e0 = 0, cnt = 0;
+    if (valid) {
+        row = A.g.row_chunk_seg[L.chunk];
+        e0 = A.g.row_chunk_beg[L.chunk];
+        cnt = min(A.g.chunk, A.g.rowptr[row + 1] - e0);
+    }
+    if (!__any(valid)) return;
+    const int f0 = L.sl * 4;
+    const int h = f0 / A.d;
+    const float4 qv = ld4(A.q + (int64_t)row * A.ld + f0);
+    float qq = 0.f;
+    if constexpr (MetricTraits<METRIC>::fam == FAM_COS)
+        qq = grp_sum(qv.x * qv.x + qv.y * qv.y + qv.z * qv.z + qv.w * qv.w, A.lph);
+    const float prm = A.mparam ? A.mparam[h] : 1.f;
+    float m = -INFINITY, l = 0.f;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int mycol = 0;
+    for (int jj = 0; __any(jj < cnt); jj += UNROLL) {
+        if ((jj % LPR) == 0) mycol = (jj + L.sl < cnt) ? A.g.col[e0 + jj + L.sl] : 0;
+        float4 kv[UNROLL], vv[UNROLL];
 #pragma unroll
-        for (int c = 0; c < VEC; ++c) D = fmaf(dov[c], ov[c], D);
-        D = grp_sum(active ? D : 0.f, A.lph);
-        float qq = 0.f;
-        if constexpr (MetricTraits<METRIC>::fam == FAM_COS) {
-#pragma unroll
-            for (int c = 0; c < VEC; ++c) qq = fmaf(qv[c], qv[c], qq);
-            qq = grp_sum(active ? qq : 0.f, A.lph);
+        for (int u = 0; u < UNROLL; ++u) {
+            const int j = __shfl(mycol, L.base + ((jj + u) % LPR), WAVE);
+            const float* kr = A.k + (int64_t)j * A.ld + f0;
+            const float* vr = A.v + (int64_t)j * A.ld + f0;
+            kv[u] = ld4(kr);
+            vv[u] = ld4(vr);
         }
-        const float lse = A.lse_in[row * A.heads + h];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const bool live = jj + u < cnt;
+            float a, b;
+            partial4<METRIC>(qv, kv[u], a, b);
+            a = grp_sum(a, A.lph);
+            if constexpr (MetricTraits<METRIC>::fam == FAM_COS) b = grp_sum(b, A.lph);
+            if (!live) continue;
+            const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
+            const float mn = fmaxf(m, s);
+            const float corr = __expf(m - mn);
+            const float p = __expf(s - mn);
+            l = fmaf(l, corr, p);
+            float pw = p;
+            if (A.p_drop > 0.f) {
+                const uint64_t idx = (uint64_t)(e0 + jj + u) * (uint64_t)A.heads + (uint64_t)h;
+                pw = (uniform01(A.seed, idx) >= A.p_drop) ? p * A.inv_keep : 0.f;
+            }
+            acc.x = fmaf(acc.x, corr, pw * vv[u].x);
+            acc.y = fmaf(acc.y, corr, pw * vv[u].y);
+            acc.z = fmaf(acc.z, corr, pw * vv[u].z);
+            acc.w = fmaf(acc.w, corr, pw * vv[u].w);
+            m = mn;
+        }
+    }
+    if (!valid) return;
+    const int part = A.g.row_chunk_part[L.chunk];
+    if (part < 0) {
+        const float inv = (l > 0.f) ? 1.f / l : NAN;
+        st4(A.out + (int64_t)row * A.H + f0, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
+        if ((L.sl % A.lph) == 0) A.lse[(int64_t)row * A.heads + h] = m + __logf(l);
+    } else {
+        st4(A.part_v + (int64_t)part * A.H + f0, acc);
+        if ((L.sl % A.lph) == 0) {
+            A.part_m[(int64_t)part * A.heads + h] = m;
+            A.part_l[(int64_t)part * A.heads + h] = l;
+        }
+    }
+}
+
+// Merge the partial softmax states of multi-chunk rows, in chunk order.  One wave per row,
+// lane owns 4 features (H <= 256).
+__global__ void __launch_bounds__(BLK) k_geo_fwd_merge(GeoArgs A) {
+    const int64_t k = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6);
+    if (k >= A.g.row_counts[1]) return;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int f0 = lane * 4;
+    if (f0 >= A.H) return;
+    const int h = f0 / A.d;
+    const int row = A.g.row_multi[k];
+    const int c0 = A.g.row_chunk_ptr[row], c1 = A.g.row_chunk_ptr[row + 1];
+    float M = -INFINITY, Lsum = 0.f;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int c = c0; c < c1; ++c) {
+        const int part = A.g.row_chunk_part[c];
+        const float m = A.part_m[(int64_t)part * A.heads + h];
+        const float l = A.part_l[(int64_t)part * A.heads + h];
+        const float4 a = ld4(A.part_v + (int64_t)part * A.H + f0);
+        const float mn = fmaxf(M, m);
+        const float ca = (M == -INFINITY) ? 0.f : __expf(M - mn);
+        const float cb = (m == -INFINITY) ? 0.f : __expf(m - mn);
+        Lsum = Lsum * ca + l * cb;
+        acc.x = acc.x * ca + a.x * cb;
+        acc.y = acc.y * ca + a.y * cb;
+        acc.z = acc.z * ca + a.z * cb;
+        acc.w = acc.w * ca + a.w * cb;
+        M = mn;
+    }
+    const float inv = (Lsum > 0.f) ? 1.f / Lsum : NAN;
+    st4(A.out + (int64_t)row * A.H + f0, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
+    if ((lane % A.lph) == 0) A.lse[(int64_t)row * A.heads + h] = M + __logf(Lsum);
+}
+
+// ------------------------------------------------------------------ backward, row pass (CSR chunks)
+template <int METRIC, int LPR>
+__global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
+    __shared__ float red[BLK];
+    Lanes<LPR> L;
+    const int nchunks = A.g.row_counts[0];
+    const bool valid = L.chunk < nchunks;
+    int row = 0, e0 = 0, cnt = 0;
+    if (valid) {
+        row = A.g.row_chunk_seg[L.chunk];
+        e0 = A.g.row_chunk_beg[L.chunk];
+        cnt = min(A.g.chunk, A.g.rowptr[row + 1] - e0);
+    }
+    const int f0 = L.sl * 4;
+    const int h = f0 / A.d;
+    float prm_acc = 0.f;
+    if (__any(valid)) {
+        const float4 qv = ld4(A.q + (int64_t)row * A.ld + f0);
+        const float4 ov = ld4(A.o + (int64_t)row * A.H + f0);
+        const float4 dov = ld4(A.dout + (int64_t)row * A.H + f0);
+        const float D = grp_sum(dov.x * ov.x + dov.y * ov.y + dov.z * ov.z + dov.w * ov.w, A.lph);
+        float qq = 0.f;
+        if constexpr (MetricTraits<METRIC>::fam == FAM_COS)
+            qq = grp_sum(qv.x * qv.x + qv.y * qv.y + qv.z * qv.z + qv.w * qv.w, A.lph);
+        const float lse = A.lse_in[(int64_t)row * A.heads + h];
         const float prm = A.mparam ? A.mparam[h] : 1.f;
-        float dqa[VEC];
+        float4 dq = make_float4(0.f, 0.f, 0.f, 0.f);
+        int mycol = 0;
+        for (int jj = 0; __any(jj < cnt); jj += UNROLL) {
+            if ((jj % LPR) == 0) mycol = (jj + L.sl < cnt) ? A.g.col[e0 + jj + L.sl] : 0;
+            float4 kv[UNROLL], vv[UNROLL];
 #pragma unroll
-        for (int c = 0; c < VEC; ++c) dqa[c] = 0.f;
-        const int e0 = A.rowptr[row], e1 = A.rowptr[row + 1];
-        for (int base = e0; base < e1; base += WAVE) {
-            const int cnt = min(WAVE, e1 - base);
-            const int mycol = (lane < cnt) ? A.col[base + lane] : 0;
-            for (int jj = 0; jj < cnt; jj += UNROLL) {
-                float kv[UNROLL][VEC], vv[UNROLL][VEC];
+            for (int u = 0; u < UNROLL; ++u) {
+                const int j = __shfl(mycol, L.base + ((jj + u) % LPR), WAVE);
+                kv[u] = ld4(A.k + (int64_t)j * A.ld + f0);
+                vv[u] = ld4(A.v + (int64_t)j * A.ld + f0);
+            }
 #pragma unroll
-                for (int u = 0; u < UNROLL; ++u) {
-                    const int j = __builtin_amdgcn_readlane(mycol, min(jj + u, cnt - 1));
-                    load_vec<VEC>(A.k + (int64_t)j * A.ld + fo, kv[u]);
-                    load_vec<VEC>(A.v + (int64_t)j * A.ld + fo, vv[u]);
+            for (int u = 0; u < UNROLL; ++u) {
+                const bool live = jj + u < cnt;
+                float a, b;
+                partial4<METRIC>(qv, kv[u], a, b);
+                float dp = dov.x * vv[u].x + dov.y * vv[u].y + dov.z * vv[u].z + dov.w * vv[u].w;
+                a = grp_sum(a, A.lph);
+                dp = grp_sum(dp, A.lph);
+                if constexpr (MetricTraits<METRIC>::fam == FAM_COS) b = grp_sum(b, A.lph);
+                if (!live) continue;
+                const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
+                const float p = __expf(s - lse);
+                if (A.p_drop > 0.f) {
+                    const uint64_t idx = (uint64_t)(e0 + jj + u) * (uint64_t)A.heads + (uint64_t)h;
+                    dp = (uniform01(A.seed, idx) >= A.p_drop) ? dp * A.inv_keep : 0.f;
                 }
+                const float ds = p * (dp - D);
+                const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
 #pragma unroll
-                for (int u = 0; u < UNROLL; ++u) {
-                    if (jj + u >= cnt) break;
-                    float a, b, dp = 0.f;
-                    pair_partial<METRIC, VEC>(qv, kv[u], a, b);
-#pragma unroll
-                    for (int c = 0; c < VEC; ++c) dp = fmaf(dov[c], vv[u][c], dp);
-                    a = grp_sum(a, A.lph);
-                    dp = grp_sum(dp, A.lph);
-                    if constexpr (MetricTraits<METRIC>::fam == FAM_COS) b = grp_sum(b, A.lph);
-                    const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
-                    const float p = __expf(s - lse);
-                    if (A.p_drop > 0.f) {
-                        const uint64_t idx = (uint64_t)(base + jj + u) * (uint64_t)A.heads + (uint64_t)h;
-                        dp = (uniform01(A.seed, idx) >= A.p_drop) ? dp * A.inv_keep : 0.f;
-                    }
-                    const float ds = p * (dp - D);
-                    const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
-#pragma unroll
-                    for (int c = 0; c < VEC; ++c) {
-                        float t = fmaf(g.cq_q, qv[c], g.cq_k * kv[u][c]);
-                        if constexpr (MetricTraits<METRIC>::fam == FAM_ABS) {
-                            const float dfc = qv[c] - kv[u][c];
-                            t = g.sg * ((dfc > 0.f) ? 1.f : (dfc < 0.f ? -1.f : 0.f));
-                        }
-                        dqa[c] = fmaf(ds, t, dqa[c]);
-                    }
-                    prm_acc = fmaf(ds, g.dprm, prm_acc);
+                for (int c = 0; c < 4; ++c) {
+                    const float qc = f4(qv, c), kc = f4(kv[u], c);
+                    float t = fmaf(g.cq_q, qc, g.cq_k * kc);
+                    if constexpr (MetricTraits<METRIC>::fam == FAM_ABS) t = g.sg * sgnf(qc - kc);
+                    const float r = ds * t;
+                    if (c == 0) dq.x += r; else if (c == 1) dq.y += r; else if (c == 2) dq.z += r; else dq.w += r;
                 }
+                prm_acc = fmaf(ds, g.dprm, prm_acc);
             }
         }
-        if (active) {
-            store_vec<VEC>(A.dq + row * A.ldd + f0, dqa);
-            if ((lane % A.lph) == 0) A.delta[row * A.heads + h] = D;
+        if (valid) {
+            const int part = A.g.row_chunk_part[L.chunk];
+            if (part < 0) st4(A.dq + (int64_t)row * A.ldd + f0, dq);
+            else st4(A.part_v + (int64_t)part * A.H + f0, dq);
+            if ((L.sl % A.lph) == 0 && A.g.row_chunk_ptr[row] == L.chunk) A.delta[(int64_t)row * A.heads + h] = D;
         }
     }
     if (A.prm_partial) {
-        // one value per (wave, head): lanes with lane % lph == 0 own a head
-        red[wid][lane] = (row < A.N && active && (lane % A.lph) == 0) ? prm_acc : 0.f;
+        red[threadIdx.x] = (valid && (L.sl % A.lph) == 0) ? prm_acc : 0.f;
         __syncthreads();
         if (threadIdx.x < A.heads) {
-            float s = 0.f;
-            const int lane0 = threadIdx.x * A.lph;   // first lane of head threadIdx.x (VEC*lph = d)
-            for (int w = 0; w < ROWS_PER_BLK; ++w) s += red[w][lane0];
-            A.prm_partial[blk * A.heads + threadIdx.x] = s;
+            float sacc = 0.f;
+            const int off = threadIdx.x * A.lph;            // lane of head threadIdx.x inside a group
+            for (int w = 0; w < BLK / WAVE; ++w)
+                for (int sg = 0; sg < Lanes<LPR>::RPW; ++sg) sacc += red[w * WAVE + sg * LPR + off];
+            A.prm_partial[(int64_t)blockIdx.x * A.heads + threadIdx.x] = sacc;
         }
     }
 }
 
-// ------------------------------------------------------------------ backward, column pass
-template <int METRIC, int VEC>
-__global__ void __launch_bounds__(BLK) k_geo_bwd_col(GeoArgs A) {
+// Sum partial rows (bwd row: dq; bwd col: dk|dv) of multi-chunk segments in chunk order.
+__global__ void __launch_bounds__(BLK) k_geo_sum_parts(const int32_t* __restrict__ counts,
+                                                       const int32_t* __restrict__ multi,
+                                                       const int32_t* __restrict__ chunk_ptr,
+                                                       const int32_t* __restrict__ chunk_part,
+                                                       const float* __restrict__ part, int width,
+                                                       float* __restrict__ dst0, float* __restrict__ dst1,
+                                                       int64_t ldd, int H) {
+    const int64_t k = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6);
+    if (k >= counts[1]) return;
     const int lane = threadIdx.x & (WAVE - 1);
-    const int64_t colj = xcd_remap(blockIdx.x, gridDim.x) * ROWS_PER_BLK + (threadIdx.x >> 6);
-    if (colj >= A.N) return;
-    const int f0 = lane * VEC;
-    const bool active = f0 < A.H;
-    const int fo = active ? f0 : 0;
-    const int h = fo / A.d;
-    float kv[VEC], vv[VEC];
-    load_vec<VEC>(A.k + colj * A.ld + fo, kv);
-    load_vec<VEC>(A.v + colj * A.ld + fo, vv);
+    const int seg = multi[k];
+    const int c0 = chunk_ptr[seg], c1 = chunk_ptr[seg + 1];
+    for (int f0 = lane * 4; f0 < width; f0 += WAVE * 4) {
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int c = c0; c < c1; ++c) {
+            const float4 a = ld4(part + (int64_t)chunk_part[c] * width + f0);
+            s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+        }
+        float* dst = (f0 < H) ? dst0 + (int64_t)seg * ldd + f0 : dst1 + (int64_t)seg * ldd + (f0 - H);
+        st4(dst, s);
+    }
+}
+
+// ------------------------------------------------------------------ backward, column pass (CSC chunks)
+template <int METRIC, int LPR>
+__global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
+    Lanes<LPR> L;
+    const int nchunks = A.g.col_counts[0];
+    const bool valid = L.chunk < nchunks;
+    int colj = 0, e0 = 0, cnt = 0;
+    if (valid) {
+        colj = A.g.col_chunk_seg[L.chunk];
+        e0 = A.g.col_chunk_beg[L.chunk];
+        cnt = min(A.g.chunk, A.g.csc_ptr[colj + 1] - e0);
+    }
+    if (!__any(valid)) return;
+    const int f0 = L.sl * 4;
+    const int h = f0 / A.d;
+    const float4 kv = ld4(A.k + (int64_t)colj * A.ld + f0);
+    const float4 vv = ld4(A.v + (int64_t)colj * A.ld + f0);
     const float prm = A.mparam ? A.mparam[h] : 1.f;
-    float dka[VEC], dva[VEC];
+    float4 dk = make_float4(0.f, 0.f, 0.f, 0.f), dv = make_float4(0.f, 0.f, 0.f, 0.f);
+    int myrow = 0, myeid = 0;
+    for (int jj = 0; __any(jj < cnt); jj += UNROLL) {
+        if ((jj % LPR) == 0) {
+            const bool in = jj + L.sl < cnt;
+            myrow = in ? A.g.csc_row[e0 + jj + L.sl] : 0;
+            myeid = in ? A.g.csc_eid[e0 + jj + L.sl] : 0;
+        }
+        float4 qv[UNROLL], dov[UNROLL];
+        float lse[UNROLL], D[UNROLL];
+        int eid[UNROLL];
 #pragma unroll
-    for (int c = 0; c < VEC; ++c) { dka[c] = 0.f; dva[c] = 0.f; }
-    const int e0 = A.csc_ptr[colj], e1 = A.csc_ptr[colj + 1];
-    for (int base = e0; base < e1; base += WAVE) {
-        const int cnt = min(WAVE, e1 - base);
-        const int myrow = (lane < cnt) ? A.csc_row[base + lane] : 0;
-        const int myeid = (lane < cnt) ? A.csc_eid[base + lane] : 0;
-        for (int jj = 0; jj < cnt; jj += UNROLL) {
-            float qv[UNROLL][VEC], dov[UNROLL][VEC], lse[UNROLL], D[UNROLL];
+        for (int u = 0; u < UNROLL; ++u) {
+            const int src = L.base + ((jj + u) % LPR);
+            const int i = __shfl(myrow, src, WAVE);
+            eid[u] = __shfl(myeid, src, WAVE);
+            qv[u] = ld4(A.q + (int64_t)i * A.ld + f0);
+            dov[u] = ld4(A.dout + (int64_t)i * A.H + f0);
+            lse[u] = A.lse_in[(int64_t)i * A.heads + h];
+            D[u] = A.delta[(int64_t)i * A.heads + h];
+        }
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const int i = __builtin_amdgcn_readlane(myrow, min(jj + u, cnt - 1));
-                load_vec<VEC>(A.q + (int64_t)i * A.ld + fo, qv[u]);
-                load_vec<VEC>(A.dout + (int64_t)i * A.H + fo, dov[u]);
-                lse[u] = A.lse_in[(int64_t)i * A.heads + h];
-                D[u] = A.delta[(int64_t)i * A.heads + h];
+        for (int u = 0; u < UNROLL; ++u) {
+            const bool live = jj + u < cnt;
+            float a, b, qq = 0.f;
+            partial4<METRIC>(qv[u], kv, a, b);
+            float dp = dov[u].x * vv.x + dov[u].y * vv.y + dov[u].z * vv.z + dov[u].w * vv.w;
+            a = grp_sum(a, A.lph);
+            dp = grp_sum(dp, A.lph);
+            if constexpr (MetricTraits<METRIC>::fam == FAM_COS) {
+                b = grp_sum(b, A.lph);
+                qq = grp_sum(qv[u].x * qv[u].x + qv[u].y * qv[u].y + qv[u].z * qv[u].z + qv[u].w * qv[u].w,
+                             A.lph);
             }
+            if (!live) continue;
+            const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
+            const float p = __expf(s - lse[u]);
+            float pw = p;
+            if (A.p_drop > 0.f) {
+                const bool keep = uniform01(A.seed, (uint64_t)eid[u] * (uint64_t)A.heads + (uint64_t)h) >= A.p_drop;
+                dp = keep ? dp * A.inv_keep : 0.f;
+                pw = keep ? p * A.inv_keep : 0.f;
+            }
+            const float ds = p * (dp - D[u]);
+            const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                if (jj + u >= cnt) break;
-                float a, b, dp = 0.f, qq = 0.f;
-                pair_partial<METRIC, VEC>(qv[u], kv, a, b);
-#pragma unroll
-                for (int c = 0; c < VEC; ++c) dp = fmaf(dov[u][c], vv[c], dp);
-                a = grp_sum(a, A.lph);
-                dp = grp_sum(dp, A.lph);
-                if constexpr (MetricTraits<METRIC>::fam == FAM_COS) {
-                    b = grp_sum(b, A.lph);
-#pragma unroll
-                    for (int c = 0; c < VEC; ++c) qq = fmaf(qv[u][c], qv[u][c], qq);
-                    qq = grp_sum(active ? qq : 0.f, A.lph);
-                }
-                const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
-                const float p = __expf(s - lse[u]);
-                float pw = p;
-                if (A.p_drop > 0.f) {
-                    const int eid = __builtin_amdgcn_readlane(myeid, jj + u);
-                    const uint64_t idx = (uint64_t)eid * (uint64_t)A.heads + (uint64_t)h;
-                    const bool keep = uniform01(A.seed, idx) >= A.p_drop;
-                    dp = keep ? dp * A.inv_keep : 0.f;
-                    pw = keep ? p * A.inv_keep : 0.f;
-                }
-                const float ds = p * (dp - D[u]);
-                const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
-#pragma unroll
-                for (int c = 0; c < VEC; ++c) {
-                    float t = fmaf(g.ck_q, qv[u][c], g.ck_k * kv[c]);
-                    if constexpr (MetricTraits<METRIC>::fam == FAM_ABS) {
-                        const float dfc = qv[u][c] - kv[c];
-                        t = -g.sg * ((dfc > 0.f) ? 1.f : (dfc < 0.f ? -1.f : 0.f));
-                    }
-                    dka[c] = fmaf(ds, t, dka[c]);
-                    dva[c] = fmaf(pw, dov[u][c], dva[c]);
-                }
+            for (int c = 0; c < 4; ++c) {
+                const float qc = f4(qv[u], c), kc = f4(kv, c);
+                float t = fmaf(g.ck_q, qc, g.ck_k * kc);
+                if constexpr (MetricTraits<METRIC>::fam == FAM_ABS) t = -g.sg * sgnf(qc - kc);
+                const float r = ds * t, w = pw * f4(dov[u], c);
+                if (c == 0) { dk.x += r; dv.x += w; }
+                else if (c == 1) { dk.y += r; dv.y += w; }
+                else if (c == 2) { dk.z += r; dv.z += w; }
+                else { dk.w += r; dv.w += w; }
             }
         }
     }
-    if (!active) return;
-    store_vec<VEC>(A.dk + colj * A.ldd + f0, dka);
-    store_vec<VEC>(A.dv + colj * A.ldd + f0, dva);
+    if (!valid) return;
+    const int part = A.g.col_chunk_part[L.chunk];
+    if (part < 0) {
+        st4(A.dk + (int64_t)colj * A.ldd + f0, dk);
+        st4(A.dv + (int64_t)colj * A.ldd + f0, dv);
+    } else {
+        st4(A.part_v2 + (int64_t)part * 2 * A.H + f0, dk);
+        st4(A.part_v2 + (int64_t)part * 2 * A.H + A.H + f0, dv);
+    }
 }
 
 // Deterministic reduction of per-block parameter-gradient partials.
@@ -443,9 +541,9 @@ __global__ void __launch_bounds__(BLK) k_reduce_partials(const float* __restrict
     if (threadIdx.x == 0) out[h] = red[0];
 }
 
-// Optional per-edge attention weights (post-dropout), [nnz, heads].  Generic
-// one-thread-per-(row, head) walker: only used for return_attention_weights and
-// the geometric_bias path of the standalone GeometricAttention API.
+// =================================================================== fallback path (any H, d)
+// One thread per (row, head), whole rows, no chunking.  Correct for every shape;
+// used only when the fast path's lane geometry does not fit.
 template <int METRIC>
 __global__ void __launch_bounds__(BLK) k_geo_alpha(GeoArgs A, float* __restrict__ alpha) {
     const int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x;
@@ -457,8 +555,8 @@ __global__ void __launch_bounds__(BLK) k_geo_alpha(GeoArgs A, float* __restrict_
     for (int c = 0; c < A.d; ++c) qq = fmaf(qr[c], qr[c], qq);
     const float prm = A.mparam ? A.mparam[h] : 1.f;
     const float lse = A.lse[row * A.heads + h];
-    for (int e = A.rowptr[row]; e < A.rowptr[row + 1]; ++e) {
-        const float* kr = A.k + (int64_t)A.col[e] * A.ld + h * A.d;
+    for (int e = A.g.rowptr[row]; e < A.g.rowptr[row + 1]; ++e) {
+        const float* kr = A.k + (int64_t)A.g.col[e] * A.ld + h * A.d;
         float a = 0.f, b = 0.f;
         for (int c = 0; c < A.d; ++c) {
             float qa[1] = {qr[c]}, ka[1] = {kr[c]}, pa, pb;
@@ -473,8 +571,6 @@ __global__ void __launch_bounds__(BLK) k_geo_alpha(GeoArgs A, float* __restrict_
     }
 }
 
-// ------------------------------------------------------------------ generic fallback
-// One thread per (row, head); any H, d (used when H is not a power of two <= 256).
 template <int METRIC>
 __global__ void __launch_bounds__(BLK) k_geo_fwd_generic(GeoArgs A) {
     const int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x;
@@ -489,8 +585,8 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_generic(GeoArgs A) {
     float m = -INFINITY, l = 0.f;
     float* orow = A.out + row * (int64_t)A.H + h * d;
     for (int c = 0; c < d; ++c) orow[c] = 0.f;
-    for (int e = A.rowptr[row]; e < A.rowptr[row + 1]; ++e) {
-        const int64_t j = A.col[e];
+    for (int e = A.g.rowptr[row]; e < A.g.rowptr[row + 1]; ++e) {
+        const int64_t j = A.g.col[e];
         const float* kr = A.k + j * A.ld + h * d;
         const float* vr = A.v + j * A.ld + h * d;
         float a = 0.f, b = 0.f;
@@ -533,8 +629,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_generic(GeoArgs A) {
     const float prm = A.mparam ? A.mparam[h] : 1.f;
     const float lse = A.lse_in[row * A.heads + h];
     float prm_acc = 0.f;
-    for (int e = A.rowptr[row]; e < A.rowptr[row + 1]; ++e) {
-        const int64_t j = A.col[e];
+    for (int e = A.g.rowptr[row]; e < A.g.rowptr[row + 1]; ++e) {
+        const int64_t j = A.g.col[e];
         const float* kr = A.k + j * A.ld + h * d;
         const float* vr = A.v + j * A.ld + h * d;
         float a = 0.f, b = 0.f, dp = 0.f;
@@ -553,16 +649,13 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_generic(GeoArgs A) {
         const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
         for (int c = 0; c < d; ++c) {
             float tt = fmaf(g.cq_q, qr[c], g.cq_k * kr[c]);
-            if constexpr (MetricTraits<METRIC>::fam == FAM_ABS) {
-                const float dfc = qr[c] - kr[c];
-                tt = g.sg * ((dfc > 0.f) ? 1.f : (dfc < 0.f ? -1.f : 0.f));
-            }
+            if constexpr (MetricTraits<METRIC>::fam == FAM_ABS) tt = g.sg * sgnf(qr[c] - kr[c]);
             dqr[c] = fmaf(ds, tt, dqr[c]);
         }
         prm_acc = fmaf(ds, g.dprm, prm_acc);
     }
     A.delta[row * A.heads + h] = D;
-    if (A.prm_partial) A.prm_partial[t] = prm_acc;   // [N*heads] partials: reduced per head below
+    if (A.prm_partial) A.prm_partial[t] = prm_acc;   // [N*heads] partials, reduced per head
 }
 
 template <int METRIC>
@@ -578,9 +671,9 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_generic(GeoArgs A) {
     float* dvr = A.dv + colj * A.ldd + h * d;
     for (int c = 0; c < d; ++c) { dkr[c] = 0.f; dvr[c] = 0.f; }
     const float prm = A.mparam ? A.mparam[h] : 1.f;
-    for (int e = A.csc_ptr[colj]; e < A.csc_ptr[colj + 1]; ++e) {
-        const int64_t i = A.csc_row[e];
-        const int eid = A.csc_eid[e];
+    for (int e = A.g.csc_ptr[colj]; e < A.g.csc_ptr[colj + 1]; ++e) {
+        const int64_t i = A.g.csc_row[e];
+        const int eid = A.g.csc_eid[e];
         const float* qr = A.q + i * A.ld + h * d;
         const float* dor = A.dout + i * (int64_t)A.H + h * d;
         float a = 0.f, b = 0.f, dp = 0.f, qq = 0.f;
@@ -604,103 +697,109 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_generic(GeoArgs A) {
         const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
         for (int c = 0; c < d; ++c) {
             float tt = fmaf(g.ck_q, qr[c], g.ck_k * kr[c]);
-            if constexpr (MetricTraits<METRIC>::fam == FAM_ABS) {
-                const float dfc = qr[c] - kr[c];
-                tt = -g.sg * ((dfc > 0.f) ? 1.f : (dfc < 0.f ? -1.f : 0.f));
-            }
+            if constexpr (MetricTraits<METRIC>::fam == FAM_ABS) tt = -g.sg * sgnf(qr[c] - kr[c]);
             dkr[c] = fmaf(ds, tt, dkr[c]);
             dvr[c] = fmaf(pw, dor[c], dvr[c]);
         }
     }
 }
 
-// ------------------------------------------------------------------ dispatch
-// Fast path: H a power of two in [1, 256] (VEC = max(1, H/64) floats per lane)
-// and d a multiple of VEC with d/VEC a power of two.
-int pick_vec(int H, int d) {
-    if (H <= 0 || H > 256 || (H & (H - 1))) return 0;
-    const int vec = H <= 64 ? 1 : H / 64;
-    if (d % vec) return 0;
-    const int lph = d / vec;
-    if (lph < 1 || (lph & (lph - 1)) || lph > 64) return 0;
-    return vec;
+// =================================================================== dispatch
+// Fast path: H = 4*LPR with LPR in {8,16,32,64} and d = 4*LPH with LPH a power of two.
+int pick_lpr(int H, int d) {
+    if (d % 4 != 0) return 0;
+    const int lph = d / 4;
+    if (lph & (lph - 1)) return 0;
+    if (H == 32 || H == 64 || H == 128 || H == 256) return H / 4;
+    return 0;
 }
 
 enum Pass { P_FWD, P_BWD_ROW, P_BWD_COL, P_ALPHA };
 
+int64_t chunk_blocks(const GeoArgs& A, int lpr) {
+    const int64_t rpw = WAVE / lpr;
+    const int64_t waves = (A.g.chunk_cap + rpw - 1) / rpw;
+    return std::max<int64_t>(1, (waves + (BLK / WAVE) - 1) / (BLK / WAVE));
+}
+
+template <int METRIC, int LPR>
+void launch_fast(Pass pass, const GeoArgs& A, hipStream_t s) {
+    const dim3 g((unsigned)chunk_blocks(A, LPR));
+    if (pass == P_FWD) k_geo_fwd_chunk<METRIC, LPR><<<g, BLK, 0, s>>>(A);
+    else if (pass == P_BWD_ROW) k_geo_bwd_row_chunk<METRIC, LPR><<<g, BLK, 0, s>>>(A);
+    else k_geo_bwd_col_chunk<METRIC, LPR><<<g, BLK, 0, s>>>(A);
+}
+
 template <int METRIC>
-int launch_metric(Pass pass, int vec, const GeoArgs& A, hipStream_t s, float* alpha) {
-    const int64_t nblk_fast = (A.N + ROWS_PER_BLK - 1) / ROWS_PER_BLK;
-    const int64_t nblk_gen = (A.N * A.heads + BLK - 1) / BLK;
-    dim3 gf((unsigned)nblk_fast), gg((unsigned)nblk_gen);
+int launch_metric(Pass pass, int lpr, const GeoArgs& A, hipStream_t s, float* alpha) {
+    const dim3 gg((unsigned)((A.N * A.heads + BLK - 1) / BLK));
     if (pass == P_ALPHA) {
         k_geo_alpha<METRIC><<<gg, BLK, 0, s>>>(A, alpha);
         return TAGAN_OK;
     }
-#define TAGAN_GEO_CASE(V)                                                                     \
-    case V:                                                                                   \
-        if (pass == P_FWD) k_geo_fwd<METRIC, V><<<gf, BLK, 0, s>>>(A);                         \
-        else if (pass == P_BWD_ROW) k_geo_bwd_row<METRIC, V><<<gf, BLK, 0, s>>>(A);            \
-        else k_geo_bwd_col<METRIC, V><<<gf, BLK, 0, s>>>(A);                                   \
-        return TAGAN_OK;
-    switch (vec) {
-        TAGAN_GEO_CASE(1)
-        TAGAN_GEO_CASE(2)
-        TAGAN_GEO_CASE(4)
-        default:
-            break;
+    switch (lpr) {
+        case 8: launch_fast<METRIC, 8>(pass, A, s); return TAGAN_OK;
+        case 16: launch_fast<METRIC, 16>(pass, A, s); return TAGAN_OK;
+        case 32: launch_fast<METRIC, 32>(pass, A, s); return TAGAN_OK;
+        case 64: launch_fast<METRIC, 64>(pass, A, s); return TAGAN_OK;
+        default: break;
     }
-#undef TAGAN_GEO_CASE
     if (pass == P_FWD) k_geo_fwd_generic<METRIC><<<gg, BLK, 0, s>>>(A);
     else if (pass == P_BWD_ROW) k_geo_bwd_row_generic<METRIC><<<gg, BLK, 0, s>>>(A);
     else k_geo_bwd_col_generic<METRIC><<<gg, BLK, 0, s>>>(A);
     return TAGAN_OK;
 }
 
-int launch(int metric, Pass pass, int vec, const GeoArgs& A, hipStream_t s, float* alpha = nullptr) {
+int launch(int metric, Pass pass, int lpr, const GeoArgs& A, hipStream_t s, float* alpha = nullptr) {
     switch (metric) {
-        case TAGAN_METRIC_EUCLIDEAN: return launch_metric<TAGAN_METRIC_EUCLIDEAN>(pass, vec, A, s, alpha);
+        case TAGAN_METRIC_EUCLIDEAN: return launch_metric<TAGAN_METRIC_EUCLIDEAN>(pass, lpr, A, s, alpha);
         case TAGAN_METRIC_SQUARED_EUCLIDEAN:
-            return launch_metric<TAGAN_METRIC_SQUARED_EUCLIDEAN>(pass, vec, A, s, alpha);
-        case TAGAN_METRIC_MANHATTAN: return launch_metric<TAGAN_METRIC_MANHATTAN>(pass, vec, A, s, alpha);
+            return launch_metric<TAGAN_METRIC_SQUARED_EUCLIDEAN>(pass, lpr, A, s, alpha);
+        case TAGAN_METRIC_MANHATTAN: return launch_metric<TAGAN_METRIC_MANHATTAN>(pass, lpr, A, s, alpha);
         case TAGAN_METRIC_COSINE_SIMILARITY:
-            return launch_metric<TAGAN_METRIC_COSINE_SIMILARITY>(pass, vec, A, s, alpha);
+            return launch_metric<TAGAN_METRIC_COSINE_SIMILARITY>(pass, lpr, A, s, alpha);
         case TAGAN_METRIC_COSINE_DISTANCE:
-            return launch_metric<TAGAN_METRIC_COSINE_DISTANCE>(pass, vec, A, s, alpha);
-        case TAGAN_METRIC_DOT_PRODUCT: return launch_metric<TAGAN_METRIC_DOT_PRODUCT>(pass, vec, A, s, alpha);
+            return launch_metric<TAGAN_METRIC_COSINE_DISTANCE>(pass, lpr, A, s, alpha);
+        case TAGAN_METRIC_DOT_PRODUCT: return launch_metric<TAGAN_METRIC_DOT_PRODUCT>(pass, lpr, A, s, alpha);
         case TAGAN_METRIC_SCALED_DOT_PRODUCT:
-            return launch_metric<TAGAN_METRIC_SCALED_DOT_PRODUCT>(pass, vec, A, s, alpha);
+            return launch_metric<TAGAN_METRIC_SCALED_DOT_PRODUCT>(pass, lpr, A, s, alpha);
         case TAGAN_METRIC_GAUSSIAN_KERNEL:
-            return launch_metric<TAGAN_METRIC_GAUSSIAN_KERNEL>(pass, vec, A, s, alpha);
-        case TAGAN_METRIC_RBF_KERNEL: return launch_metric<TAGAN_METRIC_RBF_KERNEL>(pass, vec, A, s, alpha);
+            return launch_metric<TAGAN_METRIC_GAUSSIAN_KERNEL>(pass, lpr, A, s, alpha);
+        case TAGAN_METRIC_RBF_KERNEL: return launch_metric<TAGAN_METRIC_RBF_KERNEL>(pass, lpr, A, s, alpha);
         default:
             set_error("geo_attn: unsupported metric %d", metric);
             return TAGAN_ERR_UNSUPPORTED;
     }
 }
 
-int check_common(int dtype, int metric, int64_t N, int heads, int d, int64_t ld, float p_drop) {
+int check_common(int dtype, int metric, const tagan_graph* g, int heads, int d, int64_t ld, float p_drop) {
     TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "geo_attn: dtype %d unsupported", dtype);
     TAGAN_REQUIRE(metric >= 0 && metric <= TAGAN_METRIC_RBF_KERNEL, TAGAN_ERR_UNSUPPORTED,
                   "geo_attn: unsupported metric %d", metric);
-    TAGAN_REQUIRE(N > 0 && heads > 0 && d > 0, TAGAN_ERR_ARG, "geo_attn: bad sizes N=%lld heads=%d d=%d",
-                  (long long)N, heads, d);
+    TAGAN_REQUIRE(g != nullptr && g->n_nodes > 0 && g->rowptr && g->col, TAGAN_ERR_ARG, "geo_attn: bad graph");
+    TAGAN_REQUIRE(heads > 0 && d > 0, TAGAN_ERR_ARG, "geo_attn: bad sizes heads=%d d=%d", heads, d);
     TAGAN_REQUIRE(ld >= (int64_t)heads * d, TAGAN_ERR_ARG, "geo_attn: ld %lld < H", (long long)ld);
     TAGAN_REQUIRE(p_drop >= 0.f && p_drop < 1.f, TAGAN_ERR_ARG, "geo_attn: p_drop %f", (double)p_drop);
+    const int lpr = pick_lpr(heads * d, d);
+    if (lpr) {
+        TAGAN_REQUIRE(g->chunk > 0 && g->chunk_cap > 0 && g->row_chunk_ptr && g->row_chunk_seg &&
+                          g->row_chunk_beg && g->row_chunk_part && g->row_multi && g->row_counts,
+                      TAGAN_ERR_ARG, "geo_attn: graph lacks row chunk lists");
+        TAGAN_REQUIRE(((uintptr_t)0 == (ld % 4)), TAGAN_ERR_ARG, "geo_attn: ld must be a multiple of 4");
+    }
     return TAGAN_OK;
 }
 
-GeoArgs make_args(int64_t N, int heads, int d, const int32_t* rowptr, const int32_t* col, const void* q,
-                  const void* k, const void* v, int64_t ld, const float* mparam, float p_drop, uint64_t seed) {
+GeoArgs make_args(const tagan_graph* g, int heads, int d, const void* q, const void* k, const void* v, int64_t ld,
+                  const float* mparam, float p_drop, uint64_t seed) {
     GeoArgs A{};
-    A.N = N;
+    A.g = *g;
+    A.N = g->n_nodes;
     A.heads = heads;
     A.d = d;
     A.H = heads * d;
-    const int vec = pick_vec(A.H, d);
-    A.lph = vec ? d / vec : 1;
-    A.rowptr = rowptr;
-    A.col = col;
+    const int lpr = pick_lpr(A.H, d);
+    A.lph = lpr ? d / 4 : 1;
     A.q = (const float*)q;
     A.k = (const float*)k;
     A.v = (const float*)v;
@@ -713,64 +812,109 @@ GeoArgs make_args(int64_t N, int heads, int d, const int32_t* rowptr, const int3
     return A;
 }
 
+size_t fwd_ws(const tagan_graph* g, int heads, int d) {
+    if (!pick_lpr(heads * d, d)) return 0;
+    return align_up((size_t)g->part_cap * (2 * heads + heads * d) * 4, 256);
+}
+
+struct BwdWs {
+    size_t delta, prm, pv, pv2, total;
+};
+
+BwdWs bwd_ws(const tagan_graph* g, int heads, int d) {
+    BwdWs w{};
+    const int H = heads * d;
+    const int lpr = pick_lpr(H, d);
+    size_t off = 0;
+    auto take = [&](size_t b) { size_t o = off; off = align_up(off + b, 256); return o; };
+    w.delta = take((size_t)g->n_nodes * heads * 4);
+    int64_t nprm = g->n_nodes;
+    if (lpr) {
+        GeoArgs tmp{};
+        tmp.g = *g;
+        nprm = std::max<int64_t>(nprm, chunk_blocks(tmp, lpr));
+    }
+    w.prm = take((size_t)nprm * heads * 4);
+    w.pv = take(lpr ? (size_t)g->part_cap * H * 4 : 0);
+    w.pv2 = take(lpr ? (size_t)g->part_cap * 2 * H * 4 : 0);
+    w.total = off;
+    return w;
+}
+
 }  // namespace
 }  // namespace tagan
 
 extern "C" {
 
-int tagan_geo_attn_fwd(int dtype, int metric, int64_t n_nodes, int32_t heads, int32_t head_dim,
-                       const int32_t* rowptr, const int32_t* col, const void* q, const void* k, const void* v,
-                       int64_t ld_qkv, const float* metric_param, float p_drop, uint64_t seed, void* out,
-                       float* lse, float* edge_alpha, void* stream) {
+size_t tagan_geo_attn_fwd_workspace(const tagan_graph* g, int32_t heads, int32_t head_dim) {
+    if (!g || heads <= 0 || head_dim <= 0) return 0;
+    return tagan::fwd_ws(g, heads, head_dim);
+}
+
+int tagan_geo_attn_fwd(int dtype, int metric, const tagan_graph* g, int32_t heads, int32_t head_dim, const void* q,
+                       const void* k, const void* v, int64_t ld_qkv, const float* metric_param, float p_drop,
+                       uint64_t seed, void* out, float* lse, float* edge_alpha, void* workspace,
+                       size_t workspace_bytes, void* stream) {
     using namespace tagan;
-    int rc = check_common(dtype, metric, n_nodes, heads, head_dim, ld_qkv, p_drop);
+    int rc = check_common(dtype, metric, g, heads, head_dim, ld_qkv, p_drop);
     if (rc) return rc;
-    TAGAN_REQUIRE(rowptr && col && q && k && v && out && lse, TAGAN_ERR_ARG, "geo_attn_fwd: null pointer");
-    GeoArgs A = make_args(n_nodes, heads, head_dim, rowptr, col, q, k, v, ld_qkv, metric_param, p_drop, seed);
+    TAGAN_REQUIRE(q && k && v && out && lse, TAGAN_ERR_ARG, "geo_attn_fwd: null pointer");
+    const size_t need = fwd_ws(g, heads, head_dim);
+    TAGAN_REQUIRE(need == 0 || (workspace && workspace_bytes >= need), TAGAN_ERR_WORKSPACE,
+                  "geo_attn_fwd: workspace %zu < %zu", workspace_bytes, need);
+    GeoArgs A = make_args(g, heads, head_dim, q, k, v, ld_qkv, metric_param, p_drop, seed);
     A.out = (float*)out;
     A.lse = lse;
+    if (need) {
+        A.part_m = (float*)workspace;
+        A.part_l = A.part_m + g->part_cap * heads;
+        A.part_v = A.part_l + g->part_cap * heads;
+    }
     hipStream_t s = as_stream(stream);
-    const int vec = pick_vec(A.H, head_dim);
-    rc = launch(metric, P_FWD, vec, A, s);
+    const int lpr = pick_lpr(A.H, head_dim);
+    rc = launch(metric, P_FWD, lpr, A, s);
     if (rc) return rc;
     TAGAN_CHECK_LAUNCH("geo_attn_fwd");
+    if (lpr) {
+        const unsigned gm = (unsigned)((g->part_cap + (BLK / WAVE) - 1) / (BLK / WAVE));
+        k_geo_fwd_merge<<<gm, BLK, 0, s>>>(A);
+        TAGAN_CHECK_LAUNCH("geo_attn_fwd_merge");
+    }
     if (edge_alpha) {
-        rc = launch(metric, P_ALPHA, vec, A, s, edge_alpha);
+        rc = launch(metric, P_ALPHA, lpr, A, s, edge_alpha);
         if (rc) return rc;
         TAGAN_CHECK_LAUNCH("geo_attn_alpha");
     }
     return TAGAN_OK;
 }
 
-size_t tagan_geo_attn_bwd_workspace(int64_t n_nodes, int32_t heads) {
-    using namespace tagan;
-    if (n_nodes <= 0 || heads <= 0) return 0;
-    const int64_t nblk = (n_nodes + ROWS_PER_BLK - 1) / ROWS_PER_BLK;
-    const size_t delta = align_up((size_t)n_nodes * heads * 4, 256);
-    const size_t part = align_up((size_t)std::max<int64_t>(nblk, n_nodes) * heads * 4, 256);
-    return delta + part;
+size_t tagan_geo_attn_bwd_workspace(const tagan_graph* g, int32_t heads, int32_t head_dim) {
+    if (!g || g->n_nodes <= 0 || heads <= 0 || head_dim <= 0) return 0;
+    return tagan::bwd_ws(g, heads, head_dim).total;
 }
 
-int tagan_geo_attn_bwd(int dtype, int metric, int64_t n_nodes, int32_t heads, int32_t head_dim,
-                       const int32_t* rowptr, const int32_t* col, const int32_t* csc_ptr, const int32_t* csc_row,
-                       const int32_t* csc_eid, const void* q, const void* k, const void* v, int64_t ld_qkv,
-                       const float* metric_param, float p_drop, uint64_t seed, const void* out, const float* lse,
-                       const void* dout, void* dq, void* dk, void* dv, int64_t ld_dqkv, float* dmetric_param,
-                       void* workspace, size_t workspace_bytes, void* stream) {
+int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t heads, int32_t head_dim, const void* q,
+                       const void* k, const void* v, int64_t ld_qkv, const float* metric_param, float p_drop,
+                       uint64_t seed, const void* out, const float* lse, const void* dout, void* dq, void* dk,
+                       void* dv, int64_t ld_dqkv, float* dmetric_param, void* workspace, size_t workspace_bytes,
+                       void* stream) {
     using namespace tagan;
-    int rc = check_common(dtype, metric, n_nodes, heads, head_dim, ld_qkv, p_drop);
+    int rc = check_common(dtype, metric, g, heads, head_dim, ld_qkv, p_drop);
     if (rc) return rc;
-    TAGAN_REQUIRE(rowptr && col && csc_ptr && csc_row && csc_eid && q && k && v && out && lse && dout && dq &&
-                      dk && dv,
+    TAGAN_REQUIRE(g->csc_ptr && g->csc_row && g->csc_eid && q && k && v && out && lse && dout && dq && dk && dv,
                   TAGAN_ERR_ARG, "geo_attn_bwd: null pointer");
-    TAGAN_REQUIRE(ld_dqkv >= (int64_t)heads * head_dim, TAGAN_ERR_ARG, "geo_attn_bwd: ld_dqkv < H");
-    const size_t need = tagan_geo_attn_bwd_workspace(n_nodes, heads);
-    TAGAN_REQUIRE(workspace && workspace_bytes >= need, TAGAN_ERR_WORKSPACE, "geo_attn_bwd: workspace %zu < %zu",
-                  workspace_bytes, need);
-    GeoArgs A = make_args(n_nodes, heads, head_dim, rowptr, col, q, k, v, ld_qkv, metric_param, p_drop, seed);
-    A.csc_ptr = csc_ptr;
-    A.csc_row = csc_row;
-    A.csc_eid = csc_eid;
+    TAGAN_REQUIRE(ld_dqkv >= (int64_t)heads * head_dim && ld_dqkv % 4 == 0, TAGAN_ERR_ARG, "geo_attn_bwd: ld_dqkv");
+    const BwdWs w = bwd_ws(g, heads, head_dim);
+    TAGAN_REQUIRE(workspace && workspace_bytes >= w.total, TAGAN_ERR_WORKSPACE, "geo_attn_bwd: workspace %zu < %zu",
+                  workspace_bytes, w.total);
+    const int H = heads * head_dim;
+    const int lpr = pick_lpr(H, head_dim);
+    if (lpr) {
+        TAGAN_REQUIRE(g->col_chunk_ptr && g->col_chunk_seg && g->col_chunk_beg && g->col_chunk_part &&
+                          g->col_multi && g->col_counts,
+                      TAGAN_ERR_ARG, "geo_attn_bwd: graph lacks column chunk lists");
+    }
+    GeoArgs A = make_args(g, heads, head_dim, q, k, v, ld_qkv, metric_param, p_drop, seed);
     A.o = (const float*)out;
     A.lse_in = lse;
     A.dout = (const float*)dout;
@@ -778,22 +922,34 @@ int tagan_geo_attn_bwd(int dtype, int metric, int64_t n_nodes, int32_t heads, in
     A.dk = (float*)dk;
     A.dv = (float*)dv;
     A.ldd = ld_dqkv;
-    A.delta = (float*)workspace;
+    char* ws = (char*)workspace;
+    A.delta = (float*)(ws + w.delta);
     const bool want_prm = dmetric_param != nullptr && metric_param != nullptr &&
                           (metric == TAGAN_METRIC_GAUSSIAN_KERNEL || metric == TAGAN_METRIC_RBF_KERNEL);
-    A.prm_partial = want_prm ? (float*)((char*)workspace + align_up((size_t)n_nodes * heads * 4, 256)) : nullptr;
+    A.prm_partial = want_prm ? (float*)(ws + w.prm) : nullptr;
+    A.part_v = (float*)(ws + w.pv);
+    A.part_v2 = (float*)(ws + w.pv2);
     hipStream_t s = as_stream(stream);
-    const int vec = pick_vec(A.H, head_dim);
-    rc = launch(metric, P_BWD_ROW, vec, A, s);
+    rc = launch(metric, P_BWD_ROW, lpr, A, s);
     if (rc) return rc;
     TAGAN_CHECK_LAUNCH("geo_attn_bwd_row");
-    rc = launch(metric, P_BWD_COL, vec, A, s);
+    const unsigned gm = (unsigned)((g->part_cap + (BLK / WAVE) - 1) / (BLK / WAVE));
+    if (lpr) {
+        k_geo_sum_parts<<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr, g->row_chunk_part,
+                                           A.part_v, H, A.dq, A.dq, A.ldd, H);
+        TAGAN_CHECK_LAUNCH("geo_attn_bwd_row_merge");
+    }
+    rc = launch(metric, P_BWD_COL, lpr, A, s);
     if (rc) return rc;
     TAGAN_CHECK_LAUNCH("geo_attn_bwd_col");
+    if (lpr) {
+        k_geo_sum_parts<<<gm, BLK, 0, s>>>(g->col_counts, g->col_multi, g->col_chunk_ptr, g->col_chunk_part,
+                                           A.part_v2, 2 * H, A.dk, A.dv, A.ldd, H);
+        TAGAN_CHECK_LAUNCH("geo_attn_bwd_col_merge");
+    }
     if (dmetric_param) {
         if (want_prm) {
-            // fast path: one partial per (block, head); generic path: one per (row, head)
-            const int64_t nparts = vec ? (n_nodes + ROWS_PER_BLK - 1) / ROWS_PER_BLK : n_nodes;
+            const int64_t nparts = lpr ? chunk_blocks(A, lpr) : g->n_nodes;
             k_reduce_partials<<<heads, BLK, 0, s>>>(A.prm_partial, nparts, heads, dmetric_param);
             TAGAN_CHECK_LAUNCH("geo_attn_bwd_reduce");
         } else {

@@ -10,6 +10,7 @@
 Every output and workspace is allocated here from PyTorch's caching allocator;
 kernels are launched on the current HIP stream.
 """
+import ctypes
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -25,9 +26,12 @@ def new_seed() -> int:
 
 
 # ----------------------------------------------------------------------------- graph
+CHUNK = 128   # max CSR/CSC entries per work chunk (power-law hubs are split)
+
+
 @dataclass
 class SnapshotGraph:
-    """CSR by source (query) row and CSC by destination, int32, device-resident."""
+    """CSR by source (query) row + CSC by destination + chunked work lists, int32, device-resident."""
     num_nodes: int
     rowptr: torch.Tensor
     col: torch.Tensor
@@ -36,12 +40,54 @@ class SnapshotGraph:
     csc_eid: torch.Tensor
     nnz: torch.Tensor              # int64[1] on device
     node_counts: Sequence[int]
+    row_chunks: Optional[tuple] = None   # (chunk_ptr, seg, beg, part, multi, counts)
+    col_chunks: Optional[tuple] = None
+    chunk: int = CHUNK
+    chunk_cap: int = 0
+    part_cap: int = 0
+    _struct: object = None
 
     def nnz_host(self) -> int:
         return int(self.nnz.item())
 
+    def struct(self):
+        """ctypes ``tagan_graph`` pointing at this graph's device arrays (kept alive by self)."""
+        if self._struct is None:
+            r, c = self.row_chunks, self.col_chunks
+            p = lambda t: t.data_ptr()  # noqa: E731
+            self._struct = _lib.TaganGraph(self.num_nodes, p(self.rowptr), p(self.col), p(self.csc_ptr),
+                                           p(self.csc_row), p(self.csc_eid), self.chunk, self.chunk_cap,
+                                           self.part_cap, *[p(t) for t in r], *[p(t) for t in c])
+        return ctypes.byref(self._struct)
 
-def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], validate: bool = True) -> SnapshotGraph:
+
+def _chunk_lists(seg_ptr: torch.Tensor, n: int, nnz_cap: int, chunk: int):
+    L = lib()
+    dev = seg_ptr.device
+    cap = int(L.tagan_chunk_capacity(n, nnz_cap, chunk))
+    pcap = int(L.tagan_part_capacity(nnz_cap, chunk))
+    buf = torch.empty(n + 1 + 4 * cap + pcap + 4, dtype=torch.int32, device=dev)
+    chunk_ptr = buf[:n + 1]
+    o = n + 1
+    seg, beg, part = buf[o:o + cap], buf[o + cap:o + 2 * cap], buf[o + 2 * cap:o + 3 * cap]
+    multi = buf[o + 4 * cap:o + 4 * cap + pcap]
+    counts = buf[o + 4 * cap + pcap:]
+    wsb = L.tagan_graph_chunks_workspace(n)
+    ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
+    check(L.tagan_graph_chunks(ptr(seg_ptr), n, chunk, ptr(chunk_ptr), ptr(seg), ptr(beg), ptr(part), ptr(multi),
+                               ptr(counts), ptr(ws), wsb, stream_of(seg_ptr)), "tagan_graph_chunks")
+    return (chunk_ptr, seg, beg, part, multi, counts), cap, pcap
+
+
+def _finish(g: SnapshotGraph, nnz_cap: int, chunk: int = CHUNK) -> SnapshotGraph:
+    g.row_chunks, g.chunk_cap, g.part_cap = _chunk_lists(g.rowptr, g.num_nodes, nnz_cap, chunk)
+    g.col_chunks, _, _ = _chunk_lists(g.csc_ptr, g.num_nodes, nnz_cap, chunk)
+    g.chunk = chunk
+    return g
+
+
+def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], validate: bool = True,
+                chunk: int = CHUNK) -> SnapshotGraph:
     """CSR/CSC of the block-diagonal union of snapshot adjacencies (+ self-loops, de-duplicated).
 
     ``edge_indices[g]`` is snapshot g's [2, E_g] edge_index with local node ids.
@@ -64,12 +110,10 @@ def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], va
     meta = torch.tensor(e_ptr + n_ptr, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
     edge_ptr, node_ptr = meta[:len(e_ptr)], meta[len(e_ptr):]
     cap = E + N
-    i32 = dict(dtype=torch.int32, device=dev)
-    rowptr = torch.empty(N + 1, **i32)
-    col = torch.empty(cap, **i32)
-    csc_ptr = torch.empty(N + 1, **i32)
-    csc_row = torch.empty(cap, **i32)
-    csc_eid = torch.empty(cap, **i32)
+    buf = torch.empty(2 * (N + 1) + 3 * cap, dtype=torch.int32, device=dev)
+    rowptr, csc_ptr = buf[:N + 1], buf[N + 1:2 * (N + 1)]
+    o = 2 * (N + 1)
+    col, csc_row, csc_eid = buf[o:o + cap], buf[o + cap:o + 2 * cap], buf[o + 2 * cap:o + 3 * cap]
     scal = torch.empty(2, dtype=torch.int64, device=dev)
     nnz = scal[0:1]
     err = scal[1:2].view(torch.int32)[:1]
@@ -81,7 +125,7 @@ def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], va
                             stream_of(ei)), "tagan_csr_build")
     if validate and int(err.item()) != 0:
         raise IndexError("edge_index contains an index out of range for its snapshot's node count")
-    return SnapshotGraph(N, rowptr, col, csc_ptr, csc_row, csc_eid, nnz, list(node_counts))
+    return _finish(SnapshotGraph(N, rowptr, col, csc_ptr, csc_row, csc_eid, nnz, list(node_counts)), cap, chunk)
 
 
 def graph_from_dense_mask(mask: torch.Tensor) -> SnapshotGraph:
@@ -107,8 +151,10 @@ def _graph_from_pairs(src, dst, N, node_counts):
     cptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)
     cptr[1:] = torch.cumsum(ccounts, 0)
     i32 = torch.int32
-    return SnapshotGraph(N, rowptr.to(i32), dst.to(i32), cptr.to(i32), src[order].to(i32), order.to(i32),
-                         torch.tensor([nnz], dtype=torch.int64, device=dev), list(node_counts))
+    g = SnapshotGraph(N, rowptr.to(i32), dst.to(i32).contiguous(), cptr.to(i32), src[order].to(i32).contiguous(),
+                      order.to(i32).contiguous(), torch.tensor([nnz], dtype=torch.int64, device=dev),
+                      list(node_counts))
+    return _finish(g, max(nnz, 1))
 
 
 # ----------------------------------------------------------------------------- geometric attention
@@ -124,12 +170,8 @@ class GeoAttnFn(torch.autograd.Function):
         d = H // heads
         out = torch.empty(N, H, device=qkv.device, dtype=torch.float32)
         lse = torch.empty(N, heads, device=qkv.device, dtype=torch.float32)
-        base = qkv.data_ptr()
-        es = qkv.element_size()
         prm = param.detach().contiguous() if param is not None else None
-        check(lib().tagan_geo_attn_fwd(_lib.TAGAN_F32, metric, N, heads, d, ptr(graph.rowptr), ptr(graph.col),
-                                       base, base + H * es, base + 2 * H * es, H3, ptr(prm), float(p_drop),
-                                       seed, ptr(out), ptr(lse), None, stream_of(qkv)), "tagan_geo_attn_fwd")
+        _geo_fwd(qkv, graph, metric, heads, prm, p_drop, seed, out, lse, None)
         ctx.save_for_backward(qkv, out, lse, prm)
         ctx.graph, ctx.metric, ctx.heads, ctx.p_drop, ctx.seed = graph, metric, heads, p_drop, seed
         ctx.has_param = param is not None
@@ -146,18 +188,32 @@ class GeoAttnFn(torch.autograd.Function):
         dout = dout.contiguous()
         dqkv = torch.empty_like(qkv)
         L = lib()
-        ws_bytes = L.tagan_geo_attn_bwd_workspace(N, heads)
+        gs = g.struct()
+        ws_bytes = L.tagan_geo_attn_bwd_workspace(gs, heads, d)
         ws = torch.empty(int(ws_bytes), dtype=torch.uint8, device=qkv.device)
         dprm = torch.empty(heads, device=qkv.device, dtype=torch.float32) if ctx.has_param and \
             ctx.needs_input_grad[1] else None
         base, es = qkv.data_ptr(), qkv.element_size()
         dbase = dqkv.data_ptr()
-        check(L.tagan_geo_attn_bwd(_lib.TAGAN_F32, ctx.metric, N, heads, d, ptr(g.rowptr), ptr(g.col),
-                                   ptr(g.csc_ptr), ptr(g.csc_row), ptr(g.csc_eid), base, base + H * es,
-                                   base + 2 * H * es, H3, ptr(prm), float(ctx.p_drop), ctx.seed, ptr(out),
-                                   ptr(lse), ptr(dout), dbase, dbase + H * es, dbase + 2 * H * es, H3, ptr(dprm),
-                                   ptr(ws), ws_bytes, stream_of(qkv)), "tagan_geo_attn_bwd")
+        check(L.tagan_geo_attn_bwd(_lib.TAGAN_F32, ctx.metric, gs, heads, d, base, base + H * es, base + 2 * H * es,
+                                   H3, ptr(prm), float(ctx.p_drop), ctx.seed, ptr(out), ptr(lse), ptr(dout), dbase,
+                                   dbase + H * es, dbase + 2 * H * es, H3, ptr(dprm), ptr(ws), ws_bytes,
+                                   stream_of(qkv)), "tagan_geo_attn_bwd")
         return dqkv, dprm, None, None, None, None, None
+
+
+def _geo_fwd(qkv, graph, metric, heads, prm, p_drop, seed, out, lse, alpha):
+    N, H3 = qkv.shape
+    H = H3 // 3
+    d = H // heads
+    L = lib()
+    gs = graph.struct()
+    ws_bytes = L.tagan_geo_attn_fwd_workspace(gs, heads, d)
+    ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=qkv.device)
+    base, es = qkv.data_ptr(), qkv.element_size()
+    check(L.tagan_geo_attn_fwd(_lib.TAGAN_F32, metric, gs, heads, d, base, base + H * es, base + 2 * H * es, H3,
+                               ptr(prm), float(p_drop), seed, ptr(out), ptr(lse), ptr(alpha), ptr(ws), ws_bytes,
+                               stream_of(qkv)), "tagan_geo_attn_fwd")
 
 
 def geo_edge_alpha(qkv, graph: SnapshotGraph, metric: int, heads: int, param=None, p_drop=0.0, seed=0):
@@ -167,12 +223,8 @@ def geo_edge_alpha(qkv, graph: SnapshotGraph, metric: int, heads: int, param=Non
     out = torch.empty(N, H, device=qkv.device)
     lse = torch.empty(N, heads, device=qkv.device)
     alpha = torch.empty(int(graph.col.numel()), heads, device=qkv.device)
-    base, es = qkv.data_ptr(), qkv.element_size()
     prm = param.detach().contiguous() if param is not None else None
-    check(lib().tagan_geo_attn_fwd(_lib.TAGAN_F32, metric, N, heads, H // heads, ptr(graph.rowptr),
-                                   ptr(graph.col), base, base + H * es, base + 2 * H * es, H3, ptr(prm),
-                                   float(p_drop), seed, ptr(out), ptr(lse), ptr(alpha), stream_of(qkv)),
-          "tagan_geo_attn_fwd(alpha)")
+    _geo_fwd(qkv, graph, metric, heads, prm, p_drop, seed, out, lse, alpha)
     return alpha[:graph.nnz_host()]
 
 

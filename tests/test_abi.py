@@ -42,23 +42,35 @@ def test_uniform_matches_numpy_restatement():
 
 def test_workspace_queries_are_host_only():
     L = _lib.lib()
-    assert L.tagan_geo_attn_bwd_workspace(1000, 8) >= 1000 * 8 * 4
+    g = _lib.TaganGraph()
+    g.n_nodes, g.chunk = 1000, 128
+    g.chunk_cap = L.tagan_chunk_capacity(1000, 12000, 128)
+    g.part_cap = L.tagan_part_capacity(12000, 128)
+    assert g.chunk_cap == 1000 + 12000 // 128 + 1 and g.part_cap == 2 * (12000 // 128) + 2
+    assert L.tagan_geo_attn_bwd_workspace(ctypes.byref(g), 8, 16) >= 1000 * 8 * 4
+    assert L.tagan_geo_attn_fwd_workspace(ctypes.byref(g), 8, 16) >= g.part_cap * (16 + 128) * 4
     assert L.tagan_temporal_attn_bwd_workspace(100, 32, 8) >= 8 * 63 * 4
-    assert L.tagan_geo_attn_bwd_workspace(0, 8) == 0
+    g.n_nodes = 0
+    assert L.tagan_geo_attn_bwd_workspace(ctypes.byref(g), 8, 16) == 0
 
 
 def test_argument_validation_reports_errors():
     L = _lib.lib()
-    rc = L.tagan_geo_attn_fwd(0, 99, 10, 4, 16, None, None, None, None, None, 64, None, 0.0, 0, None, None, None,
-                              None)
+    g = _lib.TaganGraph()
+    rc = L.tagan_geo_attn_fwd(0, 99, ctypes.byref(g), 4, 16, None, None, None, 64, None, 0.0, 0, None, None, None,
+                              None, 0, None)
     assert rc == -2
     assert b"metric" in L.tagan_last_error()
+    rc = L.tagan_geo_attn_fwd(0, 0, ctypes.byref(g), 4, 16, None, None, None, 64, None, 0.0, 0, None, None, None,
+                              None, 0, None)
+    assert rc == -1 and b"graph" in L.tagan_last_error()
     rc = L.tagan_temporal_attn_fwd(1, 10, 4, 2, 8, None, None, None, 0, 0, None, None, 0, None, 0, 0, 0, 0.0, 0,
                                    None, 0, 0, None, None, None)
     assert rc == -2
-    rc = L.tagan_geo_attn_fwd(0, 0, 10, 4, 16, None, None, None, None, None, 64, None, 1.5, 0, None, None, None,
-                              None)
-    assert rc == -1
+    g.n_nodes, g.rowptr, g.col = 10, 16, 16   # non-null dummies: validation fails before any launch
+    rc = L.tagan_geo_attn_fwd(0, 0, ctypes.byref(g), 4, 16, None, None, None, 64, None, 1.5, 0, None, None, None,
+                              None, 0, None)
+    assert rc == -1 and b"p_drop" in L.tagan_last_error()
 
 
 def test_no_cpu_path():

@@ -230,3 +230,91 @@ def test_deterministic_with_dropout(dev):
         grads.append(torch.cat([p.grad.flatten() for p in model.parameters() if p.grad is not None]))
     assert torch.equal(grads[0], grads[1]), "backward is not bitwise reproducible"
     assert torch.isfinite(grads[0]).all()
+
+
+# ----------------------------------------------------------------------------- chunked work decomposition
+def _hub_graph(n, seed):
+    """Random graph plus a hub (node 0 <-> everyone): rows and columns far longer than one chunk."""
+    g = torch.Generator().manual_seed(seed)
+    ei = torch.randint(0, n, (2, 4 * n), generator=g)
+    hub = torch.stack([torch.zeros(n, dtype=torch.long), torch.arange(n)])
+    return torch.cat([ei, hub, hub.flip(0)], 1)
+
+
+@pytest.mark.parametrize("metric", list(oracle.METRICS))
+@pytest.mark.parametrize("chunk", [4, 16, 128])
+def test_geo_kernel_chunked_vs_oracle(dev, metric, chunk):
+    """Multi-chunk rows/columns (merge passes) against the float64 oracle edge-softmax."""
+    from tagan_amd import _lib
+    from tagan_amd.kernels import GeoAttnFn, build_graph
+    counts = [300, 257]
+    H, heads = 128, 8
+    eis = [_hub_graph(n, 5 + i) for i, n in enumerate(counts)]
+    graph = build_graph([e.to(dev) for e in eis], counts, chunk=chunk)
+    N = sum(counts)
+    g = torch.Generator().manual_seed(1)
+    qkv = (torch.randn(N, 3 * H, generator=g) * 0.5)
+    param = torch.linspace(0.7, 1.3, heads) if metric in ("gaussian_kernel", "rbf_kernel") else None
+    x = qkv.to(dev).requires_grad_(True)
+    pd = param.to(dev).requires_grad_(True) if param is not None else None
+    out = GeoAttnFn.apply(x, pd, graph, _lib.METRIC_IDS[metric], heads, 0.0, 0)
+    gout = torch.randn(N, H, generator=g)
+    (out * gout.to(dev)).sum().backward()
+    # oracle: block-diagonal CSR of the same snapshots, float64
+    rps, cols, off = [], [], 0
+    for n, ei in zip(counts, eis):
+        rp, c = oracle.csr_from_edge_index(ei, n)
+        rps.append(rp[:-1] + (sum(len(x) for x in cols)))
+        cols.append(c + off)
+        off += n
+    rowptr = torch.cat(rps + [torch.tensor([sum(len(x) for x in cols)])])
+    col = torch.cat(cols)
+    q64 = qkv.double().requires_grad_(True)
+    p64 = param.double().requires_grad_(True) if param is not None else None
+    P = {"m.distance_param": p64} if p64 is not None else {}
+    d = H // heads
+    q = q64[:, :H].view(1, N, heads, d).transpose(1, 2)
+    k = q64[:, H:2 * H].view(1, N, heads, d).transpose(1, 2)
+    v = q64[:, 2 * H:].view(1, N, heads, d).transpose(1, 2)
+    ctx = oracle.tagan_oracle._sparse_context(q, k, v, metric, P, "m", p64 is not None, None, (rowptr, col))
+    ref = ctx.transpose(1, 2).reshape(N, H)
+    (ref * gout.double()).sum().backward()
+    G.assert_close("out", out, ref, OUT_ATOL, OUT_RTOL)
+    G.assert_close("dqkv", x.grad, q64.grad, GRAD_ATOL, GRAD_RTOL)
+    if param is not None:
+        G.assert_close("dparam", pd.grad, p64.grad, 1e-3, 1e-3)
+
+
+def test_geo_kernel_dropout_matches_regenerated_mask(dev):
+    """Dropout on attention weights: the kernel's counter-based mask, regenerated on the host, reproduces it."""
+    import numpy as np
+    from tagan_amd import _lib
+    from tagan_amd.kernels import GeoAttnFn, build_graph
+    from test_abi import _splitmix_uniform
+    n, H, heads, p, seed = 400, 64, 4, 0.3, 987654321
+    ei = _hub_graph(n, 3)
+    graph = build_graph([ei.to(dev)], [n], chunk=16)
+    g = torch.Generator().manual_seed(2)
+    qkv = torch.randn(n, 3 * H, generator=g) * 0.5
+    x = qkv.to(dev).requires_grad_(True)
+    out = GeoAttnFn.apply(x, None, graph, 0, heads, p, seed)
+    gout = torch.randn(n, H, generator=g)
+    (out * gout.to(dev)).sum().backward()
+    rowptr, col = oracle.csr_from_edge_index(ei, n)
+    E = col.numel()
+    u = _splitmix_uniform(seed, np.arange(E * heads, dtype=np.uint64)).reshape(E, heads)
+    keep = torch.from_numpy((u >= p).astype(np.float64)) / (1 - p)
+    q64 = qkv.double().requires_grad_(True)
+    d = H // heads
+    src = torch.repeat_interleave(torch.arange(n), rowptr.diff())
+    qf, kf, vf = (q64[:, i * H:(i + 1) * H].view(n, heads, d) for i in range(3))
+    s = -torch.sqrt(((qf[src] - kf[col]) ** 2).sum(-1) + 1e-8)
+    m = torch.full((n, heads), float("-inf"), dtype=torch.float64).scatter_reduce(
+        0, src[:, None].expand(-1, heads), s, reduce="amax")
+    e = torch.exp(s - m[src])
+    a = e / torch.zeros(n, heads, dtype=torch.float64).index_add(0, src, e)[src]
+    ref = torch.zeros(n, heads, d, dtype=torch.float64).index_add(0, src, (a * keep)[:, :, None] * vf[col])
+    ref = ref.reshape(n, H)
+    (ref * gout.double()).sum().backward()
+    G.assert_close("out", out, ref, OUT_ATOL, OUT_RTOL)
+    G.assert_close("dqkv", x.grad, q64.grad, GRAD_ATOL, GRAD_RTOL)
