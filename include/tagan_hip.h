@@ -199,6 +199,28 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
                             float* dbias_table, float* dbias_dense,
                             void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Row LayerNorm with fused residual + dropout.  Replaces the ATen chain
+ * output_dropout(proj) + identity -> layer_norm2 (geometric_attention.py:586-596,
+ * temporal_attention.py:1190-1200) and plain layer_norm1 (b = NULL, p_drop = 0).
+ *   s = dropout(a; p_drop, seed) + b     (index of element (r,c) = r*H + c)
+ *   y = (s - mean) / sqrt(var + eps) * gamma + beta       (biased var, as torch)
+ * s_out (optional) keeps s for the backward pass; mean/rstd: [M].
+ * Supported H: tagan_layernorm_supported(H) (32, 64, 128, 256, 512).
+ * ------------------------------------------------------------------------- */
+int tagan_layernorm_supported(int32_t H);
+int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, const float* b,
+                            float p_drop, uint64_t seed, const float* gamma, const float* beta,
+                            float eps, float* s_out, float* y, float* mean, float* rstd, void* stream);
+/* Backward: ds = dL/ds (the residual branch's gradient), da = ds masked/scaled
+ * by the same dropout (the projection branch's gradient), dgamma/dbeta [H]
+ * (block partials summed in block order).  Any of ds/da/dgamma/dbeta may be NULL. */
+size_t tagan_layernorm_bwd_workspace(int64_t M, int32_t H);
+int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s, const float* mean,
+                        const float* rstd, const float* gamma, const float* dy, float p_drop, uint64_t seed,
+                        float* ds, float* da, float* dgamma, float* dbeta,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

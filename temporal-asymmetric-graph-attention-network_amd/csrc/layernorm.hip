@@ -1,0 +1,276 @@
+// Row LayerNorm with fused residual + dropout for the TAGAN layers on gfx950.
+//
+// Replaces, per layer, the ATen chain  output_dropout(proj) + identity -> LayerNorm
+// (geometric_attention.py:586-596, temporal_attention.py:1190-1200) and the plain
+// layer_norm1 (:541-542, :985-986).  HBM-bound elementwise/reduction work: a group
+// of LPR = H/(4*NV) lanes owns one row (NV float4 per lane), mean / variance are
+// XOR-butterfly reductions inside the group, two-pass in registers (no Welford
+// round-off), rstd = 1/sqrt(var+eps).  Backward recomputes x̂ from the saved LN
+// input and (mean, rstd); dγ/dβ are per-block partials summed in block order.
+#include "common.cuh"
+
+namespace tagan {
+namespace {
+
+constexpr int BLK = 256;
+
+template <int LPR>
+__device__ __forceinline__ float row_sum(float x) {
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+struct LnArgs {
+    int64_t M;
+    int H;
+    const float* a;
+    const float* b;
+    float p_drop, inv_keep;
+    uint64_t seed;
+    const float* gamma;
+    const float* beta;
+    float eps;
+    float* s_out;
+    float* y;
+    float* mean;
+    float* rstd;
+    // backward
+    const float* s_in;
+    const float* dy;
+    float* ds;
+    float* da;
+    float* part;   // [gridDim.x, 2H]
+};
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ float4 drop4(const LnArgs& A, float4 v, int64_t base) {
+    if (A.p_drop <= 0.f) return v;
+    v.x = uniform01(A.seed, base + 0) >= A.p_drop ? v.x * A.inv_keep : 0.f;
+    v.y = uniform01(A.seed, base + 1) >= A.p_drop ? v.y * A.inv_keep : 0.f;
+    v.z = uniform01(A.seed, base + 2) >= A.p_drop ? v.z * A.inv_keep : 0.f;
+    v.w = uniform01(A.seed, base + 3) >= A.p_drop ? v.w * A.inv_keep : 0.f;
+    return v;
+}
+
+template <int LPR, int NV>
+__global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
+    constexpr int RPW = WAVE / LPR;
+    const int lane = threadIdx.x & (WAVE - 1), sl = lane % LPR;
+    const int64_t wave = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6);
+    const int64_t row = wave * RPW + lane / LPR;
+    if (row >= A.M) return;
+    const int H = A.H;
+    float4 v[NV];
+    float sum = 0.f;
+#pragma unroll
+    for (int n = 0; n < NV; ++n) {
+        const int c = (n * LPR + sl) * 4;
+        const int64_t off = row * H + c;
+        float4 x = ld4(A.a + off);
+        x = drop4(A, x, off);
+        if (A.b) {
+            const float4 r = ld4(A.b + off);
+            x.x += r.x; x.y += r.y; x.z += r.z; x.w += r.w;
+        }
+        v[n] = x;
+        if (A.s_out) st4(A.s_out + off, x);
+        sum += (x.x + x.y) + (x.z + x.w);
+    }
+    const float mean = row_sum<LPR>(sum) / (float)H;
+    float sq = 0.f;
+#pragma unroll
+    for (int n = 0; n < NV; ++n) {
+        const float dx = v[n].x - mean, dyv = v[n].y - mean, dz = v[n].z - mean, dw = v[n].w - mean;
+        sq += (dx * dx + dyv * dyv) + (dz * dz + dw * dw);
+    }
+    const float var = row_sum<LPR>(sq) / (float)H;
+    const float rstd = 1.f / sqrtf(var + A.eps);
+#pragma unroll
+    for (int n = 0; n < NV; ++n) {
+        const int c = (n * LPR + sl) * 4;
+        const float4 g = ld4(A.gamma + c), be = ld4(A.beta + c);
+        float4 o;
+        o.x = (v[n].x - mean) * rstd * g.x + be.x;
+        o.y = (v[n].y - mean) * rstd * g.y + be.y;
+        o.z = (v[n].z - mean) * rstd * g.z + be.z;
+        o.w = (v[n].w - mean) * rstd * g.w + be.w;
+        st4(A.y + row * H + c, o);
+    }
+    if (sl == 0) {
+        A.mean[row] = mean;
+        A.rstd[row] = rstd;
+    }
+}
+
+template <int LPR, int NV>
+__global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
+    constexpr int RPW = WAVE / LPR;
+    __shared__ float red[BLK / WAVE][RPW][2 * 4 * NV * LPR];
+    const int lane = threadIdx.x & (WAVE - 1), sl = lane % LPR, sub = lane / LPR, w = threadIdx.x >> 6;
+    const int H = A.H;
+    float4 dg[NV], db[NV];
+#pragma unroll
+    for (int n = 0; n < NV; ++n) {
+        dg[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+        db[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int64_t nwaves = (int64_t)gridDim.x * (BLK / WAVE);
+    for (int64_t wave = blockIdx.x * (int64_t)(BLK / WAVE) + w; wave * RPW < A.M; wave += nwaves) {
+        const int64_t row = wave * RPW + sub;
+        const bool live = row < A.M;
+        const int64_t r = live ? row : 0;
+        const float mean = A.mean[r], rstd = A.rstd[r];
+        float4 xh[NV], gd[NV];
+        float c1 = 0.f, c2 = 0.f;
+#pragma unroll
+        for (int n = 0; n < NV; ++n) {
+            const int c = (n * LPR + sl) * 4;
+            const float4 s = ld4(A.s_in + r * H + c), d = ld4(A.dy + r * H + c), g = ld4(A.gamma + c);
+            xh[n] = make_float4((s.x - mean) * rstd, (s.y - mean) * rstd, (s.z - mean) * rstd, (s.w - mean) * rstd);
+            gd[n] = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
+            c1 += (gd[n].x * xh[n].x + gd[n].y * xh[n].y) + (gd[n].z * xh[n].z + gd[n].w * xh[n].w);
+            c2 += (gd[n].x + gd[n].y) + (gd[n].z + gd[n].w);
+            if (live) {
+                dg[n].x += d.x * xh[n].x; dg[n].y += d.y * xh[n].y; dg[n].z += d.z * xh[n].z; dg[n].w += d.w * xh[n].w;
+                db[n].x += d.x; db[n].y += d.y; db[n].z += d.z; db[n].w += d.w;
+            }
+        }
+        c1 = row_sum<LPR>(c1) / (float)H;
+        c2 = row_sum<LPR>(c2) / (float)H;
+        if (!live) continue;
+#pragma unroll
+        for (int n = 0; n < NV; ++n) {
+            const int c = (n * LPR + sl) * 4;
+            float4 o;
+            o.x = rstd * (gd[n].x - c1 * xh[n].x - c2);
+            o.y = rstd * (gd[n].y - c1 * xh[n].y - c2);
+            o.z = rstd * (gd[n].z - c1 * xh[n].z - c2);
+            o.w = rstd * (gd[n].w - c1 * xh[n].w - c2);
+            if (A.ds) st4(A.ds + row * H + c, o);
+            if (A.da) st4(A.da + row * H + c, drop4(A, o, row * H + c));
+        }
+    }
+    if (A.part) {
+#pragma unroll
+        for (int n = 0; n < NV; ++n) {
+            const int c = (n * LPR + sl) * 4;
+            st4(&red[w][sub][c], dg[n]);
+            st4(&red[w][sub][H + c], db[n]);
+        }
+        __syncthreads();
+        for (int x = threadIdx.x; x < 2 * H; x += BLK) {
+            float s = 0.f;
+            for (int ww = 0; ww < BLK / WAVE; ++ww)
+                for (int ss = 0; ss < RPW; ++ss) s += red[ww][ss][x];
+            A.part[(int64_t)blockIdx.x * 2 * H + x] = s;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(BLK) k_ln_sum_parts(const float* __restrict__ part, int nblk, int n,
+                                                      float* __restrict__ dgamma, float* __restrict__ dbeta, int H) {
+    __shared__ float red[BLK / WAVE][WAVE];
+    const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x >> 6;
+    const int x = blockIdx.x * WAVE + lane;
+    float s = 0.f;
+    if (x < n)
+        for (int b = w; b < nblk; b += BLK / WAVE) s += part[(int64_t)b * n + x];
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && x < n) {
+        const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+        if (x < H) { if (dgamma) dgamma[x] = t; }
+        else if (dbeta) dbeta[x - H] = t;
+    }
+}
+
+// Geometry: H = 4 * LPR * NV with LPR in {8,16,32,64}, NV in {1,2}.
+bool geometry(int H, int& lpr, int& nv) {
+    switch (H) {
+        case 32: lpr = 8; nv = 1; return true;
+        case 64: lpr = 16; nv = 1; return true;
+        case 128: lpr = 32; nv = 1; return true;
+        case 256: lpr = 64; nv = 1; return true;
+        case 512: lpr = 64; nv = 2; return true;
+        default: return false;
+    }
+}
+
+constexpr int LN_BWD_BLOCKS = 1024;
+
+}  // namespace
+}  // namespace tagan
+
+extern "C" {
+
+int tagan_layernorm_supported(int32_t H) {
+    int l, n;
+    return tagan::geometry(H, l, n) ? 1 : 0;
+}
+
+int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, const float* b, float p_drop,
+                            uint64_t seed, const float* gamma, const float* beta, float eps, float* s_out, float* y,
+                            float* mean, float* rstd, void* stream) {
+    using namespace tagan;
+    int lpr, nv;
+    TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "layernorm: dtype %d", dtype);
+    TAGAN_REQUIRE(geometry(H, lpr, nv), TAGAN_ERR_UNSUPPORTED, "layernorm: H=%d unsupported", H);
+    TAGAN_REQUIRE(M > 0 && a && gamma && beta && y && mean && rstd, TAGAN_ERR_ARG, "layernorm_fwd: bad args");
+    TAGAN_REQUIRE(p_drop >= 0.f && p_drop < 1.f, TAGAN_ERR_ARG, "layernorm_fwd: p_drop");
+    LnArgs A{};
+    A.M = M; A.H = H; A.a = a; A.b = b; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
+    A.gamma = gamma; A.beta = beta; A.eps = eps; A.s_out = s_out; A.y = y; A.mean = mean; A.rstd = rstd;
+    const int64_t rpw = WAVE / lpr;
+    const dim3 g((unsigned)(((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE)));
+    hipStream_t s = as_stream(stream);
+    if (lpr == 8) k_ln_fwd<8, 1><<<g, BLK, 0, s>>>(A);
+    else if (lpr == 16) k_ln_fwd<16, 1><<<g, BLK, 0, s>>>(A);
+    else if (lpr == 32) k_ln_fwd<32, 1><<<g, BLK, 0, s>>>(A);
+    else if (nv == 1) k_ln_fwd<64, 1><<<g, BLK, 0, s>>>(A);
+    else k_ln_fwd<64, 2><<<g, BLK, 0, s>>>(A);
+    TAGAN_CHECK_LAUNCH("layernorm_fwd");
+    return TAGAN_OK;
+}
+
+size_t tagan_layernorm_bwd_workspace(int64_t M, int32_t H) {
+    (void)M;
+    return (size_t)tagan::LN_BWD_BLOCKS * 2 * H * sizeof(float);
+}
+
+int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, const float* mean, const float* rstd,
+                        const float* gamma, const float* dy, float p_drop, uint64_t seed, float* ds, float* da,
+                        float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes, void* stream) {
+    using namespace tagan;
+    int lpr, nv;
+    TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "layernorm: dtype %d", dtype);
+    TAGAN_REQUIRE(geometry(H, lpr, nv), TAGAN_ERR_UNSUPPORTED, "layernorm: H=%d unsupported", H);
+    TAGAN_REQUIRE(M > 0 && s_in && mean && rstd && gamma && dy, TAGAN_ERR_ARG, "layernorm_bwd: bad args");
+    const bool want = dgamma || dbeta;
+    TAGAN_REQUIRE(!want || (workspace && workspace_bytes >= tagan_layernorm_bwd_workspace(M, H)),
+                  TAGAN_ERR_WORKSPACE, "layernorm_bwd: workspace");
+    LnArgs A{};
+    A.M = M; A.H = H; A.gamma = gamma; A.s_in = s_in; A.mean = (float*)mean; A.rstd = (float*)rstd; A.dy = dy;
+    A.ds = ds; A.da = da; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
+    A.part = want ? (float*)workspace : nullptr;
+    const int64_t rpw = WAVE / lpr;
+    const int64_t need = ((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE);
+    const int nblk = (int)std::min<int64_t>(need, LN_BWD_BLOCKS);
+    hipStream_t s = as_stream(stream);
+    if (lpr == 8) k_ln_bwd<8, 1><<<nblk, BLK, 0, s>>>(A);
+    else if (lpr == 16) k_ln_bwd<16, 1><<<nblk, BLK, 0, s>>>(A);
+    else if (lpr == 32) k_ln_bwd<32, 1><<<nblk, BLK, 0, s>>>(A);
+    else if (nv == 1) k_ln_bwd<64, 1><<<nblk, BLK, 0, s>>>(A);
+    else k_ln_bwd<64, 2><<<nblk, BLK, 0, s>>>(A);
+    TAGAN_CHECK_LAUNCH("layernorm_bwd");
+    if (want) {
+        const int n = 2 * H;
+        k_ln_sum_parts<<<(n + WAVE - 1) / WAVE, BLK, 0, s>>>(A.part, nblk, n, dgamma, dbeta, H);
+        TAGAN_CHECK_LAUNCH("layernorm_bwd_sum");
+    }
+    return TAGAN_OK;
+}
+
+}  // extern "C"

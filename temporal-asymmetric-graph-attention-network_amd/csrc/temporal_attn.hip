@@ -277,13 +277,296 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd(TArgs A, const float* __restr
     }
 }
 
+// Sum block partials [nblk][n] over blocks: one workgroup per 64 outputs, the
+// 4 waves split the blocks in fixed strides, then a fixed-order LDS combine —
+// deterministic and fully parallel.
 __global__ void __launch_bounds__(BLK) k_sum_parts(const float* __restrict__ part, int nblk, int n,
                                                    float* __restrict__ out) {
-    const int x = blockIdx.x * BLK + threadIdx.x;
-    if (x >= n) return;
+    __shared__ float red[NW][WAVE];
+    const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x >> 6;
+    const int x = blockIdx.x * WAVE + lane;
     float s = 0.f;
-    for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * n + x];
-    out[x] = s;
+    if (x < n)
+        for (int b = w; b < nblk; b += NW) s += part[(int64_t)b * n + x];
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && x < n) out[x] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+// =================================================================== v2: LDS-staged fast path
+// One workgroup per node row; the row's Q/K/V (and dO) of a group of G heads are
+// staged into LDS with coalesced float4 loads, then one thread per (head, step)
+// runs the online softmax over LDS rows (threads of one head read the same K/V
+// row: LDS broadcast).  Gate: d in {4,8,16,32,64,128} and at least one head per
+// LDS budget; otherwise the v1 kernels above run.
+constexpr size_t FWD_LDS_BUDGET = 64 * 1024;
+constexpr size_t BWD_LDS_BUDGET = 96 * 1024;
+
+size_t v2_fwd_lds(int G, int T, int d) { return ((size_t)3 * G * T * d + (size_t)G * (2 * T - 1)) * sizeof(float); }
+size_t v2_bwd_lds(int G, int T, int d, int heads) {
+    return ((size_t)4 * G * T * d + (size_t)2 * G * T + (size_t)G * (2 * T - 1) + (size_t)heads * (2 * T - 1)) *
+           sizeof(float);
+}
+
+int v2_groups(bool bwd, int T, int d, int heads) {
+    if (!(d == 4 || d == 8 || d == 16 || d == 32 || d == 64 || d == 128)) return 0;
+    int G = heads;
+    while (G > 0 && (bwd ? v2_bwd_lds(G, T, d, heads) > BWD_LDS_BUDGET : v2_fwd_lds(G, T, d) > FWD_LDS_BUDGET)) --G;
+    return G;
+}
+
+template <int D>
+__device__ __forceinline__ float dotD(const float* __restrict__ a, const float* __restrict__ b) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; c += 4) {
+        const float4 x = *(const float4*)(a + c), y = *(const float4*)(b + c);
+        s = fmaf(x.x, y.x, s);
+        s = fmaf(x.y, y.y, s);
+        s = fmaf(x.z, y.z, s);
+        s = fmaf(x.w, y.w, s);
+    }
+    return s;
+}
+
+template <int D>
+__device__ __forceinline__ void stage_rows(float* __restrict__ dst, const float* __restrict__ src, int64_t row_off,
+                                           int64_t s_t, int h0, int gc, int T) {
+    constexpr int D4 = D / 4;
+    const int per = T * D4;
+    for (int x = threadIdx.x; x < gc * per; x += BLK) {
+        const int hl = x / per, rem = x - hl * per, t = rem / D4, c = rem - t * D4;
+        *(float4*)(dst + (hl * T + t) * D + c * 4) =
+            *(const float4*)(src + row_off + (int64_t)t * s_t + (h0 + hl) * D + c * 4);
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(BLK) k_tattn_fwd_v2(TArgs A, const float* __restrict__ q,
+                                                      const float* __restrict__ k, const float* __restrict__ v,
+                                                      int G) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int T = A.T, NB = 2 * T - 1;
+    float* Qs = sm;
+    float* Ks = Qs + G * T * D;
+    float* Vs = Ks + G * T * D;
+    float* Bs = Vs + G * T * D;
+    for (int64_t r = blockIdx.x; r < A.rows; r += gridDim.x) {
+        for (int h0 = 0; h0 < A.heads; h0 += G) {
+            const int gc = min(G, A.heads - h0);
+            stage_rows<D>(Qs, q, r * A.s_row, A.s_t, h0, gc, T);
+            stage_rows<D>(Ks, k, r * A.s_row, A.s_t, h0, gc, T);
+            stage_rows<D>(Vs, v, r * A.s_row, A.s_t, h0, gc, T);
+            for (int x = threadIdx.x; x < gc * NB; x += BLK) Bs[x] = A.bias_table ? A.bias_table[h0 * NB + x] : 0.f;
+            __syncthreads();
+            for (int it = threadIdx.x; it < gc * T; it += BLK) {
+                const int hl = it / T, i = it - hl * T, h = h0 + hl;
+                const float* qi = Qs + (hl * T + i) * D;
+                const float* kb = Ks + hl * T * D;
+                const float* vb = Vs + hl * T * D;
+                const float* bb = Bs + hl * NB + i + T - 1;     // bb[-j] = bias of (i, j)
+                float acc[D];
+#pragma unroll
+                for (int c = 0; c < D; ++c) acc[c] = 0.f;
+                float m = -INFINITY, l = 0.f;
+                for (int j = 0; j < T; ++j) {
+                    if (!keep_ij(A, r, h, i, j)) continue;
+                    float bias = bb[-j];
+                    if (A.bias_dense) bias += A.bias_dense[r * A.bias_bstride + (((int64_t)h * T + i) * T + j)];
+                    const float s = fmaf(dotD<D>(qi, kb + j * D), A.inv_sqrt_d, bias);
+                    const float mn = fmaxf(m, s);
+                    const float corr = __expf(m - mn);
+                    const float p = __expf(s - mn);
+                    l = fmaf(l, corr, p);
+                    const float pw = p * drop_scale(A, r, h, i, j);
+                    const float* vj = vb + j * D;
+#pragma unroll
+                    for (int c = 0; c < D; c += 4) {
+                        const float4 vv = *(const float4*)(vj + c);
+                        acc[c] = fmaf(acc[c], corr, pw * vv.x);
+                        acc[c + 1] = fmaf(acc[c + 1], corr, pw * vv.y);
+                        acc[c + 2] = fmaf(acc[c + 2], corr, pw * vv.z);
+                        acc[c + 3] = fmaf(acc[c + 3], corr, pw * vv.w);
+                    }
+                    m = mn;
+                }
+                float* orow = A.out + r * A.o_row + (int64_t)i * A.o_t + h * D;
+                const float inv_l = (l > 0.f) ? 1.f / l : NAN;
+#pragma unroll
+                for (int c = 0; c < D; c += 4)
+                    *(float4*)(orow + c) = make_float4(acc[c] * inv_l, acc[c + 1] * inv_l, acc[c + 2] * inv_l,
+                                                       acc[c + 3] * inv_l);
+                const float ls = m + __logf(l);
+                A.lse[(r * A.heads + h) * T + i] = ls;
+                if (A.attn) {
+                    float* ar = A.attn + ((r * A.heads + h) * T + i) * (int64_t)T;
+                    for (int j = 0; j < T; ++j) {
+                        float a = 0.f;
+                        if (keep_ij(A, r, h, i, j)) {
+                            float bias = bb[-j];
+                            if (A.bias_dense) bias += A.bias_dense[r * A.bias_bstride + (((int64_t)h * T + i) * T + j)];
+                            const float s = fmaf(dotD<D>(qi, kb + j * D), A.inv_sqrt_d, bias);
+                            a = __expf(s - ls) * drop_scale(A, r, h, i, j);
+                        }
+                        ar[j] = (l > 0.f) ? a : NAN;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(BLK) k_tattn_bwd_v2(TArgs A, const float* __restrict__ q,
+                                                      const float* __restrict__ k, const float* __restrict__ v,
+                                                      const float* __restrict__ dout, const float* __restrict__ lse,
+                                                      int G) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int T = A.T, NB = 2 * T - 1;
+    float* Qs = sm;
+    float* Ks = Qs + G * T * D;
+    float* Vs = Ks + G * T * D;
+    float* Os = Vs + G * T * D;          // dO
+    float* Ls = Os + G * T * D;          // lse   [G][T]
+    float* Del = Ls + G * T;             // delta [G][T]
+    float* Bs = Del + G * T;             // bias  [G][NB]
+    float* Acc = Bs + G * NB;            // dbias [heads][NB], persistent over rows
+    for (int x = threadIdx.x; x < A.heads * NB; x += BLK) Acc[x] = 0.f;
+    for (int64_t r = blockIdx.x; r < A.rows; r += gridDim.x) {
+        for (int h0 = 0; h0 < A.heads; h0 += G) {
+            const int gc = min(G, A.heads - h0);
+            __syncthreads();
+            stage_rows<D>(Qs, q, r * A.s_row, A.s_t, h0, gc, T);
+            stage_rows<D>(Ks, k, r * A.s_row, A.s_t, h0, gc, T);
+            stage_rows<D>(Vs, v, r * A.s_row, A.s_t, h0, gc, T);
+            stage_rows<D>(Os, dout, r * A.do_row, A.do_t, h0, gc, T);
+            for (int x = threadIdx.x; x < gc * T; x += BLK) Ls[x] = lse[(r * A.heads + h0) * T + x];
+            for (int x = threadIdx.x; x < gc * NB; x += BLK) Bs[x] = A.bias_table ? A.bias_table[h0 * NB + x] : 0.f;
+            __syncthreads();
+            // ---- phase A: (head, i): delta_i, dq_i, optional per-pair ds
+            for (int it = threadIdx.x; it < gc * T; it += BLK) {
+                const int hl = it / T, i = it - hl * T, h = h0 + hl;
+                const float* qi = Qs + (hl * T + i) * D;
+                const float* doi = Os + (hl * T + i) * D;
+                const float* kb = Ks + hl * T * D;
+                const float* vb = Vs + hl * T * D;
+                const float* bb = Bs + hl * NB + i + T - 1;
+                const float* orow = A.o_in + r * A.o_row + (int64_t)i * A.o_t + h * D;
+                float Di = 0.f;
+#pragma unroll
+                for (int c = 0; c < D; c += 4) {
+                    const float4 o4 = *(const float4*)(orow + c), d4 = *(const float4*)(doi + c);
+                    Di = fmaf(d4.x, o4.x, Di);
+                    Di = fmaf(d4.y, o4.y, Di);
+                    Di = fmaf(d4.z, o4.z, Di);
+                    Di = fmaf(d4.w, o4.w, Di);
+                }
+                Del[hl * T + i] = Di;
+                const float li = Ls[hl * T + i];
+                float dq[D];
+#pragma unroll
+                for (int c = 0; c < D; ++c) dq[c] = 0.f;
+                for (int j = 0; j < T; ++j) {
+                    float ds = 0.f;
+                    if (keep_ij(A, r, h, i, j)) {
+                        float bias = bb[-j];
+                        if (A.bias_dense) bias += A.bias_dense[r * A.bias_bstride + (((int64_t)h * T + i) * T + j)];
+                        const float s = fmaf(dotD<D>(qi, kb + j * D), A.inv_sqrt_d, bias);
+                        const float p = __expf(s - li);
+                        ds = p * (dotD<D>(doi, vb + j * D) * drop_scale(A, r, h, i, j) - Di);
+                        const float* kj = kb + j * D;
+#pragma unroll
+                        for (int c = 0; c < D; c += 4) {
+                            const float4 k4 = *(const float4*)(kj + c);
+                            dq[c] = fmaf(ds, k4.x, dq[c]);
+                            dq[c + 1] = fmaf(ds, k4.y, dq[c + 1]);
+                            dq[c + 2] = fmaf(ds, k4.z, dq[c + 2]);
+                            dq[c + 3] = fmaf(ds, k4.w, dq[c + 3]);
+                        }
+                    }
+                    if (A.dbias_dense) A.dbias_dense[((r * A.heads + h) * T + i) * (int64_t)T + j] = ds;
+                }
+                float* dqr = A.dq + r * A.d_row + (int64_t)i * A.d_t + h * D;
+#pragma unroll
+                for (int c = 0; c < D; c += 4)
+                    *(float4*)(dqr + c) = make_float4(dq[c] * A.inv_sqrt_d, dq[c + 1] * A.inv_sqrt_d,
+                                                      dq[c + 2] * A.inv_sqrt_d, dq[c + 3] * A.inv_sqrt_d);
+            }
+            __syncthreads();
+            // ---- phase B: (head, j): dk_j, dv_j
+            for (int it = threadIdx.x; it < gc * T; it += BLK) {
+                const int hl = it / T, j = it - hl * T, h = h0 + hl;
+                const float* kj = Ks + (hl * T + j) * D;
+                const float* vj = Vs + (hl * T + j) * D;
+                const float* bb = Bs + hl * NB - j + T - 1;     // bb[i] = bias of (i, j)
+                float dk[D], dv[D];
+#pragma unroll
+                for (int c = 0; c < D; ++c) {
+                    dk[c] = 0.f;
+                    dv[c] = 0.f;
+                }
+                for (int i = 0; i < T; ++i) {
+                    if (!keep_ij(A, r, h, i, j)) continue;
+                    const float* qi = Qs + (hl * T + i) * D;
+                    const float* doi = Os + (hl * T + i) * D;
+                    float bias = bb[i];
+                    if (A.bias_dense) bias += A.bias_dense[r * A.bias_bstride + (((int64_t)h * T + i) * T + j)];
+                    const float s = fmaf(dotD<D>(qi, kj), A.inv_sqrt_d, bias);
+                    const float p = __expf(s - Ls[hl * T + i]);
+                    const float sc = drop_scale(A, r, h, i, j);
+                    const float ds = p * (dotD<D>(doi, vj) * sc - Del[hl * T + i]);
+                    const float pw = p * sc;
+#pragma unroll
+                    for (int c = 0; c < D; c += 4) {
+                        const float4 q4 = *(const float4*)(qi + c), d4 = *(const float4*)(doi + c);
+                        dk[c] = fmaf(ds, q4.x, dk[c]);
+                        dk[c + 1] = fmaf(ds, q4.y, dk[c + 1]);
+                        dk[c + 2] = fmaf(ds, q4.z, dk[c + 2]);
+                        dk[c + 3] = fmaf(ds, q4.w, dk[c + 3]);
+                        dv[c] = fmaf(pw, d4.x, dv[c]);
+                        dv[c + 1] = fmaf(pw, d4.y, dv[c + 1]);
+                        dv[c + 2] = fmaf(pw, d4.z, dv[c + 2]);
+                        dv[c + 3] = fmaf(pw, d4.w, dv[c + 3]);
+                    }
+                }
+                float* dkr = A.dk + r * A.d_row + (int64_t)j * A.d_t + h * D;
+                float* dvr = A.dv + r * A.d_row + (int64_t)j * A.d_t + h * D;
+#pragma unroll
+                for (int c = 0; c < D; c += 4) {
+                    *(float4*)(dkr + c) = make_float4(dk[c] * A.inv_sqrt_d, dk[c + 1] * A.inv_sqrt_d,
+                                                      dk[c + 2] * A.inv_sqrt_d, dk[c + 3] * A.inv_sqrt_d);
+                    *(float4*)(dvr + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
+                }
+            }
+            // ---- phase C: (head, diagonal i-j) sums of ds for the bias table (fixed order)
+            if (A.part) {
+                for (int it = threadIdx.x; it < gc * NB; it += BLK) {
+                    const int hl = it / NB, dl = it - hl * NB, h = h0 + hl;
+                    const int delta = dl - (T - 1);            // i - j
+                    const float bias = Bs[hl * NB + dl];
+                    float sum = 0.f;
+                    for (int i = max(0, delta); i < min(T, T + delta); ++i) {
+                        const int j = i - delta;
+                        if (!keep_ij(A, r, h, i, j)) continue;
+                        const float* qi = Qs + (hl * T + i) * D;
+                        const float* doi = Os + (hl * T + i) * D;
+                        float b = bias;
+                        if (A.bias_dense) b += A.bias_dense[r * A.bias_bstride + (((int64_t)h * T + i) * T + j)];
+                        const float s = fmaf(dotD<D>(qi, Ks + (hl * T + j) * D), A.inv_sqrt_d, b);
+                        const float p = __expf(s - Ls[hl * T + i]);
+                        sum += p * (dotD<D>(doi, Vs + (hl * T + j) * D) * drop_scale(A, r, h, i, j) -
+                                    Del[hl * T + i]);
+                    }
+                    Acc[h * NB + dl] += sum;
+                }
+            }
+        }
+    }
+    if (A.part) {
+        __syncthreads();
+        for (int x = threadIdx.x; x < A.heads * NB; x += BLK) A.part[(int64_t)blockIdx.x * A.heads * NB + x] = Acc[x];
+    }
 }
 
 int pick_D(int d) {
@@ -295,7 +578,7 @@ int pick_D(int d) {
     return 0;
 }
 
-int grid_rows(int64_t rows) { return (int)std::min<int64_t>(rows, 256 * 8); }
+int grid_rows(int64_t rows) { return (int)std::min<int64_t>(rows, 256 * 4); }
 
 int check(int dtype, int64_t rows, int T, int heads, int d, float p_drop) {
     TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "temporal_attn: dtype %d unsupported", dtype);
@@ -356,6 +639,20 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     const float* qf = (const float*)q;
     const float* kf = (const float*)k;
     const float* vf = (const float*)v;
+    const int G = (s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0) ? v2_groups(false, T, head_dim, heads) : 0;
+    if (G > 0) {
+        const size_t lds = v2_fwd_lds(G, T, head_dim);
+        switch (head_dim) {
+            case 4: k_tattn_fwd_v2<4><<<g, BLK, lds, s>>>(A, qf, kf, vf, G); break;
+            case 8: k_tattn_fwd_v2<8><<<g, BLK, lds, s>>>(A, qf, kf, vf, G); break;
+            case 16: k_tattn_fwd_v2<16><<<g, BLK, lds, s>>>(A, qf, kf, vf, G); break;
+            case 32: k_tattn_fwd_v2<32><<<g, BLK, lds, s>>>(A, qf, kf, vf, G); break;
+            case 64: k_tattn_fwd_v2<64><<<g, BLK, lds, s>>>(A, qf, kf, vf, G); break;
+            default: k_tattn_fwd_v2<128><<<g, BLK, lds, s>>>(A, qf, kf, vf, G); break;
+        }
+        TAGAN_CHECK_LAUNCH("temporal_attn_fwd_v2");
+        return TAGAN_OK;
+    }
     switch (pick_D(head_dim)) {
         case 8: k_tattn_fwd<8><<<g, BLK, 0, s>>>(A, qf, kf, vf); break;
         case 16: k_tattn_fwd<16><<<g, BLK, 0, s>>>(A, qf, kf, vf); break;
@@ -415,7 +712,21 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     const float* kf = (const float*)k;
     const float* vf = (const float*)v;
     const float* df = (const float*)dout;
-    switch (pick_D(head_dim)) {
+    const int G = (s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0 && do_t % 4 == 0 &&
+                   do_row % 4 == 0 && d_t % 4 == 0 && d_row % 4 == 0)
+                      ? v2_groups(true, T, head_dim, heads)
+                      : 0;
+    if (G > 0) {
+        const size_t l2 = v2_bwd_lds(G, T, head_dim, heads);
+        switch (head_dim) {
+            case 4: k_tattn_bwd_v2<4><<<g, BLK, l2, s>>>(A, qf, kf, vf, df, lse, G); break;
+            case 8: k_tattn_bwd_v2<8><<<g, BLK, l2, s>>>(A, qf, kf, vf, df, lse, G); break;
+            case 16: k_tattn_bwd_v2<16><<<g, BLK, l2, s>>>(A, qf, kf, vf, df, lse, G); break;
+            case 32: k_tattn_bwd_v2<32><<<g, BLK, l2, s>>>(A, qf, kf, vf, df, lse, G); break;
+            case 64: k_tattn_bwd_v2<64><<<g, BLK, l2, s>>>(A, qf, kf, vf, df, lse, G); break;
+            default: k_tattn_bwd_v2<128><<<g, BLK, l2, s>>>(A, qf, kf, vf, df, lse, G); break;
+        }
+    } else switch (pick_D(head_dim)) {
         case 8: k_tattn_bwd<8><<<g, BLK, lds, s>>>(A, qf, kf, vf, df, lse); break;
         case 16: k_tattn_bwd<16><<<g, BLK, lds, s>>>(A, qf, kf, vf, df, lse); break;
         case 32: k_tattn_bwd<32><<<g, BLK, lds, s>>>(A, qf, kf, vf, df, lse); break;
@@ -425,7 +736,7 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     TAGAN_CHECK_LAUNCH("temporal_attn_bwd");
     if (dbias_table) {
         const int n = heads * (2 * T - 1);
-        k_sum_parts<<<(n + BLK - 1) / BLK, BLK, 0, s>>>(A.part, nblk, n, dbias_table);
+        k_sum_parts<<<(n + WAVE - 1) / WAVE, BLK, 0, s>>>(A.part, nblk, n, dbias_table);
         TAGAN_CHECK_LAUNCH("temporal_attn_bwd_sum");
     }
     return TAGAN_OK;

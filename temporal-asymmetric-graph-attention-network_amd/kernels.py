@@ -302,8 +302,116 @@ class TemporalAttnFn(torch.autograd.Function):
         return dqkv, dbt, dbd, None, None, None, None, None, None
 
 
+
+
+# ----------------------------------------------------------------------------- projections
+def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, rows: int = 2048) -> torch.Tensor:
+    """dW = dyᵀ·x for K = dy.shape[0] >> M, N: split-K batched GEMM (hipBLASLt) + ordered sum.
+
+    A single [M,K]x[K,N] GEMM with K = 320k runs at 15-30 TF/s on gfx950; splitting K
+    into 2048-row slices gives hipBLASLt a batched problem it tiles well (≈110 TF/s
+    fp32) and sums the slices in a fixed order (profiles/).
+    """
+    K, M = dy2.shape
+    N = x2.shape[1]
+    if K < 4 * rows:
+        return dy2.t() @ x2
+    c = K // rows
+    main = c * rows
+    dw = torch.bmm(dy2[:main].view(c, rows, M).transpose(1, 2), x2[:main].view(c, rows, N)).sum(0)
+    if main < K:
+        dw = dw + dy2[main:].t() @ x2[main:]
+    return dw
+
+
+class LinearFn(torch.autograd.Function):
+    """y = x·Wᵀ + b with the split-K weight gradient above."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return torch.nn.functional.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ w).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = weight_grad(dy2, x.reshape(-1, x.shape[-1]).contiguous())
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = dy2.sum(0)
+        return dx, dw, db
+
+
+def linear(x, w, b=None):
+    return LinearFn.apply(x, w, b)
+
+
 def fused_qkv(x, q_lin, k_lin, v_lin):
     """One GEMM for the three projections (hipBLASLt via torch): [.., H] -> [.., 3H] = q | k | v."""
     w = torch.cat([q_lin.weight, k_lin.weight, v_lin.weight], 0)
     b = torch.cat([q_lin.bias, k_lin.bias, v_lin.bias], 0)
-    return torch.nn.functional.linear(x, w, b)
+    return linear(x, w, b)
+
+
+# ----------------------------------------------------------------------------- layer norm
+class AddLayerNormFn(torch.autograd.Function):
+    """y = LayerNorm(dropout(a) + b) (b optional) on the HIP kernels of csrc/layernorm.hip."""
+
+    @staticmethod
+    def forward(ctx, a, b, gamma, beta, eps: float, p_drop: float, seed: int):
+        require_hip(a)
+        H = a.shape[-1]
+        a2 = a.reshape(-1, H).contiguous()
+        M = a2.shape[0]
+        b2 = b.reshape(-1, H).contiguous() if b is not None else None
+        keep_s = b is not None or p_drop > 0
+        s = torch.empty_like(a2) if keep_s else None
+        y = torch.empty_like(a2)
+        mean = torch.empty(M, device=a.device)
+        rstd = torch.empty(M, device=a.device)
+        check(lib().tagan_add_layernorm_fwd(_lib.TAGAN_F32, M, H, ptr(a2), ptr(b2), float(p_drop), seed,
+                                            ptr(gamma), ptr(beta), float(eps), ptr(s), ptr(y), ptr(mean),
+                                            ptr(rstd), stream_of(a2)), "tagan_add_layernorm_fwd")
+        ctx.save_for_backward(s if keep_s else a2, mean, rstd, gamma)
+        ctx.cfg = (p_drop, seed, b is not None, a.shape)
+        return y.view(a.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        s, mean, rstd, gamma = ctx.saved_tensors
+        p_drop, seed, has_b, shape = ctx.cfg
+        H = shape[-1]
+        dy2 = dy.reshape(-1, H).contiguous()
+        M = dy2.shape[0]
+        need_a, need_b = ctx.needs_input_grad[0], has_b and ctx.needs_input_grad[1]
+        da = torch.empty_like(dy2) if need_a else None
+        ds = torch.empty_like(dy2) if need_b else None
+        dg = torch.empty(H, device=dy.device) if ctx.needs_input_grad[2] else None
+        dbt = torch.empty(H, device=dy.device) if ctx.needs_input_grad[3] else None
+        L = lib()
+        wsb = L.tagan_layernorm_bwd_workspace(M, H)
+        ws = torch.empty(int(wsb), dtype=torch.uint8, device=dy.device)
+        check(L.tagan_layernorm_bwd(_lib.TAGAN_F32, M, H, ptr(s), ptr(mean), ptr(rstd), ptr(gamma), ptr(dy2),
+                                    float(p_drop), seed, ptr(ds), ptr(da), ptr(dg), ptr(dbt), ptr(ws), wsb,
+                                    stream_of(dy2)), "tagan_layernorm_bwd")
+        return (da.view(shape) if da is not None else None, ds.view(shape) if ds is not None else None,
+                dg, dbt, None, None, None)
+
+
+def layer_norm(x, ln: torch.nn.LayerNorm):
+    """LayerNorm on the HIP kernel when the width is supported (else ATen's, same math)."""
+    if x.is_cuda and lib().tagan_layernorm_supported(x.shape[-1]):
+        return AddLayerNormFn.apply(x, None, ln.weight, ln.bias, ln.eps, 0.0, 0)
+    return ln(x)
+
+
+def dropout_add_layer_norm(a, b, ln: torch.nn.LayerNorm, p: float):
+    """LayerNorm(dropout(a) + b) fused (the residual tail of every attention layer)."""
+    if a.is_cuda and lib().tagan_layernorm_supported(a.shape[-1]):
+        return AddLayerNormFn.apply(a, b, ln.weight, ln.bias, ln.eps, float(p), new_seed() if p > 0 else 0)
+    return ln(torch.nn.functional.dropout(a, p, True) + b)

@@ -5,9 +5,9 @@ initialisation order and forward signature (geometric_attention.py:228-607), so
 reference ``state_dict``s load unchanged and ``torch.manual_seed(s)`` yields the
 same initial weights.  The forward runs:
 
-  LN1 (torch) -> one fused QKV GEMM (hipBLASLt) -> ``tagan_geo_attn_fwd``
+  LN1 (HIP) -> one fused QKV GEMM (hipBLASLt) -> ``tagan_geo_attn_fwd``
   (metric score, edge-softmax, attn-dropout, A·V over the mask's CSR; HIP)
-  -> out-proj GEMM -> dropout -> residual -> LN2
+  -> out-proj GEMM -> fused dropout + residual + LN2 (HIP)
 
 Dense masks become CSR (``graph_from_dense_mask``); TAGANGraphAttention hands in
 a prebuilt snapshot CSR through ``forward_graph``.  There is no CPU path.
@@ -20,7 +20,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib
-from ..kernels import GeoAttnFn, SnapshotGraph, fused_qkv, graph_from_dense_mask, new_seed
+from ..kernels import (GeoAttnFn, SnapshotGraph, dropout_add_layer_norm, fused_qkv, graph_from_dense_mask,
+                       layer_norm, linear, new_seed)
 
 
 class DistanceMetric:
@@ -130,15 +131,16 @@ class GeometricAttention(nn.Module):
     def forward_graph(self, x: torch.Tensor, graph: SnapshotGraph) -> torch.Tensor:
         """Hot path: x [N, H] (N = all nodes of a snapshot batch), graph = their CSR/CSC."""
         identity = x
-        h = self.layer_norm1(x) if self.use_layer_norm else x
+        h = layer_norm(x, self.layer_norm1) if self.use_layer_norm else x
         qkv = fused_qkv(h, self.q_linear, self.k_linear, self.v_linear).contiguous()
         p = self.attn_dropout.p if self.training else 0.0
         ctx = GeoAttnFn.apply(qkv, self._metric_param(), graph, self.metric_id, self.num_heads, p,
                               new_seed() if p > 0 else 0)
-        out = self.output_dropout(self.output_proj(ctx)) + identity
+        proj = linear(ctx, self.output_proj.weight, self.output_proj.bias)
+        p_out = self.output_dropout.p if self.training else 0.0
         if self.use_layer_norm:
-            out = self.layer_norm2(out)
-        return out
+            return dropout_add_layer_norm(proj, identity, self.layer_norm2, p_out)
+        return F.dropout(proj, p_out, True) + identity
 
     def forward(self, x: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                 geometric_bias: Optional[torch.Tensor] = None) -> torch.Tensor:

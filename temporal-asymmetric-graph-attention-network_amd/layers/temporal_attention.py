@@ -2,10 +2,10 @@
 
 ``TimeEncoding``, ``TemporalAttention`` and ``AsymmetricTemporalAttention`` keep
 the reference constructors, parameter names/shapes and initialisation order.
-Forward = LN1 (torch) -> fused QKV GEMM (hipBLASLt) -> ``tagan_temporal_attn_fwd``
+Forward = LN1 (HIP) -> fused QKV GEMM (hipBLASLt) -> ``tagan_temporal_attn_fwd``
 (QKᵀ/√d + folded relative-position/asymmetric-kernel bias table [+ time bias]
 -> masks -> softmax -> attn-dropout -> A·V per node row, HIP) -> out-proj GEMM
--> dropout -> residual -> LN2.
+-> fused dropout + residual + LN2 (HIP).
 
 Snapshot lists are kept **time-major** ([T, N_max, H], the natural result of
 stacking snapshots) — the kernel takes strides, so the reference's
@@ -23,7 +23,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..kernels import TemporalAttnFn, TemporalMask, fused_qkv, new_seed
+from ..kernels import (TemporalAttnFn, TemporalMask, dropout_add_layer_norm, fused_qkv, layer_norm, linear,
+                       new_seed)
 
 
 class MaskBroadcastError(RuntimeError):
@@ -207,7 +208,7 @@ class TemporalAttention(nn.Module):
         else:
             B, T, H = x.shape
         identity = x
-        hx = self.layer_norm1(x) if self.use_layer_norm else x
+        hx = layer_norm(x, self.layer_norm1) if self.use_layer_norm else x
         qkv = fused_qkv(hx, self.q_linear, self.k_linear, self.v_linear).contiguous()
         if _known_ones_mask:
             bias_dense, mask, explode = None, self._ones_mask_fast(B, T), False
@@ -219,10 +220,11 @@ class TemporalAttention(nn.Module):
         p = self.attn_dropout.p if self.training else 0.0
         ctx, attn = TemporalAttnFn.apply(qkv, self._bias_table(T, x.device), bias_dense, time_major,
                                          self.num_heads, mask, p, new_seed() if p > 0 else 0, want_attn)
-        out = self.output_dropout(self.output_proj(ctx)) + identity
+        proj = linear(ctx, self.output_proj.weight, self.output_proj.bias)
+        p_out = self.output_dropout.p if self.training else 0.0
         if self.use_layer_norm:
-            out = self.layer_norm2(out)
-        return out, attn
+            return dropout_add_layer_norm(proj, identity, self.layer_norm2, p_out), attn
+        return F.dropout(proj, p_out, True) + identity, attn
 
     def _ones_mask_fast(self, B, T):
         # an all-ones [T,T] mask expands to every (b, h): nothing is masked beyond the causal flag

@@ -24,7 +24,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .kernels import build_graph
+from .kernels import build_graph, layer_norm, linear
 from .layers.classification import ClassificationModule, TemporalLossModule
 from .layers.graph_attention import TAGANGraphAttention
 from .layers.temporal_attention import AsymmetricTemporalAttention, MaskBroadcastError
@@ -99,12 +99,12 @@ class TAGAN(nn.Module):
             counts.append(int(x.shape[0]))
         x_cat = torch.cat(xs, 0) if len(xs) > 1 else xs[0]
         graph = build_graph(eis, counts)
-        h = self.node_embedding(x_cat)
+        h = linear(x_cat, self.node_embedding.weight, self.node_embedding.bias)
         skip = h
         for i, layer in enumerate(self.geometric_attention_layers):
             h = layer.forward_graph(h, graph)
             if i == 0:
-                h = h + (self.skip_layer_norm(skip) if self.skip_layer_norm is not None else skip)
+                h = h + (layer_norm(skip, self.skip_layer_norm) if self.skip_layer_norm is not None else skip)
         weights = [{"node_attention": None} for _ in graph_sequence] if return_attention_weights else []
         return h, counts, weights
 
