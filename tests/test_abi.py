@@ -85,3 +85,9 @@ def test_metric_table_matches_header():
         src = f.read()
     for name, mid in _lib.METRIC_IDS.items():
         assert ("TAGAN_METRIC_%s = %d" % (name.upper(), mid)) in src
+
+
+def test_every_header_symbol_has_a_ctypes_signature():
+    """A missing argtypes entry turns float arguments into ctypes errors at call time."""
+    missing = [s for s in _lib.header_symbols() if s not in _lib._SIGNATURES]
+    assert not missing, missing
