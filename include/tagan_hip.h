@@ -221,6 +221,59 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s, const f
                         float* ds, float* da, float* dgamma, float* dbeta,
                         void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * NodeMemoryBank on the device.  Replaces src/tagan/utils/memory_bank.py:14-360
+ * (a dict of per-node CPU tensors):  update (:65-173), get_state(s) (:175-211),
+ * update_state (:235-244), decay_all (:222-225).  All arrays are caller-owned
+ * device memory; tagan_membank_init formats them.
+ *   tkeys/tvals [tcap]   id -> slot hash (tcap a power of two, load <= 1/2)
+ *   slot arrays [cap]    slot_id (INT64_MIN = free), slot_tpos, inact,
+ *                        last_seen (INT64_MIN = unset), born, touch, and the
+ *                        per-call scratch first_occ/last_ok/occ_count
+ *   states [cap, H]      fp32 node states
+ *   free_list [cap]      freed slots
+ *   fkeys/fcount [fcap]  per-id appearance counts (never pruned, :97, :165)
+ *   ctl int64[8]         {slots used (high-water), free_top, stored, tombstones,
+ *                         distinct ids, error flags, -, -}
+ * `epoch` is a caller counter, unique per call; `timestep` as in the reference.
+ * ------------------------------------------------------------------------- */
+typedef struct tagan_membank {
+    int64_t cap, tcap, fcap;
+    int32_t H;
+    int64_t* tkeys;
+    int32_t* tvals;
+    int64_t* slot_id;
+    int32_t* slot_tpos;
+    float* states;
+    int32_t* inact;
+    int64_t* last_seen;
+    int32_t* born;
+    int32_t* touch;
+    int32_t* first_occ;
+    int32_t* last_ok;
+    int32_t* occ_count;
+    int32_t* free_list;
+    int64_t* fkeys;
+    int64_t* fcount;
+    int64_t* ctl;
+} tagan_membank;
+
+int tagan_membank_init(const tagan_membank* bank, void* stream);
+/* ids[n] -> slots[n] (-1 if absent).  insert != 0 inserts absent ids as zero
+ * states with inactivity 0 (get_states semantics).  scratch: int32[2n]. */
+int tagan_membank_lookup(const tagan_membank* bank, const int64_t* ids, int64_t n, int insert, int32_t epoch,
+                         int32_t* slots, int32_t* scratch, void* stream);
+/* One NodeMemoryBank.update(ids, states, timestep) (states [n, H], row stride ld). */
+int tagan_membank_update(const tagan_membank* bank, const int64_t* ids, int64_t n, const float* states,
+                         int64_t ld, int64_t timestep, double decay, int32_t max_inactivity, int32_t epoch,
+                         uint64_t seed, int32_t* slots, int32_t* scratch, void* stream);
+/* out[n, H] = states[slots] (zeros where slot < 0). */
+int tagan_membank_gather(const tagan_membank* bank, const int32_t* slots, int64_t n, float* out, void* stream);
+/* states *= factor for every stored slot (decay_all). */
+int tagan_membank_scale(const tagan_membank* bank, float factor, void* stream);
+/* Copy every stored node of src into a freshly formatted dst (growth / tombstone purge). */
+int tagan_membank_rehash(const tagan_membank* src, const tagan_membank* dst, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,7 +55,20 @@ _SIGNATURES = {
     "tagan_layernorm_bwd_workspace": (_sz, [_i64, _i32]),
     "tagan_layernorm_bwd": (_c.c_int, [_c.c_int, _i64, _i32, _p, _p, _p, _p, _p, _f32, _u64, _p, _p, _p, _p, _p,
                                        _sz, _p]),
+    "tagan_membank_init": (_c.c_int, [_p, _p]),
+    "tagan_membank_lookup": (_c.c_int, [_p, _p, _i64, _c.c_int, _i32, _p, _p, _p]),
+    "tagan_membank_update": (_c.c_int, [_p, _p, _i64, _p, _i64, _i64, _c.c_double, _i32, _i32, _u64, _p, _p, _p]),
+    "tagan_membank_gather": (_c.c_int, [_p, _p, _i64, _p, _p]),
+    "tagan_membank_scale": (_c.c_int, [_p, _f32, _p]),
+    "tagan_membank_rehash": (_c.c_int, [_p, _p, _p]),
 }
+
+
+class TaganMembank(ctypes.Structure):
+    """Mirror of ``struct tagan_membank`` (include/tagan_hip.h)."""
+    _fields_ = [("cap", _i64), ("tcap", _i64), ("fcap", _i64), ("H", _i32)] + \
+        [(n, _p) for n in ("tkeys", "tvals", "slot_id", "slot_tpos", "states", "inact", "last_seen", "born", "touch",
+                           "first_occ", "last_ok", "occ_count", "free_list", "fkeys", "fcount", "ctl")]
 
 
 class TaganGraph(ctypes.Structure):

@@ -1,0 +1,58 @@
+"""Data-parallel gradient exchange (tagan_amd.distributed) on CPU with gloo, world_size 2.
+
+The GPU path runs the same code over RCCL (backend "nccl"); the collective
+pattern — one flat fp32 bucket, SUM then /world — is backend independent.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import tagan_amd  # noqa: F401
+    from tagan_amd.distributed import GradBucket, broadcast_parameters
+    torch.manual_seed(100 + rank)                         # ranks start different ...
+    model = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Linear(5, 3), torch.nn.Linear(3, 2))
+    broadcast_parameters(model)                           # ... and are synchronised from rank 0
+    for p in model.parameters():
+        results["w%d" % rank] = torch.cat([q.detach().flatten() for q in model.parameters()])
+    x = torch.randn(4, 6, generator=torch.Generator().manual_seed(rank))
+    loss = model[:2](x).sum()                            # last layer unused -> grad None on every rank
+    loss.backward()
+    local = torch.cat([p.grad.flatten() for p in model.parameters() if p.grad is not None])
+    results["local%d" % rank] = local.clone()
+    GradBucket(model.parameters()).allreduce_mean()
+    results["avg%d" % rank] = torch.cat([p.grad.flatten() for p in model.parameters() if p.grad is not None])
+    results["none%d" % rank] = [p.grad is None for p in model.parameters()]
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_bucket_allreduce_world2():
+    port = _free_port()
+    with mp.Manager() as m:
+        res = m.dict()
+        mp.spawn(_worker, args=(2, port, res), nprocs=2, join=True)
+        res = dict(res)
+    assert torch.equal(res["w0"], res["w1"])
+    want = (res["local0"] + res["local1"]) / 2
+    assert torch.allclose(res["avg0"], want, atol=1e-7)
+    assert torch.equal(res["avg0"], res["avg1"])
+    assert res["none0"] == res["none1"] == [False, False, False, False, True, True]

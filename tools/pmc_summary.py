@@ -1,0 +1,47 @@
+"""Fold two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over tools/roofline_kernels.py into
+profiles/pmc_<config>.json: HBM bytes per launch group (fwd + bwd of one geometric layer).
+
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 64 B per 128-B request of a wide
+coalesced read, i.e. half the bytes -> doubled; WRITE_SIZE is exact for 16-B/lane stores.  Both are in KiB.
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+GEO = ("k_geo_fwd", "k_geo_bwd", "k_geo_sum_parts")
+
+
+def load(pattern, counter):
+    per_kernel = defaultdict(list)
+    for path in glob.glob(pattern, recursive=True):
+        for r in csv.DictReader(open(path)):
+            if r.get("Counter_Name") != counter:
+                continue
+            name = r["Kernel_Name"]
+            if any(g in name for g in GEO):
+                per_kernel[name.split("(")[0].split("<")[0].split("::")[-1]].append(float(r["Counter_Value"]))
+    return per_kernel
+
+
+def main():
+    fetch_dir, write_dir, config, out = sys.argv[1:5]
+    f = load(fetch_dir + "/**/*counter_collection.csv", "FETCH_SIZE")
+    w = load(write_dir + "/**/*counter_collection.csv", "WRITE_SIZE")
+    # one launch group = one fwd + one bwd = each kernel once; use the median dispatch of each kernel
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+    fetch = {k: 2 * 1024 * med(v) for k, v in f.items()}
+    write = {k: 1024 * med(v) for k, v in w.items()}
+    total = sum(fetch.values()) + sum(write.values())
+    rec = {"config": config, "hbm_bytes_per_launch_group": int(total),
+           "fetch_bytes_corrected": {k: int(v) for k, v in fetch.items()},
+           "write_bytes": {k: int(v) for k, v in write.items()},
+           "note": "FETCH_SIZE x2 (gfx950 half-count of wide reads), WRITE_SIZE exact; KiB -> bytes; "
+                   "median dispatch per kernel; kernels: " + ", ".join(sorted(set(fetch) | set(write)))}
+    json.dump(rec, open(out, "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
