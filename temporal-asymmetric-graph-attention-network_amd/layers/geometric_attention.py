@@ -147,14 +147,52 @@ class GeometricAttention(nn.Module):
         """x [B,S,H]; mask [B,S,S] (0 = masked) or None (dense); see geometric_attention.py:518-598."""
         B, S, H = x.shape
         if geometric_bias is not None:
-            raise NotImplementedError("geometric_bias (post-softmax re-normalisation, geometric_attention.py:567-575) "
-                                      "is not implemented on the HIP path yet")
+            return self._forward_dense_bias(x, attention_mask, geometric_bias)
         if attention_mask is None or attention_mask.shape[-2:] != (S, S):
             mask = torch.ones(B, S, S, device=x.device)       # mismatched masks -> full attention (:482-498)
         else:
             mask = attention_mask.expand(B, S, S) if attention_mask.dim() == 3 else attention_mask
         graph = graph_from_dense_mask(mask)
         return self.forward_graph(x.reshape(B * S, H), graph).view(B, S, H)
+
+    def _forward_dense_bias(self, x, attention_mask, geometric_bias):
+        """geometric_bias path (geometric_attention.py:564-575): the bias is added to the POST-softmax
+        weights of every (i, j) pair and re-normalised over all j, so attention becomes dense.
+        Never reached from TAGAN (graph_attention.py passes None); runs as dense device tensor ops."""
+        B, S, H = x.shape
+        h, d = self.num_heads, self.head_dim
+        identity = x
+        hx = layer_norm(x, self.layer_norm1) if self.use_layer_norm else x
+        qkv = fused_qkv(hx, self.q_linear, self.k_linear, self.v_linear)
+        q, k, v = (t.reshape(B, S, h, d).transpose(1, 2) for t in qkv.split(H, dim=-1))
+        if self.distance_metric == "scaled_dot_product":
+            scores = torch.matmul(q, k.transpose(-2, -1)) / math.sqrt(d)
+        else:
+            prm = self._metric_param()
+            per_head = []
+            for hh in range(h):
+                fn = self.distance_fn
+                if prm is not None:
+                    fn = (lambda a, b, s=prm[hh]: DistanceMetric.gaussian_kernel(a, b, s)) \
+                        if self.distance_metric == "gaussian_kernel" else \
+                        (lambda a, b, g=prm[hh]: DistanceMetric.rbf_kernel(a, b, g))
+                sc = fn(q[:, hh, :, None, :], k[:, hh, None, :, :])
+                if self.distance_metric in ("euclidean", "squared_euclidean", "manhattan", "cosine_distance"):
+                    sc = -sc
+                per_head.append(sc)
+            scores = torch.stack(per_head, 1)
+        if attention_mask is not None:
+            em = attention_mask.unsqueeze(1) if attention_mask.shape[-2:] == scores.shape[-2:] else \
+                torch.ones(B, 1, S, S, device=x.device)
+            scores = scores.masked_fill(em == 0, float("-inf"))
+        w = self.attn_dropout(torch.softmax(scores, dim=-1))
+        w = self.attn_dropout(torch.softmax(w + geometric_bias.unsqueeze(1), dim=-1))
+        ctx = torch.matmul(w, v).transpose(1, 2).reshape(B, S, H)
+        proj = linear(ctx, self.output_proj.weight, self.output_proj.bias)
+        p_out = self.output_dropout.p if self.training else 0.0
+        if self.use_layer_norm:
+            return dropout_add_layer_norm(proj, identity, self.layer_norm2, p_out)
+        return F.dropout(proj, p_out, True) + identity
 
     def extra_repr(self) -> str:
         return (f"hidden_dim={self.hidden_dim}, num_heads={self.num_heads}, "

@@ -88,14 +88,15 @@ def test_graph_attention_golden(dev, case):
         G.assert_close("grad " + name, params[name].grad, g, GRAD_ATOL, GRAD_RTOL)
 
 
-@pytest.mark.parametrize("case", [c for c in G.case_names("geo_") if "bias" not in c])
+@pytest.mark.parametrize("case", G.case_names("geo_"))
 def test_geometric_attention_golden(dev, case):
     from tagan_amd.layers import GeometricAttention
     meta, t = G.load(case)
     mod = _load(GeometricAttention(meta["H"], meta["heads"], 0.0, meta["metric"], True), G.state_dict(t), dev)
     x = t["in.x"].to(dev).requires_grad_(True)
     mask = t.get("in.mask")
-    out = mod(x, mask.to(dev) if mask is not None else None)
+    bias = t.get("in.bias")
+    out = mod(x, mask.to(dev) if mask is not None else None, bias.to(dev) if bias is not None else None)
     G.assert_close("out", out, t["out"], OUT_ATOL, OUT_RTOL)
     (out * t["in.grad_out"].to(dev)).sum().backward()
     G.assert_close("grad x", x.grad, t["grad.x"], GRAD_ATOL, GRAD_RTOL)

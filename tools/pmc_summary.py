@@ -7,6 +7,7 @@ coalesced read, i.e. half the bytes -> doubled; WRITE_SIZE is exact for 16-B/lan
 import csv
 import glob
 import json
+import re
 import sys
 from collections import defaultdict
 
@@ -20,8 +21,9 @@ def load(pattern, counter):
             if r.get("Counter_Name") != counter:
                 continue
             name = r["Kernel_Name"]
-            if any(g in name for g in GEO):
-                per_kernel[name.split("(")[0].split("<")[0].split("::")[-1]].append(float(r["Counter_Value"]))
+            m = re.search(r"(k_geo_[a-z_]+)", name)
+            if m:
+                per_kernel[m.group(1)].append(float(r["Counter_Value"]))
     return per_kernel
 
 
@@ -29,10 +31,12 @@ def main():
     fetch_dir, write_dir, config, out = sys.argv[1:5]
     f = load(fetch_dir + "/**/*counter_collection.csv", "FETCH_SIZE")
     w = load(write_dir + "/**/*counter_collection.csv", "WRITE_SIZE")
-    # one launch group = one fwd + one bwd = each kernel once; use the median dispatch of each kernel
+    # one launch group = one fwd + one bwd: fwd_chunk, fwd_merge, bwd_row_chunk, bwd_col_chunk once each and
+    # k_geo_sum_parts twice (row and column merges); median dispatch of each kernel
     med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
-    fetch = {k: 2 * 1024 * med(v) for k, v in f.items()}
-    write = {k: 1024 * med(v) for k, v in w.items()}
+    times = {"k_geo_sum_parts": 2}
+    fetch = {k: 2 * 1024 * med(v) * times.get(k, 1) for k, v in f.items()}
+    write = {k: 1024 * med(v) * times.get(k, 1) for k, v in w.items()}
     total = sum(fetch.values()) + sum(write.values())
     rec = {"config": config, "hbm_bytes_per_launch_group": int(total),
            "fetch_bytes_corrected": {k: int(v) for k, v in fetch.items()},
