@@ -15,8 +15,8 @@
  *     thread-local message for the last failure on the calling thread.
  *   - Device arrays are row-major.  "ld" arguments are row strides in elements.
  *   - dtype: TAGAN_F32 (fp32 storage, fp32 math).  Other values -> TAGAN_ERR_UNSUPPORTED.
- *   - Dropout masks are counter-based: keep(u) with u = tagan_uniform(seed, index),
- *     index layouts documented per kernel, so tests can regenerate them.
+ *   - Dropout masks are counter-based: keep(u) with u = tagan_uniform(seed, stream, counter)
+ *     (stream/counter layouts documented per kernel), so tests can regenerate them.
  */
 #ifndef TAGAN_HIP_H
 #define TAGAN_HIP_H
@@ -57,8 +57,9 @@ const char* tagan_last_error(void);
 int tagan_version(void);
 int tagan_device_arch(char* buf, int len);   /* e.g. "gfx950"; needs a device */
 
-/* Counter-based uniform in [0,1) used by every dropout mask (splitmix64 finaliser). */
-float tagan_uniform(uint64_t seed, uint64_t index);
+/* Counter-based uniform in [0,1) used by every dropout mask: a 32-bit key mixed from
+ * (seed, stream) by four lowbias32 rounds, then u = lowbias32(counter ^ key) >> 8 / 2^24. */
+float tagan_uniform(uint64_t seed, uint64_t stream, uint32_t counter);
 
 /* ---------------------------------------------------------------------------
  * Snapshot CSR builder.  Replaces graph_attention.py:96-105
@@ -139,7 +140,7 @@ typedef struct tagan_graph {
  *          fused [n,3H] buffer).  out: [n_nodes, H] (ld = H).
  *   lse:   [n_nodes, heads] log-sum-exp of the row's scores (saved for bwd).
  *   edge_alpha (optional): [nnz, heads] post-dropout attention weights.
- * Dropout index layout: edge e (CSR position), head h -> index e*heads + h.
+ * Dropout layout: stream = head h, counter = edge e (CSR position).
  * A row with no entries yields NaN (softmax over all -inf, as the reference).
  * ------------------------------------------------------------------------- */
 size_t tagan_geo_attn_fwd_workspace(const tagan_graph* g, int32_t heads, int32_t head_dim);
@@ -174,7 +175,7 @@ int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t head
  *        mask[r*mask_bstride + h*mask_hstride + i*T + j]; causal != 0 adds j<=i.
  *   out: element (r,t,f) at out[r*o_row + t*o_t + f];  lse: [rows, heads, T].
  *   attn (optional): [rows, heads, T, T] post-dropout weights.
- * Dropout index layout: ((r*heads + h)*T + i)*T + j.
+ * Dropout layout: stream = r*heads + h, counter = i*T + j.
  * ------------------------------------------------------------------------- */
 int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim,
                             const void* q, const void* k, const void* v, int64_t s_row, int64_t s_t,
@@ -203,7 +204,7 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
  * Row LayerNorm with fused residual + dropout.  Replaces the ATen chain
  * output_dropout(proj) + identity -> layer_norm2 (geometric_attention.py:586-596,
  * temporal_attention.py:1190-1200) and plain layer_norm1 (b = NULL, p_drop = 0).
- *   s = dropout(a; p_drop, seed) + b     (index of element (r,c) = r*H + c)
+ *   s = dropout(a; p_drop, seed) + b     (element (r,c): stream r, counter c)
  *   y = (s - mean) / sqrt(var + eps) * gamma + beta       (biased var, as torch)
  * s_out (optional) keeps s for the backward pass; mean/rstd: [M].
  * Supported H: tagan_layernorm_supported(H) (32, 64, 128, 256, 512).

@@ -11,7 +11,7 @@ import re
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtagan_hip.so")
+LIB_PATH = os.environ.get("TAGAN_LIB") or os.path.join(_HERE, "libtagan_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tagan_hip.h")
 
 TAGAN_F32 = 0
@@ -29,7 +29,7 @@ _SIGNATURES = {
     "tagan_last_error": (_c.c_char_p, []),
     "tagan_version": (_c.c_int, []),
     "tagan_device_arch": (_c.c_int, [_c.c_char_p, _c.c_int]),
-    "tagan_uniform": (_f32, [_u64, _u64]),
+    "tagan_uniform": (_f32, [_u64, _u64, _c.c_uint32]),
     "tagan_csr_build_workspace": (_sz, [_i64, _i64]),
     "tagan_csr_build": (_c.c_int, [_p, _i64, _i64, _p, _p, _i32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
     "tagan_chunk_capacity": (_i64, [_i64, _i64, _i32]),

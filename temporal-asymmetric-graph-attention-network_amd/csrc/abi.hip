@@ -30,6 +30,8 @@ int tagan_device_arch(char* buf, int len) {
     return TAGAN_OK;
 }
 
-float tagan_uniform(uint64_t seed, uint64_t index) { return tagan::uniform01(seed, index); }
+float tagan_uniform(uint64_t seed, uint64_t stream, uint32_t counter) {
+    return tagan::drop_u(tagan::drop_key(seed, stream), counter);
+}
 
 }  // extern "C"

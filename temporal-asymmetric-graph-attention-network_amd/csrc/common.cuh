@@ -46,13 +46,29 @@ static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; 
 // ---------------------------------------------------------------- device helpers
 constexpr int WAVE = 64;
 
-// splitmix64 finaliser: counter-based uniform in [0,1) shared by every dropout mask.
-__host__ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t index) {
-    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (index + 1ull);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+// Dropout masks: counter-based, two-level.  A 32-bit key per (seed, stream) is mixed once
+// (per lane / per row, amortised), then each element costs one lowbias32 round
+// (2 integer multiplies) on (counter ^ key).  Streams / counters per kernel are
+// documented in include/tagan_hip.h.  lowbias32: C. Wellons' 2-multiply integer hash.
+__host__ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__host__ __device__ __forceinline__ uint32_t drop_key(uint64_t seed, uint64_t stream) {
+    uint32_t k = lowbias32((uint32_t)seed ^ 0x9E3779B9u);
+    k = lowbias32(k ^ (uint32_t)(seed >> 32));
+    k = lowbias32(k ^ (uint32_t)stream);
+    return lowbias32(k ^ (uint32_t)(stream >> 32));
+}
+
+// uniform in [0,1) with 24-bit resolution
+__host__ __device__ __forceinline__ float drop_u(uint32_t key, uint32_t counter) {
+    return (float)(lowbias32(counter ^ key) >> 8) * (1.0f / 16777216.0f);
 }
 
 // XOR-butterfly sum over aligned groups of G lanes (G power of two <= 64).
@@ -72,6 +88,50 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nblk) {
     const int64_t q = nblk / 8, r = nblk % 8;
     const int64_t x = bid % 8, k = bid / 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
+// Deterministic column sums of a [nblk, n] partials table (per-block dγ/dβ, bias-table
+// grads): one 1024-thread block per 64 columns, wave w sums rows w, w+16, ... with four
+// independent accumulators (loads in flight), then a fixed-order LDS tree.  Column x < split
+// goes to out0[x], the rest to out1[x - split] (either may be null).
+constexpr int COLSUM_BLK = 1024;
+namespace {
+__global__ void __launch_bounds__(COLSUM_BLK) k_colsum_parts(const float* __restrict__ part, int nblk, int n,
+                                                            float* __restrict__ out0, float* __restrict__ out1,
+                                                            int split) {
+    constexpr int NW = COLSUM_BLK / WAVE;
+    __shared__ float red[NW][WAVE];
+    const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x >> 6;
+    const int x = blockIdx.x * WAVE + lane;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    if (x < n) {
+        int b = w;
+        for (; b + 3 * NW < nblk; b += 4 * NW) {
+            s0 += part[(int64_t)b * n + x];
+            s1 += part[(int64_t)(b + NW) * n + x];
+            s2 += part[(int64_t)(b + 2 * NW) * n + x];
+            s3 += part[(int64_t)(b + 3 * NW) * n + x];
+        }
+        for (; b < nblk; b += NW) s0 += part[(int64_t)b * n + x];
+    }
+    red[w][lane] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+#pragma unroll
+    for (int half = NW / 2; half > 0; half >>= 1) {
+        if (w < half) red[w][lane] += red[w + half][lane];
+        __syncthreads();
+    }
+    if (w == 0 && x < n) {
+        if (x < split) { if (out0) out0[x] = red[0][lane]; }
+        else if (out1) out1[x - split] = red[0][lane];
+    }
+}
+
+}  // namespace
+
+static inline void launch_colsum(const float* part, int nblk, int n, float* out0, float* out1, int split,
+                                 hipStream_t s) {
+    k_colsum_parts<<<(n + WAVE - 1) / WAVE, COLSUM_BLK, 0, s>>>(part, nblk, n, out0, out1, split);
 }
 
 }  // namespace tagan

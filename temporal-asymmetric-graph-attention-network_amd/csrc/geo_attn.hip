@@ -27,7 +27,6 @@ namespace tagan {
 namespace {
 
 constexpr int BLK = 256;
-constexpr int ROWS_PER_BLK = BLK / WAVE;
 
 enum Family { FAM_DOT, FAM_SQ, FAM_ABS, FAM_COS };
 
@@ -41,8 +40,20 @@ struct MetricTraits {
                                    : FAM_SQ;
 };
 
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over aligned groups of lph lanes (lph = d/4, wave-uniform).  DPP quad_perm xor1 / xor2,
+// row_half_mirror, row_mirror instead of ds_bpermute shuffles: every lane of a group ends with
+// the same value, bitwise equal to the xor-butterfly (each step adds two equal partial sums).
 __device__ __forceinline__ float grp_sum(float x, int lph) {
-    for (int o = 1; o < lph; o <<= 1) x += __shfl_xor(x, o, 64);
+    if (lph > 1) x += dpp<0xB1>(x);
+    if (lph > 2) x += dpp<0x4E>(x);
+    if (lph > 4) x += dpp<0x141>(x);
+    if (lph > 8) x += dpp<0x140>(x);
+    for (int o = 16; o < lph; o <<= 1) x += __shfl_xor(x, o, 64);
     return x;
 }
 
@@ -73,7 +84,7 @@ template <int METRIC>
 __device__ __forceinline__ float finalize(float a, float b, float qq, float inv_sqrt_d, float prm) {
     if constexpr (METRIC == TAGAN_METRIC_SCALED_DOT_PRODUCT) return a * inv_sqrt_d;
     if constexpr (METRIC == TAGAN_METRIC_DOT_PRODUCT) return a;
-    if constexpr (METRIC == TAGAN_METRIC_EUCLIDEAN) return -sqrtf(a + 1e-8f);
+    if constexpr (METRIC == TAGAN_METRIC_EUCLIDEAN) return -__builtin_amdgcn_sqrtf(a + 1e-8f);   // v_sqrt_f32 (1 ulp)
     if constexpr (METRIC == TAGAN_METRIC_SQUARED_EUCLIDEAN) return -a;
     if constexpr (METRIC == TAGAN_METRIC_MANHATTAN) return -a;
     if constexpr (METRIC == TAGAN_METRIC_GAUSSIAN_KERNEL) return __expf(-a / (2.f * prm * prm));
@@ -106,7 +117,7 @@ __device__ __forceinline__ Grad score_grad(float a, float b, float qq, float s, 
         g.ck_q = 1.f;
     } else if constexpr (MetricTraits<METRIC>::fam == FAM_SQ) {
         float c;  // ∂s/∂(q-k) = c·(q-k)
-        if constexpr (METRIC == TAGAN_METRIC_EUCLIDEAN) c = 1.f / s;           // s = -r  ->  -(q-k)/r
+        if constexpr (METRIC == TAGAN_METRIC_EUCLIDEAN) c = __builtin_amdgcn_rcpf(s);   // s = -r  ->  -(q-k)/r
         else if constexpr (METRIC == TAGAN_METRIC_SQUARED_EUCLIDEAN) c = -2.f;
         else if constexpr (METRIC == TAGAN_METRIC_GAUSSIAN_KERNEL) {
             c = -s / (prm * prm);
@@ -190,7 +201,10 @@ struct GeoArgs {
     float inv_sqrt_d;
 };
 
-constexpr int UNROLL = 4;
+#ifndef TAGAN_GEO_UNROLL
+#define TAGAN_GEO_UNROLL 2
+#endif
+constexpr int UNROLL = TAGAN_GEO_UNROLL;
 
 __device__ __forceinline__ float sgnf(float x) { return (x > 0.f) ? 1.f : (x < 0.f ? -1.f : 0.f); }
 
@@ -236,6 +250,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
     if (!__any(valid)) return;
     const int f0 = L.sl * 4;
     const int h = f0 / A.d;
+    const uint32_t dkey = drop_key(A.seed, (uint64_t)h);
     const float4 qv = ld4(A.q + (int64_t)row * A.ld + f0);
     float qq = 0.f;
     if constexpr (MetricTraits<METRIC>::fam == FAM_COS)
@@ -270,8 +285,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
             l = fmaf(l, corr, p);
             float pw = p;
             if (A.p_drop > 0.f) {
-                const uint64_t idx = (uint64_t)(e0 + jj + u) * (uint64_t)A.heads + (uint64_t)h;
-                pw = (uniform01(A.seed, idx) >= A.p_drop) ? p * A.inv_keep : 0.f;
+                pw = (drop_u(dkey, (uint32_t)(e0 + jj + u)) >= A.p_drop) ? p * A.inv_keep : 0.f;
             }
             acc.x = fmaf(acc.x, corr, pw * vv[u].x);
             acc.y = fmaf(acc.y, corr, pw * vv[u].y);
@@ -343,6 +357,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
     }
     const int f0 = L.sl * 4;
     const int h = f0 / A.d;
+    const uint32_t dkey = drop_key(A.seed, (uint64_t)h);
     float prm_acc = 0.f;
     if (__any(valid)) {
         const float4 qv = ld4(A.q + (int64_t)row * A.ld + f0);
@@ -378,8 +393,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
                 const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
                 const float p = __expf(s - lse);
                 if (A.p_drop > 0.f) {
-                    const uint64_t idx = (uint64_t)(e0 + jj + u) * (uint64_t)A.heads + (uint64_t)h;
-                    dp = (uniform01(A.seed, idx) >= A.p_drop) ? dp * A.inv_keep : 0.f;
+                    dp = (drop_u(dkey, (uint32_t)(e0 + jj + u)) >= A.p_drop) ? dp * A.inv_keep : 0.f;
                 }
                 const float ds = p * (dp - D);
                 const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
@@ -453,6 +467,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
     if (!__any(valid)) return;
     const int f0 = L.sl * 4;
     const int h = f0 / A.d;
+    const uint32_t dkey = drop_key(A.seed, (uint64_t)h);
     const float4 kv = ld4(A.k + (int64_t)colj * A.ld + f0);
     const float4 vv = ld4(A.v + (int64_t)colj * A.ld + f0);
     const float prm = A.mparam ? A.mparam[h] : 1.f;
@@ -495,7 +510,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
             const float p = __expf(s - lse[u]);
             float pw = p;
             if (A.p_drop > 0.f) {
-                const bool keep = uniform01(A.seed, (uint64_t)eid[u] * (uint64_t)A.heads + (uint64_t)h) >= A.p_drop;
+                const bool keep = drop_u(dkey, (uint32_t)eid[u]) >= A.p_drop;
                 dp = keep ? dp * A.inv_keep : 0.f;
                 pw = keep ? p * A.inv_keep : 0.f;
             }
@@ -566,7 +581,7 @@ __global__ void __launch_bounds__(BLK) k_geo_alpha(GeoArgs A, float* __restrict_
         }
         float p = __expf(finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm) - lse);
         if (A.p_drop > 0.f)
-            p = (uniform01(A.seed, (uint64_t)e * A.heads + h) >= A.p_drop) ? p * A.inv_keep : 0.f;
+            p = (drop_u(drop_key(A.seed, (uint64_t)h), (uint32_t)e) >= A.p_drop) ? p * A.inv_keep : 0.f;
         alpha[(int64_t)e * A.heads + h] = p;
     }
 }
@@ -601,7 +616,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_generic(GeoArgs A) {
         l = fmaf(l, corr, p);
         float pw = p;
         if (A.p_drop > 0.f)
-            pw = (uniform01(A.seed, (uint64_t)e * A.heads + h) >= A.p_drop) ? p * A.inv_keep : 0.f;
+            pw = (drop_u(drop_key(A.seed, (uint64_t)h), (uint32_t)e) >= A.p_drop) ? p * A.inv_keep : 0.f;
         for (int c = 0; c < d; ++c) orow[c] = fmaf(orow[c], corr, pw * vr[c]);
         m = mn;
     }
@@ -644,7 +659,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_generic(GeoArgs A) {
         const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
         const float p = __expf(s - lse);
         if (A.p_drop > 0.f)
-            dp = (uniform01(A.seed, (uint64_t)e * A.heads + h) >= A.p_drop) ? dp * A.inv_keep : 0.f;
+            dp = (drop_u(drop_key(A.seed, (uint64_t)h), (uint32_t)e) >= A.p_drop) ? dp * A.inv_keep : 0.f;
         const float ds = p * (dp - D);
         const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
         for (int c = 0; c < d; ++c) {
@@ -689,7 +704,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_generic(GeoArgs A) {
         const float p = __expf(s - A.lse_in[i * A.heads + h]);
         float pw = p;
         if (A.p_drop > 0.f) {
-            const bool keep = uniform01(A.seed, (uint64_t)eid * A.heads + h) >= A.p_drop;
+            const bool keep = drop_u(drop_key(A.seed, (uint64_t)h), (uint32_t)eid) >= A.p_drop;
             dp = keep ? dp * A.inv_keep : 0.f;
             pw = keep ? p * A.inv_keep : 0.f;
         }

@@ -46,12 +46,14 @@ struct LnArgs {
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
-__device__ __forceinline__ float4 drop4(const LnArgs& A, float4 v, int64_t base) {
+// dropout stream = row, counter = column
+__device__ __forceinline__ float4 drop4(const LnArgs& A, float4 v, int64_t row, int c) {
     if (A.p_drop <= 0.f) return v;
-    v.x = uniform01(A.seed, base + 0) >= A.p_drop ? v.x * A.inv_keep : 0.f;
-    v.y = uniform01(A.seed, base + 1) >= A.p_drop ? v.y * A.inv_keep : 0.f;
-    v.z = uniform01(A.seed, base + 2) >= A.p_drop ? v.z * A.inv_keep : 0.f;
-    v.w = uniform01(A.seed, base + 3) >= A.p_drop ? v.w * A.inv_keep : 0.f;
+    const uint32_t key = drop_key(A.seed, (uint64_t)row);
+    v.x = drop_u(key, (uint32_t)c + 0) >= A.p_drop ? v.x * A.inv_keep : 0.f;
+    v.y = drop_u(key, (uint32_t)c + 1) >= A.p_drop ? v.y * A.inv_keep : 0.f;
+    v.z = drop_u(key, (uint32_t)c + 2) >= A.p_drop ? v.z * A.inv_keep : 0.f;
+    v.w = drop_u(key, (uint32_t)c + 3) >= A.p_drop ? v.w * A.inv_keep : 0.f;
     return v;
 }
 
@@ -70,7 +72,7 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
         const int c = (n * LPR + sl) * 4;
         const int64_t off = row * H + c;
         float4 x = ld4(A.a + off);
-        x = drop4(A, x, off);
+        x = drop4(A, x, row, c);
         if (A.b) {
             const float4 r = ld4(A.b + off);
             x.x += r.x; x.y += r.y; x.z += r.z; x.w += r.w;
@@ -150,7 +152,7 @@ __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
             o.z = rstd * (gd[n].z - c1 * xh[n].z - c2);
             o.w = rstd * (gd[n].w - c1 * xh[n].w - c2);
             if (A.ds) st4(A.ds + row * H + c, o);
-            if (A.da) st4(A.da + row * H + c, drop4(A, o, row * H + c));
+            if (A.da) st4(A.da + row * H + c, drop4(A, o, row, c));
         }
     }
     if (A.part) {
@@ -167,23 +169,6 @@ __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
                 for (int ss = 0; ss < RPW; ++ss) s += red[ww][ss][x];
             A.part[(int64_t)blockIdx.x * 2 * H + x] = s;
         }
-    }
-}
-
-__global__ void __launch_bounds__(BLK) k_ln_sum_parts(const float* __restrict__ part, int nblk, int n,
-                                                      float* __restrict__ dgamma, float* __restrict__ dbeta, int H) {
-    __shared__ float red[BLK / WAVE][WAVE];
-    const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x >> 6;
-    const int x = blockIdx.x * WAVE + lane;
-    float s = 0.f;
-    if (x < n)
-        for (int b = w; b < nblk; b += BLK / WAVE) s += part[(int64_t)b * n + x];
-    red[w][lane] = s;
-    __syncthreads();
-    if (w == 0 && x < n) {
-        const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-        if (x < H) { if (dgamma) dgamma[x] = t; }
-        else if (dbeta) dbeta[x - H] = t;
     }
 }
 
@@ -267,7 +252,7 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, cons
     TAGAN_CHECK_LAUNCH("layernorm_bwd");
     if (want) {
         const int n = 2 * H;
-        k_ln_sum_parts<<<(n + WAVE - 1) / WAVE, BLK, 0, s>>>(A.part, nblk, n, dgamma, dbeta, H);
+        launch_colsum(A.part, nblk, n, dgamma, dbeta, H, s);
         TAGAN_CHECK_LAUNCH("layernorm_bwd_sum");
     }
     return TAGAN_OK;

@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(BLK) k_fold(tagan_membank B, const int64_t* __
             const float p = row[c];                                        // NaN row: recover from memory
             v = reapp ? add_rn(mul_rn(w, p), mul_rn(w1, p)) : p;
         } else {
-            v = uniform01(seed, (uint64_t)s * B.H + c) * 0.01f;            // NaN on a new node: rand * 0.01
+            v = drop_u(drop_key(seed, (uint64_t)s), (uint32_t)c) * 0.01f;           // NaN on a new node: rand * 0.01
         }
         row[c] = v;
     }

@@ -70,10 +70,14 @@ __device__ __forceinline__ float bias_ij(const TArgs& A, int64_t r, int h, int i
     return b;
 }
 
-__device__ __forceinline__ float drop_scale(const TArgs& A, int64_t r, int h, int i, int j) {
+__device__ __forceinline__ uint32_t tkey(const TArgs& A, int64_t r, int h) {
+    return A.p_drop > 0.f ? drop_key(A.seed, (uint64_t)r * A.heads + h) : 0u;
+}
+
+// dropout stream = r*heads + h, counter = i*T + j
+__device__ __forceinline__ float drop_scale(const TArgs& A, uint32_t key, int i, int j) {
     if (A.p_drop <= 0.f) return 1.f;
-    const uint64_t idx = (((uint64_t)r * A.heads + h) * A.T + i) * (uint64_t)A.T + j;
-    return uniform01(A.seed, idx) >= A.p_drop ? A.inv_keep : 0.f;
+    return drop_u(key, (uint32_t)(i * A.T + j)) >= A.p_drop ? A.inv_keep : 0.f;
 }
 
 template <int D>
@@ -90,6 +94,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_fwd(TArgs A, const float* __restr
     const int T = A.T, d = A.d;
     for (int64_t r = blockIdx.x; r < A.rows; r += gridDim.x) {
         for (int h = wid; h < A.heads; h += NW) {
+            const uint32_t drk = tkey(A, r, h);
             const float* kb = k + r * A.s_row + h * d;
             const float* vb = v + r * A.s_row + h * d;
             for (int i0 = 0; i0 < T; i0 += WAVE) {
@@ -114,7 +119,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_fwd(TArgs A, const float* __restr
                     const float corr = __expf(m - mn);
                     const float p = __expf(s - mn);
                     l = fmaf(l, corr, p);
-                    const float pw = p * drop_scale(A, r, h, ii, j);
+                    const float pw = p * drop_scale(A, drk, ii, j);
 #pragma unroll
                     for (int c = 0; c < D; ++c)
                         if (c < d) acc[c] = fmaf(acc[c], corr, pw * vr[c]);
@@ -139,7 +144,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_fwd(TArgs A, const float* __restr
                             float a = 0.f;
                             if (keep_ij(A, r, h, i, j)) {
                                 s = fmaf(s, A.inv_sqrt_d, bias_ij(A, r, h, i, j));
-                                a = __expf(s - ls) * drop_scale(A, r, h, i, j);
+                                a = __expf(s - ls) * drop_scale(A, drk, i, j);
                             }
                             ar[j] = (l > 0.f) ? a : NAN;
                         }
@@ -166,6 +171,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd(TArgs A, const float* __restr
     __syncthreads();
     for (int64_t r = blockIdx.x; r < A.rows; r += gridDim.x) {
         for (int h = wid; h < A.heads; h += NW) {
+            const uint32_t drk = tkey(A, r, h);
             const float* qb = q + r * A.s_row + h * d;
             const float* kb = k + r * A.s_row + h * d;
             const float* vb = v + r * A.s_row + h * d;
@@ -201,7 +207,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd(TArgs A, const float* __restr
                     if (keep_ij(A, r, h, ii, j)) {
                         s = fmaf(s, A.inv_sqrt_d, bias_ij(A, r, h, ii, j));
                         const float p = __expf(s - li);
-                        ds = p * (dp * drop_scale(A, r, h, ii, j) - Di);
+                        ds = p * (dp * drop_scale(A, drk, ii, j) - Di);
                     }
 #pragma unroll
                     for (int c = 0; c < D; ++c)
@@ -246,7 +252,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd(TArgs A, const float* __restr
                     if (keep_ij(A, r, h, i, jj)) {
                         s = fmaf(s, A.inv_sqrt_d, bias_ij(A, r, h, i, jj));
                         const float p = __expf(s - lsb[i]);
-                        const float sc = drop_scale(A, r, h, i, jj);
+                        const float sc = drop_scale(A, drk, i, jj);
                         pw = p * sc;
                         ds = p * (dp * sc - delta[i]);
                     }
@@ -277,21 +283,6 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd(TArgs A, const float* __restr
     }
 }
 
-// Sum block partials [nblk][n] over blocks: one workgroup per 64 outputs, the
-// 4 waves split the blocks in fixed strides, then a fixed-order LDS combine —
-// deterministic and fully parallel.
-__global__ void __launch_bounds__(BLK) k_sum_parts(const float* __restrict__ part, int nblk, int n,
-                                                   float* __restrict__ out) {
-    __shared__ float red[NW][WAVE];
-    const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x >> 6;
-    const int x = blockIdx.x * WAVE + lane;
-    float s = 0.f;
-    if (x < n)
-        for (int b = w; b < nblk; b += NW) s += part[(int64_t)b * n + x];
-    red[w][lane] = s;
-    __syncthreads();
-    if (w == 0 && x < n) out[x] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-}
 
 // =================================================================== v2: LDS-staged fast path
 // One workgroup per node row; the row's Q/K/V (and dO) of a group of G heads are
@@ -361,6 +352,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_fwd_v2(TArgs A, const float* __re
             __syncthreads();
             for (int it = threadIdx.x; it < gc * T; it += BLK) {
                 const int hl = it / T, i = it - hl * T, h = h0 + hl;
+                const uint32_t drk = tkey(A, r, h);
                 const float* qi = Qs + (hl * T + i) * D;
                 const float* kb = Ks + hl * T * D;
                 const float* vb = Vs + hl * T * D;
@@ -378,7 +370,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_fwd_v2(TArgs A, const float* __re
                     const float corr = __expf(m - mn);
                     const float p = __expf(s - mn);
                     l = fmaf(l, corr, p);
-                    const float pw = p * drop_scale(A, r, h, i, j);
+                    const float pw = p * drop_scale(A, drk, i, j);
                     const float* vj = vb + j * D;
 #pragma unroll
                     for (int c = 0; c < D; c += 4) {
@@ -406,7 +398,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_fwd_v2(TArgs A, const float* __re
                             float bias = bb[-j];
                             if (A.bias_dense) bias += A.bias_dense[r * A.bias_bstride + (((int64_t)h * T + i) * T + j)];
                             const float s = fmaf(dotD<D>(qi, kb + j * D), A.inv_sqrt_d, bias);
-                            a = __expf(s - ls) * drop_scale(A, r, h, i, j);
+                            a = __expf(s - ls) * drop_scale(A, drk, i, j);
                         }
                         ar[j] = (l > 0.f) ? a : NAN;
                     }
@@ -447,6 +439,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd_v2(TArgs A, const float* __re
             // ---- phase A: (head, i): delta_i, dq_i, optional per-pair ds
             for (int it = threadIdx.x; it < gc * T; it += BLK) {
                 const int hl = it / T, i = it - hl * T, h = h0 + hl;
+                const uint32_t drk = tkey(A, r, h);
                 const float* qi = Qs + (hl * T + i) * D;
                 const float* doi = Os + (hl * T + i) * D;
                 const float* kb = Ks + hl * T * D;
@@ -474,7 +467,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd_v2(TArgs A, const float* __re
                         if (A.bias_dense) bias += A.bias_dense[r * A.bias_bstride + (((int64_t)h * T + i) * T + j)];
                         const float s = fmaf(dotD<D>(qi, kb + j * D), A.inv_sqrt_d, bias);
                         const float p = __expf(s - li);
-                        ds = p * (dotD<D>(doi, vb + j * D) * drop_scale(A, r, h, i, j) - Di);
+                        ds = p * (dotD<D>(doi, vb + j * D) * drop_scale(A, drk, i, j) - Di);
                         const float* kj = kb + j * D;
 #pragma unroll
                         for (int c = 0; c < D; c += 4) {
@@ -497,6 +490,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd_v2(TArgs A, const float* __re
             // ---- phase B: (head, j): dk_j, dv_j
             for (int it = threadIdx.x; it < gc * T; it += BLK) {
                 const int hl = it / T, j = it - hl * T, h = h0 + hl;
+                const uint32_t drk = tkey(A, r, h);
                 const float* kj = Ks + (hl * T + j) * D;
                 const float* vj = Vs + (hl * T + j) * D;
                 const float* bb = Bs + hl * NB - j + T - 1;     // bb[i] = bias of (i, j)
@@ -514,7 +508,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd_v2(TArgs A, const float* __re
                     if (A.bias_dense) bias += A.bias_dense[r * A.bias_bstride + (((int64_t)h * T + i) * T + j)];
                     const float s = fmaf(dotD<D>(qi, kj), A.inv_sqrt_d, bias);
                     const float p = __expf(s - Ls[hl * T + i]);
-                    const float sc = drop_scale(A, r, h, i, j);
+                    const float sc = drop_scale(A, drk, i, j);
                     const float ds = p * (dotD<D>(doi, vj) * sc - Del[hl * T + i]);
                     const float pw = p * sc;
 #pragma unroll
@@ -543,6 +537,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd_v2(TArgs A, const float* __re
             if (A.part) {
                 for (int it = threadIdx.x; it < gc * NB; it += BLK) {
                     const int hl = it / NB, dl = it - hl * NB, h = h0 + hl;
+                    const uint32_t drk = tkey(A, r, h);
                     const int delta = dl - (T - 1);            // i - j
                     const float bias = Bs[hl * NB + dl];
                     float sum = 0.f;
@@ -555,7 +550,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd_v2(TArgs A, const float* __re
                         if (A.bias_dense) b += A.bias_dense[r * A.bias_bstride + (((int64_t)h * T + i) * T + j)];
                         const float s = fmaf(dotD<D>(qi, Ks + (hl * T + j) * D), A.inv_sqrt_d, b);
                         const float p = __expf(s - Ls[hl * T + i]);
-                        sum += p * (dotD<D>(doi, Vs + (hl * T + j) * D) * drop_scale(A, r, h, i, j) -
+                        sum += p * (dotD<D>(doi, Vs + (hl * T + j) * D) * drop_scale(A, drk, i, j) -
                                     Del[hl * T + i]);
                     }
                     Acc[h * NB + dl] += sum;
@@ -736,7 +731,7 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     TAGAN_CHECK_LAUNCH("temporal_attn_bwd");
     if (dbias_table) {
         const int n = heads * (2 * T - 1);
-        k_sum_parts<<<(n + WAVE - 1) / WAVE, BLK, 0, s>>>(A.part, nblk, n, dbias_table);
+        launch_colsum(A.part, nblk, n, dbias_table, nullptr, n, s);
         TAGAN_CHECK_LAUNCH("temporal_attn_bwd_sum");
     }
     return TAGAN_OK;

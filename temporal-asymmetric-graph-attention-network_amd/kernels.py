@@ -26,7 +26,7 @@ def new_seed() -> int:
 
 
 # ----------------------------------------------------------------------------- graph
-CHUNK = 128   # max CSR/CSC entries per work chunk (power-law hubs are split)
+CHUNK = 64   # max CSR/CSC entries per work chunk (power-law hubs are split)
 
 
 @dataclass

@@ -19,25 +19,49 @@ def test_library_loads_and_exports_header_symbols():
     assert L.tagan_version() >= 1
 
 
-def _splitmix_uniform(seed, idx):
-    """numpy restatement of tagan::uniform01 (common.cuh) used to regenerate dropout masks in tests."""
-    m = np.uint64(0xFFFFFFFFFFFFFFFF)
+def _lowbias32(x):
+    x = np.asarray(x, dtype=np.uint32)
     with np.errstate(over="ignore"):
-        z = (np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * (np.asarray(idx, dtype=np.uint64) + np.uint64(1))) & m
-        z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & m
-        z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & m
-        z = z ^ (z >> np.uint64(31))
-    return (z >> np.uint64(40)).astype(np.float64) / 16777216.0
+        x = x ^ (x >> np.uint32(16))
+        x = x * np.uint32(0x7FEB352D)
+        x = x ^ (x >> np.uint32(15))
+        x = x * np.uint32(0x846CA68B)
+        x = x ^ (x >> np.uint32(16))
+    return x
+
+
+def _drop_uniform(seed, stream, counter):
+    """numpy restatement of tagan::drop_u(drop_key(seed, stream), counter) (common.cuh), used to
+    regenerate dropout masks in tests; stream and counter broadcast against each other."""
+    seed = int(seed)
+    stream = np.asarray(stream, dtype=np.uint64)
+    k = _lowbias32(np.uint32(seed & 0xFFFFFFFF) ^ np.uint32(0x9E3779B9))
+    k = _lowbias32(k ^ np.uint32(seed >> 32))
+    k = _lowbias32(k ^ (stream & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+    k = _lowbias32(k ^ (stream >> np.uint64(32)).astype(np.uint32))
+    u = _lowbias32(np.asarray(counter, dtype=np.uint32) ^ k) >> np.uint32(8)
+    return u.astype(np.float64) / 16777216.0
 
 
 def test_uniform_matches_numpy_restatement():
     L = _lib.lib()
-    for seed in (0, 1, 123456789, 2 ** 62 - 1):
-        idx = np.array([0, 1, 2, 1000, 2 ** 40 + 3], dtype=np.uint64)
-        want = _splitmix_uniform(seed, idx)
-        got = np.array([L.tagan_uniform(seed, int(i)) for i in idx])
-        np.testing.assert_array_equal(got.astype(np.float32), want.astype(np.float32))
-        assert ((got >= 0) & (got < 1)).all()
+    for seed in (0, 1, 123456789, 2 ** 62 - 1, 2 ** 64 - 1):
+        for stream in (0, 7, 2 ** 33 + 5):
+            ctr = np.array([0, 1, 2, 1000, 2 ** 31 + 3, 2 ** 32 - 1], dtype=np.uint32)
+            want = _drop_uniform(seed, stream, ctr)
+            got = np.array([L.tagan_uniform(seed, stream, int(c)) for c in ctr])
+            np.testing.assert_array_equal(got.astype(np.float32), want.astype(np.float32))
+            assert ((got >= 0) & (got < 1)).all()
+
+
+def test_uniform_statistics():
+    """Keep-rate and independence of the mask bits across streams / counters (p = 0.1)."""
+    u = _drop_uniform(42, np.arange(64, dtype=np.uint64)[:, None], np.arange(20000, dtype=np.uint32)[None, :])
+    keep = u >= 0.1
+    assert abs(keep.mean() - 0.9) < 2e-3
+    assert abs(u.mean() - 0.5) < 2e-3
+    c = np.corrcoef(u[:8].reshape(8, -1))
+    assert np.abs(c - np.eye(8)).max() < 0.03
 
 
 def test_workspace_queries_are_host_only():

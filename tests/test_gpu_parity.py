@@ -291,7 +291,7 @@ def test_geo_kernel_dropout_matches_regenerated_mask(dev):
     import numpy as np
     from tagan_amd import _lib
     from tagan_amd.kernels import GeoAttnFn, build_graph
-    from test_abi import _splitmix_uniform
+    from test_abi import _drop_uniform
     n, H, heads, p, seed = 400, 64, 4, 0.3, 987654321
     ei = _hub_graph(n, 3)
     graph = build_graph([ei.to(dev)], [n], chunk=16)
@@ -303,7 +303,7 @@ def test_geo_kernel_dropout_matches_regenerated_mask(dev):
     (out * gout.to(dev)).sum().backward()
     rowptr, col = oracle.csr_from_edge_index(ei, n)
     E = col.numel()
-    u = _splitmix_uniform(seed, np.arange(E * heads, dtype=np.uint64)).reshape(E, heads)
+    u = _drop_uniform(seed, np.arange(heads, dtype=np.uint64)[None, :], np.arange(E, dtype=np.uint32)[:, None])
     keep = torch.from_numpy((u >= p).astype(np.float64)) / (1 - p)
     q64 = qkv.double().requires_grad_(True)
     d = H // heads
