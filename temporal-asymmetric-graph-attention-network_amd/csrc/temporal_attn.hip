@@ -564,6 +564,289 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd_v2(TArgs A, const float* __re
     }
 }
 
+// =================================================================== v3: one wave per (row, head group)
+// The fast path for T <= 64 and head_dim in {8,16,32,64} without attention-weight output.
+// A wave owns HPW = 64/LG heads of one node row (LG = lanes per head >= T; lane = step),
+// so its K/V (fwd) or K/V then Q/dO (bwd) live in a private LDS slice written and read by
+// the same wave — no workgroup barriers, 64-thread workgroups, many waves per CU to hide
+// the strided time-major loads.  Waves are persistent over units (row, head group); a
+// wave always keeps the same head group, so the backward's bias-table gradient is a
+// per-wave LDS table updated conflict-free (at a fixed query step i, the lanes j of a head
+// hit distinct diagonals i-j) in a fixed order — deterministic — and written once as a
+// partial row for the ordered column sum.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int D>
+__device__ __forceinline__ void ld_row(const float* __restrict__ p, float (&r)[D]) {
+#pragma unroll
+    for (int c = 0; c < D; c += 4) {
+        const float4 t = *(const float4*)(p + c);
+        r[c] = t.x; r[c + 1] = t.y; r[c + 2] = t.z; r[c + 3] = t.w;
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void st_row(float* __restrict__ p, const float (&r)[D], float scale) {
+#pragma unroll
+    for (int c = 0; c < D; c += 4)
+        *(float4*)(p + c) = make_float4(r[c] * scale, r[c + 1] * scale, r[c + 2] * scale, r[c + 3] * scale);
+}
+
+template <int D>
+__device__ __forceinline__ float dot_rl(const float (&a)[D], const float* __restrict__ b) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; c += 4) {
+        const float4 y = *(const float4*)(b + c);
+        s = fmaf(a[c], y.x, s);
+        s = fmaf(a[c + 1], y.y, s);
+        s = fmaf(a[c + 2], y.z, s);
+        s = fmaf(a[c + 3], y.w, s);
+    }
+    return s;
+}
+
+template <int D>
+__device__ __forceinline__ float dot_rr(const float (&a)[D], const float (&b)[D]) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) s = fmaf(a[c], b[c], s);
+    return s;
+}
+
+// axpy with an LDS row: acc = acc*corr + w*row
+template <int D>
+__device__ __forceinline__ void axpy_l(float (&acc)[D], float corr, float w, const float* __restrict__ row) {
+#pragma unroll
+    for (int c = 0; c < D; c += 4) {
+        const float4 y = *(const float4*)(row + c);
+        acc[c] = fmaf(acc[c], corr, w * y.x);
+        acc[c + 1] = fmaf(acc[c + 1], corr, w * y.y);
+        acc[c + 2] = fmaf(acc[c + 2], corr, w * y.z);
+        acc[c + 3] = fmaf(acc[c + 3], corr, w * y.w);
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void fma_l(float (&acc)[D], float w, const float* __restrict__ row) {
+#pragma unroll
+    for (int c = 0; c < D; c += 4) {
+        const float4 y = *(const float4*)(row + c);
+        acc[c] = fmaf(w, y.x, acc[c]);
+        acc[c + 1] = fmaf(w, y.y, acc[c + 1]);
+        acc[c + 2] = fmaf(w, y.z, acc[c + 2]);
+        acc[c + 3] = fmaf(w, y.w, acc[c + 3]);
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void to_lds(float* __restrict__ p, const float (&r)[D]) {
+#pragma unroll
+    for (int c = 0; c < D; c += 4) *(float4*)(p + c) = make_float4(r[c], r[c + 1], r[c + 2], r[c + 3]);
+}
+
+constexpr int V3_BLK = WAVE;
+
+size_t v3_fwd_lds(int T, int D, int HPW) { return (size_t)HPW * (2 * T * D + align_up(2 * T - 1, 4)) * 4; }
+size_t v3_bwd_lds(int T, int D, int HPW) {
+    return (size_t)HPW * (2 * T * D + 2 * T + 2 * align_up(2 * T - 1, 4)) * 4;
+}
+
+template <int D, int LG>
+__global__ void __launch_bounds__(V3_BLK) k_tattn_fwd_v3(TArgs A, const float* __restrict__ q,
+                                                         const float* __restrict__ k, const float* __restrict__ v,
+                                                         int n_hg) {
+    constexpr int HPW = WAVE / LG;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int T = A.T, NB = 2 * T - 1, NBp = (NB + 3) & ~3;
+    const int lane = threadIdx.x, hl = lane / LG, li = lane % LG;
+    float* Ks = sm;                  // [HPW][T][D]
+    float* Vs = Ks + HPW * T * D;    // [HPW][T][D]
+    float* Bs = Vs + HPW * T * D;    // [HPW][NBp]
+    const int64_t units = A.rows * n_hg;
+    const bool live = li < T;
+    const int i = live ? li : T - 1;
+    for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
+        const int64_t r = u / n_hg;
+        const int h0 = (int)(u - r * n_hg) * HPW, h = h0 + hl;
+        const bool hok = h < A.heads;
+        const int hc = hok ? h : A.heads - 1;
+        const int64_t base = r * A.s_row + (int64_t)i * A.s_t + hc * D;
+        float qv[D], kv[D], vv[D];
+        ld_row<D>(q + base, qv);
+        ld_row<D>(k + base, kv);
+        ld_row<D>(v + base, vv);
+        wave_sync();   // previous unit's LDS reads are done before the slice is rewritten
+        to_lds<D>(Ks + (hl * T + i) * D, kv);
+        to_lds<D>(Vs + (hl * T + i) * D, vv);
+        for (int x = li; x < NB; x += LG) Bs[hl * NBp + x] = A.bias_table ? A.bias_table[hc * NB + x] : 0.f;
+        wave_sync();
+        const uint32_t drk = tkey(A, r, hc);
+        const float* kb = Ks + hl * T * D;
+        const float* vb = Vs + hl * T * D;
+        const float* bb = Bs + hl * NBp + i + T - 1;   // bb[-j] = bias of (i, j)
+        float acc[D];
+#pragma unroll
+        for (int c = 0; c < D; ++c) acc[c] = 0.f;
+        float m = -INFINITY, l = 0.f;
+#pragma unroll 1
+        for (int j = 0; j < T; ++j) {
+            if (!keep_ij(A, r, hc, i, j)) continue;
+            float bias = bb[-j];
+            if (A.bias_dense) bias += A.bias_dense[r * A.bias_bstride + (((int64_t)hc * T + i) * T + j)];
+            const float s = fmaf(dot_rl<D>(qv, kb + j * D), A.inv_sqrt_d, bias);
+            const float mn = fmaxf(m, s);
+            const float corr = __expf(m - mn);
+            const float p = __expf(s - mn);
+            l = fmaf(l, corr, p);
+            axpy_l<D>(acc, corr, p * drop_scale(A, drk, i, j), vb + j * D);
+            m = mn;
+        }
+        if (live && hok) {
+            const float inv_l = (l > 0.f) ? 1.f / l : NAN;
+            st_row<D>(A.out + r * A.o_row + (int64_t)i * A.o_t + h * D, acc, inv_l);
+            A.lse[(r * A.heads + h) * T + i] = m + __logf(l);
+        }
+    }
+}
+
+template <int D, int LG>
+__global__ void __launch_bounds__(V3_BLK) k_tattn_bwd_v3(TArgs A, const float* __restrict__ q,
+                                                         const float* __restrict__ k, const float* __restrict__ v,
+                                                         const float* __restrict__ dout,
+                                                         const float* __restrict__ lse, int n_hg) {
+    constexpr int HPW = WAVE / LG;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int T = A.T, NB = 2 * T - 1, NBp = (NB + 3) & ~3;
+    const int lane = threadIdx.x, hl = lane / LG, li = lane % LG;
+    float* X1 = sm;                   // [HPW][T][D]  K in phase A, Q in phase B
+    float* X2 = X1 + HPW * T * D;     // [HPW][T][D]  V in phase A, dO in phase B
+    float* Ls = X2 + HPW * T * D;     // [HPW][T]
+    float* Dl = Ls + HPW * T;         // [HPW][T]
+    float* Bs = Dl + HPW * T;         // [HPW][NBp]
+    float* Acc = Bs + HPW * NBp;      // [HPW][NBp] bias-table gradient of this wave's head group
+    for (int x = lane; x < HPW * NBp; x += WAVE) Acc[x] = 0.f;
+    const int64_t units = A.rows * n_hg;
+    const bool live = li < T;
+    const int i = live ? li : T - 1;   // this lane's step: query i in phase A, key j in phase B
+    const int hg = (int)(blockIdx.x % n_hg);
+    for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
+        const int64_t r = u / n_hg;
+        const int h = hg * HPW + hl;
+        const bool hok = h < A.heads;
+        const int hc = hok ? h : A.heads - 1;
+        const int64_t base = r * A.s_row + (int64_t)i * A.s_t + hc * D;
+        float qv[D], kv[D], vv[D], dov[D];
+        ld_row<D>(q + base, qv);
+        ld_row<D>(k + base, kv);
+        ld_row<D>(v + base, vv);
+        ld_row<D>(dout + r * A.do_row + (int64_t)i * A.do_t + hc * D, dov);   // kv/vv die after staging
+        float Di;
+        {
+            float ov[D];
+            ld_row<D>(A.o_in + r * A.o_row + (int64_t)i * A.o_t + hc * D, ov);
+            Di = dot_rr<D>(dov, ov);
+        }
+        const float li_lse = lse[(r * A.heads + hc) * T + i];
+        wave_sync();
+        to_lds<D>(X1 + (hl * T + i) * D, kv);
+        to_lds<D>(X2 + (hl * T + i) * D, vv);
+        Ls[hl * T + i] = li_lse;
+        Dl[hl * T + i] = Di;
+        for (int x = li; x < NB; x += LG) Bs[hl * NBp + x] = A.bias_table ? A.bias_table[hc * NB + x] : 0.f;
+        wave_sync();
+        const uint32_t drk = tkey(A, r, hc);
+        // ---- phase A (lane = query i): dq_i
+        {
+            const float* kb = X1 + hl * T * D;
+            const float* vb = X2 + hl * T * D;
+            const float* bb = Bs + hl * NBp + i + T - 1;
+            float dq[D];
+#pragma unroll
+            for (int c = 0; c < D; ++c) dq[c] = 0.f;
+    #pragma unroll 1
+        for (int j = 0; j < T; ++j) {
+                if (!keep_ij(A, r, hc, i, j)) continue;
+                float bias = bb[-j];
+                if (A.bias_dense) bias += A.bias_dense[r * A.bias_bstride + (((int64_t)hc * T + i) * T + j)];
+                const float s = fmaf(dot_rl<D>(qv, kb + j * D), A.inv_sqrt_d, bias);
+                const float p = __expf(s - li_lse);
+                const float ds = p * (dot_rl<D>(dov, vb + j * D) * drop_scale(A, drk, i, j) - Di);
+                fma_l<D>(dq, ds, kb + j * D);
+            }
+            if (live && hok) st_row<D>(A.dq + r * A.d_row + (int64_t)i * A.d_t + h * D, dq, A.inv_sqrt_d);
+        }
+        wave_sync();
+        // swap: each lane takes its own K/V row back from LDS and leaves its Q/dO row in its place
+        // (same lane, same address: no cross-lane hazard once phase A's reads are done)
+        float* x1 = X1 + (hl * T + i) * D;
+        float* x2 = X2 + (hl * T + i) * D;
+        ld_row<D>(x1, kv);
+        ld_row<D>(x2, vv);
+        to_lds<D>(x1, qv);
+        to_lds<D>(x2, dov);
+        wave_sync();
+        // ---- phase B (lane = key j): dk_j, dv_j, bias-table / dense-bias gradient
+        {
+            const int j = i;
+            const float* qb = X1 + hl * T * D;
+            const float* ob = X2 + hl * T * D;
+            const float* bb = Bs + hl * NBp - j + T - 1;   // bb[i'] = bias of (i', j)
+            float* ab = Acc + hl * NBp - j + T - 1;         // ab[i'] accumulates diagonal i'-j
+            float dk[D], dv[D];
+#pragma unroll
+            for (int c = 0; c < D; ++c) {
+                dk[c] = 0.f;
+                dv[c] = 0.f;
+            }
+            const bool acc_ok = live && hok && A.part;
+#pragma unroll 1
+            for (int ii = 0; ii < T; ++ii) {
+                float ds = 0.f;
+                if (keep_ij(A, r, hc, ii, j)) {
+                    float bias = bb[ii];
+                    if (A.bias_dense) bias += A.bias_dense[r * A.bias_bstride + (((int64_t)hc * T + ii) * T + j)];
+                    const float s = fmaf(dot_rl<D>(kv, qb + ii * D), A.inv_sqrt_d, bias);
+                    const float p = __expf(s - Ls[hl * T + ii]);
+                    const float sc = drop_scale(A, drk, ii, j);
+                    ds = p * (dot_rl<D>(vv, ob + ii * D) * sc - Dl[hl * T + ii]);
+                    fma_l<D>(dk, ds, qb + ii * D);
+                    fma_l<D>(dv, p * sc, ob + ii * D);
+                    if (acc_ok) ab[ii] += ds;
+                }
+                if (A.dbias_dense && live && hok)
+                    A.dbias_dense[((r * A.heads + h) * T + ii) * (int64_t)T + j] = ds;
+            }
+            if (live && hok) {
+                st_row<D>(A.dk + r * A.d_row + (int64_t)j * A.d_t + h * D, dk, A.inv_sqrt_d);
+                st_row<D>(A.dv + r * A.d_row + (int64_t)j * A.d_t + h * D, dv, 1.f);
+            }
+        }
+    }
+    if (A.part) {
+        wave_sync();
+        // partial row blockIdx / n_hg holds this wave's head group's columns
+        float* prow = A.part + (int64_t)(blockIdx.x / n_hg) * A.heads * NB;
+        for (int x = lane; x < HPW * NB; x += WAVE) {
+            const int hh = x / NB, c = x - hh * NB, h = hg * HPW + hh;
+            if (h < A.heads) prow[h * NB + c] = Acc[hh * NBp + c];
+        }
+    }
+}
+
+int v3_lanes(int T) { return T <= 16 ? 16 : T <= 32 ? 32 : T <= 64 ? 64 : 0; }
+
+#ifndef TAGAN_TATTN_V3
+#define TAGAN_TATTN_V3 1
+#endif
+bool v3_ok(int T, int d) {
+    return TAGAN_TATTN_V3 && v3_lanes(T) != 0 && (d == 8 || d == 16 || d == 32 || d == 64);
+}
+
 int pick_D(int d) {
     if (d <= 8) return 8;
     if (d <= 16) return 16;
@@ -634,7 +917,21 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     const float* qf = (const float*)q;
     const float* kf = (const float*)k;
     const float* vf = (const float*)v;
-    const int G = (s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0) ? v2_groups(false, T, head_dim, heads) : 0;
+    const bool al4 = s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0;
+    if (al4 && !attn && v3_ok(T, head_dim)) {
+        const int LG = v3_lanes(T), HPW = WAVE / LG, n_hg = (heads + HPW - 1) / HPW;
+        const dim3 g3((unsigned)(grid_rows(rows) * n_hg));
+        const size_t lds = v3_fwd_lds(T, head_dim, HPW);
+#define TAGAN_V3F(DD, LL) k_tattn_fwd_v3<DD, LL><<<g3, V3_BLK, lds, s>>>(A, qf, kf, vf, n_hg)
+#define TAGAN_V3F_D(LL) switch (head_dim) { case 8: TAGAN_V3F(8, LL); break; case 16: TAGAN_V3F(16, LL); break; \
+                                            case 32: TAGAN_V3F(32, LL); break; default: TAGAN_V3F(64, LL); break; }
+        if (LG == 16) { TAGAN_V3F_D(16) } else if (LG == 32) { TAGAN_V3F_D(32) } else { TAGAN_V3F_D(64) }
+#undef TAGAN_V3F_D
+#undef TAGAN_V3F
+        TAGAN_CHECK_LAUNCH("temporal_attn_fwd_v3");
+        return TAGAN_OK;
+    }
+    const int G = al4 ? v2_groups(false, T, head_dim, heads) : 0;
     if (G > 0) {
         const size_t lds = v2_fwd_lds(G, T, head_dim);
         switch (head_dim) {
@@ -707,10 +1004,28 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     const float* kf = (const float*)k;
     const float* vf = (const float*)v;
     const float* df = (const float*)dout;
-    const int G = (s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0 && do_t % 4 == 0 &&
-                   do_row % 4 == 0 && d_t % 4 == 0 && d_row % 4 == 0)
-                      ? v2_groups(true, T, head_dim, heads)
-                      : 0;
+    const bool al4 = s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0 && do_t % 4 == 0 &&
+                     do_row % 4 == 0 && d_t % 4 == 0 && d_row % 4 == 0;
+    if (al4 && v3_ok(T, head_dim)) {
+        // grid = nblk partial rows x n_hg head groups; block b keeps head group b % n_hg
+        const int LG = v3_lanes(T), HPW = WAVE / LG, n_hg = (heads + HPW - 1) / HPW;
+        const dim3 g3((unsigned)(nblk * n_hg));
+        const size_t lds = v3_bwd_lds(T, head_dim, HPW);
+#define TAGAN_V3B(DD, LL) k_tattn_bwd_v3<DD, LL><<<g3, V3_BLK, lds, s>>>(A, qf, kf, vf, df, lse, n_hg)
+#define TAGAN_V3B_D(LL) switch (head_dim) { case 8: TAGAN_V3B(8, LL); break; case 16: TAGAN_V3B(16, LL); break; \
+                                            case 32: TAGAN_V3B(32, LL); break; default: TAGAN_V3B(64, LL); break; }
+        if (LG == 16) { TAGAN_V3B_D(16) } else if (LG == 32) { TAGAN_V3B_D(32) } else { TAGAN_V3B_D(64) }
+#undef TAGAN_V3B_D
+#undef TAGAN_V3B
+        TAGAN_CHECK_LAUNCH("temporal_attn_bwd_v3");
+        if (dbias_table) {
+            const int n = heads * (2 * T - 1);
+            launch_colsum(A.part, nblk, n, dbias_table, nullptr, n, s);
+            TAGAN_CHECK_LAUNCH("temporal_attn_bwd_sum");
+        }
+        return TAGAN_OK;
+    }
+    const int G = al4 ? v2_groups(true, T, head_dim, heads) : 0;
     if (G > 0) {
         const size_t l2 = v2_bwd_lds(G, T, head_dim, heads);
         switch (head_dim) {

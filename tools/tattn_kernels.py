@@ -1,0 +1,91 @@
+"""Time the temporal attention kernels (fwd, bwd) alone at a config's shape.
+
+    python tools/tattn_kernels.py [--config c2] [--p 0.1] [--reps 20]
+
+Layout as in the model: Q|K|V of the time-major [T, N, 3H] projection (row stride 3H,
+step stride N*3H), the folded [heads, 2T-1] bias table, bias-table gradient on.
+Algorithmic bytes: fwd reads Q,K,V and writes O (+ LSE); bwd reads Q,K,V,O,dO (+ LSE)
+and writes dQ,dK,dV.  TAGAN_LIB=<path> selects an alternative build.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import tagan_amd  # noqa: E402,F401
+from tagan_amd import _lib, synthetic  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--p", type=float, default=0.1)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--causal", type=int, default=0)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    N, _E, T, H, heads = synthetic.CONFIGS[a.config][:5]
+    d = H // heads
+    g = torch.Generator(device=dev).manual_seed(3)
+    qkv = torch.randn(T, N, 3 * H, device=dev, generator=g)
+    out = torch.empty(T, N, H, device=dev)
+    dout = torch.randn(T, N, H, device=dev, generator=g)
+    dqkv = torch.empty_like(qkv)
+    lse = torch.empty(N, heads, T, device=dev)
+    table = torch.randn(heads, 2 * T - 1, device=dev, generator=g) * 0.1
+    dtable = torch.empty_like(table)
+    L = _lib.lib()
+    wsb = L.tagan_temporal_attn_bwd_workspace(N, T, heads)
+    ws = torch.empty(max(int(wsb), 1), dtype=torch.uint8, device=dev)
+    sp = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    b, db, es = qkv.data_ptr(), dqkv.data_ptr(), 4
+    sr, st = 3 * H, N * 3 * H
+
+    def fwd():
+        _lib.check(L.tagan_temporal_attn_fwd(0, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, st,
+                                             _lib.ptr(table), None, 0, None, 0, 0, a.causal, a.p, 99,
+                                             _lib.ptr(out), H, N * H, _lib.ptr(lse), None, sp), "fwd")
+
+    def bwd():
+        _lib.check(L.tagan_temporal_attn_bwd(0, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, st,
+                                             _lib.ptr(table), None, 0, None, 0, 0, a.causal, a.p, 99,
+                                             _lib.ptr(out), H, N * H, _lib.ptr(lse), _lib.ptr(dout), H, N * H,
+                                             db, db + H * es, db + 2 * H * es, sr, st, _lib.ptr(dtable), None,
+                                             _lib.ptr(ws), wsb, sp), "bwd")
+
+    for _ in range(3):
+        fwd()
+        bwd()
+    stream = torch.cuda.current_stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    tf = tb = 0.0
+    for _ in range(a.reps):
+        ev[0].record(stream)
+        fwd()
+        ev[1].record(stream)
+        bwd()
+        ev[2].record(stream)
+        ev[2].synchronize()
+        tf += ev[0].elapsed_time(ev[1])
+        tb += ev[1].elapsed_time(ev[2])
+    tf, tb = tf / a.reps, tb / a.reps
+    unit = N * T * H * 4
+    bf = 4 * unit + N * heads * T * 4
+    bb = 8 * unit + N * heads * T * 4
+    chk = [float(out.double().abs().sum()), float(dqkv.double().abs().sum()), float(dtable.double().abs().sum())]
+    print(json.dumps({"lib": os.environ.get("TAGAN_LIB", "default"), "config": a.config, "rows": N, "T": T,
+                      "heads": heads, "d": d, "p": a.p, "ms_fwd": round(tf, 4), "ms_bwd": round(tb, 4),
+                      "gbs_fwd": round(bf / tf / 1e6, 1), "gbs_bwd": round(bb / tb / 1e6, 1),
+                      "frac_hbm": round((bf + bb) / (tf + tb) / 1e6 / bench.HBM_PEAK_GBS, 4),
+                      "checksums": chk}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
