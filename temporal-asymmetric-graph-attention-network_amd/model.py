@@ -109,9 +109,10 @@ class TAGAN(nn.Module):
         return h, counts, weights
 
     @staticmethod
-    def _time_major(x_cat: torch.Tensor, counts: List[int]) -> torch.Tensor:
+    def _time_major(x_cat: torch.Tensor, counts: List[int], n_max: Optional[int] = None) -> torch.Tensor:
         """Concatenated snapshots -> zero-padded [T, N_max, H] (temporal_attention.py:928-968 minus permute)."""
-        T, n_max, H = len(counts), max(counts), x_cat.shape[1]
+        T, H = len(counts), x_cat.shape[1]
+        n_max = max(counts) if n_max is None else n_max
         if all(c == n_max for c in counts):
             return x_cat.view(T, n_max, H)
         out = x_cat.new_zeros(T, n_max, H)
@@ -140,8 +141,6 @@ class TAGAN(nn.Module):
 
     def forward(self, graph_sequence: List[Snapshot], labels: Optional[torch.Tensor] = None,
                 return_attention_weights: bool = False) -> Dict[str, Any]:
-        device = next(self.parameters()).device
-        T = len(graph_sequence)
         for snap in graph_sequence:
             _unpack(snap)   # format validation of model.py:187-200
         x_cat, counts, geo_w = self.encode_snapshots(graph_sequence, return_attention_weights)
@@ -150,8 +149,16 @@ class TAGAN(nn.Module):
         out_tm, temp_w = self._temporal(xt, return_attention_weights)
         if return_attention_weights:
             self.last_temp_attn_weights = temp_w
+        outputs = self.head(self._pool(out_tm), labels)
+        if return_attention_weights:
+            outputs["geometric_attention_weights"] = geo_w
+            outputs["temporal_attention_weights"] = temp_w
+        return outputs
+
+    def head(self, pooled: torch.Tensor, labels: Optional[torch.Tensor] = None) -> Dict[str, Any]:
+        """graph_features -> classification head -> loss / predictions (model.py:377-459); pooled [T, H]."""
+        T = pooled.shape[0]
         batch_size = labels.shape[0] if (labels is not None and labels.dim() > 0) else 1
-        pooled = self._pool(out_tm)
         if batch_size > 1:
             graph_features = torch.cat([pooled.unsqueeze(0), pooled.new_zeros(batch_size - 1, T, pooled.shape[1])])
         else:
@@ -172,11 +179,7 @@ class TAGAN(nn.Module):
         else:
             predictions = F.softmax(logits, dim=1)
             self.last_predictions = predictions
-        outputs = {"logits": logits, "predictions": predictions, "loss": loss}
-        if return_attention_weights:
-            outputs["geometric_attention_weights"] = geo_w
-            outputs["temporal_attention_weights"] = temp_w
-        return outputs
+        return {"logits": logits, "predictions": predictions, "loss": loss}
 
     def infer(self, graph_sequence, return_probs: bool = True) -> Dict[str, Any]:
         self.eval()
