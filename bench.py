@@ -122,6 +122,37 @@ def roofline(model, seq, cfg, reps=20):
             "ms_fwd": round(tf * 1e3, 4), "ms_bwd": round(tb * 1e3, 4)}
 
 
+def breakdown(model, seq, fwd, bwd, opt, cfg, reps=5):
+    """Per-phase time of one step (CSR build and optimizer reported separately), measured
+    after the timed region with HIP events on the current stream, mean of ``reps`` (all ranks in lockstep)."""
+    from tagan_amd.kernels import build_graph
+    stream = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    acc = [0.0] * 4
+    eis = [ei for _, ei, _, _ in seq]
+    counts = [int(x.shape[0]) for x, _, _, _ in seq]
+    for _ in range(reps):
+        opt.zero_grad(set_to_none=True)
+        ev[0].record(stream)
+        build_graph(eis, counts)
+        ev[1].record(stream)
+        out = fwd()
+        ev[2].record(stream)
+        bwd(out)
+        ev[3].record(stream)
+        torch.nn.utils.clip_grad_norm_(model.parameters(), cfg.gradient_clip_val)
+        opt.step()
+        ev[4].record(stream)
+        ev[4].synchronize()
+        for i in range(4):
+            acc[i] += ev[i].elapsed_time(ev[i + 1])
+    names = ("csr_build_ms", "forward_ms", "backward_ms", "optimizer_ms")
+    res = {n: round(a / reps, 3) for n, a in zip(names, acc)}
+    res["note"] = ("forward includes its own CSR build; backward includes the gradient exchange; "
+                   "optimizer = clip_grad_norm_ + Adam")
+    return res
+
+
 def cpu_baseline(cfg, name, model_state, n_snap, min_seconds=10.0):
     """CPU oracle (sparse CSR restatement of the reference) on a bounded sample of the same workload:
     whole sequences of ``n_snap`` snapshots, fwd+bwd, repeated until ``min_seconds`` of CPU work."""
@@ -181,21 +212,28 @@ def main():
         sync = ShardGradSync(list(model.named_parameters()))
         labels = torch.tensor([1.0], device=dev)
 
-        def forward_backward():
-            out = sharded(seq, counts_all, labels)
+        def fwd():
+            return sharded(seq, counts_all, labels)
+
+        def bwd(out):
             out["loss"].backward()
             sync.sync()
-            return out
     else:
         bucket = GradBucket(model.parameters())
         seq = synthetic.make_sequence(args.config, dev, seed=1000 + rank)
         labels = torch.tensor([1.0 if rank % 2 == 0 else 0.0], device=dev)
 
-        def forward_backward():
-            out = model(seq, labels=labels)
+        def fwd():
+            return model(seq, labels=labels)
+
+        def bwd(out):
             out["loss"].backward()
             bucket.allreduce_mean()
-            return out
+
+    def forward_backward():
+        out = fwd()
+        bwd(out)
+        return out
 
     def step():
         opt.zero_grad(set_to_none=True)
@@ -235,6 +273,7 @@ def main():
                    "sequences_per_step": seqs_per_step, "snapshots_per_sequence": T,
                    "parallelism": ("snapshot-shard%d" % world) if args.shard else ("dp%d" % world)},
     }
+    rec["breakdown"] = breakdown(model, seq, fwd, bwd, opt, cfg)
     if rank == 0 and not args.no_roofline:
         rec["roofline"] = roofline(model, seq, cfg)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -3,20 +3,37 @@
 Module tree, parameter names/shapes and initialisation order match the
 reference (41 tensors at hidden_dim=64), so reference state_dicts load.
 
-Forward keeps the SHIPPED contract (SURVEY.md header fact 4): in the
+``forward`` keeps the SHIPPED contract (SURVEY.md header fact 4): in the
 reference, ``TemporalPropagation.forward`` can never return —
   * node-id lists + no bank   -> UnboundLocalError (temporal_propagation.py:1231)
   * node-id lists + a bank    -> AttributeError 'restrict_temporal_attention' (:1287)
   * any other input           -> TypeError len(NodeMemoryBank) (:1485/:1505)
 and TAGAN.forward falls back to identity (model.py:302-309).  This module
-raises the same exception types without spending the dead compute; the TAGAN
-host path (``tagan_amd.model``) takes the identity branch explicitly instead of
-through an exception.  The submodules below are usable on their own.
+raises the same exception types without spending the dead compute.
+
+``forward_intended`` is the compute the reference was written to do with tensor
+masks (pinned by the tprop_* fixtures, G6): GRU evolution
+over T -> windowed skip connection -> output_proj -> dropout -> LayerNorm.  It runs
+time-major ([T, N, H], node rows independent) on the device: the x-side of all three
+GRU gates for all T steps is ONE GEMM, each recurrent step is two GEMMs on the hidden
+state plus gate elementwise work, LayerNorms and the residual tails run on the HIP
+LayerNorm kernels, the window aggregation is one pooling pass over T.  TAGAN uses it
+when constructed with ``temporal_propagation="intended"`` (default "shipped").
+The submodules keep their reference list-in/list-out forwards (on the same device
+code) for standalone use.
 """
 from typing import Any, List, Optional
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
+
+from .._lib import require_hip
+from ..kernels import dropout_add_layer_norm, layer_norm, linear
+
+
+def _ln(x, mod):
+    return layer_norm(x, mod) if mod is not None else x
 
 
 class TemporalGRUCell(nn.Module):
@@ -39,30 +56,49 @@ class TemporalGRUCell(nn.Module):
         nn.init.constant_(self.reset_gate.bias, 1.0)
         nn.init.constant_(self.update_gate.bias, 1.0)
 
+    def x_gates(self, x: torch.Tensor) -> torch.Tensor:
+        """x-side of the three gates for any number of rows: [.., D_in] -> [.., 3*H_c] (LN_x, one GEMM)."""
+        D = self.input_dim
+        x = _ln(x, self.layer_norm_x if self.use_layer_norm else None)
+        w = torch.cat([self.reset_gate.weight[:, :D], self.update_gate.weight[:, :D],
+                       self.candidate.weight[:, :D]], 0)
+        b = torch.cat([self.reset_gate.bias, self.update_gate.bias, self.candidate.bias], 0)
+        return linear(x, w, b)
+
+    def step(self, gx: torch.Tensor, h: Optional[torch.Tensor], time_diff: Optional[torch.Tensor] = None):
+        """One recurrent step (temporal_propagation.py:475-551) given the precomputed x-side ``gx``."""
+        D, hc = self.input_dim, self.hidden_dim
+        if h is None:
+            hn = None
+        else:
+            hn = _ln(h, self.layer_norm_h if self.use_layer_norm else None)
+            if time_diff is not None:
+                hn = hn * torch.exp(-torch.clamp(time_diff, min=0.0, max=10.0)).unsqueeze(1)
+        if hn is None:   # h = 0: the recurrent GEMMs vanish
+            rz = torch.sigmoid(gx[:, :2 * hc])
+            z = rz[:, hc:]
+            h_new = z * torch.tanh(gx[:, 2 * hc:])
+        else:
+            w_rz = torch.cat([self.reset_gate.weight[:, D:], self.update_gate.weight[:, D:]], 0)
+            rz = torch.sigmoid(gx[:, :2 * hc] + linear(hn, w_rz))
+            r, z = rz[:, :hc], rz[:, hc:]
+            h_tilde = torch.tanh(gx[:, 2 * hc:] + linear(r * hn, self.candidate.weight[:, D:]))
+            h_new = (1 - z) * hn + z * h_tilde
+        h_new = self.dropout_layer(h_new)
+        return _ln(h_new, self.layer_norm_out if self.use_layer_norm else None)
+
     def forward(self, x, h=None, time_diff=None):
+        require_hip(x, h)
         if x.dim() == 1:
             x = x.unsqueeze(0)
-        if self.use_layer_norm:
-            x = self.layer_norm_x(x)
-        if h is None:
-            h = torch.zeros(x.size(0), self.hidden_dim, device=x.device, dtype=x.dtype)
-        elif self.use_layer_norm:
-            h = self.layer_norm_h(h)
-        if time_diff is not None:
-            h = h * torch.exp(-torch.clamp(time_diff, min=0.0, max=10.0)).unsqueeze(1)
-        if h.dim() == 1:
+        if h is not None and h.dim() == 1:
             h = h.unsqueeze(0)
-        if x.size(0) != h.size(0):
+        if h is not None and x.size(0) != h.size(0):
             if x.size(0) == 1:
                 x = x.expand(h.size(0), -1)
             elif h.size(0) == 1:
                 h = h.expand(x.size(0), -1)
-        xh = torch.cat([x, h], dim=-1)
-        r = torch.sigmoid(self.reset_gate(xh))
-        z = torch.sigmoid(self.update_gate(xh))
-        h_tilde = torch.tanh(self.candidate(torch.cat([x, r * h], dim=-1)))
-        h_new = self.dropout_layer((1 - z) * h + z * h_tilde)
-        return self.layer_norm_out(h_new) if self.use_layer_norm else h_new
+        return self.step(self.x_gates(x), h, time_diff)
 
 
 class TemporalEvolutionLayer(nn.Module):
@@ -85,30 +121,37 @@ class TemporalEvolutionLayer(nn.Module):
         nn.init.xavier_uniform_(self.output_projection.weight)
         nn.init.zeros_(self.output_projection.bias)
 
-    def forward(self, node_features_seq: List[torch.Tensor], time_stamps: Optional[torch.Tensor] = None):
-        T = len(node_features_seq)
+    def forward_time_major(self, xt: torch.Tensor, time_stamps: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """xt [T, N, D_in] -> [T, N, H] (temporal_propagation.py:648-755)."""
+        require_hip(xt)
+        T = xt.shape[0]
         has_time = time_stamps is not None and self.time_aware
+        gx = self.forward_cell.x_gates(xt)
         fwd, h = [], None
         for t in range(T):
             td = time_stamps[:, t] - time_stamps[:, t - 1] if (has_time and t > 0) else None
-            h = self.forward_cell(node_features_seq[t], h, td)
+            h = self.forward_cell.step(gx[t], h, td)
             fwd.append(h)
+        states = torch.stack(fwd, 0)
         if self.bidirectional:
+            gb = self.backward_cell.x_gates(xt)
             bwd, hb = [None] * T, None
             for t in range(T - 1, -1, -1):
                 td = time_stamps[:, t + 1] - time_stamps[:, t] if (has_time and t < T - 1) else None
-                hb = self.backward_cell(node_features_seq[t], hb, td)
+                hb = self.backward_cell.step(gb[t], hb, td)
                 bwd[t] = hb
-            states = [torch.cat([fwd[t], bwd[t]], dim=1) for t in range(T)]
-        else:
-            states = fwd
-        out = []
-        for t in range(T):
-            y = self.dropout_layer(self.output_projection(states[t]))
-            if self.residual and self.input_dim == self.hidden_dim:
-                y = y + node_features_seq[t]
-            out.append(self.layer_norm(y) if self.use_layer_norm else y)
-        return out
+            states = torch.cat([states, torch.stack(bwd, 0)], -1)
+        y = linear(states, self.output_projection.weight, self.output_projection.bias)
+        res = xt if (self.residual and self.input_dim == self.hidden_dim) else None
+        if self.use_layer_norm and res is not None:
+            return dropout_add_layer_norm(y, res, self.layer_norm, self.dropout if self.training else 0.0)
+        y = self.dropout_layer(y)
+        if res is not None:
+            y = y + res
+        return _ln(y, self.layer_norm if self.use_layer_norm else None)
+
+    def forward(self, node_features_seq: List[torch.Tensor], time_stamps: Optional[torch.Tensor] = None):
+        return list(self.forward_time_major(torch.stack(node_features_seq, 0), time_stamps).unbind(0))
 
 
 class TemporalSkipConnection(nn.Module):
@@ -133,31 +176,35 @@ class TemporalSkipConnection(nn.Module):
             nn.init.xavier_uniform_(lin.weight)
             nn.init.zeros_(lin.bias)
 
-    def forward(self, node_features_seq: List[torch.Tensor], time_weights=None):
-        T = len(node_features_seq)
-        proj = []
-        for f in node_features_seq:
-            p = self.input_proj(f)
-            if self.apply_activation:
-                p = self.act_fn(p)
-            if self.use_layer_norm:
-                p = self.layer_norm1(p)
-            proj.append(self.dropout_layer(p))
-        agg = []
-        for t in range(T):
-            win = torch.stack(proj[max(0, t - self.window_size): min(T, t + self.window_size + 1)], 0)
-            if self.aggregation == "mean":
-                agg.append(win.mean(0))
-            elif self.aggregation == "max":
-                agg.append(win.max(0)[0])
-            else:
-                agg.append(win.sum(0))
-        out = [self.dropout_layer(self.output_proj(self.act_fn(a))) for a in agg]
+    def forward_time_major(self, xt: torch.Tensor) -> torch.Tensor:
+        """xt [T, N, D] -> [T, N, D] (temporal_propagation.py:846-946); windows of ±window_size over T."""
+        require_hip(xt)
+        T, N, _ = xt.shape
+        p = linear(xt, self.input_proj.weight, self.input_proj.bias)
+        if self.apply_activation:
+            p = self.act_fn(p)
+        p = self.dropout_layer(_ln(p, self.layer_norm1 if self.use_layer_norm else None))
+        Hd = p.shape[-1]
+        w = self.window_size
+        seq = p.permute(1, 2, 0).reshape(N * Hd, 1, T)          # pooling runs along T
+        k = 2 * w + 1
+        if self.aggregation == "mean":
+            agg = F.avg_pool1d(seq, k, 1, w, count_include_pad=False) if w > 0 else seq
+        elif self.aggregation == "max":
+            agg = F.max_pool1d(seq, k, 1, w) if w > 0 else seq
+        else:
+            agg = F.avg_pool1d(seq, k, 1, w, count_include_pad=True) * k if w > 0 else seq
+        agg = agg.reshape(N, Hd, T).permute(2, 0, 1)
+        out = linear(self.act_fn(agg), self.output_proj.weight, self.output_proj.bias)
+        if self.residual and self.use_layer_norm:
+            return dropout_add_layer_norm(out, xt, self.layer_norm2, self.dropout if self.training else 0.0)
+        out = self.dropout_layer(out)
         if self.residual:
-            out = [o + x for o, x in zip(out, node_features_seq)]
-        if self.use_layer_norm:
-            out = [self.layer_norm2(o) for o in out]
-        return out
+            out = out + xt
+        return _ln(out, self.layer_norm2 if self.use_layer_norm else None)
+
+    def forward(self, node_features_seq: List[torch.Tensor], time_weights=None):
+        return list(self.forward_time_major(torch.stack(node_features_seq, 0)).unbind(0))
 
 
 class TemporalGatingUnit(nn.Module):
@@ -182,17 +229,26 @@ class TemporalGatingUnit(nn.Module):
             nn.init.zeros_(lin.bias)
 
     def forward(self, current_feat, previous_feat):
+        """temporal_propagation.py:1022-1067."""
+        require_hip(current_feat, previous_feat)
         if self.use_layer_norm:
-            current_feat = self.layer_norm_in1(current_feat)
-            previous_feat = self.layer_norm_in2(previous_feat)
+            current_feat = layer_norm(current_feat, self.layer_norm_in1)
+            previous_feat = layer_norm(previous_feat, self.layer_norm_in2)
         comb = torch.cat([current_feat, previous_feat], dim=1)
-        u = torch.sigmoid(self.update_gate(comb))
-        r = torch.sigmoid(self.reset_gate(comb))
-        cand = torch.tanh(self.output_gate(torch.cat([current_feat, r * previous_feat], dim=1)))
-        out = self.dropout_layer((1 - u) * current_feat + u * cand)
+        ur = torch.sigmoid(linear(comb, torch.cat([self.update_gate.weight, self.reset_gate.weight], 0),
+                                  torch.cat([self.update_gate.bias, self.reset_gate.bias], 0)))
+        D = self.input_dim
+        u, r = ur[:, :D], ur[:, D:]
+        cand = torch.tanh(linear(torch.cat([current_feat, r * previous_feat], dim=1), self.output_gate.weight,
+                                 self.output_gate.bias))
+        out = (1 - u) * current_feat + u * cand
+        if self.residual and self.use_layer_norm:
+            return dropout_add_layer_norm(out, current_feat, self.layer_norm_out,
+                                          self.dropout if self.training else 0.0)
+        out = self.dropout_layer(out)
         if self.residual:
             out = out + current_feat
-        return self.layer_norm_out(out) if self.use_layer_norm else out
+        return layer_norm(out, self.layer_norm_out) if self.use_layer_norm else out
 
 
 class TemporalPropagation(nn.Module):
@@ -240,6 +296,16 @@ class TemporalPropagation(nn.Module):
             raise AttributeError("'TemporalPropagation' object has no attribute 'restrict_temporal_attention'")
         self.temporal_mask = None
         raise TypeError("object of type 'NodeMemoryBank' has no len()")
+
+    def forward_intended(self, xt: torch.Tensor, time_stamps: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Intended compute, tensor-mask form (temporal_propagation.py:1345-1500): xt [T, N, H] time-major,
+        time_stamps [N, T] or None -> [T, N, H]."""
+        require_hip(xt)
+        x = self.evolution_layer.forward_time_major(xt, time_stamps)
+        if self.use_skip_connection:
+            x = self.skip_connection.forward_time_major(x)
+        x = self.dropout_layer(linear(x, self.output_proj.weight, self.output_proj.bias))
+        return layer_norm(x, self.layer_norm) if self.use_layer_norm else x
 
     def extra_repr(self) -> str:
         return (f"input_dim={self.input_dim}, hidden_dim={self.hidden_dim}, dropout={self.dropout}, "

@@ -46,8 +46,16 @@ def _unpack(snapshot):
 
 
 class TAGAN(nn.Module):
-    def __init__(self, config: TAGANConfig):
+    """``temporal_propagation``: "shipped" (default) reproduces the reference, whose
+    TemporalPropagation never returns (identity); "intended" runs its tensor-mask compute
+    (TemporalPropagation.forward_intended, pinned by the G6 fixtures) on the padded
+    time-major features before the temporal attention."""
+
+    def __init__(self, config: TAGANConfig, temporal_propagation: str = "shipped"):
         super().__init__()
+        if temporal_propagation not in ("shipped", "intended"):
+            raise ValueError("temporal_propagation must be 'shipped' or 'intended'")
+        self.temporal_propagation_mode = temporal_propagation
         self.config = config
         self.memory_bank = NodeMemoryBank(hidden_dim=config.hidden_dim, decay_factor=0.8,
                                           max_inactivity=config.temporal_window_size)
@@ -146,6 +154,8 @@ class TAGAN(nn.Module):
         x_cat, counts, geo_w = self.encode_snapshots(graph_sequence, return_attention_weights)
         # TemporalPropagation never returns in the shipped code: identity (model.py:276-309).
         xt = self._time_major(x_cat, counts)
+        if self.temporal_propagation_mode == "intended":
+            xt = self.temporal_propagation.forward_intended(xt)
         out_tm, temp_w = self._temporal(xt, return_attention_weights)
         if return_attention_weights:
             self.last_temp_attn_weights = temp_w

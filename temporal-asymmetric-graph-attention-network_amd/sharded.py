@@ -147,7 +147,9 @@ class SnapshotShardedTAGAN:
             x_cat, counts, _ = model.encode_snapshots(snaps)
             return x_cat, counts
 
-        def temporal(xt):
+        def temporal(xt):   # propagation (intended mode) and attention are both per node row
+            if model.temporal_propagation_mode == "intended":
+                xt = model.temporal_propagation.forward_intended(xt)
             return model._temporal(xt, False)[0]
 
         return cls(encode, temporal, model.head, group)

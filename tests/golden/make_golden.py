@@ -21,6 +21,11 @@ Cases (SURVEY.md §8c G1–G5):
   geo_*        GeometricAttention standalone (dense mask, no mask, geometric_bias).
   tatt_*       AsymmetricTemporalAttention / TemporalAttention (temporal_attention.py).
   membank_*    NodeMemoryBank.update/get_states/update_state/decay_all traces.
+  tprop_*      TemporalPropagation's intended compute (G6): TemporalEvolutionLayer (GRU over T,
+               time-aware / bidirectional), TemporalSkipConnection (mean/max/sum windows),
+               TemporalGatingUnit, and the full forward with tensor masks — reachable only with a
+               fixture-time ``NodeMemoryBank.__len__`` (the shipped class has none, so
+               temporal_propagation.py:1505 raises TypeError).
 
 Usage:  python tests/golden/make_golden.py [case-prefix ...]
 """
@@ -56,12 +61,16 @@ def _import_reference():
             from src.tagan.layers.temporal_attention import (
                 TemporalAttention, AsymmetricTemporalAttention)
             from src.tagan.utils.memory_bank import NodeMemoryBank
+            from src.tagan.layers.temporal_propagation import (
+                TemporalPropagation, TemporalEvolutionLayer, TemporalSkipConnection, TemporalGatingUnit)
     finally:
         os.chdir(cwd)
     return dict(TAGAN=TAGAN, TAGANConfig=TAGANConfig, TAGANGraphAttention=TAGANGraphAttention,
                 GeometricAttention=GeometricAttention, TemporalAttention=TemporalAttention,
                 AsymmetricTemporalAttention=AsymmetricTemporalAttention,
-                NodeMemoryBank=NodeMemoryBank)
+                NodeMemoryBank=NodeMemoryBank, TemporalPropagation=TemporalPropagation,
+                TemporalEvolutionLayer=TemporalEvolutionLayer, TemporalSkipConnection=TemporalSkipConnection,
+                TemporalGatingUnit=TemporalGatingUnit)
 
 
 def quiet(fn, *a, **k):
@@ -305,6 +314,65 @@ def tatt_case(R, case, cls, ctor_kw, x_kind, B=5, T=6, H=32, heads=4, seed=21,
     save(case, t, meta)
 
 
+# --------------------------------------------------------------------------- temporal propagation (G6)
+def tprop_case(R, case, kind, ctor_kw, B=7, T=6, H=32, seed=31, with_time=True):
+    torch.manual_seed(seed)
+    kw = dict(dropout=0.0)
+    kw.update(ctor_kw)
+    g = torch.Generator().manual_seed(seed + 1)
+    t = {}
+    kwargs = {}
+    ts = None
+    if with_time:
+        ts = torch.cumsum(torch.rand(B, T, generator=g) * 3.0, dim=1)
+        t["in.time_stamps"] = ts
+    if kind == "gating":
+        mod = R["TemporalGatingUnit"](input_dim=H, **kw)
+        cur = torch.randn(B, H, generator=g).requires_grad_(True)
+        prev = torch.randn(B, H, generator=g).requires_grad_(True)
+        xs = [cur, prev]
+        out = quiet(mod, cur, prev)
+        t["in.current"], t["in.previous"] = cur.detach(), prev.detach()
+        outs = [out]
+    else:
+        xs = [torch.randn(B, H, generator=g).requires_grad_(True) for _ in range(T)]
+        for i, xi in enumerate(xs):
+            t[f"in.x.{i}"] = xi.detach()
+        if kind == "evolution":
+            mod = R["TemporalEvolutionLayer"](input_dim=H, hidden_dim=H, **kw)
+            outs = quiet(mod, xs, ts)
+        elif kind == "skip":
+            mod = R["TemporalSkipConnection"](input_dim=H, **kw)
+            outs = quiet(mod, xs)
+        else:   # full TemporalPropagation.forward, tensor masks, bank with a fixture-time __len__
+            NMB = R["NodeMemoryBank"]
+            had = "__len__" in NMB.__dict__
+            NMB.__len__ = lambda self: len(self.node_states)
+            try:
+                mod = R["TemporalPropagation"](input_dim=H, hidden_dim=H, **kw)
+                bank = NMB(hidden_dim=H)
+                masks = [torch.ones(B) for _ in range(T)]
+                outs, _bank = quiet(mod, xs, masks, ts, bank)
+            finally:
+                if not had:
+                    del NMB.__len__
+    gouts = [torch.randn(o.shape, generator=g) for o in outs]
+    quiet(sum((o * go).sum() for o, go in zip(outs, gouts)).backward)
+    for i, (o, go) in enumerate(zip(outs, gouts)):
+        t[f"out.{i}"] = o
+        t[f"in.grad_out.{i}"] = go
+    for i, xi in enumerate(xs):
+        t[f"grad.x.{i}"] = xi.grad
+    for k, v in mod.state_dict().items():
+        t["sd." + k] = v
+    for n, p in mod.named_parameters():
+        if p.grad is not None:
+            t["grad." + n] = p.grad
+    meta = dict(kind="tprop", module=kind, ctor=kw, B=B, T=T, H=H, with_time=with_time,
+                anchors=["src/tagan/layers/temporal_propagation.py:402-558,561-765,768-957,960-1075,1078-1522"])
+    save(case, t, meta)
+
+
 # --------------------------------------------------------------------------- memory bank
 def membank_case(R, case, seed=5, H=8, decay=0.8, max_inactivity=3):
     g = torch.Generator().manual_seed(seed)
@@ -413,6 +481,20 @@ def main(prefixes):
                                                       mask_kind="rand_BTT")))
     # G5
     cases.append(("membank_trace", lambda: membank_case(R, "membank_trace")))
+    # G6
+    cases.append(("tprop_evolution", lambda: tprop_case(R, "tprop_evolution", "evolution", {})))
+    cases.append(("tprop_evolution_notime", lambda: tprop_case(R, "tprop_evolution_notime", "evolution",
+                                                               dict(use_layer_norm=False), with_time=False)))
+    cases.append(("tprop_evolution_bidir", lambda: tprop_case(R, "tprop_evolution_bidir", "evolution",
+                                                              dict(bidirectional=True))))
+    for agg in ("mean", "max", "sum"):
+        cases.append((f"tprop_skip_{agg}", (lambda agg=agg: tprop_case(
+            R, f"tprop_skip_{agg}", "skip", dict(window_size=2, aggregation=agg), with_time=False))))
+    cases.append(("tprop_gating", lambda: tprop_case(R, "tprop_gating", "gating", {}, with_time=False)))
+    cases.append(("tprop_full", lambda: tprop_case(R, "tprop_full", "full", dict(window_size=2))))
+    cases.append(("tprop_full_bidir_notime", lambda: tprop_case(
+        R, "tprop_full_bidir_notime", "full", dict(window_size=1, bidirectional=True, aggregation="max"),
+        T=5, with_time=False)))
     for name, fn in cases:
         if prefixes and not any(name.startswith(p) for p in prefixes):
             continue

@@ -1,0 +1,107 @@
+"""GPU parity of TemporalPropagation's intended compute (tagan_amd, HIP device) against the G6
+fixtures minted from the reference (tests/golden/tprop_*), and of TAGAN(temporal_propagation=
+"intended") against the CPU oracle stages (fp64)."""
+import pytest
+import torch
+
+import golden_io as G
+import oracle
+from oracle import tprop_oracle
+from oracle.tagan_oracle import _lin, _ln, bce_loss, classification_head, graph_attention, temporal_attention
+
+pytestmark = pytest.mark.gpu
+
+OUT_ATOL, OUT_RTOL = 1e-4, 1e-4
+GRAD_ATOL, GRAD_RTOL = 1e-4, 1e-3
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import tagan_amd  # noqa: F401
+    return torch.device("cuda:0")
+
+
+def _module(meta):
+    from tagan_amd.layers.temporal_propagation import (TemporalEvolutionLayer, TemporalGatingUnit,
+                                                       TemporalPropagation, TemporalSkipConnection)
+    H, kw = meta["H"], dict(meta["ctor"])
+    if meta["module"] == "evolution":
+        return TemporalEvolutionLayer(input_dim=H, hidden_dim=H, **kw)
+    if meta["module"] == "skip":
+        return TemporalSkipConnection(input_dim=H, **kw)
+    if meta["module"] == "gating":
+        return TemporalGatingUnit(input_dim=H, **kw)
+    return TemporalPropagation(input_dim=H, hidden_dim=H, **kw)
+
+
+@pytest.mark.parametrize("case", G.case_names("tprop_"))
+def test_tprop_golden(dev, case):
+    meta, t = G.load(case)
+    mod = _module(meta)
+    mod.load_state_dict({k[3:]: v for k, v in t.items() if k.startswith("sd.")})
+    mod = mod.to(dev).train()
+    ts = t["in.time_stamps"].to(dev) if "in.time_stamps" in t else None
+    if meta["module"] == "gating":
+        xs = [t["in.current"].to(dev).requires_grad_(True), t["in.previous"].to(dev).requires_grad_(True)]
+        outs = [mod(*xs)]
+    else:
+        xs = [t["in.x.%d" % i].to(dev).requires_grad_(True) for i in range(meta["T"])]
+        if meta["module"] == "evolution":
+            outs = mod(xs, ts)
+        elif meta["module"] == "skip":
+            outs = mod(xs)
+        else:
+            outs = list(mod.forward_intended(torch.stack(xs, 0), ts).unbind(0))
+    for i, o in enumerate(outs):
+        G.assert_close("out.%d" % i, o, t["out.%d" % i], OUT_ATOL, OUT_RTOL)
+    sum((o * t["in.grad_out.%d" % i].to(dev)).sum() for i, o in enumerate(outs)).backward()
+    for i, x in enumerate(xs):
+        G.assert_close("grad.x.%d" % i, x.grad, t["grad.x.%d" % i], GRAD_ATOL, GRAD_RTOL)
+    for n, p in mod.named_parameters():
+        if "grad." + n in t:
+            G.assert_close("grad." + n, p.grad, t["grad." + n], GRAD_ATOL, GRAD_RTOL)
+
+
+def test_tagan_intended_mode_vs_oracle(dev):
+    """TAGAN(temporal_propagation="intended") = oracle stages with propagation inserted before attention."""
+    from tagan_amd import TAGAN, TAGANConfig
+    H, heads, T = 64, 4, 6
+    counts = [31, 40, 27, 40, 36, 33]
+    cfg = TAGANConfig(node_feature_dim=12, edge_feature_dim=0, hidden_dim=H, num_heads=heads, dropout=0.0,
+                      output_dim=1, window_size=3, temporal_window_size=2)
+    torch.manual_seed(3)
+    model = TAGAN(cfg, temporal_propagation="intended").to(dev)
+    P = {k: v.detach().cpu().double().requires_grad_(True) for k, v in model.state_dict().items()}
+    g = torch.Generator().manual_seed(9)
+    seq = [(torch.randn(n, 12, generator=g), torch.randint(0, n, (2, 3 * n), generator=g), None, list(range(n)))
+           for n in counts]
+    labels = torch.tensor([1.0])
+    out = model([(x.to(dev), ei.to(dev), None, ids) for x, ei, _, ids in seq], labels.to(dev))
+    out["loss"].backward()
+    # oracle: per-snapshot stage, zero-padded time-major, propagation, temporal attention, pooling, head
+    hs = []
+    for x, ei, _, _ in seq:
+        h = _lin(x.double(), P, "node_embedding")
+        skip = h
+        for i in range(2):
+            h = graph_attention(h, ei, P, "geometric_attention_layers.%d" % i, heads, "euclidean", True, False)
+            if i == 0:
+                h = h + _ln(skip, P, "skip_layer_norm")
+        hs.append(h)
+    n_max = max(counts)
+    xt = torch.stack([torch.cat([h, h.new_zeros(n_max - h.shape[0], H)]) for h in hs], 0)
+    xs = tprop_oracle.propagation(list(xt.unbind(0)), None, P, "temporal_propagation", window_size=2)
+    ot = temporal_attention(xs, P, "temporal_attention", heads, attention_mask=torch.ones(T, T, dtype=xt.dtype),
+                            asymmetric_window_size=3)                       # [N, T, H]
+    gf = ot.reshape(T, -1, H).mean(1).unsqueeze(0)
+    logits = classification_head(gf, P, True)
+    loss = bce_loss(logits, labels.double())
+    loss.backward()
+    assert abs(float(out["loss"]) - float(loss)) < 1e-5
+    for n, p in model.named_parameters():
+        if P[n].grad is None:
+            assert p.grad is None or not p.grad.any(), n
+            continue
+        G.assert_close("grad." + n, p.grad, P[n].grad, GRAD_ATOL, GRAD_RTOL)

@@ -150,3 +150,60 @@ def test_csr_semantics():
     assert col.tolist() == [0, 1, 1, 0, 2, 0, 3]
     with pytest.raises(IndexError):
         oracle.csr_from_edge_index(torch.tensor([[0], [4]]), 4)
+
+
+def _tprop_run(meta, t, P, prop):
+    """Run one tprop_* case through ``prop`` (oracle.tprop_oracle or the device module's functional form)."""
+    kind, kw = meta["module"], dict(meta["ctor"])
+    kw.pop("dropout", None)
+    ts = t.get("in.time_stamps")
+    if kind == "gating":
+        cur = t["in.current"].clone().requires_grad_(True)
+        prev = t["in.previous"].clone().requires_grad_(True)
+        return [prop.gating_unit(cur, prev, P, "", **{k: v for k, v in kw.items() if k == "residual"})], [cur, prev]
+    xs = [t["in.x.%d" % i].clone().requires_grad_(True) for i in range(meta["T"])]
+    if kind == "evolution":
+        outs = prop.evolution_layer(xs, ts, P, "", kw.get("time_aware", True), kw.get("bidirectional", False),
+                                    kw.get("residual", True))
+    elif kind == "skip":
+        outs = prop.skip_connection(xs, P, "", kw.get("window_size", 3), kw.get("aggregation", "mean"),
+                                    kw.get("residual", True))
+    else:
+        outs = prop.propagation(xs, ts, P, "", kw.get("time_aware", True), kw.get("bidirectional", False),
+                                kw.get("use_skip_connection", True), kw.get("window_size", 3),
+                                kw.get("aggregation", "mean"), kw.get("residual", True))
+    return outs, xs
+
+
+@pytest.mark.parametrize("case", G.case_names("tprop_"))
+def test_temporal_propagation_intended(case):
+    from oracle import tprop_oracle
+    meta, t = G.load(case)
+    sd = {k[3:].lstrip("."): v for k, v in t.items() if k.startswith("sd.")}
+    P = _leaves(sd)
+    # the oracle takes "<prefix>.<param>" names; with an empty prefix strip the leading dot it adds
+    P = _DotKeys(P)
+    outs, xs = _tprop_run(meta, t, P, tprop_oracle)
+    for i, o in enumerate(outs):
+        G.assert_close("out.%d" % i, o, t["out.%d" % i], ATOL, RTOL)
+    sum((o * t["in.grad_out.%d" % i]).sum() for i, o in enumerate(outs)).backward()
+    for i, x in enumerate(xs):
+        G.assert_close("grad.x.%d" % i, x.grad, t["grad.x.%d" % i], ATOL, RTOL)
+    for k, v in P.items():
+        if "grad." + k in t:
+            G.assert_close("grad." + k, v.grad, t["grad." + k], ATOL, RTOL)
+        else:
+            assert v.grad is None or not v.grad.any(), k
+
+
+class _DotKeys(dict):
+    """Parameter mapping that also answers ".name" for "name" (empty module prefix)."""
+
+    def __getitem__(self, k):
+        return super().__getitem__(k[1:] if k.startswith(".") else k)
+
+    def __contains__(self, k):
+        return super().__contains__(k[1:] if k.startswith(".") else k)
+
+    def get(self, k, d=None):
+        return self[k] if k in self else d
