@@ -74,12 +74,13 @@ float tagan_uniform(uint64_t seed, uint64_t stream, uint32_t counter);
  * Capacity of col/csc_* must be >= n_edges + n_nodes.  *nnz_out and *err_out
  * are device int64/int32 scalars; *err_out != 0 if any index was out of range
  * (those edges are dropped; the reference raises IndexError).
- * n_nodes < 2^31.
+ * max_graph_nodes = the largest snapshot's node count (<= 0: n_nodes); it sets
+ * the width of the local-id field of the sort keys.  n_nodes < 2^31.
  * ------------------------------------------------------------------------- */
 size_t tagan_csr_build_workspace(int64_t n_edges, int64_t n_nodes);
 int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges,
                     const int64_t* edge_ptr, const int64_t* node_ptr, int32_t n_graphs,
-                    int64_t n_nodes,
+                    int64_t n_nodes, int64_t max_graph_nodes,
                     int32_t* rowptr, int32_t* col,
                     int32_t* csc_ptr, int32_t* csc_row, int32_t* csc_eid,
                     int64_t* nnz_out, int32_t* err_out,

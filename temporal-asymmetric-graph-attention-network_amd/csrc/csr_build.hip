@@ -1,8 +1,10 @@
 // Snapshot CSR/CSC builder: the sparse form of graph_attention.py:96-105
 //   adj = zeros(N,N); adj[edge_index[0], edge_index[1]] = 1; adj += eye(N)
 // for a block-diagonal batch of snapshots.  Integer/byte work: HBM-bound,
-// no MFMA.  Keys (src<<32 | dst) are radix-sorted with rocPRIM, de-duplicated,
-// scattered into CSR; the CSC (with CSR edge ids) is a second key-value sort.
+// no MFMA.  Keys (global src << LB | local dst), LB = bits of the largest
+// snapshot, are radix-sorted with rocPRIM over only LB + bits(N) bits (33 at
+// C2 instead of 64), de-duplicated, scattered into CSR; the CSC (with CSR edge
+// ids) is a second key-value sort of (global dst << LB | local src).
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -24,12 +26,17 @@ __device__ __forceinline__ int find_graph(const int64_t* __restrict__ edge_ptr, 
     return lo;
 }
 
+// Graph of global node n (n < N): binary search in node_ptr[0..G].
+__device__ __forceinline__ int64_t node_base(const int64_t* __restrict__ node_ptr, int G, int64_t n) {
+    return node_ptr[find_graph(node_ptr, G, n)];
+}
+
 __global__ void __launch_bounds__(BLK) k_make_keys(const int64_t* __restrict__ ei, int64_t ld_ei, int64_t E,
                                                    const int64_t* __restrict__ edge_ptr,
                                                    const int64_t* __restrict__ node_ptr, int G,
-                                                   int64_t N, uint64_t* __restrict__ keys,
+                                                   int64_t N, int LB, uint64_t* __restrict__ keys,
                                                    int32_t* __restrict__ err) {
-    const uint64_t sentinel = (uint64_t)N << 32;
+    const uint64_t sentinel = (uint64_t)N << LB;
     for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < E + N; p += (int64_t)gridDim.x * BLK) {
         uint64_t key;
         if (p < E) {
@@ -43,32 +50,34 @@ __global__ void __launch_bounds__(BLK) k_make_keys(const int64_t* __restrict__ e
                 atomicOr(err, 1);
                 key = sentinel;
             } else {
-                key = ((uint64_t)(base + s) << 32) | (uint64_t)(base + d);
+                key = ((uint64_t)(base + s) << LB) | (uint64_t)d;
             }
         } else {
-            const uint64_t i = (uint64_t)(p - E);   // self-loop of global node i (the "+ eye")
-            key = (i << 32) | i;
+            const int64_t i = p - E;                // self-loop of global node i (the "+ eye")
+            key = ((uint64_t)i << LB) | (uint64_t)(i - node_base(node_ptr, G, i));
         }
         keys[p] = key;
     }
 }
 
 __global__ void __launch_bounds__(BLK) k_unique_flags(const uint64_t* __restrict__ keys, int64_t M, int64_t N,
-                                                      int32_t* __restrict__ flags) {
-    const uint64_t sentinel = (uint64_t)N << 32;
+                                                      int LB, int32_t* __restrict__ flags) {
+    const uint64_t sentinel = (uint64_t)N << LB;
     for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
         const uint64_t k = keys[p];
         flags[p] = (k < sentinel && (p == 0 || keys[p - 1] != k)) ? 1 : 0;
     }
 }
 
-// Scatter unique keys into CSR; emit CSC keys (dst<<32 | src) with value = CSR position.
+// Scatter unique keys into CSR; emit CSC keys (dst << LB | local src) with value = CSR position.
 __global__ void __launch_bounds__(BLK) k_scatter_csr(const uint64_t* __restrict__ keys,
                                                      const int32_t* __restrict__ flags,
-                                                     const int32_t* __restrict__ pos, int64_t M, int64_t N,
+                                                     const int32_t* __restrict__ pos, int64_t M, int64_t N, int LB,
+                                                     const int64_t* __restrict__ node_ptr, int G,
                                                      int32_t* __restrict__ rowptr, int32_t* __restrict__ col,
                                                      uint64_t* __restrict__ ckeys, int32_t* __restrict__ cvals,
                                                      int64_t* __restrict__ nnz_out) {
+    const uint64_t lmask = ((uint64_t)1 << LB) - 1;
     for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
         if (p == M - 1) {
             const int64_t nnz = (int64_t)pos[p] + flags[p];
@@ -77,19 +86,21 @@ __global__ void __launch_bounds__(BLK) k_scatter_csr(const uint64_t* __restrict_
         }
         if (!flags[p]) continue;
         const uint64_t k = keys[p];
-        const int32_t r = (int32_t)(k >> 32), c = (int32_t)(k & 0xffffffffu);
+        const int64_t r = (int64_t)(k >> LB);
+        const int64_t base = node_base(node_ptr, G, r);
+        const int32_t c = (int32_t)(base + (int64_t)(k & lmask));
         const int32_t q = pos[p];
         col[q] = c;
-        if (p == 0 || (int32_t)(keys[p - 1] >> 32) != r) rowptr[r] = q;   // every row has its self-loop
-        ckeys[q] = ((uint64_t)c << 32) | (uint64_t)r;
+        if (p == 0 || (int64_t)(keys[p - 1] >> LB) != r) rowptr[r] = q;   // every row has its self-loop
+        ckeys[q] = ((uint64_t)c << LB) | (uint64_t)(r - base);
         cvals[q] = q;
     }
 }
 
 __global__ void __launch_bounds__(BLK) k_fill_tail(uint64_t* __restrict__ ckeys, int32_t* __restrict__ cvals,
-                                                   const int64_t* __restrict__ nnz_p, int64_t M, int64_t N) {
+                                                   const int64_t* __restrict__ nnz_p, int64_t M, int64_t N, int LB) {
     const int64_t nnz = *nnz_p;
-    const uint64_t sentinel = (uint64_t)N << 32;
+    const uint64_t sentinel = (uint64_t)N << LB;
     for (int64_t p = nnz + blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
         ckeys[p] = sentinel;
         cvals[p] = -1;
@@ -98,16 +109,18 @@ __global__ void __launch_bounds__(BLK) k_fill_tail(uint64_t* __restrict__ ckeys,
 
 __global__ void __launch_bounds__(BLK) k_scatter_csc(const uint64_t* __restrict__ ckeys,
                                                      const int32_t* __restrict__ cvals,
-                                                     const int64_t* __restrict__ nnz_p, int64_t N,
+                                                     const int64_t* __restrict__ nnz_p, int64_t N, int LB,
+                                                     const int64_t* __restrict__ node_ptr, int G,
                                                      int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_row,
                                                      int32_t* __restrict__ csc_eid) {
     const int64_t nnz = *nnz_p;
+    const uint64_t lmask = ((uint64_t)1 << LB) - 1;
     for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * BLK) {
         const uint64_t k = ckeys[p];
-        const int32_t c = (int32_t)(k >> 32);
-        csc_row[p] = (int32_t)(k & 0xffffffffu);
+        const int64_t c = (int64_t)(k >> LB);
+        csc_row[p] = (int32_t)(node_base(node_ptr, G, c) + (int64_t)(k & lmask));
         csc_eid[p] = cvals[p];
-        if (p == 0 || (int32_t)(ckeys[p - 1] >> 32) != c) csc_ptr[c] = (int32_t)p;
+        if (p == 0 || (int64_t)(ckeys[p - 1] >> LB) != c) csc_ptr[c] = (int32_t)p;
         if (p == nnz - 1) csc_ptr[N] = (int32_t)nnz;
     }
 }
@@ -164,7 +177,8 @@ size_t tagan_csr_build_workspace(int64_t n_edges, int64_t n_nodes) {
 }
 
 int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, const int64_t* edge_ptr,
-                    const int64_t* node_ptr, int32_t n_graphs, int64_t n_nodes, int32_t* rowptr, int32_t* col,
+                    const int64_t* node_ptr, int32_t n_graphs, int64_t n_nodes, int64_t max_graph_nodes,
+                    int32_t* rowptr, int32_t* col,
                     int32_t* csc_ptr, int32_t* csc_row, int32_t* csc_eid, int64_t* nnz_out, int32_t* err_out,
                     void* workspace, size_t workspace_bytes, void* stream) {
     using namespace tagan;
@@ -190,15 +204,18 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     void* temp = ws + w.temp;
     const int64_t M = n_edges + n_nodes;
     const int bits = key_bits(n_nodes);
+    TAGAN_REQUIRE(max_graph_nodes <= n_nodes, TAGAN_ERR_ARG, "tagan_csr_build: max_graph_nodes > n_nodes");
+    const int LB = key_bits(max_graph_nodes > 0 ? max_graph_nodes : n_nodes);   // local ids 0..max-1 fit
+    const int sort_bits = LB + bits;
 
     TAGAN_CHECK_HIP(hipMemsetAsync(err_out, 0, sizeof(int32_t), s), "csr_build memset");
     k_make_keys<<<grid_for(M), BLK, 0, s>>>(edge_index, ld_ei, n_edges, edge_ptr, node_ptr, n_graphs, n_nodes,
-                                            keys_a, err_out);
+                                            LB, keys_a, err_out);
     TAGAN_CHECK_LAUNCH("csr_build.make_keys");
     size_t tb = w.temp_bytes;
-    TAGAN_CHECK_HIP(rocprim::radix_sort_keys(temp, tb, keys_a, keys_b, (size_t)M, 0, 32 + bits, s),
+    TAGAN_CHECK_HIP(rocprim::radix_sort_keys(temp, tb, keys_a, keys_b, (size_t)M, 0, sort_bits, s),
                     "csr_build radix_sort_keys");
-    k_unique_flags<<<grid_for(M), BLK, 0, s>>>(keys_b, M, n_nodes, flags);
+    k_unique_flags<<<grid_for(M), BLK, 0, s>>>(keys_b, M, n_nodes, LB, flags);
     TAGAN_CHECK_LAUNCH("csr_build.unique_flags");
     tb = w.temp_bytes;
     TAGAN_CHECK_HIP(rocprim::exclusive_scan(temp, tb, flags, pos, 0, (size_t)M, rocprim::plus<int32_t>(), s),
@@ -206,16 +223,17 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     // keys_a is free now: reuse it as the unsorted CSC key buffer; cvals via csc_eid scratch? use csc_row.
     uint64_t* ckeys_a = keys_a;
     int32_t* cvals_a = csc_row;   // staging only; overwritten by the final CSC scatter
-    k_scatter_csr<<<grid_for(M), BLK, 0, s>>>(keys_b, flags, pos, M, n_nodes, rowptr, col, ckeys_a, cvals_a,
-                                              nnz_out);
+    k_scatter_csr<<<grid_for(M), BLK, 0, s>>>(keys_b, flags, pos, M, n_nodes, LB, node_ptr, n_graphs, rowptr, col,
+                                              ckeys_a, cvals_a, nnz_out);
     TAGAN_CHECK_LAUNCH("csr_build.scatter_csr");
-    k_fill_tail<<<grid_for(M), BLK, 0, s>>>(ckeys_a, cvals_a, nnz_out, M, n_nodes);
+    k_fill_tail<<<grid_for(M), BLK, 0, s>>>(ckeys_a, cvals_a, nnz_out, M, n_nodes, LB);
     TAGAN_CHECK_LAUNCH("csr_build.fill_tail");
     tb = w.temp_bytes;
     TAGAN_CHECK_HIP(rocprim::radix_sort_pairs(temp, tb, ckeys_a, ckeys_b, cvals_a, cvals_b, (size_t)M, 0,
-                                              32 + bits, s),
+                                              sort_bits, s),
                     "csr_build radix_sort_pairs");
-    k_scatter_csc<<<grid_for(M), BLK, 0, s>>>(ckeys_b, cvals_b, nnz_out, n_nodes, csc_ptr, csc_row, csc_eid);
+    k_scatter_csc<<<grid_for(M), BLK, 0, s>>>(ckeys_b, cvals_b, nnz_out, n_nodes, LB, node_ptr, n_graphs, csc_ptr,
+                                              csc_row, csc_eid);
     TAGAN_CHECK_LAUNCH("csr_build.scatter_csc");
     return TAGAN_OK;
 }

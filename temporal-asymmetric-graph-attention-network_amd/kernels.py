@@ -107,7 +107,7 @@ def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], va
     n_ptr = [0]
     for n in node_counts:
         n_ptr.append(n_ptr[-1] + int(n))
-    meta = torch.tensor(e_ptr + n_ptr, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+    meta = torch.tensor(e_ptr + n_ptr, dtype=torch.int64).to(dev)   # a few hundred bytes; no pinned alloc per call
     edge_ptr, node_ptr = meta[:len(e_ptr)], meta[len(e_ptr):]
     cap = E + N
     buf = torch.empty(2 * (N + 1) + 3 * cap, dtype=torch.int32, device=dev)
@@ -120,7 +120,8 @@ def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], va
     L = lib()
     ws_bytes = L.tagan_csr_build_workspace(E, N)
     ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=dev)
-    check(L.tagan_csr_build(ptr(ei), E, E, ptr(edge_ptr), ptr(node_ptr), len(eis), N, ptr(rowptr), ptr(col),
+    check(L.tagan_csr_build(ptr(ei), E, E, ptr(edge_ptr), ptr(node_ptr), len(eis), N, max(n_ptr[i + 1] - n_ptr[i]
+                            for i in range(len(eis))), ptr(rowptr), ptr(col),
                             ptr(csc_ptr), ptr(csc_row), ptr(csc_eid), ptr(nnz), ptr(err), ptr(ws), ws_bytes,
                             stream_of(ei)), "tagan_csr_build")
     if validate and int(err.item()) != 0:
