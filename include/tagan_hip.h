@@ -276,6 +276,20 @@ int tagan_membank_scale(const tagan_membank* bank, float factor, void* stream);
 /* Copy every stored node of src into a freshly formatted dst (growth / tombstone purge). */
 int tagan_membank_rehash(const tagan_membank* src, const tagan_membank* dst, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Graph-feature pooling.  Replaces model.py:377-427: the reference pools the
+ * node-major temporal output [N, T, H] as gf[t] = mean(out.view(T, -1, H)[t]),
+ * i.e. the mean of node-major flat rows [t*N, (t+1)*N) (flat row f = n*T + t').
+ * Input here is time-major x[T][N][H] with row strides ld_row (node) and
+ * ld_t (step), in elements; out = gf [T, H].  Deterministic (ordered partials).
+ * Backward: dx[t'][n] = g[(n*T + t') / N] / N.
+ * ------------------------------------------------------------------------- */
+size_t tagan_pool_workspace(int32_t T, int32_t H);
+int tagan_pool_fwd(int dtype, int32_t T, int64_t N, int32_t H, const float* x, int64_t ld_row, int64_t ld_t,
+                   float* out, void* workspace, size_t workspace_bytes, void* stream);
+int tagan_pool_bwd(int dtype, int32_t T, int64_t N, int32_t H, const float* g, float* dx, int64_t ld_row,
+                   int64_t ld_t, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,6 +31,9 @@ _SIGNATURES = {
     "tagan_device_arch": (_c.c_int, [_c.c_char_p, _c.c_int]),
     "tagan_uniform": (_f32, [_u64, _u64, _c.c_uint32]),
     "tagan_csr_build_workspace": (_sz, [_i64, _i64]),
+    "tagan_pool_workspace": (_sz, [_i32, _i32]),
+    "tagan_pool_fwd": (_c.c_int, [_c.c_int, _i32, _i64, _i32, _p, _i64, _i64, _p, _p, _sz, _p]),
+    "tagan_pool_bwd": (_c.c_int, [_c.c_int, _i32, _i64, _i32, _p, _p, _i64, _i64, _p]),
     "tagan_csr_build": (_c.c_int, [_p, _i64, _i64, _p, _p, _i32, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _sz,
                                    _p]),
     "tagan_chunk_capacity": (_i64, [_i64, _i64, _i32]),

@@ -93,12 +93,12 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nblk) {
 // Deterministic column sums of a [nblk, n] partials table (per-block dγ/dβ, bias-table
 // grads): one 1024-thread block per 64 columns, wave w sums rows w, w+16, ... with four
 // independent accumulators (loads in flight), then a fixed-order LDS tree.  Column x < split
-// goes to out0[x], the rest to out1[x - split] (either may be null).
+// goes to out0[x], the rest to out1[x - split] (either may be null), times ``scale``.
 constexpr int COLSUM_BLK = 1024;
 namespace {
 __global__ void __launch_bounds__(COLSUM_BLK) k_colsum_parts(const float* __restrict__ part, int nblk, int n,
                                                             float* __restrict__ out0, float* __restrict__ out1,
-                                                            int split) {
+                                                            int split, float scale) {
     constexpr int NW = COLSUM_BLK / WAVE;
     __shared__ float red[NW][WAVE];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x >> 6;
@@ -122,16 +122,17 @@ __global__ void __launch_bounds__(COLSUM_BLK) k_colsum_parts(const float* __rest
         __syncthreads();
     }
     if (w == 0 && x < n) {
-        if (x < split) { if (out0) out0[x] = red[0][lane]; }
-        else if (out1) out1[x - split] = red[0][lane];
+        const float v = scale == 1.f ? red[0][lane] : red[0][lane] * scale;
+        if (x < split) { if (out0) out0[x] = v; }
+        else if (out1) out1[x - split] = v;
     }
 }
 
 }  // namespace
 
 static inline void launch_colsum(const float* part, int nblk, int n, float* out0, float* out1, int split,
-                                 hipStream_t s) {
-    k_colsum_parts<<<(n + WAVE - 1) / WAVE, COLSUM_BLK, 0, s>>>(part, nblk, n, out0, out1, split);
+                                 hipStream_t s, float scale = 1.f) {
+    k_colsum_parts<<<(n + WAVE - 1) / WAVE, COLSUM_BLK, 0, s>>>(part, nblk, n, out0, out1, split, scale);
 }
 
 }  // namespace tagan

@@ -244,40 +244,44 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
 namespace tagan {
 namespace {
 
+// Per segment: {chunks, is_multi, partial slots}; ONE exclusive scan over the triple gives each
+// segment's first chunk, its index among multi segments and its first partial slot.
+struct Tri {
+    int32_t a, b, c;
+};
+struct TriPlus {
+    __host__ __device__ Tri operator()(const Tri& x, const Tri& y) const { return Tri{x.a + y.a, x.b + y.b, x.c + y.c}; }
+};
+
 __global__ void __launch_bounds__(BLK) k_chunk_count(const int32_t* __restrict__ ptr, int64_t n, int chunk,
-                                                     int32_t* __restrict__ nch, int32_t* __restrict__ ismulti,
-                                                     int32_t* __restrict__ npart) {
+                                                     Tri* __restrict__ cnt) {
     for (int64_t s = blockIdx.x * (int64_t)BLK + threadIdx.x; s < n; s += (int64_t)gridDim.x * BLK) {
         const int deg = ptr[s + 1] - ptr[s];
         const int c = deg <= chunk ? 1 : (deg + chunk - 1) / chunk;
-        nch[s] = c;
-        ismulti[s] = c > 1;
-        npart[s] = c > 1 ? c : 0;
+        cnt[s] = Tri{c, c > 1 ? 1 : 0, c > 1 ? c : 0};
     }
 }
 
 __global__ void __launch_bounds__(BLK) k_chunk_fill(const int32_t* __restrict__ ptr, int64_t n, int chunk,
-                                                    const int32_t* __restrict__ nch,
-                                                    const int32_t* __restrict__ cstart,
-                                                    const int32_t* __restrict__ midx,
-                                                    const int32_t* __restrict__ pbase,
+                                                    const Tri* __restrict__ cnt, const Tri* __restrict__ off,
                                                     int32_t* __restrict__ chunk_ptr, int32_t* __restrict__ seg,
                                                     int32_t* __restrict__ beg, int32_t* __restrict__ part,
                                                     int32_t* __restrict__ multi, int32_t* __restrict__ counts) {
     for (int64_t s = blockIdx.x * (int64_t)BLK + threadIdx.x; s < n; s += (int64_t)gridDim.x * BLK) {
-        const int c = nch[s], c0 = cstart[s], e0 = ptr[s];
-        chunk_ptr[s] = c0;
+        const int c = cnt[s].a, e0 = ptr[s];
+        const Tri o = off[s];
+        chunk_ptr[s] = o.a;
         for (int k = 0; k < c; ++k) {
-            seg[c0 + k] = (int32_t)s;
-            beg[c0 + k] = e0 + k * chunk;
-            part[c0 + k] = c > 1 ? pbase[s] + k : -1;
+            seg[o.a + k] = (int32_t)s;
+            beg[o.a + k] = e0 + k * chunk;
+            part[o.a + k] = c > 1 ? o.c + k : -1;
         }
-        if (c > 1) multi[midx[s]] = (int32_t)s;
+        if (c > 1) multi[o.b] = (int32_t)s;
         if (s == n - 1) {
-            chunk_ptr[n] = c0 + c;
-            counts[0] = c0 + c;
-            counts[1] = midx[s] + (c > 1);
-            counts[2] = pbase[s] + (c > 1 ? c : 0);
+            chunk_ptr[n] = o.a + c;
+            counts[0] = o.a + c;
+            counts[1] = o.b + (c > 1);
+            counts[2] = o.c + (c > 1 ? c : 0);
         }
     }
 }
@@ -299,9 +303,8 @@ size_t tagan_graph_chunks_workspace(int64_t n) {
     using namespace tagan;
     if (n <= 0) return 0;
     size_t t = 0;
-    (void)rocprim::exclusive_scan(nullptr, t, (int32_t*)nullptr, (int32_t*)nullptr, 0, (size_t)n,
-                                  rocprim::plus<int32_t>());
-    return 6 * align_up((size_t)n * 4, 256) + align_up(t, 256);
+    (void)rocprim::exclusive_scan(nullptr, t, (Tri*)nullptr, (Tri*)nullptr, Tri{0, 0, 0}, (size_t)n, TriPlus());
+    return 2 * align_up((size_t)n * sizeof(Tri), 256) + align_up(t, 256);
 }
 
 int tagan_graph_chunks(const int32_t* seg_ptr, int64_t n, int32_t chunk, int32_t* chunk_ptr, int32_t* chunk_seg,
@@ -315,23 +318,15 @@ int tagan_graph_chunks(const int32_t* seg_ptr, int64_t n, int32_t chunk, int32_t
     TAGAN_REQUIRE(workspace && workspace_bytes >= need, TAGAN_ERR_WORKSPACE, "tagan_graph_chunks: workspace");
     hipStream_t s = as_stream(stream);
     char* ws = (char*)workspace;
-    const size_t a = align_up((size_t)n * 4, 256);
-    int32_t* nch = (int32_t*)ws;
-    int32_t* ism = (int32_t*)(ws + a);
-    int32_t* npt = (int32_t*)(ws + 2 * a);
-    int32_t* cst = (int32_t*)(ws + 3 * a);
-    int32_t* mid = (int32_t*)(ws + 4 * a);
-    int32_t* pbs = (int32_t*)(ws + 5 * a);
-    void* temp = ws + 6 * a;
-    size_t tb = need - 6 * a;
-    k_chunk_count<<<grid_for(n), BLK, 0, s>>>(seg_ptr, n, chunk, nch, ism, npt);
+    const size_t a = align_up((size_t)n * sizeof(Tri), 256);
+    Tri* cnt = (Tri*)ws;
+    Tri* off = (Tri*)(ws + a);
+    void* temp = ws + 2 * a;
+    size_t tb = need - 2 * a;
+    k_chunk_count<<<grid_for(n), BLK, 0, s>>>(seg_ptr, n, chunk, cnt);
     TAGAN_CHECK_LAUNCH("graph_chunks.count");
-    TAGAN_CHECK_HIP(rocprim::exclusive_scan(temp, tb, nch, cst, 0, (size_t)n, rocprim::plus<int32_t>(), s), "scan");
-    tb = need - 6 * a;
-    TAGAN_CHECK_HIP(rocprim::exclusive_scan(temp, tb, ism, mid, 0, (size_t)n, rocprim::plus<int32_t>(), s), "scan");
-    tb = need - 6 * a;
-    TAGAN_CHECK_HIP(rocprim::exclusive_scan(temp, tb, npt, pbs, 0, (size_t)n, rocprim::plus<int32_t>(), s), "scan");
-    k_chunk_fill<<<grid_for(n), BLK, 0, s>>>(seg_ptr, n, chunk, nch, cst, mid, pbs, chunk_ptr, chunk_seg, chunk_beg,
+    TAGAN_CHECK_HIP(rocprim::exclusive_scan(temp, tb, cnt, off, Tri{0, 0, 0}, (size_t)n, TriPlus(), s), "scan");
+    k_chunk_fill<<<grid_for(n), BLK, 0, s>>>(seg_ptr, n, chunk, cnt, off, chunk_ptr, chunk_seg, chunk_beg,
                                              chunk_part, multi_seg, counts);
     TAGAN_CHECK_LAUNCH("graph_chunks.fill");
     return TAGAN_OK;

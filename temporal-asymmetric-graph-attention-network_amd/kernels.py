@@ -416,3 +416,36 @@ def dropout_add_layer_norm(a, b, ln: torch.nn.LayerNorm, p: float):
     if a.is_cuda and lib().tagan_layernorm_supported(a.shape[-1]):
         return AddLayerNormFn.apply(a, b, ln.weight, ln.bias, ln.eps, float(p), new_seed() if p > 0 else 0)
     return ln(torch.nn.functional.dropout(a, p, True) + b)
+
+
+# ----------------------------------------------------------------------------- pooling
+class PoolFn(torch.autograd.Function):
+    """gf [T, H] of model.py:377-427 from the time-major temporal output [T, N, H] (csrc/pool.hip)."""
+
+    @staticmethod
+    def forward(ctx, x_tm):
+        require_hip(x_tm)
+        T, N, H = x_tm.shape
+        assert x_tm.stride(2) == 1 and x_tm.dtype == torch.float32
+        out = torch.empty(T, H, device=x_tm.device, dtype=torch.float32)
+        L = lib()
+        wsb = L.tagan_pool_workspace(T, H)
+        ws = torch.empty(int(wsb), dtype=torch.uint8, device=x_tm.device)
+        check(L.tagan_pool_fwd(_lib.TAGAN_F32, T, N, H, ptr(x_tm), x_tm.stride(1), x_tm.stride(0), ptr(out), ptr(ws),
+                               wsb, stream_of(x_tm)), "tagan_pool_fwd")
+        ctx.shape = (T, N, H)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        T, N, H = ctx.shape
+        g = g.contiguous()
+        dx = torch.empty(T, N, H, device=g.device, dtype=torch.float32)
+        check(lib().tagan_pool_bwd(_lib.TAGAN_F32, T, N, H, ptr(g), ptr(dx), H, N * H, stream_of(g)),
+              "tagan_pool_bwd")
+        return dx
+
+
+def pool_time_major(x_tm: torch.Tensor) -> torch.Tensor:
+    return PoolFn.apply(x_tm)
+

@@ -24,7 +24,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .kernels import build_graph, layer_norm, linear
+from .kernels import build_graph, layer_norm, linear, pool_time_major
 from .layers.classification import ClassificationModule, TemporalLossModule
 from .layers.graph_attention import TAGANGraphAttention
 from .layers.temporal_attention import AsymmetricTemporalAttention, MaskBroadcastError
@@ -143,6 +143,8 @@ class TAGAN(nn.Module):
         [t*N, (t+1)*N) — not a per-snapshot mean.  Flat row r = n*T + t' lives at
         time-major row t'*N + n.
         """
+        if out_tm.shape[-1] % 4 == 0 and out_tm.stride(2) == 1:
+            return pool_time_major(out_tm)                      # csrc/pool.hip
         T, N, H = out_tm.shape
         node_major = out_tm.transpose(0, 1).reshape(T, N, H)   # == out.view(T, -1, H) of the reference
         return node_major.mean(1)
