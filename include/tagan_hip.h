@@ -214,14 +214,16 @@ int tagan_layernorm_supported(int32_t H);
 int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, const float* b,
                             float p_drop, uint64_t seed, const float* gamma, const float* beta,
                             float eps, float* s_out, float* y, float* mean, float* rstd, void* stream);
-/* Backward: ds = dL/ds (the residual branch's gradient), da = ds masked/scaled
- * by the same dropout (the projection branch's gradient), dgamma/dbeta [H]
- * (block partials summed in block order).  Any of ds/da/dgamma/dbeta may be NULL. */
+/* Backward: ds = dL/ds (+ dres when given: the gradient of the LN input's other
+ * consumer, fused instead of a separate add), da = dL/ds masked/scaled by the same
+ * dropout (the projection branch's gradient), dgamma/dbeta [H], dsum_a [H] = column
+ * sums of da (the projection's bias gradient); block partials summed in block order.
+ * Any of dres/ds/da/dgamma/dbeta/dsum_a may be NULL. */
 size_t tagan_layernorm_bwd_workspace(int64_t M, int32_t H);
 int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s, const float* mean,
-                        const float* rstd, const float* gamma, const float* dy, float p_drop, uint64_t seed,
-                        float* ds, float* da, float* dgamma, float* dbeta,
-                        void* workspace, size_t workspace_bytes, void* stream);
+                        const float* rstd, const float* gamma, const float* dy, const float* dres,
+                        float p_drop, uint64_t seed, float* ds, float* da, float* dgamma, float* dbeta,
+                        float* dsum_a, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * NodeMemoryBank on the device.  Replaces src/tagan/utils/memory_bank.py:14-360

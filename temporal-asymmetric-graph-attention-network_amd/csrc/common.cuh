@@ -90,7 +90,7 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nblk) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
-// Deterministic column sums of a [nblk, n] partials table (per-block dγ/dβ, bias-table
+// Deterministic column sums of a [nblk, n] (row stride ld) partials table (per-block dγ/dβ, bias-table
 // grads): one 1024-thread block per 64 columns, wave w sums rows w, w+16, ... with four
 // independent accumulators (loads in flight), then a fixed-order LDS tree.  Column x < split
 // goes to out0[x], the rest to out1[x - split] (either may be null), times ``scale``.
@@ -98,7 +98,7 @@ constexpr int COLSUM_BLK = 1024;
 namespace {
 __global__ void __launch_bounds__(COLSUM_BLK) k_colsum_parts(const float* __restrict__ part, int nblk, int n,
                                                             float* __restrict__ out0, float* __restrict__ out1,
-                                                            int split, float scale) {
+                                                            int split, float scale, int64_t ld) {
     constexpr int NW = COLSUM_BLK / WAVE;
     __shared__ float red[NW][WAVE];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x >> 6;
@@ -107,12 +107,12 @@ __global__ void __launch_bounds__(COLSUM_BLK) k_colsum_parts(const float* __rest
     if (x < n) {
         int b = w;
         for (; b + 3 * NW < nblk; b += 4 * NW) {
-            s0 += part[(int64_t)b * n + x];
-            s1 += part[(int64_t)(b + NW) * n + x];
-            s2 += part[(int64_t)(b + 2 * NW) * n + x];
-            s3 += part[(int64_t)(b + 3 * NW) * n + x];
+            s0 += part[(int64_t)b * ld + x];
+            s1 += part[(int64_t)(b + NW) * ld + x];
+            s2 += part[(int64_t)(b + 2 * NW) * ld + x];
+            s3 += part[(int64_t)(b + 3 * NW) * ld + x];
         }
-        for (; b < nblk; b += NW) s0 += part[(int64_t)b * n + x];
+        for (; b < nblk; b += NW) s0 += part[(int64_t)b * ld + x];
     }
     red[w][lane] = (s0 + s1) + (s2 + s3);
     __syncthreads();
@@ -130,9 +130,11 @@ __global__ void __launch_bounds__(COLSUM_BLK) k_colsum_parts(const float* __rest
 
 }  // namespace
 
+// ld = row stride of the partials table (default n)
 static inline void launch_colsum(const float* part, int nblk, int n, float* out0, float* out1, int split,
-                                 hipStream_t s, float scale = 1.f) {
-    k_colsum_parts<<<(n + WAVE - 1) / WAVE, COLSUM_BLK, 0, s>>>(part, nblk, n, out0, out1, split, scale);
+                                 hipStream_t s, float scale = 1.f, int64_t ld = -1) {
+    k_colsum_parts<<<(n + WAVE - 1) / WAVE, COLSUM_BLK, 0, s>>>(part, nblk, n, out0, out1, split, scale,
+                                                                ld < 0 ? n : ld);
 }
 
 }  // namespace tagan

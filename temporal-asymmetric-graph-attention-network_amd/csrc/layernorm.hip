@@ -38,9 +38,10 @@ struct LnArgs {
     // backward
     const float* s_in;
     const float* dy;
+    const float* dres;   // optional gradient added to ds (the other consumer of the LN input)
     float* ds;
     float* da;
-    float* part;   // [gridDim.x, 2H]
+    float* part;   // [gridDim.x, 3H]: dgamma | dbeta | column sums of da (projection-bias gradient)
 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -110,14 +111,15 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
 template <int LPR, int NV>
 __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
     constexpr int RPW = WAVE / LPR;
-    __shared__ float red[BLK / WAVE][RPW][2 * 4 * NV * LPR];
+    __shared__ float red[BLK / WAVE][RPW][3 * 4 * NV * LPR];
     const int lane = threadIdx.x & (WAVE - 1), sl = lane % LPR, sub = lane / LPR, w = threadIdx.x >> 6;
     const int H = A.H;
-    float4 dg[NV], db[NV];
+    float4 dg[NV], db[NV], dsa[NV];
 #pragma unroll
     for (int n = 0; n < NV; ++n) {
         dg[n] = make_float4(0.f, 0.f, 0.f, 0.f);
         db[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+        dsa[n] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const int64_t nwaves = (int64_t)gridDim.x * (BLK / WAVE);
     for (int64_t wave = blockIdx.x * (int64_t)(BLK / WAVE) + w; wave * RPW < A.M; wave += nwaves) {
@@ -151,8 +153,18 @@ __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
             o.y = rstd * (gd[n].y - c1 * xh[n].y - c2);
             o.z = rstd * (gd[n].z - c1 * xh[n].z - c2);
             o.w = rstd * (gd[n].w - c1 * xh[n].w - c2);
-            if (A.ds) st4(A.ds + row * H + c, o);
-            if (A.da) st4(A.da + row * H + c, drop4(A, o, row, c));
+            if (A.da || A.part) {
+                const float4 a = drop4(A, o, row, c);
+                if (A.da) st4(A.da + row * H + c, a);
+                dsa[n].x += a.x; dsa[n].y += a.y; dsa[n].z += a.z; dsa[n].w += a.w;
+            }
+            if (A.ds) {
+                if (A.dres) {
+                    const float4 e = ld4(A.dres + row * H + c);
+                    o.x += e.x; o.y += e.y; o.z += e.z; o.w += e.w;
+                }
+                st4(A.ds + row * H + c, o);
+            }
         }
     }
     if (A.part) {
@@ -161,13 +173,14 @@ __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
             const int c = (n * LPR + sl) * 4;
             st4(&red[w][sub][c], dg[n]);
             st4(&red[w][sub][H + c], db[n]);
+            st4(&red[w][sub][2 * H + c], dsa[n]);
         }
         __syncthreads();
-        for (int x = threadIdx.x; x < 2 * H; x += BLK) {
+        for (int x = threadIdx.x; x < 3 * H; x += BLK) {
             float s = 0.f;
             for (int ww = 0; ww < BLK / WAVE; ++ww)
                 for (int ss = 0; ss < RPW; ++ss) s += red[ww][ss][x];
-            A.part[(int64_t)blockIdx.x * 2 * H + x] = s;
+            A.part[(int64_t)blockIdx.x * 3 * H + x] = s;
         }
     }
 }
@@ -222,23 +235,24 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
 
 size_t tagan_layernorm_bwd_workspace(int64_t M, int32_t H) {
     (void)M;
-    return (size_t)tagan::LN_BWD_BLOCKS * 2 * H * sizeof(float);
+    return (size_t)tagan::LN_BWD_BLOCKS * 3 * H * sizeof(float);
 }
 
 int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, const float* mean, const float* rstd,
-                        const float* gamma, const float* dy, float p_drop, uint64_t seed, float* ds, float* da,
-                        float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes, void* stream) {
+                        const float* gamma, const float* dy, const float* dres, float p_drop, uint64_t seed,
+                        float* ds, float* da, float* dgamma, float* dbeta, float* dsum_a, void* workspace,
+                        size_t workspace_bytes, void* stream) {
     using namespace tagan;
     int lpr, nv;
     TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "layernorm: dtype %d", dtype);
     TAGAN_REQUIRE(geometry(H, lpr, nv), TAGAN_ERR_UNSUPPORTED, "layernorm: H=%d unsupported", H);
     TAGAN_REQUIRE(M > 0 && s_in && mean && rstd && gamma && dy, TAGAN_ERR_ARG, "layernorm_bwd: bad args");
-    const bool want = dgamma || dbeta;
+    const bool want = dgamma || dbeta || dsum_a;
     TAGAN_REQUIRE(!want || (workspace && workspace_bytes >= tagan_layernorm_bwd_workspace(M, H)),
                   TAGAN_ERR_WORKSPACE, "layernorm_bwd: workspace");
     LnArgs A{};
     A.M = M; A.H = H; A.gamma = gamma; A.s_in = s_in; A.mean = (float*)mean; A.rstd = (float*)rstd; A.dy = dy;
-    A.ds = ds; A.da = da; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
+    A.dres = dres; A.ds = ds; A.da = da; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
     A.part = want ? (float*)workspace : nullptr;
     const int64_t rpw = WAVE / lpr;
     const int64_t need = ((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE);
@@ -250,10 +264,13 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, cons
     else if (nv == 1) k_ln_bwd<64, 1><<<nblk, BLK, 0, s>>>(A);
     else k_ln_bwd<64, 2><<<nblk, BLK, 0, s>>>(A);
     TAGAN_CHECK_LAUNCH("layernorm_bwd");
-    if (want) {
-        const int n = 2 * H;
-        launch_colsum(A.part, nblk, n, dgamma, dbeta, H, s);
+    if (dgamma || dbeta) {
+        launch_colsum(A.part, nblk, 2 * H, dgamma, dbeta, H, s, 1.f, 3 * H);
         TAGAN_CHECK_LAUNCH("layernorm_bwd_sum");
+    }
+    if (dsum_a) {
+        launch_colsum(A.part + 2 * H, nblk, H, dsum_a, nullptr, H, s, 1.f, 3 * H);
+        TAGAN_CHECK_LAUNCH("layernorm_bwd_sum_a");
     }
     return TAGAN_OK;
 }

@@ -1,0 +1,201 @@
+"""One autograd node per attention layer: LN1 -> QKV GEMM -> attention core -> out-proj -> add+LN2.
+
+Both attention layers of the hot path share this shape — GeometricAttention.forward
+(geometric_attention.py:518-598) around the edge-softmax core and the temporal attention
+(temporal_attention.py:1006-1205) around the per-row core.  Composed from per-op autograd
+nodes the backward pays for: a separate gradient add where the layer input feeds both LN1 and
+the residual, a separate reduction for the out-proj bias, weight concatenations, and ~15
+autograd nodes of host overhead per layer.  Here the backward is written out once:
+
+    LN2 bwd (HIP)   -> d(residual), d(out-proj output) and, fused, the out-proj bias gradient
+    out-proj        -> dctx = do·W_o (GEMM), dW_o (split-K GEMM)
+    core bwd (HIP)  -> dqkv (+ metric parameter / bias-table gradients)
+    QKV             -> dh = dqkv·W_qkv (GEMM), dW_qkv (split-K GEMM), db_qkv
+    LN1 bwd (HIP)   -> dx = LN1ᵀ(dh) + d(residual), the add fused into the kernel
+
+Cores: ``GeoCore`` (tagan_geo_attn_*) and ``TemporalCore`` (tagan_temporal_attn_*).
+"""
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, require_hip, stream_of
+from .kernels import TemporalMask, _geo_fwd, weight_grad
+
+
+# ----------------------------------------------------------------------------- raw LayerNorm calls
+def ln_fwd(a2, b2, p_drop, seed, gamma, beta, eps, keep_s):
+    M, H = a2.shape
+    s = torch.empty_like(a2) if keep_s else None
+    y = torch.empty_like(a2)
+    mean = torch.empty(M, device=a2.device)
+    rstd = torch.empty(M, device=a2.device)
+    check(lib().tagan_add_layernorm_fwd(_lib.TAGAN_F32, M, H, ptr(a2), ptr(b2), float(p_drop), seed, ptr(gamma),
+                                        ptr(beta), float(eps), ptr(s), ptr(y), ptr(mean), ptr(rstd), stream_of(a2)),
+          "tagan_add_layernorm_fwd")
+    return y, s, mean, rstd
+
+
+def ln_bwd(s, mean, rstd, gamma, dy2, dres, p_drop, seed, want_ds, want_da, want_sum_a):
+    M, H = dy2.shape
+    dev = dy2.device
+    ds = torch.empty_like(dy2) if want_ds else None
+    da = torch.empty_like(dy2) if want_da else None
+    dg = torch.empty(H, device=dev)
+    dbt = torch.empty(H, device=dev)
+    dsa = torch.empty(H, device=dev) if want_sum_a else None
+    L = lib()
+    wsb = L.tagan_layernorm_bwd_workspace(M, H)
+    ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
+    check(L.tagan_layernorm_bwd(_lib.TAGAN_F32, M, H, ptr(s), ptr(mean), ptr(rstd), ptr(gamma), ptr(dy2), ptr(dres),
+                                float(p_drop), seed, ptr(ds), ptr(da), ptr(dg), ptr(dbt), ptr(dsa), ptr(ws), wsb,
+                                stream_of(dy2)), "tagan_layernorm_bwd")
+    return ds, da, dg, dbt, dsa
+
+
+# ----------------------------------------------------------------------------- attention cores
+class GeoCore:
+    """Edge-softmax attention over a SnapshotGraph (csrc/geo_attn.hip); qkv2 [N, 3H] -> ctx [N, H]."""
+
+    def __init__(self, graph, metric: int, heads: int, p_drop: float, seed: int):
+        self.graph, self.metric, self.heads, self.p_drop, self.seed = graph, metric, heads, p_drop, seed
+
+    def fwd(self, qkv2, param, _unused):
+        N, H3 = qkv2.shape
+        out = torch.empty(N, H3 // 3, device=qkv2.device)
+        lse = torch.empty(N, self.heads, device=qkv2.device)
+        prm = param.detach().contiguous() if param is not None else None
+        _geo_fwd(qkv2, self.graph, self.metric, self.heads, prm, self.p_drop, self.seed, out, lse, None)
+        return out, (lse, prm)
+
+    def bwd(self, qkv2, out, saved, dctx, want_p1, want_p2):
+        lse, prm = saved
+        N, H3 = qkv2.shape
+        H = H3 // 3
+        d = H // self.heads
+        dqkv = torch.empty_like(qkv2)
+        L = lib()
+        gs = self.graph.struct()
+        wsb = L.tagan_geo_attn_bwd_workspace(gs, self.heads, d)
+        ws = torch.empty(int(wsb), dtype=torch.uint8, device=qkv2.device)
+        dprm = torch.empty(self.heads, device=qkv2.device) if (prm is not None and want_p1) else None
+        b, db, es = qkv2.data_ptr(), dqkv.data_ptr(), qkv2.element_size()
+        check(L.tagan_geo_attn_bwd(_lib.TAGAN_F32, self.metric, gs, self.heads, d, b, b + H * es, b + 2 * H * es, H3,
+                                   ptr(prm), float(self.p_drop), self.seed, ptr(out), ptr(lse), ptr(dctx), db,
+                                   db + H * es, db + 2 * H * es, H3, ptr(dprm), ptr(ws), wsb, stream_of(qkv2)),
+              "tagan_geo_attn_bwd")
+        return dqkv, dprm, None
+
+
+class TemporalCore:
+    """Per-row attention over T steps (csrc/temporal_attn.hip) on a [T, R, 3H] (time_major) or [R, T, 3H]
+    projection, flattened to rows."""
+
+    def __init__(self, T: int, R: int, time_major: bool, heads: int, mask: TemporalMask, p_drop: float,
+                 seed: int):
+        self.T, self.R, self.time_major = T, R, time_major
+        self.heads, self.mask, self.p_drop, self.seed = heads, mask, p_drop, seed
+
+    def _strides(self, H):
+        H3 = 3 * H
+        if self.time_major:
+            return (H3, self.R * H3), (H, self.R * H)
+        return (self.T * H3, H3), (self.T * H, H)
+
+    def fwd(self, qkv2, bias_table, bias_dense):
+        T, R, heads = self.T, self.R, self.heads
+        H = qkv2.shape[1] // 3
+        d = H // heads
+        (s_row, s_t), (o_row, o_t) = self._strides(H)
+        out = torch.empty(T * R, H, device=qkv2.device)
+        lse = torch.empty(R, heads, T, device=qkv2.device)
+        bt = bias_table.detach().contiguous() if bias_table is not None else None
+        bd = bias_dense.detach().contiguous() if bias_dense is not None else None
+        bd_stride = (0 if bd.shape[0] == 1 else heads * T * T) if bd is not None else 0
+        m = self.mask
+        b, es = qkv2.data_ptr(), qkv2.element_size()
+        check(lib().tagan_temporal_attn_fwd(_lib.TAGAN_F32, R, T, heads, d, b, b + H * es, b + 2 * H * es, s_row,
+                                            s_t, ptr(bt), ptr(bd), bd_stride, ptr(m.keep), m.bstride, m.hstride,
+                                            int(m.causal), float(self.p_drop), self.seed, ptr(out), o_row, o_t,
+                                            ptr(lse), None, stream_of(qkv2)), "tagan_temporal_attn_fwd")
+        return out, (lse, bt, bd, bd_stride)
+
+    def bwd(self, qkv2, out, saved, dctx, want_p1, want_p2):
+        lse, bt, bd, bd_stride = saved
+        T, R, heads = self.T, self.R, self.heads
+        H = qkv2.shape[1] // 3
+        d = H // heads
+        (s_row, s_t), (o_row, o_t) = self._strides(H)
+        dqkv = torch.empty_like(qkv2)
+        dev = qkv2.device
+        dbt = torch.empty(heads, 2 * T - 1, device=dev) if (bt is not None and want_p1) else None
+        dbd = torch.empty(R, heads, T, T, device=dev) if (bd is not None and want_p2) else None
+        L = lib()
+        wsb = L.tagan_temporal_attn_bwd_workspace(R, T, heads)
+        ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
+        m = self.mask
+        b, db, es = qkv2.data_ptr(), dqkv.data_ptr(), qkv2.element_size()
+        check(L.tagan_temporal_attn_bwd(_lib.TAGAN_F32, R, T, heads, d, b, b + H * es, b + 2 * H * es, s_row, s_t,
+                                        ptr(bt), ptr(bd), bd_stride, ptr(m.keep), m.bstride, m.hstride,
+                                        int(m.causal), float(self.p_drop), self.seed, ptr(out), o_row, o_t, ptr(lse),
+                                        ptr(dctx), o_row, o_t, db, db + H * es, db + 2 * H * es, s_row, s_t,
+                                        ptr(dbt), ptr(dbd), ptr(ws), wsb, stream_of(qkv2)),
+              "tagan_temporal_attn_bwd")
+        if dbd is not None and bd.shape[0] == 1:
+            dbd = dbd.sum(0, keepdim=True)
+        return dqkv, dbt, dbd
+
+
+# ----------------------------------------------------------------------------- the fused block
+class AttnBlockFn(torch.autograd.Function):
+    """y = LN2(dropout(out_proj(core(QKV(LN1(x))))) + x) with LayerNorm on both sides (use_layer_norm=True)."""
+
+    @staticmethod
+    def forward(ctx, x, p1, p2, ln1_w, ln1_b, w_qkv, b_qkv, w_o, b_o, ln2_w, ln2_b, core, eps1: float,
+                eps2: float, p_out: float, seed_out: int):
+        require_hip(x)
+        H = x.shape[-1]
+        x2 = x.reshape(-1, H).contiguous()
+        h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False)
+        qkv = torch.addmm(b_qkv, h, w_qkv.t())
+        c, saved = core.fwd(qkv, p1, p2)
+        o = torch.addmm(b_o, c, w_o.t())
+        y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True)
+        ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w)
+        ctx.inter = (h, mean1, rstd1, qkv, c, saved, s2, mean2, rstd2)
+        ctx.cfg = (core, p_out, seed_out, x.shape)
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, ln1_w, w_qkv, w_o, ln2_w = ctx.saved_tensors
+        h, mean1, rstd1, qkv, c, saved, s2, mean2, rstd2 = ctx.inter
+        core, p_out, seed_out, shape = ctx.cfg
+        ng = ctx.needs_input_grad
+        dy2 = dy.reshape(-1, shape[-1]).contiguous()
+        dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True)
+        dc = do @ w_o
+        dw_o = weight_grad(do, c) if ng[7] else None
+        dqkv, dp1, dp2 = core.bwd(qkv, c, saved, dc, ng[1], ng[2])
+        del dc, do
+        dh = dqkv @ w_qkv
+        dw_qkv = weight_grad(dqkv, h) if ng[5] else None
+        db_qkv = dqkv.sum(0) if ng[6] else None
+        del dqkv
+        dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
+        ctx.inter = None
+        return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
+                None, None, None, None, None)
+
+
+def attention_block(x, core, p1: Optional[torch.Tensor], p2: Optional[torch.Tensor], ln1, q_lin, k_lin, v_lin,
+                    out_lin, ln2, p_out: float, seed_out: int):
+    w_qkv = torch.cat([q_lin.weight, k_lin.weight, v_lin.weight], 0)
+    b_qkv = torch.cat([q_lin.bias, k_lin.bias, v_lin.bias], 0)
+    return AttnBlockFn.apply(x, p1, p2, ln1.weight, ln1.bias, w_qkv, b_qkv, out_lin.weight, out_lin.bias,
+                             ln2.weight, ln2.bias, core, ln1.eps, ln2.eps, float(p_out), seed_out)
+
+
+def fusable(x: torch.Tensor, use_layer_norm: bool) -> bool:
+    return use_layer_norm and x.is_cuda and bool(lib().tagan_layernorm_supported(x.shape[-1]))

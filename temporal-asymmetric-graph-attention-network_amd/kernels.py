@@ -397,8 +397,8 @@ class AddLayerNormFn(torch.autograd.Function):
         L = lib()
         wsb = L.tagan_layernorm_bwd_workspace(M, H)
         ws = torch.empty(int(wsb), dtype=torch.uint8, device=dy.device)
-        check(L.tagan_layernorm_bwd(_lib.TAGAN_F32, M, H, ptr(s), ptr(mean), ptr(rstd), ptr(gamma), ptr(dy2),
-                                    float(p_drop), seed, ptr(ds), ptr(da), ptr(dg), ptr(dbt), ptr(ws), wsb,
+        check(L.tagan_layernorm_bwd(_lib.TAGAN_F32, M, H, ptr(s), ptr(mean), ptr(rstd), ptr(gamma), ptr(dy2), None,
+                                    float(p_drop), seed, ptr(ds), ptr(da), ptr(dg), ptr(dbt), None, ptr(ws), wsb,
                                     stream_of(dy2)), "tagan_layernorm_bwd")
         return (da.view(shape) if da is not None else None, ds.view(shape) if ds is not None else None,
                 dg, dbt, None, None, None)

@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib
+from ..fused import GeoCore, attention_block, fusable
 from ..kernels import (GeoAttnFn, SnapshotGraph, dropout_add_layer_norm, fused_qkv, graph_from_dense_mask,
                        layer_norm, linear, new_seed)
 
@@ -130,14 +131,19 @@ class GeometricAttention(nn.Module):
 
     def forward_graph(self, x: torch.Tensor, graph: SnapshotGraph) -> torch.Tensor:
         """Hot path: x [N, H] (N = all nodes of a snapshot batch), graph = their CSR/CSC."""
+        p = self.attn_dropout.p if self.training else 0.0
+        p_out = self.output_dropout.p if self.training else 0.0
+        if fusable(x, self.use_layer_norm):   # one autograd node for the whole layer (fused.py)
+            core = GeoCore(graph, self.metric_id, self.num_heads, p, new_seed() if p > 0 else 0)
+            return attention_block(x, core, self._metric_param(), None, self.layer_norm1, self.q_linear,
+                                   self.k_linear, self.v_linear, self.output_proj, self.layer_norm2, p_out,
+                                   new_seed() if p_out > 0 else 0)
         identity = x
         h = layer_norm(x, self.layer_norm1) if self.use_layer_norm else x
         qkv = fused_qkv(h, self.q_linear, self.k_linear, self.v_linear).contiguous()
-        p = self.attn_dropout.p if self.training else 0.0
         ctx = GeoAttnFn.apply(qkv, self._metric_param(), graph, self.metric_id, self.num_heads, p,
                               new_seed() if p > 0 else 0)
         proj = linear(ctx, self.output_proj.weight, self.output_proj.bias)
-        p_out = self.output_dropout.p if self.training else 0.0
         if self.use_layer_norm:
             return dropout_add_layer_norm(proj, identity, self.layer_norm2, p_out)
         return F.dropout(proj, p_out, True) + identity

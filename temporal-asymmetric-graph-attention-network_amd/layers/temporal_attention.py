@@ -23,6 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..fused import TemporalCore, attention_block, fusable
 from ..kernels import (TemporalAttnFn, TemporalMask, dropout_add_layer_norm, fused_qkv, layer_norm, linear,
                        new_seed)
 
@@ -207,9 +208,6 @@ class TemporalAttention(nn.Module):
             T, B, H = x.shape
         else:
             B, T, H = x.shape
-        identity = x
-        hx = layer_norm(x, self.layer_norm1) if self.use_layer_norm else x
-        qkv = fused_qkv(hx, self.q_linear, self.k_linear, self.v_linear).contiguous()
         if _known_ones_mask:
             bias_dense, mask, explode = None, self._ones_mask_fast(B, T), False
         else:
@@ -218,10 +216,19 @@ class TemporalAttention(nn.Module):
             raise MaskBroadcastError("attention mask broadcast enlarges the score tensor "
                                      "(the reference raises at temporal_attention.py:1187)")
         p = self.attn_dropout.p if self.training else 0.0
+        p_out = self.output_dropout.p if self.training else 0.0
+        if not want_attn and fusable(x, self.use_layer_norm):   # one autograd node for the layer (fused.py)
+            core = TemporalCore(T, B, time_major, self.num_heads, mask, p, new_seed() if p > 0 else 0)
+            y = attention_block(x, core, self._bias_table(T, x.device), bias_dense, self.layer_norm1,
+                                self.q_linear, self.k_linear, self.v_linear, self.output_proj, self.layer_norm2,
+                                p_out, new_seed() if p_out > 0 else 0)
+            return y, None
+        identity = x
+        hx = layer_norm(x, self.layer_norm1) if self.use_layer_norm else x
+        qkv = fused_qkv(hx, self.q_linear, self.k_linear, self.v_linear).contiguous()
         ctx, attn = TemporalAttnFn.apply(qkv, self._bias_table(T, x.device), bias_dense, time_major,
                                          self.num_heads, mask, p, new_seed() if p > 0 else 0, want_attn)
         proj = linear(ctx, self.output_proj.weight, self.output_proj.bias)
-        p_out = self.output_dropout.p if self.training else 0.0
         if self.use_layer_norm:
             return dropout_add_layer_norm(proj, identity, self.layer_norm2, p_out), attn
         return F.dropout(proj, p_out, True) + identity, attn
