@@ -207,13 +207,16 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
  * temporal_attention.py:1190-1200) and plain layer_norm1 (b = NULL, p_drop = 0).
  *   s = dropout(a; p_drop, seed) + b     (element (r,c): stream r, counter c)
  *   y = (s - mean) / sqrt(var + eps) * gamma + beta       (biased var, as torch)
- * s_out (optional) keeps s for the backward pass; mean/rstd: [M].
+ * s_out (optional) keeps s for the backward pass; mean/rstd: [M].  y has row stride
+ * ldy (0 = H; a wider stride leaves room for a ones column that turns the next
+ * weight-gradient GEMM into weight + bias gradient).
  * Supported H: tagan_layernorm_supported(H) (32, 64, 128, 256, 512).
  * ------------------------------------------------------------------------- */
 int tagan_layernorm_supported(int32_t H);
 int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, const float* b,
                             float p_drop, uint64_t seed, const float* gamma, const float* beta,
-                            float eps, float* s_out, float* y, float* mean, float* rstd, void* stream);
+                            float eps, float* s_out, float* y, int64_t ldy, float* mean, float* rstd,
+                            void* stream);
 /* Backward: ds = dL/ds (+ dres when given: the gradient of the LN input's other
  * consumer, fused instead of a separate add), da = dL/ds masked/scaled by the same
  * dropout (the projection branch's gradient), dgamma/dbeta [H], dsum_a [H] = column
@@ -291,6 +294,12 @@ int tagan_pool_fwd(int dtype, int32_t T, int64_t N, int32_t H, const float* x, i
                    float* out, void* workspace, size_t workspace_bytes, void* stream);
 int tagan_pool_bwd(int dtype, int32_t T, int64_t N, int32_t H, const float* g, float* dx, int64_t ld_row,
                    int64_t ld_t, void* stream);
+
+/* Column sums of a tall row-major [M, N] matrix (row stride ld): the bias gradients of the
+ * projections (sum of dY over rows).  Two-stage, ordered, deterministic.  N % 4 == 0. */
+size_t tagan_colsum_workspace(int64_t M, int32_t N);
+int tagan_colsum(int dtype, int64_t M, int32_t N, const float* x, int64_t ld, float* out, void* workspace,
+                 size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -32,6 +32,8 @@ _SIGNATURES = {
     "tagan_uniform": (_f32, [_u64, _u64, _c.c_uint32]),
     "tagan_csr_build_workspace": (_sz, [_i64, _i64]),
     "tagan_pool_workspace": (_sz, [_i32, _i32]),
+    "tagan_colsum_workspace": (_sz, [_i64, _i32]),
+    "tagan_colsum": (_c.c_int, [_c.c_int, _i64, _i32, _p, _i64, _p, _p, _sz, _p]),
     "tagan_pool_fwd": (_c.c_int, [_c.c_int, _i32, _i64, _i32, _p, _i64, _i64, _p, _p, _sz, _p]),
     "tagan_pool_bwd": (_c.c_int, [_c.c_int, _i32, _i64, _i32, _p, _p, _i64, _i64, _p]),
     "tagan_csr_build": (_c.c_int, [_p, _i64, _i64, _p, _p, _i32, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _sz,
@@ -54,8 +56,8 @@ _SIGNATURES = {
                                            _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,
                                            _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p, _sz, _p]),
     "tagan_layernorm_supported": (_c.c_int, [_i32]),
-    "tagan_add_layernorm_fwd": (_c.c_int, [_c.c_int, _i64, _i32, _p, _p, _f32, _u64, _p, _p, _f32, _p, _p, _p,
-                                           _p, _p]),
+    "tagan_add_layernorm_fwd": (_c.c_int, [_c.c_int, _i64, _i32, _p, _p, _f32, _u64, _p, _p, _f32, _p, _p, _i64,
+                                           _p, _p, _p]),
     "tagan_layernorm_bwd_workspace": (_sz, [_i64, _i32]),
     "tagan_layernorm_bwd": (_c.c_int, [_c.c_int, _i64, _i32, _p, _p, _p, _p, _p, _p, _f32, _u64, _p, _p, _p, _p,
                                        _p, _p, _sz, _p]),

@@ -3,8 +3,9 @@
 // for a block-diagonal batch of snapshots.  Integer/byte work: HBM-bound,
 // no MFMA.  Keys (global src << LB | local dst), LB = bits of the largest
 // snapshot, are radix-sorted with rocPRIM over only LB + bits(N) bits (33 at
-// C2 instead of 64), de-duplicated, scattered into CSR; the CSC (with CSR edge
-// ids) is a second key-value sort of (global dst << LB | local src).
+// C2 instead of 64), de-duplicated, scattered into CSR.  The CSC (with CSR edge
+// ids) is a STABLE 32-bit key-value sort of the CSR entries by dst alone: the CSR
+// order is by src, so stability keeps src ascending within each column.
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -69,14 +70,15 @@ __global__ void __launch_bounds__(BLK) k_unique_flags(const uint64_t* __restrict
     }
 }
 
-// Scatter unique keys into CSR; emit CSC keys (dst << LB | local src) with value = CSR position.
+// Scatter unique keys into CSR; emit CSC keys (global dst) with value = CSR position and the
+// row of every CSR position (srcq) for the CSC scatter.
 __global__ void __launch_bounds__(BLK) k_scatter_csr(const uint64_t* __restrict__ keys,
                                                      const int32_t* __restrict__ flags,
                                                      const int32_t* __restrict__ pos, int64_t M, int64_t N, int LB,
                                                      const int64_t* __restrict__ node_ptr, int G,
                                                      int32_t* __restrict__ rowptr, int32_t* __restrict__ col,
-                                                     uint64_t* __restrict__ ckeys, int32_t* __restrict__ cvals,
-                                                     int64_t* __restrict__ nnz_out) {
+                                                     uint32_t* __restrict__ ckeys, int32_t* __restrict__ cvals,
+                                                     int32_t* __restrict__ srcq, int64_t* __restrict__ nnz_out) {
     const uint64_t lmask = ((uint64_t)1 << LB) - 1;
     for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
         if (p == M - 1) {
@@ -87,40 +89,38 @@ __global__ void __launch_bounds__(BLK) k_scatter_csr(const uint64_t* __restrict_
         if (!flags[p]) continue;
         const uint64_t k = keys[p];
         const int64_t r = (int64_t)(k >> LB);
-        const int64_t base = node_base(node_ptr, G, r);
-        const int32_t c = (int32_t)(base + (int64_t)(k & lmask));
+        const int32_t c = (int32_t)(node_base(node_ptr, G, r) + (int64_t)(k & lmask));
         const int32_t q = pos[p];
         col[q] = c;
         if (p == 0 || (int64_t)(keys[p - 1] >> LB) != r) rowptr[r] = q;   // every row has its self-loop
-        ckeys[q] = ((uint64_t)c << LB) | (uint64_t)(r - base);
+        ckeys[q] = (uint32_t)c;
         cvals[q] = q;
+        srcq[q] = (int32_t)r;
     }
 }
 
-__global__ void __launch_bounds__(BLK) k_fill_tail(uint64_t* __restrict__ ckeys, int32_t* __restrict__ cvals,
-                                                   const int64_t* __restrict__ nnz_p, int64_t M, int64_t N, int LB) {
+__global__ void __launch_bounds__(BLK) k_fill_tail(uint32_t* __restrict__ ckeys, int32_t* __restrict__ cvals,
+                                                   const int64_t* __restrict__ nnz_p, int64_t M, int64_t N) {
     const int64_t nnz = *nnz_p;
-    const uint64_t sentinel = (uint64_t)N << LB;
     for (int64_t p = nnz + blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
-        ckeys[p] = sentinel;
+        ckeys[p] = (uint32_t)N;    // sentinel: sorts after every column
         cvals[p] = -1;
     }
 }
 
-__global__ void __launch_bounds__(BLK) k_scatter_csc(const uint64_t* __restrict__ ckeys,
+__global__ void __launch_bounds__(BLK) k_scatter_csc(const uint32_t* __restrict__ ckeys,
                                                      const int32_t* __restrict__ cvals,
-                                                     const int64_t* __restrict__ nnz_p, int64_t N, int LB,
-                                                     const int64_t* __restrict__ node_ptr, int G,
+                                                     const int32_t* __restrict__ srcq,
+                                                     const int64_t* __restrict__ nnz_p, int64_t N,
                                                      int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_row,
                                                      int32_t* __restrict__ csc_eid) {
     const int64_t nnz = *nnz_p;
-    const uint64_t lmask = ((uint64_t)1 << LB) - 1;
     for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * BLK) {
-        const uint64_t k = ckeys[p];
-        const int64_t c = (int64_t)(k >> LB);
-        csc_row[p] = (int32_t)(node_base(node_ptr, G, c) + (int64_t)(k & lmask));
-        csc_eid[p] = cvals[p];
-        if (p == 0 || (int64_t)(ckeys[p - 1] >> LB) != c) csc_ptr[c] = (int32_t)p;
+        const uint32_t c = ckeys[p];
+        const int32_t q = cvals[p];
+        csc_row[p] = srcq[q];
+        csc_eid[p] = q;
+        if (p == 0 || ckeys[p - 1] != c) csc_ptr[c] = (int32_t)p;
         if (p == nnz - 1) csc_ptr[N] = (int32_t)nnz;
     }
 }
@@ -132,7 +132,7 @@ int key_bits(int64_t N) {
 }
 
 struct CsrWs {
-    size_t keys_a, keys_b, ckeys_b, cvals_b, flags, pos, temp, total;
+    size_t keys_a, keys_b, ckeys_b, cvals_b, srcq, flags, pos, temp, total;
     size_t temp_bytes;
 };
 
@@ -143,15 +143,16 @@ CsrWs plan(int64_t E, int64_t N) {
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
     w.keys_a = take(M * 8);
     w.keys_b = take(M * 8);
-    w.ckeys_b = take(M * 8);
+    w.ckeys_b = take(M * 4);
     w.cvals_b = take(M * 4);
+    w.srcq = take(M * 4);
     w.flags = take(M * 4);
     w.pos = take(M * 4);
     const int bits = key_bits(N);
     size_t t1 = 0, t2 = 0, t3 = 0;
     (void)rocprim::radix_sort_keys(nullptr, t1, (uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)M, 0, 32 + bits);
-    (void)rocprim::radix_sort_pairs(nullptr, t2, (uint64_t*)nullptr, (uint64_t*)nullptr, (int32_t*)nullptr,
-                              (int32_t*)nullptr, (size_t)M, 0, 32 + bits);
+    (void)rocprim::radix_sort_pairs(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
+                              (int32_t*)nullptr, (size_t)M, 0, bits);
     (void)rocprim::exclusive_scan(nullptr, t3, (int32_t*)nullptr, (int32_t*)nullptr, 0, (size_t)M,
                             rocprim::plus<int32_t>());
     w.temp_bytes = std::max(t1, std::max(t2, t3));
@@ -197,8 +198,9 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     char* ws = (char*)workspace;
     uint64_t* keys_a = (uint64_t*)(ws + w.keys_a);
     uint64_t* keys_b = (uint64_t*)(ws + w.keys_b);
-    uint64_t* ckeys_b = (uint64_t*)(ws + w.ckeys_b);
+    uint32_t* ckeys_b = (uint32_t*)(ws + w.ckeys_b);
     int32_t* cvals_b = (int32_t*)(ws + w.cvals_b);
+    int32_t* srcq = (int32_t*)(ws + w.srcq);
     int32_t* flags = (int32_t*)(ws + w.flags);
     int32_t* pos = (int32_t*)(ws + w.pos);
     void* temp = ws + w.temp;
@@ -221,19 +223,19 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     TAGAN_CHECK_HIP(rocprim::exclusive_scan(temp, tb, flags, pos, 0, (size_t)M, rocprim::plus<int32_t>(), s),
                     "csr_build exclusive_scan");
     // keys_a is free now: reuse it as the unsorted CSC key buffer; cvals via csc_eid scratch? use csc_row.
-    uint64_t* ckeys_a = keys_a;
+    uint32_t* ckeys_a = (uint32_t*)keys_a;
     int32_t* cvals_a = csc_row;   // staging only; overwritten by the final CSC scatter
     k_scatter_csr<<<grid_for(M), BLK, 0, s>>>(keys_b, flags, pos, M, n_nodes, LB, node_ptr, n_graphs, rowptr, col,
-                                              ckeys_a, cvals_a, nnz_out);
+                                              ckeys_a, cvals_a, srcq, nnz_out);
     TAGAN_CHECK_LAUNCH("csr_build.scatter_csr");
-    k_fill_tail<<<grid_for(M), BLK, 0, s>>>(ckeys_a, cvals_a, nnz_out, M, n_nodes, LB);
+    k_fill_tail<<<grid_for(M), BLK, 0, s>>>(ckeys_a, cvals_a, nnz_out, M, n_nodes);
     TAGAN_CHECK_LAUNCH("csr_build.fill_tail");
     tb = w.temp_bytes;
     TAGAN_CHECK_HIP(rocprim::radix_sort_pairs(temp, tb, ckeys_a, ckeys_b, cvals_a, cvals_b, (size_t)M, 0,
-                                              sort_bits, s),
+                                              bits, s),
                     "csr_build radix_sort_pairs");
-    k_scatter_csc<<<grid_for(M), BLK, 0, s>>>(ckeys_b, cvals_b, nnz_out, n_nodes, LB, node_ptr, n_graphs, csc_ptr,
-                                              csc_row, csc_eid);
+    k_scatter_csc<<<grid_for(M), BLK, 0, s>>>(ckeys_b, cvals_b, srcq, nnz_out, n_nodes, csc_ptr, csc_row,
+                                              csc_eid);
     TAGAN_CHECK_LAUNCH("csr_build.scatter_csc");
     return TAGAN_OK;
 }

@@ -42,6 +42,8 @@ struct LnArgs {
     float* ds;
     float* da;
     float* part;   // [gridDim.x, 3H]: dgamma | dbeta | column sums of da (projection-bias gradient)
+    int want_dsa;  // accumulate the column sums of da
+    int64_t ldy;   // forward output row stride (>= H)
 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -100,7 +102,7 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
         o.y = (v[n].y - mean) * rstd * g.y + be.y;
         o.z = (v[n].z - mean) * rstd * g.z + be.z;
         o.w = (v[n].w - mean) * rstd * g.w + be.w;
-        st4(A.y + row * H + c, o);
+        st4(A.y + row * A.ldy + c, o);
     }
     if (sl == 0) {
         A.mean[row] = mean;
@@ -153,7 +155,7 @@ __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
             o.y = rstd * (gd[n].y - c1 * xh[n].y - c2);
             o.z = rstd * (gd[n].z - c1 * xh[n].z - c2);
             o.w = rstd * (gd[n].w - c1 * xh[n].w - c2);
-            if (A.da || A.part) {
+            if (A.da || A.want_dsa) {
                 const float4 a = drop4(A, o, row, c);
                 if (A.da) st4(A.da + row * H + c, a);
                 dsa[n].x += a.x; dsa[n].y += a.y; dsa[n].z += a.z; dsa[n].w += a.w;
@@ -211,7 +213,7 @@ int tagan_layernorm_supported(int32_t H) {
 
 int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, const float* b, float p_drop,
                             uint64_t seed, const float* gamma, const float* beta, float eps, float* s_out, float* y,
-                            float* mean, float* rstd, void* stream) {
+                            int64_t ldy, float* mean, float* rstd, void* stream) {
     using namespace tagan;
     int lpr, nv;
     TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "layernorm: dtype %d", dtype);
@@ -221,6 +223,8 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
     LnArgs A{};
     A.M = M; A.H = H; A.a = a; A.b = b; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
     A.gamma = gamma; A.beta = beta; A.eps = eps; A.s_out = s_out; A.y = y; A.mean = mean; A.rstd = rstd;
+    A.ldy = ldy > 0 ? ldy : H;
+    TAGAN_REQUIRE(A.ldy >= H && A.ldy % 4 == 0, TAGAN_ERR_ARG, "layernorm_fwd: ldy %lld", (long long)ldy);
     const int64_t rpw = WAVE / lpr;
     const dim3 g((unsigned)(((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE)));
     hipStream_t s = as_stream(stream);
@@ -254,6 +258,7 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, cons
     A.M = M; A.H = H; A.gamma = gamma; A.s_in = s_in; A.mean = (float*)mean; A.rstd = (float*)rstd; A.dy = dy;
     A.dres = dres; A.ds = ds; A.da = da; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
     A.part = want ? (float*)workspace : nullptr;
+    A.want_dsa = dsum_a != nullptr;
     const int64_t rpw = WAVE / lpr;
     const int64_t need = ((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE);
     const int nblk = (int)std::min<int64_t>(need, LN_BWD_BLOCKS);

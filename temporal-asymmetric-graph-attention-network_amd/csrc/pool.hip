@@ -93,3 +93,62 @@ int tagan_pool_bwd(int dtype, int32_t T, int64_t N, int32_t H, const float* g, f
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------- column sums
+// Bias gradients of the projections: out[c] = sum_r x[r][c] for a tall [M, N] matrix.  Stage 1:
+// block b sums a contiguous row range with float4 lanes (N/4 lanes per row, several rows per
+// block iteration) into part[b][N]; stage 2 = the ordered column sum (k_colsum_parts).
+namespace tagan {
+namespace {
+
+constexpr int CS_BLOCKS = 512;
+
+__global__ void __launch_bounds__(BLK) k_colsum_rows(const float* __restrict__ x, int64_t M, int N, int64_t ld,
+                                                     float* __restrict__ part) {
+    __shared__ float red[4 * BLK];
+    const int lpr = N / 4, rpb = BLK / lpr;
+    const int lane = threadIdx.x % lpr, rsub = threadIdx.x / lpr;
+    const int64_t per = (M + gridDim.x - 1) / gridDim.x;
+    const int64_t a = blockIdx.x * per, b = min<int64_t>(M, a + per);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rsub < rpb)
+        for (int64_t r = a + rsub; r < b; r += rpb) {
+            const float4 v = *(const float4*)(x + r * ld + lane * 4);
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+    if (rsub < rpb) *(float4*)(red + (size_t)rsub * N + lane * 4) = acc;
+    __syncthreads();
+    for (int c = threadIdx.x; c < N; c += BLK) {
+        float s = 0.f;
+        for (int k = 0; k < rpb; ++k) s += red[(size_t)k * N + c];
+        part[(int64_t)blockIdx.x * N + c] = s;
+    }
+}
+
+}  // namespace
+}  // namespace tagan
+
+extern "C" {
+
+size_t tagan_colsum_workspace(int64_t M, int32_t N) {
+    (void)M;
+    return (size_t)tagan::CS_BLOCKS * N * sizeof(float);
+}
+
+int tagan_colsum(int dtype, int64_t M, int32_t N, const float* x, int64_t ld, float* out, void* workspace,
+                 size_t workspace_bytes, void* stream) {
+    using namespace tagan;
+    TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "colsum: dtype %d", dtype);
+    TAGAN_REQUIRE(M > 0 && N % 4 == 0 && N >= 4 && N / 4 <= BLK && ld % 4 == 0 && ld >= N && x && out,
+                  TAGAN_ERR_ARG, "colsum: bad args (N=%d)", N);
+    TAGAN_REQUIRE(workspace && workspace_bytes >= tagan_colsum_workspace(M, N), TAGAN_ERR_WORKSPACE, "colsum: ws");
+    const int nblk = (int)std::min<int64_t>(CS_BLOCKS, (M + 63) / 64);
+    hipStream_t s = as_stream(stream);
+    k_colsum_rows<<<nblk, BLK, 0, s>>>(x, M, N, ld, (float*)workspace);
+    TAGAN_CHECK_LAUNCH("colsum_rows");
+    launch_colsum((float*)workspace, nblk, N, out, nullptr, N, s);
+    TAGAN_CHECK_LAUNCH("colsum_parts");
+    return TAGAN_OK;
+}
+
+}  // extern "C"

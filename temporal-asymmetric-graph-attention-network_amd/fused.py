@@ -21,19 +21,21 @@ import torch
 
 from . import _lib
 from ._lib import check, lib, ptr, require_hip, stream_of
-from .kernels import TemporalMask, _geo_fwd, weight_grad
+from .kernels import TemporalMask, _geo_fwd, colsum, weight_grad
 
 
 # ----------------------------------------------------------------------------- raw LayerNorm calls
-def ln_fwd(a2, b2, p_drop, seed, gamma, beta, eps, keep_s):
+def ln_fwd(a2, b2, p_drop, seed, gamma, beta, eps, keep_s, y=None):
+    """LN(dropout(a2) + b2); ``y`` may be a wider row-strided buffer ([M, ld], first H columns written)."""
     M, H = a2.shape
     s = torch.empty_like(a2) if keep_s else None
-    y = torch.empty_like(a2)
+    if y is None:
+        y = torch.empty_like(a2)
     mean = torch.empty(M, device=a2.device)
     rstd = torch.empty(M, device=a2.device)
     check(lib().tagan_add_layernorm_fwd(_lib.TAGAN_F32, M, H, ptr(a2), ptr(b2), float(p_drop), seed, ptr(gamma),
-                                        ptr(beta), float(eps), ptr(s), ptr(y), ptr(mean), ptr(rstd), stream_of(a2)),
-          "tagan_add_layernorm_fwd")
+                                        ptr(beta), float(eps), ptr(s), ptr(y), y.stride(0), ptr(mean), ptr(rstd),
+                                        stream_of(a2)), "tagan_add_layernorm_fwd")
     return y, s, mean, rstd
 
 
@@ -181,7 +183,7 @@ class AttnBlockFn(torch.autograd.Function):
         del dc, do
         dh = dqkv @ w_qkv
         dw_qkv = weight_grad(dqkv, h) if ng[5] else None
-        db_qkv = dqkv.sum(0) if ng[6] else None
+        db_qkv = colsum(dqkv) if ng[6] else None
         del dqkv
         dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
         ctx.inter = None

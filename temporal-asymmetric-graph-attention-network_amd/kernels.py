@@ -325,6 +325,18 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, rows: int = 2048) -> torch.
     return dw
 
 
+def colsum(x2):
+    """Column sums of a tall [M, N] matrix (bias gradients): HIP two-stage ordered reduction."""
+    M, N = x2.shape
+    out = torch.empty(N, device=x2.device)
+    L = lib()
+    wsb = L.tagan_colsum_workspace(M, N)
+    ws = torch.empty(max(int(wsb), 1), dtype=torch.uint8, device=x2.device)
+    check(L.tagan_colsum(_lib.TAGAN_F32, M, N, ptr(x2), x2.stride(0), ptr(out), ptr(ws), wsb, stream_of(x2)),
+          "tagan_colsum")
+    return out
+
+
 class LinearFn(torch.autograd.Function):
     """y = x·Wᵀ + b with the split-K weight gradient above."""
 
@@ -344,7 +356,7 @@ class LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = weight_grad(dy2, x.reshape(-1, x.shape[-1]).contiguous())
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = dy2.sum(0)
+            db = colsum(dy2) if (dy2.is_cuda and dy2.shape[1] % 4 == 0 and dy2.shape[1] <= 1024) else dy2.sum(0)
         return dx, dw, db
 
 
@@ -376,7 +388,7 @@ class AddLayerNormFn(torch.autograd.Function):
         mean = torch.empty(M, device=a.device)
         rstd = torch.empty(M, device=a.device)
         check(lib().tagan_add_layernorm_fwd(_lib.TAGAN_F32, M, H, ptr(a2), ptr(b2), float(p_drop), seed,
-                                            ptr(gamma), ptr(beta), float(eps), ptr(s), ptr(y), ptr(mean),
+                                            ptr(gamma), ptr(beta), float(eps), ptr(s), ptr(y), 0, ptr(mean),
                                             ptr(rstd), stream_of(a2)), "tagan_add_layernorm_fwd")
         ctx.save_for_backward(s if keep_s else a2, mean, rstd, gamma)
         ctx.cfg = (p_drop, seed, b is not None, a.shape)

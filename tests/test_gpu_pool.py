@@ -22,3 +22,17 @@ def test_pool_matches_reference_view(T, N, H):
     (out * go.cuda()).sum().backward()
     (ref * go.double()).sum().backward()
     assert torch.allclose(x.grad.double().cpu(), ref_in.grad, atol=1e-7, rtol=1e-5)
+
+
+@pytest.mark.parametrize("M,N", [(320000, 384), (1000, 128), (7, 4), (12345, 1024), (64, 36)])
+def test_colsum_matches_fp64(M, N):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from tagan_amd.kernels import colsum
+    g = torch.Generator().manual_seed(M + N)
+    base = torch.randn(M, N + 4, generator=g)
+    got = colsum(base[:, :N].cuda())                      # row stride N + 4
+    want = base[:, :N].double().sum(0)
+    assert torch.allclose(got.double().cpu(), want, atol=1e-6 * M ** 0.5, rtol=1e-5)
+    again = colsum(base[:, :N].cuda())
+    assert torch.equal(got, again)                        # ordered partials: bitwise reproducible

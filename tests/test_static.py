@@ -1,0 +1,33 @@
+"""CPU guard for code paths only the GPU exercises: every name a product module loads must be bound
+somewhere in that module (import, def, class, assignment, argument) or be a builtin."""
+import ast
+import builtins
+import os
+
+import pytest
+
+PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "temporal-asymmetric-graph-attention-network_amd")
+FILES = sorted(os.path.join(dp, f) for dp, _, fs in os.walk(PKG) for f in fs if f.endswith(".py"))
+
+
+@pytest.mark.parametrize("path", FILES, ids=[os.path.relpath(f, PKG) for f in FILES])
+def test_no_unbound_names(path):
+    tree = ast.parse(open(path).read())
+    bound = set(dir(builtins)) | {"__file__", "__name__"}
+    for node in ast.walk(tree):
+        if isinstance(node, (ast.FunctionDef, ast.AsyncFunctionDef, ast.ClassDef)):
+            bound.add(node.name)
+        elif isinstance(node, ast.Import):
+            bound.update(a.asname or a.name.split(".")[0] for a in node.names)
+        elif isinstance(node, ast.ImportFrom):
+            bound.update(a.asname or a.name for a in node.names)
+        elif isinstance(node, ast.Name) and isinstance(node.ctx, (ast.Store, ast.Del)):
+            bound.add(node.id)
+        elif isinstance(node, ast.arg):
+            bound.add(node.arg)
+        elif isinstance(node, ast.ExceptHandler) and node.name:
+            bound.add(node.name)
+    unbound = sorted({(n.id, n.lineno) for n in ast.walk(tree)
+                      if isinstance(n, ast.Name) and isinstance(n.ctx, ast.Load) and n.id not in bound})
+    assert not unbound, unbound
