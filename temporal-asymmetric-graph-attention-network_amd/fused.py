@@ -149,6 +149,65 @@ class TemporalCore:
         return dqkv, dbt, dbd
 
 
+# ----------------------------------------------------------------------------- GEMM precision
+# "fp32" (default): fp32 operands on the fp32 MFMA path.  "bf16": the projection GEMMs take bf16
+# operands with fp32 accumulation and fp32 outputs (hipBLASLt via aten::mm.dtype); every other op
+# (LayerNorm, attention cores, residual stream, optimizer) stays fp32.  Not bit-compatible with
+# the fp32 reference: tests/test_gpu_bf16.py states its tolerance.
+_GEMM_BF16 = False
+
+
+class gemm_precision:
+    def __init__(self, mode: str):
+        if mode not in ("fp32", "bf16"):
+            raise ValueError("gemm precision must be 'fp32' or 'bf16'")
+        self.bf16 = mode == "bf16"
+
+    def __enter__(self):
+        global _GEMM_BF16
+        self.prev, _GEMM_BF16 = _GEMM_BF16, self.bf16
+
+    def __exit__(self, *exc):
+        global _GEMM_BF16
+        _GEMM_BF16 = self.prev
+
+
+def _b(t):
+    return t if t.dtype == torch.bfloat16 else t.to(torch.bfloat16)
+
+
+def _addmm(bias, a, w, bf):
+    """bias + a·wᵀ -> fp32."""
+    if bf:
+        return torch.addmm(bias, _b(a), _b(w).t(), out_dtype=torch.float32)
+    return torch.addmm(bias, a, w.t())
+
+
+def _mm(a, w, bf):
+    """a·w -> fp32."""
+    if bf:
+        return torch.mm(_b(a), _b(w), out_dtype=torch.float32)
+    return a @ w
+
+
+def _wgrad(dy, x, bf, rows: int = 2048):
+    """dyᵀ·x (split-K) -> fp32."""
+    if not bf:
+        return weight_grad(dy, x, rows)
+    dy, x = _b(dy), _b(x)
+    K, M = dy.shape
+    N = x.shape[1]
+    if K < 4 * rows:
+        return torch.mm(dy.t(), x, out_dtype=torch.float32)
+    c = K // rows
+    main = c * rows
+    dw = torch.bmm(dy[:main].view(c, rows, M).transpose(1, 2), x[:main].view(c, rows, N),
+                   out_dtype=torch.float32).sum(0)
+    if main < K:
+        dw = dw + torch.mm(dy[main:].t(), x[main:], out_dtype=torch.float32)
+    return dw
+
+
 # ----------------------------------------------------------------------------- the fused block
 class AttnBlockFn(torch.autograd.Function):
     """y = LN2(dropout(out_proj(core(QKV(LN1(x))))) + x) with LayerNorm on both sides (use_layer_norm=True)."""
@@ -159,31 +218,39 @@ class AttnBlockFn(torch.autograd.Function):
         require_hip(x)
         H = x.shape[-1]
         x2 = x.reshape(-1, H).contiguous()
+        bf = _GEMM_BF16
         h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False)
-        qkv = torch.addmm(b_qkv, h, w_qkv.t())
+        if bf:
+            h = _b(h)          # only the GEMMs read h: keep it in bf16
+        qkv = _addmm(b_qkv, h, w_qkv, bf)
         c, saved = core.fwd(qkv, p1, p2)
-        o = torch.addmm(b_o, c, w_o.t())
+        cg = _b(c) if bf else c
+        o = _addmm(b_o, cg, w_o, bf)
         y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True)
         ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w)
-        ctx.inter = (h, mean1, rstd1, qkv, c, saved, s2, mean2, rstd2)
-        ctx.cfg = (core, p_out, seed_out, x.shape)
+        ctx.inter = (h, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2)
+        ctx.cfg = (core, p_out, seed_out, x.shape, bf)
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, ln1_w, w_qkv, w_o, ln2_w = ctx.saved_tensors
-        h, mean1, rstd1, qkv, c, saved, s2, mean2, rstd2 = ctx.inter
-        core, p_out, seed_out, shape = ctx.cfg
+        h, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2 = ctx.inter
+        core, p_out, seed_out, shape, bf = ctx.cfg
         ng = ctx.needs_input_grad
         dy2 = dy.reshape(-1, shape[-1]).contiguous()
         dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True)
-        dc = do @ w_o
-        dw_o = weight_grad(do, c) if ng[7] else None
+        if bf:
+            do = _b(do)
+        dc = _mm(do, w_o, bf)
+        dw_o = _wgrad(do, cg, bf) if ng[7] else None
         dqkv, dp1, dp2 = core.bwd(qkv, c, saved, dc, ng[1], ng[2])
         del dc, do
-        dh = dqkv @ w_qkv
-        dw_qkv = weight_grad(dqkv, h) if ng[5] else None
         db_qkv = colsum(dqkv) if ng[6] else None
+        if bf:
+            dqkv = _b(dqkv)
+        dh = _mm(dqkv, w_qkv, bf)
+        dw_qkv = _wgrad(dqkv, h, bf) if ng[5] else None
         del dqkv
         dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
         ctx.inter = None
