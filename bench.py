@@ -39,8 +39,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-sample-snapshots", type=int, default=8)
-    ap.add_argument("--gemm", default="fp32", choices=("fp32", "bf16"),
-                    help="projection GEMM operand precision (bf16: fp32 accumulate/outputs, rest fp32)")
+    ap.add_argument("--precision", default="fp32", choices=("fp32", "bf16-gemm", "bf16"),
+                    help="fp32 (parity mode); bf16-gemm: bf16 GEMM operands; bf16: bf16 activations between "
+                         "kernels, fp32 math (BASELINE's C2 dtype)")
     ap.add_argument("--shard", action="store_true",
                     help="one sequence sharded by snapshot over all ranks (strong scaling; C5 mode) instead of "
                          "one sequence per rank (data parallel, weak scaling)")
@@ -199,7 +200,7 @@ def main():
     cfg = synthetic.config_for(args.config)
     N, E, T, H, heads = synthetic.CONFIGS[args.config][:5]
     torch.manual_seed(0)
-    model = TAGAN(cfg, gemm_precision=args.gemm).to(dev).train()
+    model = TAGAN(cfg, precision=args.precision).to(dev).train()
     broadcast_parameters(model)
     opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay)
     init_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
@@ -268,7 +269,8 @@ def main():
         "value": round(value, 3), "unit": "graph-snapshots/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "strong" if args.shard else "weak", "vs_baseline": None,
-        "dtype": "fp32" if args.gemm == "fp32" else "fp32 (bf16 GEMM operands, fp32 accumulate)",
+        "dtype": {"fp32": "fp32", "bf16-gemm": "fp32 (bf16 GEMM operands, fp32 accumulate)",
+                  "bf16": "bf16 (activations; fp32 math and accumulation)"}[args.precision],
         "data": "synthetic (seeded social-media-shaped temporal graph per rank; no dataset offline)",
         "config": {"workload": "%s: %d nodes, %d edges/snapshot, %d snapshots, hidden %d, %d heads, euclidean "
                                "metric, dropout %.1f, train step = fwd+bwd+clip+Adam"

@@ -14,7 +14,9 @@
  *   - Return 0 (TAGAN_OK) or a negative tagan_status; tagan_last_error() gives a
  *     thread-local message for the last failure on the calling thread.
  *   - Device arrays are row-major.  "ld" arguments are row strides in elements.
- *   - dtype: TAGAN_F32 (fp32 storage, fp32 math).  Other values -> TAGAN_ERR_UNSUPPORTED.
+ *   - dtype: TAGAN_F32 (fp32 storage, fp32 math) everywhere; TAGAN_BF16 (bf16 storage of the
+ *     activation tensors, fp32 math) where an entry point says so.  LSE, partials, LayerNorm
+ *     statistics and parameter gradients are fp32 in both.  Other values -> TAGAN_ERR_UNSUPPORTED.
  *   - Dropout masks are counter-based: keep(u) with u = tagan_uniform(seed, stream, counter)
  *     (stream/counter layouts documented per kernel), so tests can regenerate them.
  */
@@ -36,7 +38,7 @@ enum tagan_status {
     TAGAN_ERR_WORKSPACE = -4     /* workspace too small */
 };
 
-enum tagan_dtype { TAGAN_F32 = 0 };
+enum tagan_dtype { TAGAN_F32 = 0, TAGAN_BF16 = 1 };
 
 /* Distance metrics of DistanceMetric.get_metric (geometric_attention.py:196-225).
  * Scores are similarities: distance metrics are negated as in
@@ -207,6 +209,7 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
  * temporal_attention.py:1190-1200) and plain layer_norm1 (b = NULL, p_drop = 0).
  *   s = dropout(a; p_drop, seed) + b     (element (r,c): stream r, counter c)
  *   y = (s - mean) / sqrt(var + eps) * gamma + beta       (biased var, as torch)
+ * dtype = storage of y (TAGAN_BF16: y feeds a bf16 GEMM); a, b, s, statistics fp32.
  * s_out (optional) keeps s for the backward pass; mean/rstd: [M].  y has row stride
  * ldy (0 = H; a wider stride leaves room for a ones column that turns the next
  * weight-gradient GEMM into weight + bias gradient).
@@ -221,6 +224,7 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
  * consumer, fused instead of a separate add), da = dL/ds masked/scaled by the same
  * dropout (the projection branch's gradient), dgamma/dbeta [H], dsum_a [H] = column
  * sums of da (the projection's bias gradient); block partials summed in block order.
+ * dtype = storage of da (TAGAN_BF16: da feeds a bf16 GEMM); everything else fp32.
  * Any of dres/ds/da/dgamma/dbeta/dsum_a may be NULL. */
 size_t tagan_layernorm_bwd_workspace(int64_t M, int32_t H);
 int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s, const float* mean,
@@ -295,10 +299,11 @@ int tagan_pool_fwd(int dtype, int32_t T, int64_t N, int32_t H, const float* x, i
 int tagan_pool_bwd(int dtype, int32_t T, int64_t N, int32_t H, const float* g, float* dx, int64_t ld_row,
                    int64_t ld_t, void* stream);
 
-/* Column sums of a tall row-major [M, N] matrix (row stride ld): the bias gradients of the
- * projections (sum of dY over rows).  Two-stage, ordered, deterministic.  N % 4 == 0. */
+/* Column sums of a tall row-major [M, N] matrix (row stride ld; dtype = its storage, fp32 or
+ * bf16): the bias gradients of the projections (sum of dY over rows), fp32 out.  Two-stage,
+ * ordered, deterministic.  N % 4 == 0. */
 size_t tagan_colsum_workspace(int64_t M, int32_t N);
-int tagan_colsum(int dtype, int64_t M, int32_t N, const float* x, int64_t ld, float* out, void* workspace,
+int tagan_colsum(int dtype, int64_t M, int32_t N, const void* x, int64_t ld, float* out, void* workspace,
                  size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus

@@ -15,6 +15,12 @@ LIB_PATH = os.environ.get("TAGAN_LIB") or os.path.join(_HERE, "libtagan_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tagan_hip.h")
 
 TAGAN_F32 = 0
+TAGAN_BF16 = 1
+
+
+def dtype_code(t) -> int:
+    """C-ABI storage code of a tensor: TAGAN_BF16 for bfloat16, else TAGAN_F32."""
+    return TAGAN_BF16 if t is not None and t.dtype == torch.bfloat16 else TAGAN_F32
 METRIC_IDS = {
     "euclidean": 0, "squared_euclidean": 1, "manhattan": 2, "cosine_similarity": 3,
     "cosine_distance": 4, "dot_product": 5, "scaled_dot_product": 6, "gaussian_kernel": 7,

@@ -90,6 +90,50 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nblk) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
+// ---------------------------------------------------------------- storage types
+// Activations are stored fp32 (TAGAN_F32) or bf16 (TAGAN_BF16); math is always fp32.
+// Io<S>::ld / st move 4 consecutive elements (element index i, a multiple of 4) as a float4.
+struct bf16s {};   // tag for bf16 storage
+
+__device__ __forceinline__ uint32_t f2bf_bits(float f) {   // round to nearest even, NaN kept quiet
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return u >> 16;
+}
+
+template <typename S>
+struct Io;
+
+template <>
+struct Io<float> {
+    static constexpr int bytes = 4;
+    __device__ static __forceinline__ float4 ld(const void* p, int64_t i) {
+        return *(const float4*)((const float*)p + i);
+    }
+    __device__ static __forceinline__ void st(void* p, int64_t i, float4 v) { *(float4*)((float*)p + i) = v; }
+    __device__ static __forceinline__ float ld1(const void* p, int64_t i) { return ((const float*)p)[i]; }
+};
+
+template <>
+struct Io<bf16s> {
+    static constexpr int bytes = 2;
+    __device__ static __forceinline__ float4 ld(const void* p, int64_t i) {
+        const uint2 u = *(const uint2*)((const uint16_t*)p + i);
+        return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                           __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+    }
+    __device__ static __forceinline__ void st(void* p, int64_t i, float4 v) {
+        uint2 u;
+        u.x = f2bf_bits(v.x) | (f2bf_bits(v.y) << 16);
+        u.y = f2bf_bits(v.z) | (f2bf_bits(v.w) << 16);
+        *(uint2*)((uint16_t*)p + i) = u;
+    }
+    __device__ static __forceinline__ float ld1(const void* p, int64_t i) {
+        return __uint_as_float((uint32_t)((const uint16_t*)p)[i] << 16);
+    }
+};
+
 // Deterministic column sums of a [nblk, n] (row stride ld) partials table (per-block dγ/dβ, bias-table
 // grads): one 1024-thread block per 64 columns, wave w sums rows w, w+16, ... with four
 // independent accumulators (loads in flight), then a fixed-order LDS tree.  Column x < split

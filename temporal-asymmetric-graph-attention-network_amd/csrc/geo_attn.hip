@@ -199,6 +199,7 @@ struct GeoArgs {
     float* part_v;      // [part_cap, H]  (fwd acc / bwd dq)
     float* part_v2;     // [part_cap, 2H] (bwd col: dk | dv)
     float inv_sqrt_d;
+    int bf16;           // activation storage: 0 fp32, 1 bf16 (fast path only)
 };
 
 #ifndef TAGAN_GEO_UNROLL
@@ -236,8 +237,9 @@ struct Lanes {
 };
 
 // ------------------------------------------------------------------ forward
-template <int METRIC, int LPR>
+template <int METRIC, int LPR, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
+    using IO = Io<S>;
     Lanes<LPR> L;
     const int nchunks = A.g.row_counts[0];
     const bool valid = L.chunk < nchunks;
@@ -251,7 +253,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
     const int f0 = L.sl * 4;
     const int h = f0 / A.d;
     const uint32_t dkey = drop_key(A.seed, (uint64_t)h);
-    const float4 qv = ld4(A.q + (int64_t)row * A.ld + f0);
+    const float4 qv = IO::ld(A.q, (int64_t)row * A.ld + f0);
     float qq = 0.f;
     if constexpr (MetricTraits<METRIC>::fam == FAM_COS)
         qq = grp_sum(qv.x * qv.x + qv.y * qv.y + qv.z * qv.z + qv.w * qv.w, A.lph);
@@ -265,10 +267,8 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
             const int j = __shfl(mycol, L.base + ((jj + u) % LPR), WAVE);
-            const float* kr = A.k + (int64_t)j * A.ld + f0;
-            const float* vr = A.v + (int64_t)j * A.ld + f0;
-            kv[u] = ld4(kr);
-            vv[u] = ld4(vr);
+            kv[u] = IO::ld(A.k, (int64_t)j * A.ld + f0);
+            vv[u] = IO::ld(A.v, (int64_t)j * A.ld + f0);
         }
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
     const int part = A.g.row_chunk_part[L.chunk];
     if (part < 0) {
         const float inv = (l > 0.f) ? 1.f / l : NAN;
-        st4(A.out + (int64_t)row * A.H + f0, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
+        IO::st(A.out, (int64_t)row * A.H + f0, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
         if ((L.sl % A.lph) == 0) A.lse[(int64_t)row * A.heads + h] = m + __logf(l);
     } else {
         st4(A.part_v + (int64_t)part * A.H + f0, acc);
@@ -311,7 +311,9 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
 
 // Merge the partial softmax states of multi-chunk rows, in chunk order.  One wave per row,
 // lane owns 4 features (H <= 256).
+template <typename S>
 __global__ void __launch_bounds__(BLK) k_geo_fwd_merge(GeoArgs A) {
+    using IO = Io<S>;
     const int64_t k = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6);
     if (k >= A.g.row_counts[1]) return;
     const int lane = threadIdx.x & (WAVE - 1);
@@ -338,13 +340,14 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_merge(GeoArgs A) {
         M = mn;
     }
     const float inv = (Lsum > 0.f) ? 1.f / Lsum : NAN;
-    st4(A.out + (int64_t)row * A.H + f0, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
+    IO::st(A.out, (int64_t)row * A.H + f0, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
     if ((lane % A.lph) == 0) A.lse[(int64_t)row * A.heads + h] = M + __logf(Lsum);
 }
 
 // ------------------------------------------------------------------ backward, row pass (CSR chunks)
-template <int METRIC, int LPR>
+template <int METRIC, int LPR, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
+    using IO = Io<S>;
     __shared__ float red[BLK];
     Lanes<LPR> L;
     const int nchunks = A.g.row_counts[0];
@@ -360,9 +363,9 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
     const uint32_t dkey = drop_key(A.seed, (uint64_t)h);
     float prm_acc = 0.f;
     if (__any(valid)) {
-        const float4 qv = ld4(A.q + (int64_t)row * A.ld + f0);
-        const float4 ov = ld4(A.o + (int64_t)row * A.H + f0);
-        const float4 dov = ld4(A.dout + (int64_t)row * A.H + f0);
+        const float4 qv = IO::ld(A.q, (int64_t)row * A.ld + f0);
+        const float4 ov = IO::ld(A.o, (int64_t)row * A.H + f0);
+        const float4 dov = IO::ld(A.dout, (int64_t)row * A.H + f0);
         const float D = grp_sum(dov.x * ov.x + dov.y * ov.y + dov.z * ov.z + dov.w * ov.w, A.lph);
         float qq = 0.f;
         if constexpr (MetricTraits<METRIC>::fam == FAM_COS)
@@ -377,8 +380,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
                 const int j = __shfl(mycol, L.base + ((jj + u) % LPR), WAVE);
-                kv[u] = ld4(A.k + (int64_t)j * A.ld + f0);
-                vv[u] = ld4(A.v + (int64_t)j * A.ld + f0);
+                kv[u] = IO::ld(A.k, (int64_t)j * A.ld + f0);
+                vv[u] = IO::ld(A.v, (int64_t)j * A.ld + f0);
             }
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
@@ -410,7 +413,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
         }
         if (valid) {
             const int part = A.g.row_chunk_part[L.chunk];
-            if (part < 0) st4(A.dq + (int64_t)row * A.ldd + f0, dq);
+            if (part < 0) IO::st(A.dq, (int64_t)row * A.ldd + f0, dq);
             else st4(A.part_v + (int64_t)part * A.H + f0, dq);
             if ((L.sl % A.lph) == 0 && A.g.row_chunk_ptr[row] == L.chunk) A.delta[(int64_t)row * A.heads + h] = D;
         }
@@ -429,12 +432,13 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
 }
 
 // Sum partial rows (bwd row: dq; bwd col: dk|dv) of multi-chunk segments in chunk order.
+template <typename S>
 __global__ void __launch_bounds__(BLK) k_geo_sum_parts(const int32_t* __restrict__ counts,
                                                        const int32_t* __restrict__ multi,
                                                        const int32_t* __restrict__ chunk_ptr,
                                                        const int32_t* __restrict__ chunk_part,
                                                        const float* __restrict__ part, int width,
-                                                       float* __restrict__ dst0, float* __restrict__ dst1,
+                                                       void* __restrict__ dst0, void* __restrict__ dst1,
                                                        int64_t ldd, int H) {
     const int64_t k = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6);
     if (k >= counts[1]) return;
@@ -447,14 +451,15 @@ __global__ void __launch_bounds__(BLK) k_geo_sum_parts(const int32_t* __restrict
             const float4 a = ld4(part + (int64_t)chunk_part[c] * width + f0);
             s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
         }
-        float* dst = (f0 < H) ? dst0 + (int64_t)seg * ldd + f0 : dst1 + (int64_t)seg * ldd + (f0 - H);
-        st4(dst, s);
+        if (f0 < H) Io<S>::st(dst0, (int64_t)seg * ldd + f0, s);
+        else Io<S>::st(dst1, (int64_t)seg * ldd + (f0 - H), s);
     }
 }
 
 // ------------------------------------------------------------------ backward, column pass (CSC chunks)
-template <int METRIC, int LPR>
+template <int METRIC, int LPR, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
+    using IO = Io<S>;
     Lanes<LPR> L;
     const int nchunks = A.g.col_counts[0];
     const bool valid = L.chunk < nchunks;
@@ -468,8 +473,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
     const int f0 = L.sl * 4;
     const int h = f0 / A.d;
     const uint32_t dkey = drop_key(A.seed, (uint64_t)h);
-    const float4 kv = ld4(A.k + (int64_t)colj * A.ld + f0);
-    const float4 vv = ld4(A.v + (int64_t)colj * A.ld + f0);
+    const float4 kv = IO::ld(A.k, (int64_t)colj * A.ld + f0);
+    const float4 vv = IO::ld(A.v, (int64_t)colj * A.ld + f0);
     const float prm = A.mparam ? A.mparam[h] : 1.f;
     float4 dk = make_float4(0.f, 0.f, 0.f, 0.f), dv = make_float4(0.f, 0.f, 0.f, 0.f);
     int myrow = 0, myeid = 0;
@@ -487,8 +492,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
             const int src = L.base + ((jj + u) % LPR);
             const int i = __shfl(myrow, src, WAVE);
             eid[u] = __shfl(myeid, src, WAVE);
-            qv[u] = ld4(A.q + (int64_t)i * A.ld + f0);
-            dov[u] = ld4(A.dout + (int64_t)i * A.H + f0);
+            qv[u] = IO::ld(A.q, (int64_t)i * A.ld + f0);
+            dov[u] = IO::ld(A.dout, (int64_t)i * A.H + f0);
             lse[u] = A.lse_in[(int64_t)i * A.heads + h];
             D[u] = A.delta[(int64_t)i * A.heads + h];
         }
@@ -532,8 +537,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
     if (!valid) return;
     const int part = A.g.col_chunk_part[L.chunk];
     if (part < 0) {
-        st4(A.dk + (int64_t)colj * A.ldd + f0, dk);
-        st4(A.dv + (int64_t)colj * A.ldd + f0, dv);
+        IO::st(A.dk, (int64_t)colj * A.ldd + f0, dk);
+        IO::st(A.dv, (int64_t)colj * A.ldd + f0, dv);
     } else {
         st4(A.part_v2 + (int64_t)part * 2 * A.H + f0, dk);
         st4(A.part_v2 + (int64_t)part * 2 * A.H + A.H + f0, dv);
@@ -737,12 +742,18 @@ int64_t chunk_blocks(const GeoArgs& A, int lpr) {
     return std::max<int64_t>(1, (waves + (BLK / WAVE) - 1) / (BLK / WAVE));
 }
 
+template <int METRIC, int LPR, typename S>
+void launch_fast_s(Pass pass, const GeoArgs& A, hipStream_t s) {
+    const dim3 g((unsigned)chunk_blocks(A, LPR));
+    if (pass == P_FWD) k_geo_fwd_chunk<METRIC, LPR, S><<<g, BLK, 0, s>>>(A);
+    else if (pass == P_BWD_ROW) k_geo_bwd_row_chunk<METRIC, LPR, S><<<g, BLK, 0, s>>>(A);
+    else k_geo_bwd_col_chunk<METRIC, LPR, S><<<g, BLK, 0, s>>>(A);
+}
+
 template <int METRIC, int LPR>
 void launch_fast(Pass pass, const GeoArgs& A, hipStream_t s) {
-    const dim3 g((unsigned)chunk_blocks(A, LPR));
-    if (pass == P_FWD) k_geo_fwd_chunk<METRIC, LPR><<<g, BLK, 0, s>>>(A);
-    else if (pass == P_BWD_ROW) k_geo_bwd_row_chunk<METRIC, LPR><<<g, BLK, 0, s>>>(A);
-    else k_geo_bwd_col_chunk<METRIC, LPR><<<g, BLK, 0, s>>>(A);
+    if (A.bf16) launch_fast_s<METRIC, LPR, bf16s>(pass, A, s);
+    else launch_fast_s<METRIC, LPR, float>(pass, A, s);
 }
 
 template <int METRIC>
@@ -788,7 +799,8 @@ int launch(int metric, Pass pass, int lpr, const GeoArgs& A, hipStream_t s, floa
 }
 
 int check_common(int dtype, int metric, const tagan_graph* g, int heads, int d, int64_t ld, float p_drop) {
-    TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "geo_attn: dtype %d unsupported", dtype);
+    TAGAN_REQUIRE(dtype == TAGAN_F32 || (dtype == TAGAN_BF16 && pick_lpr(heads * d, d) != 0),
+                  TAGAN_ERR_UNSUPPORTED, "geo_attn: dtype %d unsupported for H=%d d=%d", dtype, heads * d, d);
     TAGAN_REQUIRE(metric >= 0 && metric <= TAGAN_METRIC_RBF_KERNEL, TAGAN_ERR_UNSUPPORTED,
                   "geo_attn: unsupported metric %d", metric);
     TAGAN_REQUIRE(g != nullptr && g->n_nodes > 0 && g->rowptr && g->col, TAGAN_ERR_ARG, "geo_attn: bad graph");
@@ -877,7 +889,9 @@ int tagan_geo_attn_fwd(int dtype, int metric, const tagan_graph* g, int32_t head
     const size_t need = fwd_ws(g, heads, head_dim);
     TAGAN_REQUIRE(need == 0 || (workspace && workspace_bytes >= need), TAGAN_ERR_WORKSPACE,
                   "geo_attn_fwd: workspace %zu < %zu", workspace_bytes, need);
+    TAGAN_REQUIRE(!(dtype == TAGAN_BF16 && edge_alpha), TAGAN_ERR_UNSUPPORTED, "geo_attn_fwd: edge_alpha needs fp32");
     GeoArgs A = make_args(g, heads, head_dim, q, k, v, ld_qkv, metric_param, p_drop, seed);
+    A.bf16 = dtype == TAGAN_BF16;
     A.out = (float*)out;
     A.lse = lse;
     if (need) {
@@ -892,7 +906,8 @@ int tagan_geo_attn_fwd(int dtype, int metric, const tagan_graph* g, int32_t head
     TAGAN_CHECK_LAUNCH("geo_attn_fwd");
     if (lpr) {
         const unsigned gm = (unsigned)((g->part_cap + (BLK / WAVE) - 1) / (BLK / WAVE));
-        k_geo_fwd_merge<<<gm, BLK, 0, s>>>(A);
+        if (A.bf16) k_geo_fwd_merge<bf16s><<<gm, BLK, 0, s>>>(A);
+        else k_geo_fwd_merge<float><<<gm, BLK, 0, s>>>(A);
         TAGAN_CHECK_LAUNCH("geo_attn_fwd_merge");
     }
     if (edge_alpha) {
@@ -930,6 +945,7 @@ int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t head
                       TAGAN_ERR_ARG, "geo_attn_bwd: graph lacks column chunk lists");
     }
     GeoArgs A = make_args(g, heads, head_dim, q, k, v, ld_qkv, metric_param, p_drop, seed);
+    A.bf16 = dtype == TAGAN_BF16;
     A.o = (const float*)out;
     A.lse_in = lse;
     A.dout = (const float*)dout;
@@ -950,16 +966,24 @@ int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t head
     TAGAN_CHECK_LAUNCH("geo_attn_bwd_row");
     const unsigned gm = (unsigned)((g->part_cap + (BLK / WAVE) - 1) / (BLK / WAVE));
     if (lpr) {
-        k_geo_sum_parts<<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr, g->row_chunk_part,
-                                           A.part_v, H, A.dq, A.dq, A.ldd, H);
+        if (A.bf16)
+            k_geo_sum_parts<bf16s><<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr,
+                                                      g->row_chunk_part, A.part_v, H, A.dq, A.dq, A.ldd, H);
+        else
+            k_geo_sum_parts<float><<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr,
+                                                      g->row_chunk_part, A.part_v, H, A.dq, A.dq, A.ldd, H);
         TAGAN_CHECK_LAUNCH("geo_attn_bwd_row_merge");
     }
     rc = launch(metric, P_BWD_COL, lpr, A, s);
     if (rc) return rc;
     TAGAN_CHECK_LAUNCH("geo_attn_bwd_col");
     if (lpr) {
-        k_geo_sum_parts<<<gm, BLK, 0, s>>>(g->col_counts, g->col_multi, g->col_chunk_ptr, g->col_chunk_part,
-                                           A.part_v2, 2 * H, A.dk, A.dv, A.ldd, H);
+        if (A.bf16)
+            k_geo_sum_parts<bf16s><<<gm, BLK, 0, s>>>(g->col_counts, g->col_multi, g->col_chunk_ptr,
+                                                      g->col_chunk_part, A.part_v2, 2 * H, A.dk, A.dv, A.ldd, H);
+        else
+            k_geo_sum_parts<float><<<gm, BLK, 0, s>>>(g->col_counts, g->col_multi, g->col_chunk_ptr,
+                                                      g->col_chunk_part, A.part_v2, 2 * H, A.dk, A.dv, A.ldd, H);
         TAGAN_CHECK_LAUNCH("geo_attn_bwd_col_merge");
     }
     if (dmetric_param) {

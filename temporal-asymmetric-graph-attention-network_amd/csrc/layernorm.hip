@@ -60,7 +60,7 @@ __device__ __forceinline__ float4 drop4(const LnArgs& A, float4 v, int64_t row, 
     return v;
 }
 
-template <int LPR, int NV>
+template <int LPR, int NV, typename S>
 __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
     constexpr int RPW = WAVE / LPR;
     const int lane = threadIdx.x & (WAVE - 1), sl = lane % LPR;
@@ -102,7 +102,7 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
         o.y = (v[n].y - mean) * rstd * g.y + be.y;
         o.z = (v[n].z - mean) * rstd * g.z + be.z;
         o.w = (v[n].w - mean) * rstd * g.w + be.w;
-        st4(A.y + row * A.ldy + c, o);
+        Io<S>::st(A.y, row * A.ldy + c, o);     // y in the storage type (bf16 feeds a GEMM)
     }
     if (sl == 0) {
         A.mean[row] = mean;
@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
     }
 }
 
-template <int LPR, int NV>
+template <int LPR, int NV, typename S>
 __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
     constexpr int RPW = WAVE / LPR;
     __shared__ float red[BLK / WAVE][RPW][3 * 4 * NV * LPR];
@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
             o.w = rstd * (gd[n].w - c1 * xh[n].w - c2);
             if (A.da || A.want_dsa) {
                 const float4 a = drop4(A, o, row, c);
-                if (A.da) st4(A.da + row * H + c, a);
+                if (A.da) Io<S>::st(A.da, row * H + c, a);   // da in the storage type
                 dsa[n].x += a.x; dsa[n].y += a.y; dsa[n].z += a.z; dsa[n].w += a.w;
             }
             if (A.ds) {
@@ -201,6 +201,17 @@ bool geometry(int H, int& lpr, int& nv) {
 
 constexpr int LN_BWD_BLOCKS = 1024;
 
+template <typename S, bool FWD>
+void launch_ln(int lpr, int nv, dim3 g, hipStream_t s, const LnArgs& A) {
+#define TAGAN_LN_K(L, N) (FWD ? k_ln_fwd<L, N, S> : k_ln_bwd<L, N, S>)<<<g, BLK, 0, s>>>(A)
+    if (lpr == 8) TAGAN_LN_K(8, 1);
+    else if (lpr == 16) TAGAN_LN_K(16, 1);
+    else if (lpr == 32) TAGAN_LN_K(32, 1);
+    else if (nv == 1) TAGAN_LN_K(64, 1);
+    else TAGAN_LN_K(64, 2);
+#undef TAGAN_LN_K
+}
+
 }  // namespace
 }  // namespace tagan
 
@@ -216,7 +227,7 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
                             int64_t ldy, float* mean, float* rstd, void* stream) {
     using namespace tagan;
     int lpr, nv;
-    TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "layernorm: dtype %d", dtype);
+    TAGAN_REQUIRE(dtype == TAGAN_F32 || dtype == TAGAN_BF16, TAGAN_ERR_UNSUPPORTED, "layernorm: dtype %d", dtype);
     TAGAN_REQUIRE(geometry(H, lpr, nv), TAGAN_ERR_UNSUPPORTED, "layernorm: H=%d unsupported", H);
     TAGAN_REQUIRE(M > 0 && a && gamma && beta && y && mean && rstd, TAGAN_ERR_ARG, "layernorm_fwd: bad args");
     TAGAN_REQUIRE(p_drop >= 0.f && p_drop < 1.f, TAGAN_ERR_ARG, "layernorm_fwd: p_drop");
@@ -228,11 +239,8 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
     const int64_t rpw = WAVE / lpr;
     const dim3 g((unsigned)(((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE)));
     hipStream_t s = as_stream(stream);
-    if (lpr == 8) k_ln_fwd<8, 1><<<g, BLK, 0, s>>>(A);
-    else if (lpr == 16) k_ln_fwd<16, 1><<<g, BLK, 0, s>>>(A);
-    else if (lpr == 32) k_ln_fwd<32, 1><<<g, BLK, 0, s>>>(A);
-    else if (nv == 1) k_ln_fwd<64, 1><<<g, BLK, 0, s>>>(A);
-    else k_ln_fwd<64, 2><<<g, BLK, 0, s>>>(A);
+    if (dtype == TAGAN_BF16) launch_ln<bf16s, true>(lpr, nv, g, s, A);
+    else launch_ln<float, true>(lpr, nv, g, s, A);
     TAGAN_CHECK_LAUNCH("layernorm_fwd");
     return TAGAN_OK;
 }
@@ -248,7 +256,7 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, cons
                         size_t workspace_bytes, void* stream) {
     using namespace tagan;
     int lpr, nv;
-    TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "layernorm: dtype %d", dtype);
+    TAGAN_REQUIRE(dtype == TAGAN_F32 || dtype == TAGAN_BF16, TAGAN_ERR_UNSUPPORTED, "layernorm: dtype %d", dtype);
     TAGAN_REQUIRE(geometry(H, lpr, nv), TAGAN_ERR_UNSUPPORTED, "layernorm: H=%d unsupported", H);
     TAGAN_REQUIRE(M > 0 && s_in && mean && rstd && gamma && dy, TAGAN_ERR_ARG, "layernorm_bwd: bad args");
     const bool want = dgamma || dbeta || dsum_a;
@@ -263,11 +271,8 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, cons
     const int64_t need = ((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE);
     const int nblk = (int)std::min<int64_t>(need, LN_BWD_BLOCKS);
     hipStream_t s = as_stream(stream);
-    if (lpr == 8) k_ln_bwd<8, 1><<<nblk, BLK, 0, s>>>(A);
-    else if (lpr == 16) k_ln_bwd<16, 1><<<nblk, BLK, 0, s>>>(A);
-    else if (lpr == 32) k_ln_bwd<32, 1><<<nblk, BLK, 0, s>>>(A);
-    else if (nv == 1) k_ln_bwd<64, 1><<<nblk, BLK, 0, s>>>(A);
-    else k_ln_bwd<64, 2><<<nblk, BLK, 0, s>>>(A);
+    if (dtype == TAGAN_BF16) launch_ln<bf16s, false>(lpr, nv, dim3(nblk), s, A);
+    else launch_ln<float, false>(lpr, nv, dim3(nblk), s, A);
     TAGAN_CHECK_LAUNCH("layernorm_bwd");
     if (dgamma || dbeta) {
         launch_colsum(A.part, nblk, 2 * H, dgamma, dbeta, H, s, 1.f, 3 * H);

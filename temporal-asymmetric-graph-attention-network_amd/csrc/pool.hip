@@ -103,7 +103,8 @@ namespace {
 
 constexpr int CS_BLOCKS = 512;
 
-__global__ void __launch_bounds__(BLK) k_colsum_rows(const float* __restrict__ x, int64_t M, int N, int64_t ld,
+template <typename S>
+__global__ void __launch_bounds__(BLK) k_colsum_rows(const void* __restrict__ x, int64_t M, int N, int64_t ld,
                                                      float* __restrict__ part) {
     __shared__ float red[4 * BLK];
     const int lpr = N / 4, rpb = BLK / lpr;
@@ -113,7 +114,7 @@ __global__ void __launch_bounds__(BLK) k_colsum_rows(const float* __restrict__ x
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (rsub < rpb)
         for (int64_t r = a + rsub; r < b; r += rpb) {
-            const float4 v = *(const float4*)(x + r * ld + lane * 4);
+            const float4 v = Io<S>::ld(x, r * ld + lane * 4);
             acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
         }
     if (rsub < rpb) *(float4*)(red + (size_t)rsub * N + lane * 4) = acc;
@@ -135,16 +136,17 @@ size_t tagan_colsum_workspace(int64_t M, int32_t N) {
     return (size_t)tagan::CS_BLOCKS * N * sizeof(float);
 }
 
-int tagan_colsum(int dtype, int64_t M, int32_t N, const float* x, int64_t ld, float* out, void* workspace,
+int tagan_colsum(int dtype, int64_t M, int32_t N, const void* x, int64_t ld, float* out, void* workspace,
                  size_t workspace_bytes, void* stream) {
     using namespace tagan;
-    TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "colsum: dtype %d", dtype);
+    TAGAN_REQUIRE(dtype == TAGAN_F32 || dtype == TAGAN_BF16, TAGAN_ERR_UNSUPPORTED, "colsum: dtype %d", dtype);
     TAGAN_REQUIRE(M > 0 && N % 4 == 0 && N >= 4 && N / 4 <= BLK && ld % 4 == 0 && ld >= N && x && out,
                   TAGAN_ERR_ARG, "colsum: bad args (N=%d)", N);
     TAGAN_REQUIRE(workspace && workspace_bytes >= tagan_colsum_workspace(M, N), TAGAN_ERR_WORKSPACE, "colsum: ws");
     const int nblk = (int)std::min<int64_t>(CS_BLOCKS, (M + 63) / 64);
     hipStream_t s = as_stream(stream);
-    k_colsum_rows<<<nblk, BLK, 0, s>>>(x, M, N, ld, (float*)workspace);
+    if (dtype == TAGAN_BF16) k_colsum_rows<bf16s><<<nblk, BLK, 0, s>>>(x, M, N, ld, (float*)workspace);
+    else k_colsum_rows<float><<<nblk, BLK, 0, s>>>(x, M, N, ld, (float*)workspace);
     TAGAN_CHECK_LAUNCH("colsum_rows");
     launch_colsum((float*)workspace, nblk, N, out, nullptr, N, s);
     TAGAN_CHECK_LAUNCH("colsum_parts");

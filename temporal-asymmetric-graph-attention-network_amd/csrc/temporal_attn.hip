@@ -596,6 +596,23 @@ __device__ __forceinline__ void st_row(float* __restrict__ p, const float (&r)[D
         *(float4*)(p + c) = make_float4(r[c] * scale, r[c + 1] * scale, r[c + 2] * scale, r[c + 3] * scale);
 }
 
+// Global row I/O in the activation storage type S (fp32 or bf16), element index i.
+template <int D, typename S>
+__device__ __forceinline__ void gld_row(const void* __restrict__ p, int64_t i, float (&r)[D]) {
+#pragma unroll
+    for (int c = 0; c < D; c += 4) {
+        const float4 t = Io<S>::ld(p, i + c);
+        r[c] = t.x; r[c + 1] = t.y; r[c + 2] = t.z; r[c + 3] = t.w;
+    }
+}
+
+template <int D, typename S>
+__device__ __forceinline__ void gst_row(void* __restrict__ p, int64_t i, const float (&r)[D], float scale) {
+#pragma unroll
+    for (int c = 0; c < D; c += 4)
+        Io<S>::st(p, i + c, make_float4(r[c] * scale, r[c + 1] * scale, r[c + 2] * scale, r[c + 3] * scale));
+}
+
 template <int D>
 __device__ __forceinline__ float dot_rl(const float (&a)[D], const float* __restrict__ b) {
     float s = 0.f;
@@ -656,7 +673,7 @@ size_t v3_bwd_lds(int T, int D, int HPW) {
     return (size_t)HPW * (2 * T * D + 2 * T + 2 * align_up(2 * T - 1, 4)) * 4;
 }
 
-template <int D, int LG>
+template <int D, int LG, typename S>
 __global__ void __launch_bounds__(V3_BLK) k_tattn_fwd_v3(TArgs A, const float* __restrict__ q,
                                                          const float* __restrict__ k, const float* __restrict__ v,
                                                          int n_hg) {
@@ -677,9 +694,9 @@ __global__ void __launch_bounds__(V3_BLK) k_tattn_fwd_v3(TArgs A, const float* _
         const int hc = hok ? h : A.heads - 1;
         const int64_t base = r * A.s_row + (int64_t)i * A.s_t + hc * D;
         float qv[D], kv[D], vv[D];
-        ld_row<D>(q + base, qv);
-        ld_row<D>(k + base, kv);
-        ld_row<D>(v + base, vv);
+        gld_row<D, S>(q, base, qv);
+        gld_row<D, S>(k, base, kv);
+        gld_row<D, S>(v, base, vv);
         wave_sync();   // previous unit's LDS reads are done before the slice is rewritten
         to_lds<D>(Ks + (hl * T + i) * D, kv);
         to_lds<D>(Vs + (hl * T + i) * D, vv);
@@ -708,13 +725,13 @@ __global__ void __launch_bounds__(V3_BLK) k_tattn_fwd_v3(TArgs A, const float* _
         }
         if (live && hok) {
             const float inv_l = (l > 0.f) ? 1.f / l : NAN;
-            st_row<D>(A.out + r * A.o_row + (int64_t)i * A.o_t + h * D, acc, inv_l);
+            gst_row<D, S>(A.out, r * A.o_row + (int64_t)i * A.o_t + h * D, acc, inv_l);
             A.lse[(r * A.heads + h) * T + i] = m + __logf(l);
         }
     }
 }
 
-template <int D, int LG>
+template <int D, int LG, typename S>
 __global__ void __launch_bounds__(V3_BLK) k_tattn_bwd_v3(TArgs A, const float* __restrict__ q,
                                                          const float* __restrict__ k, const float* __restrict__ v,
                                                          const float* __restrict__ dout,
@@ -741,14 +758,14 @@ __global__ void __launch_bounds__(V3_BLK) k_tattn_bwd_v3(TArgs A, const float* _
         const int hc = hok ? h : A.heads - 1;
         const int64_t base = r * A.s_row + (int64_t)i * A.s_t + hc * D;
         float qv[D], kv[D], vv[D], dov[D];
-        ld_row<D>(q + base, qv);
-        ld_row<D>(k + base, kv);
-        ld_row<D>(v + base, vv);
-        ld_row<D>(dout + r * A.do_row + (int64_t)i * A.do_t + hc * D, dov);   // kv/vv die after staging
+        gld_row<D, S>(q, base, qv);
+        gld_row<D, S>(k, base, kv);
+        gld_row<D, S>(v, base, vv);
+        gld_row<D, S>(dout, r * A.do_row + (int64_t)i * A.do_t + hc * D, dov);   // kv/vv die after staging
         float Di;
         {
             float ov[D];
-            ld_row<D>(A.o_in + r * A.o_row + (int64_t)i * A.o_t + hc * D, ov);
+            gld_row<D, S>(A.o_in, r * A.o_row + (int64_t)i * A.o_t + hc * D, ov);
             Di = dot_rr<D>(dov, ov);
         }
         const float li_lse = lse[(r * A.heads + hc) * T + i];
@@ -778,7 +795,7 @@ __global__ void __launch_bounds__(V3_BLK) k_tattn_bwd_v3(TArgs A, const float* _
                 const float ds = p * (dot_rl<D>(dov, vb + j * D) * drop_scale(A, drk, i, j) - Di);
                 fma_l<D>(dq, ds, kb + j * D);
             }
-            if (live && hok) st_row<D>(A.dq + r * A.d_row + (int64_t)i * A.d_t + h * D, dq, A.inv_sqrt_d);
+            if (live && hok) gst_row<D, S>(A.dq, r * A.d_row + (int64_t)i * A.d_t + h * D, dq, A.inv_sqrt_d);
         }
         wave_sync();
         // swap: each lane takes its own K/V row back from LDS and leaves its Q/dO row in its place
@@ -822,8 +839,8 @@ __global__ void __launch_bounds__(V3_BLK) k_tattn_bwd_v3(TArgs A, const float* _
                     A.dbias_dense[((r * A.heads + h) * T + ii) * (int64_t)T + j] = ds;
             }
             if (live && hok) {
-                st_row<D>(A.dk + r * A.d_row + (int64_t)j * A.d_t + h * D, dk, A.inv_sqrt_d);
-                st_row<D>(A.dv + r * A.d_row + (int64_t)j * A.d_t + h * D, dv, 1.f);
+                gst_row<D, S>(A.dk, r * A.d_row + (int64_t)j * A.d_t + h * D, dk, A.inv_sqrt_d);
+                gst_row<D, S>(A.dv, r * A.d_row + (int64_t)j * A.d_t + h * D, dv, 1.f);
             }
         }
     }
@@ -859,7 +876,8 @@ int pick_D(int d) {
 int grid_rows(int64_t rows) { return (int)std::min<int64_t>(rows, 256 * 4); }
 
 int check(int dtype, int64_t rows, int T, int heads, int d, float p_drop) {
-    TAGAN_REQUIRE(dtype == TAGAN_F32, TAGAN_ERR_UNSUPPORTED, "temporal_attn: dtype %d unsupported", dtype);
+    TAGAN_REQUIRE(dtype == TAGAN_F32 || dtype == TAGAN_BF16, TAGAN_ERR_UNSUPPORTED, "temporal_attn: dtype %d",
+                  dtype);
     TAGAN_REQUIRE(rows > 0 && T > 0 && heads > 0 && d > 0, TAGAN_ERR_ARG, "temporal_attn: bad sizes");
     TAGAN_REQUIRE(pick_D(d) != 0, TAGAN_ERR_UNSUPPORTED, "temporal_attn: head_dim %d > 128", d);
     TAGAN_REQUIRE(p_drop >= 0.f && p_drop < 1.f, TAGAN_ERR_ARG, "temporal_attn: p_drop %f", (double)p_drop);
@@ -918,11 +936,14 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     const float* kf = (const float*)k;
     const float* vf = (const float*)v;
     const bool al4 = s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0;
+    const bool bf = dtype == TAGAN_BF16;
+    TAGAN_REQUIRE(!bf || (al4 && !attn && v3_ok(T, head_dim)), TAGAN_ERR_UNSUPPORTED,
+                  "temporal_attn_fwd: bf16 storage needs the v3 kernels (T <= 64, head_dim 8..64, no attn output)");
     if (al4 && !attn && v3_ok(T, head_dim)) {
         const int LG = v3_lanes(T), HPW = WAVE / LG, n_hg = (heads + HPW - 1) / HPW;
         const dim3 g3((unsigned)(grid_rows(rows) * n_hg));
         const size_t lds = v3_fwd_lds(T, head_dim, HPW);
-#define TAGAN_V3F(DD, LL) k_tattn_fwd_v3<DD, LL><<<g3, V3_BLK, lds, s>>>(A, qf, kf, vf, n_hg)
+#define TAGAN_V3F(DD, LL) (bf ? k_tattn_fwd_v3<DD, LL, bf16s> : k_tattn_fwd_v3<DD, LL, float>)<<<g3, V3_BLK, lds, s>>>(A, qf, kf, vf, n_hg)
 #define TAGAN_V3F_D(LL) switch (head_dim) { case 8: TAGAN_V3F(8, LL); break; case 16: TAGAN_V3F(16, LL); break; \
                                             case 32: TAGAN_V3F(32, LL); break; default: TAGAN_V3F(64, LL); break; }
         if (LG == 16) { TAGAN_V3F_D(16) } else if (LG == 32) { TAGAN_V3F_D(32) } else { TAGAN_V3F_D(64) }
@@ -1006,12 +1027,15 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     const float* df = (const float*)dout;
     const bool al4 = s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0 && do_t % 4 == 0 &&
                      do_row % 4 == 0 && d_t % 4 == 0 && d_row % 4 == 0;
+    const bool bf = dtype == TAGAN_BF16;
+    TAGAN_REQUIRE(!bf || (al4 && v3_ok(T, head_dim)), TAGAN_ERR_UNSUPPORTED,
+                  "temporal_attn_bwd: bf16 storage needs the v3 kernels (T <= 64, head_dim 8..64)");
     if (al4 && v3_ok(T, head_dim)) {
         // grid = nblk partial rows x n_hg head groups; block b keeps head group b % n_hg
         const int LG = v3_lanes(T), HPW = WAVE / LG, n_hg = (heads + HPW - 1) / HPW;
         const dim3 g3((unsigned)(nblk * n_hg));
         const size_t lds = v3_bwd_lds(T, head_dim, HPW);
-#define TAGAN_V3B(DD, LL) k_tattn_bwd_v3<DD, LL><<<g3, V3_BLK, lds, s>>>(A, qf, kf, vf, df, lse, n_hg)
+#define TAGAN_V3B(DD, LL) (bf ? k_tattn_bwd_v3<DD, LL, bf16s> : k_tattn_bwd_v3<DD, LL, float>)<<<g3, V3_BLK, lds, s>>>(A, qf, kf, vf, df, lse, n_hg)
 #define TAGAN_V3B_D(LL) switch (head_dim) { case 8: TAGAN_V3B(8, LL); break; case 16: TAGAN_V3B(16, LL); break; \
                                             case 32: TAGAN_V3B(32, LL); break; default: TAGAN_V3B(64, LL); break; }
         if (LG == 16) { TAGAN_V3B_D(16) } else if (LG == 32) { TAGAN_V3B_D(32) } else { TAGAN_V3B_D(64) }

@@ -25,32 +25,33 @@ from .kernels import TemporalMask, _geo_fwd, colsum, weight_grad
 
 
 # ----------------------------------------------------------------------------- raw LayerNorm calls
-def ln_fwd(a2, b2, p_drop, seed, gamma, beta, eps, keep_s, y=None):
-    """LN(dropout(a2) + b2); ``y`` may be a wider row-strided buffer ([M, ld], first H columns written)."""
+def ln_fwd(a2, b2, p_drop, seed, gamma, beta, eps, keep_s, y=None, y_dtype=torch.float32):
+    """LN(dropout(a2) + b2); ``y`` may be a wider row-strided buffer ([M, ld], first H columns written);
+    y is stored in ``y_dtype`` (bf16 when it only feeds a bf16 GEMM)."""
     M, H = a2.shape
     s = torch.empty_like(a2) if keep_s else None
     if y is None:
-        y = torch.empty_like(a2)
+        y = torch.empty(M, H, device=a2.device, dtype=y_dtype)
     mean = torch.empty(M, device=a2.device)
     rstd = torch.empty(M, device=a2.device)
-    check(lib().tagan_add_layernorm_fwd(_lib.TAGAN_F32, M, H, ptr(a2), ptr(b2), float(p_drop), seed, ptr(gamma),
+    check(lib().tagan_add_layernorm_fwd(_lib.dtype_code(y), M, H, ptr(a2), ptr(b2), float(p_drop), seed, ptr(gamma),
                                         ptr(beta), float(eps), ptr(s), ptr(y), y.stride(0), ptr(mean), ptr(rstd),
                                         stream_of(a2)), "tagan_add_layernorm_fwd")
     return y, s, mean, rstd
 
 
-def ln_bwd(s, mean, rstd, gamma, dy2, dres, p_drop, seed, want_ds, want_da, want_sum_a):
+def ln_bwd(s, mean, rstd, gamma, dy2, dres, p_drop, seed, want_ds, want_da, want_sum_a, da_dtype=torch.float32):
     M, H = dy2.shape
     dev = dy2.device
     ds = torch.empty_like(dy2) if want_ds else None
-    da = torch.empty_like(dy2) if want_da else None
+    da = torch.empty(M, H, device=dev, dtype=da_dtype) if want_da else None
     dg = torch.empty(H, device=dev)
     dbt = torch.empty(H, device=dev)
     dsa = torch.empty(H, device=dev) if want_sum_a else None
     L = lib()
     wsb = L.tagan_layernorm_bwd_workspace(M, H)
     ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
-    check(L.tagan_layernorm_bwd(_lib.TAGAN_F32, M, H, ptr(s), ptr(mean), ptr(rstd), ptr(gamma), ptr(dy2), ptr(dres),
+    check(L.tagan_layernorm_bwd(_lib.dtype_code(da), M, H, ptr(s), ptr(mean), ptr(rstd), ptr(gamma), ptr(dy2), ptr(dres),
                                 float(p_drop), seed, ptr(ds), ptr(da), ptr(dg), ptr(dbt), ptr(dsa), ptr(ws), wsb,
                                 stream_of(dy2)), "tagan_layernorm_bwd")
     return ds, da, dg, dbt, dsa
@@ -65,7 +66,7 @@ class GeoCore:
 
     def fwd(self, qkv2, param, _unused):
         N, H3 = qkv2.shape
-        out = torch.empty(N, H3 // 3, device=qkv2.device)
+        out = torch.empty(N, H3 // 3, device=qkv2.device, dtype=qkv2.dtype)
         lse = torch.empty(N, self.heads, device=qkv2.device)
         prm = param.detach().contiguous() if param is not None else None
         _geo_fwd(qkv2, self.graph, self.metric, self.heads, prm, self.p_drop, self.seed, out, lse, None)
@@ -83,7 +84,7 @@ class GeoCore:
         ws = torch.empty(int(wsb), dtype=torch.uint8, device=qkv2.device)
         dprm = torch.empty(self.heads, device=qkv2.device) if (prm is not None and want_p1) else None
         b, db, es = qkv2.data_ptr(), dqkv.data_ptr(), qkv2.element_size()
-        check(L.tagan_geo_attn_bwd(_lib.TAGAN_F32, self.metric, gs, self.heads, d, b, b + H * es, b + 2 * H * es, H3,
+        check(L.tagan_geo_attn_bwd(_lib.dtype_code(qkv2), self.metric, gs, self.heads, d, b, b + H * es, b + 2 * H * es, H3,
                                    ptr(prm), float(self.p_drop), self.seed, ptr(out), ptr(lse), ptr(dctx), db,
                                    db + H * es, db + 2 * H * es, H3, ptr(dprm), ptr(ws), wsb, stream_of(qkv2)),
               "tagan_geo_attn_bwd")
@@ -110,14 +111,14 @@ class TemporalCore:
         H = qkv2.shape[1] // 3
         d = H // heads
         (s_row, s_t), (o_row, o_t) = self._strides(H)
-        out = torch.empty(T * R, H, device=qkv2.device)
+        out = torch.empty(T * R, H, device=qkv2.device, dtype=qkv2.dtype)
         lse = torch.empty(R, heads, T, device=qkv2.device)
         bt = bias_table.detach().contiguous() if bias_table is not None else None
         bd = bias_dense.detach().contiguous() if bias_dense is not None else None
         bd_stride = (0 if bd.shape[0] == 1 else heads * T * T) if bd is not None else 0
         m = self.mask
         b, es = qkv2.data_ptr(), qkv2.element_size()
-        check(lib().tagan_temporal_attn_fwd(_lib.TAGAN_F32, R, T, heads, d, b, b + H * es, b + 2 * H * es, s_row,
+        check(lib().tagan_temporal_attn_fwd(_lib.dtype_code(qkv2), R, T, heads, d, b, b + H * es, b + 2 * H * es, s_row,
                                             s_t, ptr(bt), ptr(bd), bd_stride, ptr(m.keep), m.bstride, m.hstride,
                                             int(m.causal), float(self.p_drop), self.seed, ptr(out), o_row, o_t,
                                             ptr(lse), None, stream_of(qkv2)), "tagan_temporal_attn_fwd")
@@ -138,7 +139,7 @@ class TemporalCore:
         ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
         m = self.mask
         b, db, es = qkv2.data_ptr(), dqkv.data_ptr(), qkv2.element_size()
-        check(L.tagan_temporal_attn_bwd(_lib.TAGAN_F32, R, T, heads, d, b, b + H * es, b + 2 * H * es, s_row, s_t,
+        check(L.tagan_temporal_attn_bwd(_lib.dtype_code(qkv2), R, T, heads, d, b, b + H * es, b + 2 * H * es, s_row, s_t,
                                         ptr(bt), ptr(bd), bd_stride, ptr(m.keep), m.bstride, m.hstride,
                                         int(m.causal), float(self.p_drop), self.seed, ptr(out), o_row, o_t, ptr(lse),
                                         ptr(dctx), o_row, o_t, db, db + H * es, db + 2 * H * es, s_row, s_t,
@@ -149,42 +150,51 @@ class TemporalCore:
         return dqkv, dbt, dbd
 
 
-# ----------------------------------------------------------------------------- GEMM precision
-# "fp32" (default): fp32 operands on the fp32 MFMA path.  "bf16": the projection GEMMs take bf16
-# operands with fp32 accumulation and fp32 outputs (hipBLASLt via aten::mm.dtype); every other op
-# (LayerNorm, attention cores, residual stream, optimizer) stays fp32.  Not bit-compatible with
-# the fp32 reference: tests/test_gpu_bf16.py states its tolerance.
-_GEMM_BF16 = False
+# ----------------------------------------------------------------------------- precision modes
+# "fp32" (default): fp32 storage and math everywhere, the fp32 MFMA GEMMs.
+# "bf16-gemm": the projection GEMMs take bf16 operands (fp32 accumulate, fp32 outputs); every
+#     other tensor fp32.
+# "bf16": activations between kernels in bf16 — h = LN1(x), Q|K|V, the attention output, the
+#     projection-input gradients and dQ|dK|dV — with fp32 math inside every kernel, fp32 residual
+#     stream, LayerNorm statistics, LSE, parameter gradients and optimizer (the BASELINE's C2 dtype).
+# Neither bf16 mode is bit-compatible with the fp32 reference: tests/test_gpu_bf16.py states the
+# tolerance they are held to.
+_PREC = "fp32"
+PRECISIONS = ("fp32", "bf16-gemm", "bf16")
 
 
-class gemm_precision:
+class precision:
     def __init__(self, mode: str):
-        if mode not in ("fp32", "bf16"):
-            raise ValueError("gemm precision must be 'fp32' or 'bf16'")
-        self.bf16 = mode == "bf16"
+        if mode not in PRECISIONS:
+            raise ValueError("precision must be one of %s" % (PRECISIONS,))
+        self.mode = mode
 
     def __enter__(self):
-        global _GEMM_BF16
-        self.prev, _GEMM_BF16 = _GEMM_BF16, self.bf16
+        global _PREC
+        self.prev, _PREC = _PREC, self.mode
 
     def __exit__(self, *exc):
-        global _GEMM_BF16
-        _GEMM_BF16 = self.prev
+        global _PREC
+        _PREC = self.prev
 
 
 def _b(t):
     return t if t.dtype == torch.bfloat16 else t.to(torch.bfloat16)
 
 
-def _addmm(bias, a, w, bf):
-    """bias + a·wᵀ -> fp32."""
+def _addmm(bias, a, w, bf, out_bf16=False):
+    """bias + a·wᵀ -> fp32 (or bf16 with ``out_bf16``)."""
+    if out_bf16:
+        return torch.addmm(_b(bias), _b(a), _b(w).t())
     if bf:
         return torch.addmm(bias, _b(a), _b(w).t(), out_dtype=torch.float32)
     return torch.addmm(bias, a, w.t())
 
 
-def _mm(a, w, bf):
-    """a·w -> fp32."""
+def _mm(a, w, bf, out_bf16=False):
+    """a·w -> fp32 (or bf16 with ``out_bf16``)."""
+    if out_bf16:
+        return _b(a) @ _b(w)
     if bf:
         return torch.mm(_b(a), _b(w), out_dtype=torch.float32)
     return a @ w
@@ -218,31 +228,32 @@ class AttnBlockFn(torch.autograd.Function):
         require_hip(x)
         H = x.shape[-1]
         x2 = x.reshape(-1, H).contiguous()
-        bf = _GEMM_BF16
-        h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False)
+        bf = _PREC != "fp32"          # bf16 GEMM operands
+        act = _PREC == "bf16"         # bf16 activations between kernels
+        h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False,
+                                    y_dtype=torch.bfloat16 if act else torch.float32)
         if bf:
             h = _b(h)          # only the GEMMs read h: keep it in bf16
-        qkv = _addmm(b_qkv, h, w_qkv, bf)
+        qkv = _addmm(b_qkv, h, w_qkv, bf, out_bf16=act)
         c, saved = core.fwd(qkv, p1, p2)
         cg = _b(c) if bf else c
         o = _addmm(b_o, cg, w_o, bf)
         y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True)
         ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w)
         ctx.inter = (h, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2)
-        ctx.cfg = (core, p_out, seed_out, x.shape, bf)
+        ctx.cfg = (core, p_out, seed_out, x.shape, bf, act)
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, ln1_w, w_qkv, w_o, ln2_w = ctx.saved_tensors
         h, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2 = ctx.inter
-        core, p_out, seed_out, shape, bf = ctx.cfg
+        core, p_out, seed_out, shape, bf, act = ctx.cfg
         ng = ctx.needs_input_grad
         dy2 = dy.reshape(-1, shape[-1]).contiguous()
-        dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True)
-        if bf:
-            do = _b(do)
-        dc = _mm(do, w_o, bf)
+        dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True,
+                                         da_dtype=torch.bfloat16 if bf else torch.float32)
+        dc = _mm(do, w_o, bf, out_bf16=act)
         dw_o = _wgrad(do, cg, bf) if ng[7] else None
         dqkv, dp1, dp2 = core.bwd(qkv, c, saved, dc, ng[1], ng[2])
         del dc, do

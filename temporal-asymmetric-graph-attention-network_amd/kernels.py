@@ -212,7 +212,7 @@ def _geo_fwd(qkv, graph, metric, heads, prm, p_drop, seed, out, lse, alpha):
     ws_bytes = L.tagan_geo_attn_fwd_workspace(gs, heads, d)
     ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=qkv.device)
     base, es = qkv.data_ptr(), qkv.element_size()
-    check(L.tagan_geo_attn_fwd(_lib.TAGAN_F32, metric, gs, heads, d, base, base + H * es, base + 2 * H * es, H3,
+    check(L.tagan_geo_attn_fwd(_lib.dtype_code(qkv), metric, gs, heads, d, base, base + H * es, base + 2 * H * es, H3,
                                ptr(prm), float(p_drop), seed, ptr(out), ptr(lse), ptr(alpha), ptr(ws), ws_bytes,
                                stream_of(qkv)), "tagan_geo_attn_fwd")
 
@@ -332,7 +332,7 @@ def colsum(x2):
     L = lib()
     wsb = L.tagan_colsum_workspace(M, N)
     ws = torch.empty(max(int(wsb), 1), dtype=torch.uint8, device=x2.device)
-    check(L.tagan_colsum(_lib.TAGAN_F32, M, N, ptr(x2), x2.stride(0), ptr(out), ptr(ws), wsb, stream_of(x2)),
+    check(L.tagan_colsum(_lib.dtype_code(x2), M, N, ptr(x2), x2.stride(0), ptr(out), ptr(ws), wsb, stream_of(x2)),
           "tagan_colsum")
     return out
 

@@ -24,7 +24,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .fused import gemm_precision as gemm_precision_ctx
+from .fused import precision as precision_ctx
 from .kernels import build_graph, layer_norm, linear, pool_time_major
 from .layers.classification import ClassificationModule, TemporalLossModule
 from .layers.graph_attention import TAGANGraphAttention
@@ -47,19 +47,19 @@ def _unpack(snapshot):
 
 
 class TAGAN(nn.Module):
-    """``gemm_precision``: "fp32" (default) or "bf16" (projection GEMM operands in bf16, fp32
-    accumulate/outputs; see fused.py).  ``temporal_propagation``: "shipped" (default) reproduces the reference, whose
+    """``precision``: "fp32" (default, the parity mode), "bf16-gemm" (projection GEMM operands in
+    bf16) or "bf16" (bf16 activations between kernels, fp32 math; see fused.py).  ``temporal_propagation``: "shipped" (default) reproduces the reference, whose
     TemporalPropagation never returns (identity); "intended" runs its tensor-mask compute
     (TemporalPropagation.forward_intended, pinned by the G6 fixtures) on the padded
     time-major features before the temporal attention."""
 
-    def __init__(self, config: TAGANConfig, temporal_propagation: str = "shipped", gemm_precision: str = "fp32"):
+    def __init__(self, config: TAGANConfig, temporal_propagation: str = "shipped", precision: str = "fp32"):
         super().__init__()
         if temporal_propagation not in ("shipped", "intended"):
             raise ValueError("temporal_propagation must be 'shipped' or 'intended'")
-        gemm_precision_ctx(gemm_precision)   # validates
+        precision_ctx(precision)   # validates
         self.temporal_propagation_mode = temporal_propagation
-        self.gemm_precision = gemm_precision
+        self.precision = precision
         self.config = config
         self.memory_bank = NodeMemoryBank(hidden_dim=config.hidden_dim, decay_factor=0.8,
                                           max_inactivity=config.temporal_window_size)
@@ -155,7 +155,7 @@ class TAGAN(nn.Module):
 
     def forward(self, graph_sequence: List[Snapshot], labels: Optional[torch.Tensor] = None,
                 return_attention_weights: bool = False) -> Dict[str, Any]:
-        with gemm_precision_ctx(self.gemm_precision):
+        with precision_ctx(self.precision):
             return self._forward(graph_sequence, labels, return_attention_weights)
 
     def _forward(self, graph_sequence, labels, return_attention_weights):

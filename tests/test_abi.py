@@ -88,7 +88,7 @@ def test_argument_validation_reports_errors():
     rc = L.tagan_geo_attn_fwd(0, 0, ctypes.byref(g), 4, 16, None, None, None, 64, None, 0.0, 0, None, None, None,
                               None, 0, None)
     assert rc == -1 and b"graph" in L.tagan_last_error()
-    rc = L.tagan_temporal_attn_fwd(1, 10, 4, 2, 8, None, None, None, 0, 0, None, None, 0, None, 0, 0, 0, 0.0, 0,
+    rc = L.tagan_temporal_attn_fwd(7, 10, 4, 2, 8, None, None, None, 0, 0, None, None, 0, None, 0, 0, 0, 0.0, 0,
                                    None, 0, 0, None, None, None)
     assert rc == -2
     g.n_nodes, g.rowptr, g.col = 10, 16, 16   # non-null dummies: validation fails before any launch

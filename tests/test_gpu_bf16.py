@@ -1,14 +1,17 @@
-"""bf16-GEMM mode (TAGAN(gemm_precision="bf16")): projection GEMMs take bf16 operands with fp32
-accumulation; everything else fp32.  Not bit-compatible with the reference; checked against the
-fp32 HIP model on the same inputs with a bf16-level tolerance (loss 1e-2 relative, every
-gradient within 3e-2 relative of its norm, floored at 1e-3 of the largest gradient norm)."""
+"""Reduced-precision modes (TAGAN(precision=...)), checked against the fp32 HIP model on the same
+inputs and weights (the fp32 mode is the one pinned to the reference at 1e-4):
+  "bf16-gemm": projection GEMMs take bf16 operands, fp32 accumulate/outputs — loss within 1e-2
+               relative, every gradient within 3e-2 of its norm;
+  "bf16":      bf16 activations between kernels, fp32 math — loss within 2e-2, gradients within 8e-2.
+Gradient norms are floored at 1e-3 of the largest (analytically vanishing gradients are noise)."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
 
-def test_bf16_gemm_mode_tracks_fp32(dev=None):
+@pytest.mark.parametrize("mode,loss_tol,grad_tol", [("bf16-gemm", 1e-2, 3e-2), ("bf16", 2e-2, 8e-2)])
+def test_reduced_precision_tracks_fp32(mode, loss_tol, grad_tol):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import tagan_amd  # noqa: F401
@@ -21,17 +24,17 @@ def test_bf16_gemm_mode_tracks_fp32(dev=None):
             list(range(n))) for n in (300, 280, 310, 295, 300, 305)]
     labels = torch.tensor([1.0], device=dev)
     out = {}
-    for mode in ("fp32", "bf16"):
+    for prec in ("fp32", mode):
         torch.manual_seed(1)
-        m = TAGAN(cfg, gemm_precision=mode).to(dev)
+        m = TAGAN(cfg, precision=prec).to(dev)
         r = m(seq, labels)
         r["loss"].backward()
-        out[mode] = (float(r["loss"]), {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
+        out[prec] = (float(r["loss"]), {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
     l32, g32 = out["fp32"]
-    l16, g16 = out["bf16"]
-    assert abs(l16 - l32) <= 1e-2 * abs(l32)
+    l16, g16 = out[mode]
+    assert abs(l16 - l32) <= loss_tol * abs(l32)
     assert sorted(g16) == sorted(g32)
     scale = max(float(g.norm()) for g in g32.values())
     for k in g32:   # floor: gradients that vanish analytically (e.g. key biases under softmax) are noise
         err = float((g16[k] - g32[k]).norm()) / max(float(g32[k].norm()), 1e-3 * scale)
-        assert err < 3e-2, (k, err)
+        assert err < grad_tol, (k, err)
