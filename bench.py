@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--precision", default="fp32", choices=("fp32", "bf16-gemm", "bf16"),
                     help="fp32 (parity mode); bf16-gemm: bf16 GEMM operands; bf16: bf16 activations between "
                          "kernels, fp32 math (BASELINE's C2 dtype)")
+    ap.add_argument("--no-alt-precision", action="store_true",
+                    help="skip the extra bf16-activation measurement reported as alt_precision")
     ap.add_argument("--shard", action="store_true",
                     help="one sequence sharded by snapshot over all ranks (strong scaling; C5 mode) instead of "
                          "one sequence per rank (data parallel, weak scaling)")
@@ -245,23 +247,28 @@ def main():
         opt.step()
         return out["loss"]
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    assert torch.isfinite(loss).item(), "non-finite loss"
+    def timed(steps, warmup):
+        """W untimed steps, then exactly K steps between barrier + sync; max over ranks."""
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loss = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        assert torch.isfinite(loss).item(), "non-finite loss"
+        return el
+
+    elapsed = timed(args.steps, args.warmup)
     seqs_per_step = 1 if args.shard else world
     value = seqs_per_step * T * args.steps / elapsed
     rec = {
@@ -279,6 +286,15 @@ def main():
                    "parallelism": ("snapshot-shard%d" % world) if args.shard else ("dp%d" % world)},
     }
     rec["breakdown"] = breakdown(model, seq, fwd, bwd, opt, cfg)
+    if args.precision == "fp32" and not args.no_alt_precision:
+        # the same step with bf16 activations between kernels (BASELINE's C2 dtype), fp32 math inside
+        # every kernel; held to the fp32 mode by tests/test_gpu_bf16.py (loss 2e-2, gradients 8e-2)
+        model.precision = "bf16"
+        alt = timed(args.steps, args.warmup)
+        model.precision = args.precision
+        rec["alt_precision"] = {"precision": "bf16", "value": round(seqs_per_step * T * args.steps / alt, 3),
+                                "ms_per_step": round(alt / args.steps * 1e3, 3),
+                                "dtype": "bf16 (activations; fp32 math and accumulation)"}
     if rank == 0 and not args.no_roofline:
         rec["roofline"] = roofline(model, seq, cfg)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -101,7 +101,7 @@ int tagan_pool_bwd(int dtype, int32_t T, int64_t N, int32_t H, const float* g, f
 namespace tagan {
 namespace {
 
-constexpr int CS_BLOCKS = 512;
+constexpr int CS_BLOCKS = 1024;
 
 template <typename S>
 __global__ void __launch_bounds__(BLK) k_colsum_rows(const void* __restrict__ x, int64_t M, int N, int64_t ld,
@@ -111,13 +111,27 @@ __global__ void __launch_bounds__(BLK) k_colsum_rows(const void* __restrict__ x,
     const int lane = threadIdx.x % lpr, rsub = threadIdx.x / lpr;
     const int64_t per = (M + gridDim.x - 1) / gridDim.x;
     const int64_t a = blockIdx.x * per, b = min<int64_t>(M, a + per);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (rsub < rpb)
-        for (int64_t r = a + rsub; r < b; r += rpb) {
-            const float4 v = Io<S>::ld(x, r * ld + lane * 4);
-            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
+    if (rsub < rpb) {
+        int64_t r = a + rsub;
+        for (; r + 3 * rpb < b; r += 4 * rpb) {        // four rows in flight per thread
+            const float4 v0 = Io<S>::ld(x, r * ld + lane * 4);
+            const float4 v1 = Io<S>::ld(x, (r + rpb) * ld + lane * 4);
+            const float4 v2 = Io<S>::ld(x, (r + 2 * rpb) * ld + lane * 4);
+            const float4 v3 = Io<S>::ld(x, (r + 3 * rpb) * ld + lane * 4);
+            s0.x += v0.x; s0.y += v0.y; s0.z += v0.z; s0.w += v0.w;
+            s1.x += v1.x; s1.y += v1.y; s1.z += v1.z; s1.w += v1.w;
+            s2.x += v2.x; s2.y += v2.y; s2.z += v2.z; s2.w += v2.w;
+            s3.x += v3.x; s3.y += v3.y; s3.z += v3.z; s3.w += v3.w;
         }
-    if (rsub < rpb) *(float4*)(red + (size_t)rsub * N + lane * 4) = acc;
+        for (; r < b; r += rpb) {
+            const float4 v = Io<S>::ld(x, r * ld + lane * 4);
+            s0.x += v.x; s0.y += v.y; s0.z += v.z; s0.w += v.w;
+        }
+        const float4 acc = make_float4((s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y),
+                                       (s0.z + s1.z) + (s2.z + s3.z), (s0.w + s1.w) + (s2.w + s3.w));
+        *(float4*)(red + (size_t)rsub * N + lane * 4) = acc;
+    }
     __syncthreads();
     for (int c = threadIdx.x; c < N; c += BLK) {
         float s = 0.f;
