@@ -35,7 +35,8 @@ def main():
         step()
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True,
+                 record_shapes=True) as prof:
         step()
         torch.cuda.synchronize()
     keys = ("aten::fill_", "aten::zero_", "aten::copy_", "aten::add", "aten::sum", "aten::cat", "aten::clone",
@@ -46,6 +47,10 @@ def main():
             for fr in (e.stack or [])[:6]:
                 print("      ", fr)
     print(prof.key_averages().table(sort_by="device_time_total", row_limit=40))
+    for e in prof.key_averages(group_by_input_shape=True):
+        if e.key in ("aten::add", "aten::add_", "aten::copy_", "aten::fill_", "aten::zero_", "aten::sum",
+                     "aten::mul", "aten::cat", "aten::clone"):
+            print("%-14s calls=%3d dev_us=%8.1f shapes=%s" % (e.key, e.count, e.device_time_total, e.input_shapes))
 
 
 if __name__ == "__main__":
