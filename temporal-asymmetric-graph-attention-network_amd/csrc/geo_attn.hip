@@ -205,7 +205,11 @@ struct GeoArgs {
 #ifndef TAGAN_GEO_UNROLL
 #define TAGAN_GEO_UNROLL 2
 #endif
-constexpr int UNROLL = TAGAN_GEO_UNROLL;
+#ifndef TAGAN_GEO_UNROLL8
+#define TAGAN_GEO_UNROLL8 2
+#endif
+template <int FPL>
+struct Unroll { static constexpr int v = FPL == 8 ? TAGAN_GEO_UNROLL8 : TAGAN_GEO_UNROLL; };
 
 __device__ __forceinline__ float sgnf(float x) { return (x > 0.f) ? 1.f : (x < 0.f ? -1.f : 0.f); }
 
@@ -236,10 +240,61 @@ struct Lanes {
     }
 };
 
+// ------------------------------------------------------------------ lane vectors
+// A lane owns FPL consecutive features (FPL = 4 or 8).  FPL = 8 halves the lanes per row, so a
+// wave runs twice as many chunks side by side with twice the bytes per gather instruction: the
+// edge kernels are bound by gathers in flight, not by bytes (bf16 storage alone hardly helps).
+template <typename S>
+struct IsBf16 { static constexpr bool v = false; };
+template <>
+struct IsBf16<bf16s> { static constexpr bool v = true; };
+
+template <typename S, int F>
+__device__ __forceinline__ void ldf(const void* p, int64_t i, float (&r)[F]) {
+    if constexpr (IsBf16<S>::v && F == 8) {
+        const uint4 u = *(const uint4*)((const uint16_t*)p + i);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            r[2 * c] = __uint_as_float(w[c] << 16);
+            r[2 * c + 1] = __uint_as_float(w[c] & 0xffff0000u);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < F; c += 4) {
+            const float4 t = Io<S>::ld(p, i + c);
+            r[c] = t.x; r[c + 1] = t.y; r[c + 2] = t.z; r[c + 3] = t.w;
+        }
+    }
+}
+
+template <typename S, int F>
+__device__ __forceinline__ void stf(void* p, int64_t i, const float (&r)[F]) {
+    if constexpr (IsBf16<S>::v && F == 8) {
+        uint4 u;
+        u.x = f2bf_bits(r[0]) | (f2bf_bits(r[1]) << 16);
+        u.y = f2bf_bits(r[2]) | (f2bf_bits(r[3]) << 16);
+        u.z = f2bf_bits(r[4]) | (f2bf_bits(r[5]) << 16);
+        u.w = f2bf_bits(r[6]) | (f2bf_bits(r[7]) << 16);
+        *(uint4*)((uint16_t*)p + i) = u;
+    } else {
+#pragma unroll
+        for (int c = 0; c < F; c += 4) Io<S>::st(p, i + c, make_float4(r[c], r[c + 1], r[c + 2], r[c + 3]));
+    }
+}
+
+template <int F>
+__device__ __forceinline__ float dotf(const float (&a)[F], const float (&b)[F]) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < F; ++c) s = fmaf(a[c], b[c], s);
+    return s;
+}
+
 // ------------------------------------------------------------------ forward
-template <int METRIC, int LPR, typename S>
+template <int METRIC, int LPR, int FPL, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
-    using IO = Io<S>;
+    constexpr int UN = Unroll<FPL>::v;
     Lanes<LPR> L;
     const int nchunks = A.g.row_counts[0];
     const bool valid = L.chunk < nchunks;
@@ -250,33 +305,36 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
         cnt = min(A.g.chunk, A.g.rowptr[row + 1] - e0);
     }
     if (!__any(valid)) return;
-    const int f0 = L.sl * 4;
+    const int lph = A.d / FPL;                   // lanes per head
+    const int f0 = L.sl * FPL;
     const int h = f0 / A.d;
     const uint32_t dkey = drop_key(A.seed, (uint64_t)h);
-    const float4 qv = IO::ld(A.q, (int64_t)row * A.ld + f0);
+    float qv[FPL];
+    ldf<S>(A.q, (int64_t)row * A.ld + f0, qv);
     float qq = 0.f;
-    if constexpr (MetricTraits<METRIC>::fam == FAM_COS)
-        qq = grp_sum(qv.x * qv.x + qv.y * qv.y + qv.z * qv.z + qv.w * qv.w, A.lph);
+    if constexpr (MetricTraits<METRIC>::fam == FAM_COS) qq = grp_sum(dotf(qv, qv), lph);
     const float prm = A.mparam ? A.mparam[h] : 1.f;
     float m = -INFINITY, l = 0.f;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    int mycol = 0;
-    for (int jj = 0; __any(jj < cnt); jj += UNROLL) {
-        if ((jj % LPR) == 0) mycol = (jj + L.sl < cnt) ? A.g.col[e0 + jj + L.sl] : 0;
-        float4 kv[UNROLL], vv[UNROLL];
+    float acc[FPL];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
+    for (int c = 0; c < FPL; ++c) acc[c] = 0.f;
+    int mycol = 0;
+    for (int jj = 0; __any(jj < cnt); jj += UN) {
+        if ((jj % LPR) == 0) mycol = (jj + L.sl < cnt) ? A.g.col[e0 + jj + L.sl] : 0;
+        float kv[UN][FPL], vv[UN][FPL];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
             const int j = __shfl(mycol, L.base + ((jj + u) % LPR), WAVE);
-            kv[u] = IO::ld(A.k, (int64_t)j * A.ld + f0);
-            vv[u] = IO::ld(A.v, (int64_t)j * A.ld + f0);
+            ldf<S>(A.k, (int64_t)j * A.ld + f0, kv[u]);
+            ldf<S>(A.v, (int64_t)j * A.ld + f0, vv[u]);
         }
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
+        for (int u = 0; u < UN; ++u) {
             const bool live = jj + u < cnt;
             float a, b;
-            partial4<METRIC>(qv, kv[u], a, b);
-            a = grp_sum(a, A.lph);
-            if constexpr (MetricTraits<METRIC>::fam == FAM_COS) b = grp_sum(b, A.lph);
+            pair_partial<METRIC, FPL>(qv, kv[u], a, b);
+            a = grp_sum(a, lph);
+            if constexpr (MetricTraits<METRIC>::fam == FAM_COS) b = grp_sum(b, lph);
             if (!live) continue;
             const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
             const float mn = fmaxf(m, s);
@@ -284,13 +342,9 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
             const float p = __expf(s - mn);
             l = fmaf(l, corr, p);
             float pw = p;
-            if (A.p_drop > 0.f) {
-                pw = (drop_u(dkey, (uint32_t)(e0 + jj + u)) >= A.p_drop) ? p * A.inv_keep : 0.f;
-            }
-            acc.x = fmaf(acc.x, corr, pw * vv[u].x);
-            acc.y = fmaf(acc.y, corr, pw * vv[u].y);
-            acc.z = fmaf(acc.z, corr, pw * vv[u].z);
-            acc.w = fmaf(acc.w, corr, pw * vv[u].w);
+            if (A.p_drop > 0.f) pw = (drop_u(dkey, (uint32_t)(e0 + jj + u)) >= A.p_drop) ? p * A.inv_keep : 0.f;
+#pragma unroll
+            for (int c = 0; c < FPL; ++c) acc[c] = fmaf(acc[c], corr, pw * vv[u][c]);
             m = mn;
         }
     }
@@ -298,11 +352,13 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
     const int part = A.g.row_chunk_part[L.chunk];
     if (part < 0) {
         const float inv = (l > 0.f) ? 1.f / l : NAN;
-        IO::st(A.out, (int64_t)row * A.H + f0, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
-        if ((L.sl % A.lph) == 0) A.lse[(int64_t)row * A.heads + h] = m + __logf(l);
+#pragma unroll
+        for (int c = 0; c < FPL; ++c) acc[c] *= inv;
+        stf<S>(A.out, (int64_t)row * A.H + f0, acc);
+        if ((L.sl % lph) == 0) A.lse[(int64_t)row * A.heads + h] = m + __logf(l);
     } else {
-        st4(A.part_v + (int64_t)part * A.H + f0, acc);
-        if ((L.sl % A.lph) == 0) {
+        stf<float>(A.part_v, (int64_t)part * A.H + f0, acc);
+        if ((L.sl % lph) == 0) {
             A.part_m[(int64_t)part * A.heads + h] = m;
             A.part_l[(int64_t)part * A.heads + h] = l;
         }
@@ -345,9 +401,9 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_merge(GeoArgs A) {
 }
 
 // ------------------------------------------------------------------ backward, row pass (CSR chunks)
-template <int METRIC, int LPR, typename S>
+template <int METRIC, int LPR, int FPL, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
-    using IO = Io<S>;
+    constexpr int UN = Unroll<FPL>::v;
     __shared__ float red[BLK];
     Lanes<LPR> L;
     const int nchunks = A.g.row_counts[0];
@@ -358,72 +414,72 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
         e0 = A.g.row_chunk_beg[L.chunk];
         cnt = min(A.g.chunk, A.g.rowptr[row + 1] - e0);
     }
-    const int f0 = L.sl * 4;
+    const int lph = A.d / FPL;
+    const int f0 = L.sl * FPL;
     const int h = f0 / A.d;
     const uint32_t dkey = drop_key(A.seed, (uint64_t)h);
     float prm_acc = 0.f;
     if (__any(valid)) {
-        const float4 qv = IO::ld(A.q, (int64_t)row * A.ld + f0);
-        const float4 ov = IO::ld(A.o, (int64_t)row * A.H + f0);
-        const float4 dov = IO::ld(A.dout, (int64_t)row * A.H + f0);
-        const float D = grp_sum(dov.x * ov.x + dov.y * ov.y + dov.z * ov.z + dov.w * ov.w, A.lph);
+        float qv[FPL], ov[FPL], dov[FPL];
+        ldf<S>(A.q, (int64_t)row * A.ld + f0, qv);
+        ldf<S>(A.o, (int64_t)row * A.H + f0, ov);
+        ldf<S>(A.dout, (int64_t)row * A.H + f0, dov);
+        const float D = grp_sum(dotf(dov, ov), lph);
         float qq = 0.f;
-        if constexpr (MetricTraits<METRIC>::fam == FAM_COS)
-            qq = grp_sum(qv.x * qv.x + qv.y * qv.y + qv.z * qv.z + qv.w * qv.w, A.lph);
+        if constexpr (MetricTraits<METRIC>::fam == FAM_COS) qq = grp_sum(dotf(qv, qv), lph);
         const float lse = A.lse_in[(int64_t)row * A.heads + h];
         const float prm = A.mparam ? A.mparam[h] : 1.f;
-        float4 dq = make_float4(0.f, 0.f, 0.f, 0.f);
-        int mycol = 0;
-        for (int jj = 0; __any(jj < cnt); jj += UNROLL) {
-            if ((jj % LPR) == 0) mycol = (jj + L.sl < cnt) ? A.g.col[e0 + jj + L.sl] : 0;
-            float4 kv[UNROLL], vv[UNROLL];
+        float dq[FPL];
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
+        for (int c = 0; c < FPL; ++c) dq[c] = 0.f;
+        int mycol = 0;
+        for (int jj = 0; __any(jj < cnt); jj += UN) {
+            if ((jj % LPR) == 0) mycol = (jj + L.sl < cnt) ? A.g.col[e0 + jj + L.sl] : 0;
+            float kv[UN][FPL], vv[UN][FPL];
+#pragma unroll
+            for (int u = 0; u < UN; ++u) {
                 const int j = __shfl(mycol, L.base + ((jj + u) % LPR), WAVE);
-                kv[u] = IO::ld(A.k, (int64_t)j * A.ld + f0);
-                vv[u] = IO::ld(A.v, (int64_t)j * A.ld + f0);
+                ldf<S>(A.k, (int64_t)j * A.ld + f0, kv[u]);
+                ldf<S>(A.v, (int64_t)j * A.ld + f0, vv[u]);
             }
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
+            for (int u = 0; u < UN; ++u) {
                 const bool live = jj + u < cnt;
                 float a, b;
-                partial4<METRIC>(qv, kv[u], a, b);
-                float dp = dov.x * vv[u].x + dov.y * vv[u].y + dov.z * vv[u].z + dov.w * vv[u].w;
-                a = grp_sum(a, A.lph);
-                dp = grp_sum(dp, A.lph);
-                if constexpr (MetricTraits<METRIC>::fam == FAM_COS) b = grp_sum(b, A.lph);
+                pair_partial<METRIC, FPL>(qv, kv[u], a, b);
+                float dp = dotf(dov, vv[u]);
+                a = grp_sum(a, lph);
+                dp = grp_sum(dp, lph);
+                if constexpr (MetricTraits<METRIC>::fam == FAM_COS) b = grp_sum(b, lph);
                 if (!live) continue;
                 const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
                 const float p = __expf(s - lse);
-                if (A.p_drop > 0.f) {
-                    dp = (drop_u(dkey, (uint32_t)(e0 + jj + u)) >= A.p_drop) ? dp * A.inv_keep : 0.f;
-                }
+                if (A.p_drop > 0.f) dp = (drop_u(dkey, (uint32_t)(e0 + jj + u)) >= A.p_drop) ? dp * A.inv_keep : 0.f;
                 const float ds = p * (dp - D);
                 const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float qc = f4(qv, c), kc = f4(kv[u], c);
+                for (int c = 0; c < FPL; ++c) {
+                    const float qc = qv[c], kc = kv[u][c];
                     float t = fmaf(g.cq_q, qc, g.cq_k * kc);
                     if constexpr (MetricTraits<METRIC>::fam == FAM_ABS) t = g.sg * sgnf(qc - kc);
-                    const float r = ds * t;
-                    if (c == 0) dq.x += r; else if (c == 1) dq.y += r; else if (c == 2) dq.z += r; else dq.w += r;
+                    dq[c] += ds * t;
                 }
                 prm_acc = fmaf(ds, g.dprm, prm_acc);
             }
         }
         if (valid) {
             const int part = A.g.row_chunk_part[L.chunk];
-            if (part < 0) IO::st(A.dq, (int64_t)row * A.ldd + f0, dq);
-            else st4(A.part_v + (int64_t)part * A.H + f0, dq);
-            if ((L.sl % A.lph) == 0 && A.g.row_chunk_ptr[row] == L.chunk) A.delta[(int64_t)row * A.heads + h] = D;
+            if (part < 0) stf<S>(A.dq, (int64_t)row * A.ldd + f0, dq);
+            else stf<float>(A.part_v, (int64_t)part * A.H + f0, dq);
+            if ((L.sl % lph) == 0 && A.g.row_chunk_ptr[row] == L.chunk) A.delta[(int64_t)row * A.heads + h] = D;
         }
     }
     if (A.prm_partial) {
-        red[threadIdx.x] = (valid && (L.sl % A.lph) == 0) ? prm_acc : 0.f;
+        red[threadIdx.x] = (valid && (L.sl % lph) == 0) ? prm_acc : 0.f;
         __syncthreads();
         if (threadIdx.x < A.heads) {
             float sacc = 0.f;
-            const int off = threadIdx.x * A.lph;            // lane of head threadIdx.x inside a group
+            const int off = threadIdx.x * lph;              // lane of head threadIdx.x inside a group
             for (int w = 0; w < BLK / WAVE; ++w)
                 for (int sg = 0; sg < Lanes<LPR>::RPW; ++sg) sacc += red[w * WAVE + sg * LPR + off];
             A.prm_partial[(int64_t)blockIdx.x * A.heads + threadIdx.x] = sacc;
@@ -457,9 +513,9 @@ __global__ void __launch_bounds__(BLK) k_geo_sum_parts(const int32_t* __restrict
 }
 
 // ------------------------------------------------------------------ backward, column pass (CSC chunks)
-template <int METRIC, int LPR, typename S>
+template <int METRIC, int LPR, int FPL, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
-    using IO = Io<S>;
+    constexpr int UN = Unroll<FPL>::v;
     Lanes<LPR> L;
     const int nchunks = A.g.col_counts[0];
     const bool valid = L.chunk < nchunks;
@@ -470,45 +526,48 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
         cnt = min(A.g.chunk, A.g.csc_ptr[colj + 1] - e0);
     }
     if (!__any(valid)) return;
-    const int f0 = L.sl * 4;
+    const int lph = A.d / FPL;
+    const int f0 = L.sl * FPL;
     const int h = f0 / A.d;
     const uint32_t dkey = drop_key(A.seed, (uint64_t)h);
-    const float4 kv = IO::ld(A.k, (int64_t)colj * A.ld + f0);
-    const float4 vv = IO::ld(A.v, (int64_t)colj * A.ld + f0);
+    float kv[FPL], vv[FPL];
+    ldf<S>(A.k, (int64_t)colj * A.ld + f0, kv);
+    ldf<S>(A.v, (int64_t)colj * A.ld + f0, vv);
     const float prm = A.mparam ? A.mparam[h] : 1.f;
-    float4 dk = make_float4(0.f, 0.f, 0.f, 0.f), dv = make_float4(0.f, 0.f, 0.f, 0.f);
+    float dk[FPL], dv[FPL];
+#pragma unroll
+    for (int c = 0; c < FPL; ++c) { dk[c] = 0.f; dv[c] = 0.f; }
     int myrow = 0, myeid = 0;
-    for (int jj = 0; __any(jj < cnt); jj += UNROLL) {
+    for (int jj = 0; __any(jj < cnt); jj += UN) {
         if ((jj % LPR) == 0) {
             const bool in = jj + L.sl < cnt;
             myrow = in ? A.g.csc_row[e0 + jj + L.sl] : 0;
             myeid = in ? A.g.csc_eid[e0 + jj + L.sl] : 0;
         }
-        float4 qv[UNROLL], dov[UNROLL];
-        float lse[UNROLL], D[UNROLL];
-        int eid[UNROLL];
+        float qv[UN][FPL], dov[UN][FPL];
+        float lse[UN], D[UN];
+        int eid[UN];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
+        for (int u = 0; u < UN; ++u) {
             const int src = L.base + ((jj + u) % LPR);
             const int i = __shfl(myrow, src, WAVE);
             eid[u] = __shfl(myeid, src, WAVE);
-            qv[u] = IO::ld(A.q, (int64_t)i * A.ld + f0);
-            dov[u] = IO::ld(A.dout, (int64_t)i * A.H + f0);
+            ldf<S>(A.q, (int64_t)i * A.ld + f0, qv[u]);
+            ldf<S>(A.dout, (int64_t)i * A.H + f0, dov[u]);
             lse[u] = A.lse_in[(int64_t)i * A.heads + h];
             D[u] = A.delta[(int64_t)i * A.heads + h];
         }
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
+        for (int u = 0; u < UN; ++u) {
             const bool live = jj + u < cnt;
             float a, b, qq = 0.f;
-            partial4<METRIC>(qv[u], kv, a, b);
-            float dp = dov[u].x * vv.x + dov[u].y * vv.y + dov[u].z * vv.z + dov[u].w * vv.w;
-            a = grp_sum(a, A.lph);
-            dp = grp_sum(dp, A.lph);
+            pair_partial<METRIC, FPL>(qv[u], kv, a, b);
+            float dp = dotf(dov[u], vv);
+            a = grp_sum(a, lph);
+            dp = grp_sum(dp, lph);
             if constexpr (MetricTraits<METRIC>::fam == FAM_COS) {
-                b = grp_sum(b, A.lph);
-                qq = grp_sum(qv[u].x * qv[u].x + qv[u].y * qv[u].y + qv[u].z * qv[u].z + qv[u].w * qv[u].w,
-                             A.lph);
+                b = grp_sum(b, lph);
+                qq = grp_sum(dotf(qv[u], qv[u]), lph);
             }
             if (!live) continue;
             const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
@@ -522,26 +581,23 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
             const float ds = p * (dp - D[u]);
             const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float qc = f4(qv[u], c), kc = f4(kv, c);
+            for (int c = 0; c < FPL; ++c) {
+                const float qc = qv[u][c], kc = kv[c];
                 float t = fmaf(g.ck_q, qc, g.ck_k * kc);
                 if constexpr (MetricTraits<METRIC>::fam == FAM_ABS) t = -g.sg * sgnf(qc - kc);
-                const float r = ds * t, w = pw * f4(dov[u], c);
-                if (c == 0) { dk.x += r; dv.x += w; }
-                else if (c == 1) { dk.y += r; dv.y += w; }
-                else if (c == 2) { dk.z += r; dv.z += w; }
-                else { dk.w += r; dv.w += w; }
+                dk[c] += ds * t;
+                dv[c] += pw * dov[u][c];
             }
         }
     }
     if (!valid) return;
     const int part = A.g.col_chunk_part[L.chunk];
     if (part < 0) {
-        IO::st(A.dk, (int64_t)colj * A.ldd + f0, dk);
-        IO::st(A.dv, (int64_t)colj * A.ldd + f0, dv);
+        stf<S>(A.dk, (int64_t)colj * A.ldd + f0, dk);
+        stf<S>(A.dv, (int64_t)colj * A.ldd + f0, dv);
     } else {
-        st4(A.part_v2 + (int64_t)part * 2 * A.H + f0, dk);
-        st4(A.part_v2 + (int64_t)part * 2 * A.H + A.H + f0, dv);
+        stf<float>(A.part_v2, (int64_t)part * 2 * A.H + f0, dk);
+        stf<float>(A.part_v2, (int64_t)part * 2 * A.H + A.H + f0, dv);
     }
 }
 
@@ -725,8 +781,21 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_generic(GeoArgs A) {
 }
 
 // =================================================================== dispatch
-// Fast path: H = 4*LPR with LPR in {8,16,32,64} and d = 4*LPH with LPH a power of two.
-int pick_lpr(int H, int d) {
+// Fast path: H in {32, 64, 128, 256}, d = 4*LPH with LPH a power of two.  A lane owns FPL
+// features: FPL = 8 (LPR = H/8 lanes per chunk group) where d % 8 == 0 and H >= 64 for the
+// passes TAGAN_GEO_FPL_* select, else 4.  Measured at C2/C4 (tools/geo_kernels.py):
+// the forward gains from 8 (more chunks per wave in flight); the backward passes, whose
+// register footprint at FPL = 8 halves the occupancy, do not at C2.
+#ifndef TAGAN_GEO_FPL_FWD
+#define TAGAN_GEO_FPL_FWD 8
+#endif
+#ifndef TAGAN_GEO_FPL_BWD
+#define TAGAN_GEO_FPL_BWD 4
+#endif
+
+enum Pass { P_FWD, P_BWD_ROW, P_BWD_COL, P_ALPHA };
+
+int pick_lpr(int H, int d) {   // nonzero = fast path
     if (d % 4 != 0) return 0;
     const int lph = d / 4;
     if (lph & (lph - 1)) return 0;
@@ -734,7 +803,11 @@ int pick_lpr(int H, int d) {
     return 0;
 }
 
-enum Pass { P_FWD, P_BWD_ROW, P_BWD_COL, P_ALPHA };
+int pick_fpl(int H, int d, Pass pass) {
+    const int want = pass == P_FWD ? TAGAN_GEO_FPL_FWD : TAGAN_GEO_FPL_BWD;
+    if (want == 8 && d % 8 == 0 && ((d / 8) & (d / 8 - 1)) == 0 && (H == 64 || H == 128 || H == 256)) return 8;
+    return 4;
+}
 
 int64_t chunk_blocks(const GeoArgs& A, int lpr) {
     const int64_t rpw = WAVE / lpr;
@@ -742,18 +815,18 @@ int64_t chunk_blocks(const GeoArgs& A, int lpr) {
     return std::max<int64_t>(1, (waves + (BLK / WAVE) - 1) / (BLK / WAVE));
 }
 
-template <int METRIC, int LPR, typename S>
+template <int METRIC, int LPR, int FPL, typename S>
 void launch_fast_s(Pass pass, const GeoArgs& A, hipStream_t s) {
     const dim3 g((unsigned)chunk_blocks(A, LPR));
-    if (pass == P_FWD) k_geo_fwd_chunk<METRIC, LPR, S><<<g, BLK, 0, s>>>(A);
-    else if (pass == P_BWD_ROW) k_geo_bwd_row_chunk<METRIC, LPR, S><<<g, BLK, 0, s>>>(A);
-    else k_geo_bwd_col_chunk<METRIC, LPR, S><<<g, BLK, 0, s>>>(A);
+    if (pass == P_FWD) k_geo_fwd_chunk<METRIC, LPR, FPL, S><<<g, BLK, 0, s>>>(A);
+    else if (pass == P_BWD_ROW) k_geo_bwd_row_chunk<METRIC, LPR, FPL, S><<<g, BLK, 0, s>>>(A);
+    else k_geo_bwd_col_chunk<METRIC, LPR, FPL, S><<<g, BLK, 0, s>>>(A);
 }
 
-template <int METRIC, int LPR>
+template <int METRIC, int LPR, int FPL>
 void launch_fast(Pass pass, const GeoArgs& A, hipStream_t s) {
-    if (A.bf16) launch_fast_s<METRIC, LPR, bf16s>(pass, A, s);
-    else launch_fast_s<METRIC, LPR, float>(pass, A, s);
+    if (A.bf16) launch_fast_s<METRIC, LPR, FPL, bf16s>(pass, A, s);
+    else launch_fast_s<METRIC, LPR, FPL, float>(pass, A, s);
 }
 
 template <int METRIC>
@@ -763,12 +836,23 @@ int launch_metric(Pass pass, int lpr, const GeoArgs& A, hipStream_t s, float* al
         k_geo_alpha<METRIC><<<gg, BLK, 0, s>>>(A, alpha);
         return TAGAN_OK;
     }
-    switch (lpr) {
-        case 8: launch_fast<METRIC, 8>(pass, A, s); return TAGAN_OK;
-        case 16: launch_fast<METRIC, 16>(pass, A, s); return TAGAN_OK;
-        case 32: launch_fast<METRIC, 32>(pass, A, s); return TAGAN_OK;
-        case 64: launch_fast<METRIC, 64>(pass, A, s); return TAGAN_OK;
-        default: break;
+    const int fpl = lpr ? pick_fpl(A.H, A.d, pass) : 0;
+    lpr = lpr ? A.H / fpl : 0;
+    if (fpl == 8) {
+        switch (lpr) {
+            case 8: launch_fast<METRIC, 8, 8>(pass, A, s); return TAGAN_OK;
+            case 16: launch_fast<METRIC, 16, 8>(pass, A, s); return TAGAN_OK;
+            case 32: launch_fast<METRIC, 32, 8>(pass, A, s); return TAGAN_OK;
+            default: break;
+        }
+    } else {
+        switch (lpr) {
+            case 8: launch_fast<METRIC, 8, 4>(pass, A, s); return TAGAN_OK;
+            case 16: launch_fast<METRIC, 16, 4>(pass, A, s); return TAGAN_OK;
+            case 32: launch_fast<METRIC, 32, 4>(pass, A, s); return TAGAN_OK;
+            case 64: launch_fast<METRIC, 64, 4>(pass, A, s); return TAGAN_OK;
+            default: break;
+        }
     }
     if (pass == P_FWD) k_geo_fwd_generic<METRIC><<<gg, BLK, 0, s>>>(A);
     else if (pass == P_BWD_ROW) k_geo_bwd_row_generic<METRIC><<<gg, BLK, 0, s>>>(A);
@@ -859,7 +943,7 @@ BwdWs bwd_ws(const tagan_graph* g, int heads, int d) {
     if (lpr) {
         GeoArgs tmp{};
         tmp.g = *g;
-        nprm = std::max<int64_t>(nprm, chunk_blocks(tmp, lpr));
+        nprm = std::max<int64_t>(nprm, chunk_blocks(tmp, H / pick_fpl(H, d, P_BWD_ROW)));
     }
     w.prm = take((size_t)nprm * heads * 4);
     w.pv = take(lpr ? (size_t)g->part_cap * H * 4 : 0);
@@ -988,7 +1072,7 @@ int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t head
     }
     if (dmetric_param) {
         if (want_prm) {
-            const int64_t nparts = lpr ? chunk_blocks(A, lpr) : g->n_nodes;
+            const int64_t nparts = lpr ? chunk_blocks(A, H / pick_fpl(H, head_dim, P_BWD_ROW)) : g->n_nodes;
             k_reduce_partials<<<heads, BLK, 0, s>>>(A.prm_partial, nparts, heads, dmetric_param);
             TAGAN_CHECK_LAUNCH("geo_attn_bwd_reduce");
         } else {

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--metric", type=int, default=0)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--p", type=float, default=0.1)
+    ap.add_argument("--bf16", action="store_true", help="bf16 activation storage (TAGAN_BF16)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     N0, E0, T, H, heads = synthetic.CONFIGS[a.config][:5]
@@ -42,9 +43,10 @@ def main():
     N, d = graph.num_nodes, H // heads
     E = graph.nnz_host()
     g = torch.Generator(device=dev).manual_seed(7)
-    qkv = torch.randn(N, 3 * H, device=dev, generator=g)
-    dout = torch.randn(N, H, device=dev, generator=g)
-    out = torch.empty(N, H, device=dev)
+    adt = torch.bfloat16 if a.bf16 else torch.float32
+    qkv = torch.randn(N, 3 * H, device=dev, generator=g).to(adt)
+    dout = torch.randn(N, H, device=dev, generator=g).to(adt)
+    out = torch.empty(N, H, device=dev, dtype=adt)
     lse = torch.empty(N, heads, device=dev)
     dqkv = torch.empty_like(qkv)
     prm = torch.ones(heads, device=dev)
@@ -57,16 +59,17 @@ def main():
     ws = torch.empty(max(int(wsb), 1), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
-    b, db, es = qkv.data_ptr(), dqkv.data_ptr(), 4
+    b, db, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
+    dt = _lib.TAGAN_BF16 if a.bf16 else 0
     learn = a.metric in (7, 8)
     pp, dpp = (_lib.ptr(prm), _lib.ptr(dprm)) if learn else (None, None)
 
     def fwd():
-        _lib.check(L.tagan_geo_attn_fwd(0, a.metric, gs, heads, d, b, b + H * es, b + 2 * H * es, 3 * H, pp, a.p,
+        _lib.check(L.tagan_geo_attn_fwd(dt, a.metric, gs, heads, d, b, b + H * es, b + 2 * H * es, 3 * H, pp, a.p,
                                         1234, _lib.ptr(out), _lib.ptr(lse), None, _lib.ptr(fws), fwb, sp), "fwd")
 
     def bwd():
-        _lib.check(L.tagan_geo_attn_bwd(0, a.metric, gs, heads, d, b, b + H * es, b + 2 * H * es, 3 * H, pp, a.p,
+        _lib.check(L.tagan_geo_attn_bwd(dt, a.metric, gs, heads, d, b, b + H * es, b + 2 * H * es, 3 * H, pp, a.p,
                                         1234, _lib.ptr(out), _lib.ptr(lse), _lib.ptr(dout), db, db + H * es,
                                         db + 2 * H * es, 3 * H, dpp, _lib.ptr(ws), wsb, sp), "bwd")
 
@@ -85,9 +88,9 @@ def main():
         tf += ev[0].elapsed_time(ev[1])
         tb += ev[1].elapsed_time(ev[2])
     tf, tb = tf / a.reps, tb / a.reps
-    bf, bb = bench.geo_bytes(E, N, H, heads)
+    bf, bb = bench.geo_bytes(E, N, H, heads, s=es)
     print(json.dumps({"lib": os.environ.get("TAGAN_LIB", "default"), "config": a.config, "snapshots": T,
-                      "chunk": a.chunk or CHUNK, "metric": a.metric, "nodes": N, "edges": E, "H": H, "heads": heads,
+                      "chunk": a.chunk or CHUNK, "dtype": "bf16" if a.bf16 else "f32", "metric": a.metric, "nodes": N, "edges": E, "H": H, "heads": heads,
                       "ms_fwd": round(tf, 4), "ms_bwd": round(tb, 4),
                       "gbs_fwd": round(bf / tf / 1e6, 1), "gbs_bwd": round(bb / tb / 1e6, 1),
                       "frac": round((bf + bb) / (tf + tb) / 1e6 / bench.HBM_PEAK_GBS, 4)}), flush=True)

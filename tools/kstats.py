@@ -1,0 +1,45 @@
+"""Summarise a rocprofv3 kernel_stats.csv per training step, grouped by kernel family.
+
+    python tools/kstats.py <run_kernel_stats.csv> [steps]
+
+steps defaults to the number of k_geo_fwd launches / 2 (two geometric layers per step).
+"""
+import csv
+import re
+import sys
+
+FAMILIES = [
+    ("gemm", r"^Cijk_|gemm|Gemm"),
+    ("geo", r"k_geo_"),
+    ("temporal", r"k_tattn"),
+    ("layernorm", r"k_ln_"),
+    ("csr", r"rocprim|k_scatter|k_fill_tail|k_keys|k_chunk|k_tri|csr|k_count"),
+    ("colsum/pool", r"k_colsum|k_pool"),
+    ("torch elementwise", r"elementwise|CatArray|index|gather|scatter"),
+    ("torch reduce", r"reduce_kernel"),
+    ("fill/copy", r"__amd_rocclr"),
+]
+
+
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    n_geo = sum(int(r["Calls"]) for r in rows if "k_geo_fwd_chunk" in r["Name"])
+    steps = float(sys.argv[2]) if len(sys.argv) > 2 else max(1, n_geo / 2)
+    tot = {}
+    top = []
+    for r in rows:
+        fam = next((f for f, p in FAMILIES if re.search(p, r["Name"])), "other")
+        ns = float(r["TotalDurationNs"])
+        tot[fam] = tot.get(fam, 0.0) + ns
+        top.append((ns, int(r["Calls"]), r["Name"][:110]))
+    all_ms = sum(tot.values()) / steps / 1e6
+    print("steps=%g  device ms/step=%.3f" % (steps, all_ms))
+    for f, ns in sorted(tot.items(), key=lambda x: -x[1]):
+        print("  %-18s %7.3f ms" % (f, ns / steps / 1e6))
+    print("top kernels (ms/step, calls/step):")
+    for ns, c, n in sorted(top, reverse=True)[:25]:
+        print("  %7.3f %5.1f  %s" % (ns / steps / 1e6, c / steps, n))
+
+
+if __name__ == "__main__":
+    main()
