@@ -285,6 +285,7 @@ def main():
                    "sequences_per_step": seqs_per_step, "snapshots_per_sequence": T,
                    "parallelism": ("snapshot-shard%d" % world) if args.shard else ("dp%d" % world)},
     }
+    rec["config"]["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
     rec["breakdown"] = breakdown(model, seq, fwd, bwd, opt, cfg)
     if args.precision == "fp32" and not args.no_alt_precision:
         # the same step with bf16 activations between kernels (BASELINE's C2 dtype), fp32 math inside
