@@ -565,7 +565,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd_v2(TArgs A, const float* __re
 }
 
 // =================================================================== v3: one wave per (row, head group)
-// The fast path for T <= 64 and head_dim in {8,16,32,64} without attention-weight output.
+// The fast path for T <= 128 and head_dim in {8,16,32,64} without attention-weight output.
 // A wave owns HPW = 64/LG heads of one node row (LG = lanes per head >= T; lane = step),
 // so its K/V (fwd) or K/V then Q/dO (bwd) live in a private LDS slice written and read by
 // the same wave — no workgroup barriers, 64-thread workgroups, many waves per CU to hide
@@ -668,19 +668,27 @@ __device__ __forceinline__ void to_lds(float* __restrict__ p, const float (&r)[D
 
 constexpr int V3_BLK = WAVE;
 
-size_t v3_fwd_lds(int T, int D, int HPW) { return (size_t)HPW * (2 * T * D + align_up(2 * T - 1, 4)) * 4; }
-size_t v3_bwd_lds(int T, int D, int HPW) {
-    return (size_t)HPW * (2 * T * D + 2 * T + 2 * align_up(2 * T - 1, 4)) * 4;
+// T in (64, 128]: WPH = 2 waves share one head (wave w owns steps 64w .. 64w+63), the LDS slice is
+// the block's and the syncs are block barriers; each wave keeps its own bias-gradient table.
+template <int WPH>
+__device__ __forceinline__ void v3_sync() {
+    if constexpr (WPH == 1) wave_sync();
+    else __syncthreads();
 }
 
-template <int D, int LG, typename S>
-__global__ void __launch_bounds__(V3_BLK) k_tattn_fwd_v3(TArgs A, const float* __restrict__ q,
-                                                         const float* __restrict__ k, const float* __restrict__ v,
-                                                         int n_hg) {
+size_t v3_fwd_lds(int T, int D, int HPW) { return (size_t)HPW * (2 * T * D + align_up(2 * T - 1, 4)) * 4; }
+size_t v3_bwd_lds(int T, int D, int HPW, int WPH) {
+    return (size_t)HPW * (2 * T * D + 2 * T + (1 + WPH) * align_up(2 * T - 1, 4)) * 4;
+}
+
+template <int D, int LG, typename S, int WPH>
+__global__ void __launch_bounds__(V3_BLK * WPH) k_tattn_fwd_v3(TArgs A, const float* __restrict__ q,
+                                                               const float* __restrict__ k,
+                                                               const float* __restrict__ v, int n_hg) {
     constexpr int HPW = WAVE / LG;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int T = A.T, NB = 2 * T - 1, NBp = (NB + 3) & ~3;
-    const int lane = threadIdx.x, hl = lane / LG, li = lane % LG;
+    const int lane = threadIdx.x & (WAVE - 1), hl = lane / LG, li = lane % LG + (threadIdx.x >> 6) * WAVE;
     float* Ks = sm;                  // [HPW][T][D]
     float* Vs = Ks + HPW * T * D;    // [HPW][T][D]
     float* Bs = Vs + HPW * T * D;    // [HPW][NBp]
@@ -697,11 +705,11 @@ __global__ void __launch_bounds__(V3_BLK) k_tattn_fwd_v3(TArgs A, const float* _
         gld_row<D, S>(q, base, qv);
         gld_row<D, S>(k, base, kv);
         gld_row<D, S>(v, base, vv);
-        wave_sync();   // previous unit's LDS reads are done before the slice is rewritten
+        v3_sync<WPH>();   // previous unit's LDS reads are done before the slice is rewritten
         to_lds<D>(Ks + (hl * T + i) * D, kv);
         to_lds<D>(Vs + (hl * T + i) * D, vv);
-        for (int x = li; x < NB; x += LG) Bs[hl * NBp + x] = A.bias_table ? A.bias_table[hc * NB + x] : 0.f;
-        wave_sync();
+        for (int x = li; x < NB; x += LG * WPH) Bs[hl * NBp + x] = A.bias_table ? A.bias_table[hc * NB + x] : 0.f;
+        v3_sync<WPH>();
         const uint32_t drk = tkey(A, r, hc);
         const float* kb = Ks + hl * T * D;
         const float* vb = Vs + hl * T * D;
@@ -731,22 +739,24 @@ __global__ void __launch_bounds__(V3_BLK) k_tattn_fwd_v3(TArgs A, const float* _
     }
 }
 
-template <int D, int LG, typename S>
-__global__ void __launch_bounds__(V3_BLK) k_tattn_bwd_v3(TArgs A, const float* __restrict__ q,
-                                                         const float* __restrict__ k, const float* __restrict__ v,
-                                                         const float* __restrict__ dout,
-                                                         const float* __restrict__ lse, int n_hg) {
+template <int D, int LG, typename S, int WPH>
+__global__ void __launch_bounds__(V3_BLK * WPH) k_tattn_bwd_v3(TArgs A, const float* __restrict__ q,
+                                                               const float* __restrict__ k,
+                                                               const float* __restrict__ v,
+                                                               const float* __restrict__ dout,
+                                                               const float* __restrict__ lse, int n_hg) {
     constexpr int HPW = WAVE / LG;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int T = A.T, NB = 2 * T - 1, NBp = (NB + 3) & ~3;
-    const int lane = threadIdx.x, hl = lane / LG, li = lane % LG;
+    const int lane = threadIdx.x & (WAVE - 1), hl = lane / LG, wv = threadIdx.x >> 6;
+    const int li = lane % LG + wv * WAVE;
     float* X1 = sm;                   // [HPW][T][D]  K in phase A, Q in phase B
     float* X2 = X1 + HPW * T * D;     // [HPW][T][D]  V in phase A, dO in phase B
     float* Ls = X2 + HPW * T * D;     // [HPW][T]
     float* Dl = Ls + HPW * T;         // [HPW][T]
     float* Bs = Dl + HPW * T;         // [HPW][NBp]
-    float* Acc = Bs + HPW * NBp;      // [HPW][NBp] bias-table gradient of this wave's head group
-    for (int x = lane; x < HPW * NBp; x += WAVE) Acc[x] = 0.f;
+    float* Acc = Bs + HPW * NBp;      // [WPH][HPW][NBp] bias-table gradient, one table per wave
+    for (int x = threadIdx.x; x < WPH * HPW * NBp; x += WAVE * WPH) Acc[x] = 0.f;
     const int64_t units = A.rows * n_hg;
     const bool live = li < T;
     const int i = live ? li : T - 1;   // this lane's step: query i in phase A, key j in phase B
@@ -769,13 +779,13 @@ __global__ void __launch_bounds__(V3_BLK) k_tattn_bwd_v3(TArgs A, const float* _
             Di = dot_rr<D>(dov, ov);
         }
         const float li_lse = lse[(r * A.heads + hc) * T + i];
-        wave_sync();
+        v3_sync<WPH>();
         to_lds<D>(X1 + (hl * T + i) * D, kv);
         to_lds<D>(X2 + (hl * T + i) * D, vv);
         Ls[hl * T + i] = li_lse;
         Dl[hl * T + i] = Di;
-        for (int x = li; x < NB; x += LG) Bs[hl * NBp + x] = A.bias_table ? A.bias_table[hc * NB + x] : 0.f;
-        wave_sync();
+        for (int x = li; x < NB; x += LG * WPH) Bs[hl * NBp + x] = A.bias_table ? A.bias_table[hc * NB + x] : 0.f;
+        v3_sync<WPH>();
         const uint32_t drk = tkey(A, r, hc);
         // ---- phase A (lane = query i): dq_i
         {
@@ -797,7 +807,7 @@ __global__ void __launch_bounds__(V3_BLK) k_tattn_bwd_v3(TArgs A, const float* _
             }
             if (live && hok) gst_row<D, S>(A.dq, r * A.d_row + (int64_t)i * A.d_t + h * D, dq, A.inv_sqrt_d);
         }
-        wave_sync();
+        v3_sync<WPH>();
         // swap: each lane takes its own K/V row back from LDS and leaves its Q/dO row in its place
         // (same lane, same address: no cross-lane hazard once phase A's reads are done)
         float* x1 = X1 + (hl * T + i) * D;
@@ -806,14 +816,14 @@ __global__ void __launch_bounds__(V3_BLK) k_tattn_bwd_v3(TArgs A, const float* _
         ld_row<D>(x2, vv);
         to_lds<D>(x1, qv);
         to_lds<D>(x2, dov);
-        wave_sync();
+        v3_sync<WPH>();
         // ---- phase B (lane = key j): dk_j, dv_j, bias-table / dense-bias gradient
         {
             const int j = i;
             const float* qb = X1 + hl * T * D;
             const float* ob = X2 + hl * T * D;
             const float* bb = Bs + hl * NBp - j + T - 1;   // bb[i'] = bias of (i', j)
-            float* ab = Acc + hl * NBp - j + T - 1;         // ab[i'] accumulates diagonal i'-j
+            float* ab = Acc + (wv * HPW + hl) * NBp - j + T - 1;   // ab[i'] accumulates diagonal i'-j
             float dk[D], dv[D];
 #pragma unroll
             for (int c = 0; c < D; ++c) {
@@ -845,17 +855,21 @@ __global__ void __launch_bounds__(V3_BLK) k_tattn_bwd_v3(TArgs A, const float* _
         }
     }
     if (A.part) {
-        wave_sync();
-        // partial row blockIdx / n_hg holds this wave's head group's columns
+        v3_sync<WPH>();
+        // partial row blockIdx / n_hg holds this block's head group's columns (waves summed in order)
         float* prow = A.part + (int64_t)(blockIdx.x / n_hg) * A.heads * NB;
-        for (int x = lane; x < HPW * NB; x += WAVE) {
+        for (int x = threadIdx.x; x < HPW * NB; x += WAVE * WPH) {
             const int hh = x / NB, c = x - hh * NB, h = hg * HPW + hh;
-            if (h < A.heads) prow[h * NB + c] = Acc[hh * NBp + c];
+            float a = 0.f;
+#pragma unroll
+            for (int ww = 0; ww < WPH; ++ww) a += Acc[(ww * HPW + hh) * NBp + c];
+            if (h < A.heads) prow[h * NB + c] = a;
         }
     }
 }
 
-int v3_lanes(int T) { return T <= 16 ? 16 : T <= 32 ? 32 : T <= 64 ? 64 : 0; }
+int v3_lanes(int T) { return T <= 16 ? 16 : T <= 32 ? 32 : T <= 128 ? 64 : 0; }
+int v3_wph(int T) { return T > 64 ? 2 : 1; }
 
 #ifndef TAGAN_TATTN_V3
 #define TAGAN_TATTN_V3 1
@@ -938,15 +952,16 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     const bool al4 = s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0;
     const bool bf = dtype == TAGAN_BF16;
     TAGAN_REQUIRE(!bf || (al4 && !attn && v3_ok(T, head_dim)), TAGAN_ERR_UNSUPPORTED,
-                  "temporal_attn_fwd: bf16 storage needs the v3 kernels (T <= 64, head_dim 8..64, no attn output)");
+                  "temporal_attn_fwd: bf16 storage needs the v3 kernels (T <= 128, head_dim 8..64, no attn output)");
     if (al4 && !attn && v3_ok(T, head_dim)) {
-        const int LG = v3_lanes(T), HPW = WAVE / LG, n_hg = (heads + HPW - 1) / HPW;
+        const int LG = v3_lanes(T), HPW = WAVE / LG, n_hg = (heads + HPW - 1) / HPW, WPH = v3_wph(T);
         const dim3 g3((unsigned)(grid_rows(rows) * n_hg));
         const size_t lds = v3_fwd_lds(T, head_dim, HPW);
-#define TAGAN_V3F(DD, LL) (bf ? k_tattn_fwd_v3<DD, LL, bf16s> : k_tattn_fwd_v3<DD, LL, float>)<<<g3, V3_BLK, lds, s>>>(A, qf, kf, vf, n_hg)
-#define TAGAN_V3F_D(LL) switch (head_dim) { case 8: TAGAN_V3F(8, LL); break; case 16: TAGAN_V3F(16, LL); break; \
-                                            case 32: TAGAN_V3F(32, LL); break; default: TAGAN_V3F(64, LL); break; }
-        if (LG == 16) { TAGAN_V3F_D(16) } else if (LG == 32) { TAGAN_V3F_D(32) } else { TAGAN_V3F_D(64) }
+#define TAGAN_V3F(DD, LL, W) (bf ? k_tattn_fwd_v3<DD, LL, bf16s, W> : k_tattn_fwd_v3<DD, LL, float, W>)<<<g3, V3_BLK * W, lds, s>>>(A, qf, kf, vf, n_hg)
+#define TAGAN_V3F_D(LL, W) switch (head_dim) { case 8: TAGAN_V3F(8, LL, W); break; case 16: TAGAN_V3F(16, LL, W); break; \
+                                               case 32: TAGAN_V3F(32, LL, W); break; default: TAGAN_V3F(64, LL, W); break; }
+        if (LG == 16) { TAGAN_V3F_D(16, 1) } else if (LG == 32) { TAGAN_V3F_D(32, 1) }
+        else if (WPH == 1) { TAGAN_V3F_D(64, 1) } else { TAGAN_V3F_D(64, 2) }
 #undef TAGAN_V3F_D
 #undef TAGAN_V3F
         TAGAN_CHECK_LAUNCH("temporal_attn_fwd_v3");
@@ -1029,16 +1044,17 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
                      do_row % 4 == 0 && d_t % 4 == 0 && d_row % 4 == 0;
     const bool bf = dtype == TAGAN_BF16;
     TAGAN_REQUIRE(!bf || (al4 && v3_ok(T, head_dim)), TAGAN_ERR_UNSUPPORTED,
-                  "temporal_attn_bwd: bf16 storage needs the v3 kernels (T <= 64, head_dim 8..64)");
+                  "temporal_attn_bwd: bf16 storage needs the v3 kernels (T <= 128, head_dim 8..64)");
     if (al4 && v3_ok(T, head_dim)) {
         // grid = nblk partial rows x n_hg head groups; block b keeps head group b % n_hg
-        const int LG = v3_lanes(T), HPW = WAVE / LG, n_hg = (heads + HPW - 1) / HPW;
+        const int LG = v3_lanes(T), HPW = WAVE / LG, n_hg = (heads + HPW - 1) / HPW, WPH = v3_wph(T);
         const dim3 g3((unsigned)(nblk * n_hg));
-        const size_t lds = v3_bwd_lds(T, head_dim, HPW);
-#define TAGAN_V3B(DD, LL) (bf ? k_tattn_bwd_v3<DD, LL, bf16s> : k_tattn_bwd_v3<DD, LL, float>)<<<g3, V3_BLK, lds, s>>>(A, qf, kf, vf, df, lse, n_hg)
-#define TAGAN_V3B_D(LL) switch (head_dim) { case 8: TAGAN_V3B(8, LL); break; case 16: TAGAN_V3B(16, LL); break; \
-                                            case 32: TAGAN_V3B(32, LL); break; default: TAGAN_V3B(64, LL); break; }
-        if (LG == 16) { TAGAN_V3B_D(16) } else if (LG == 32) { TAGAN_V3B_D(32) } else { TAGAN_V3B_D(64) }
+        const size_t lds = v3_bwd_lds(T, head_dim, HPW, WPH);
+#define TAGAN_V3B(DD, LL, W) (bf ? k_tattn_bwd_v3<DD, LL, bf16s, W> : k_tattn_bwd_v3<DD, LL, float, W>)<<<g3, V3_BLK * W, lds, s>>>(A, qf, kf, vf, df, lse, n_hg)
+#define TAGAN_V3B_D(LL, W) switch (head_dim) { case 8: TAGAN_V3B(8, LL, W); break; case 16: TAGAN_V3B(16, LL, W); break; \
+                                               case 32: TAGAN_V3B(32, LL, W); break; default: TAGAN_V3B(64, LL, W); break; }
+        if (LG == 16) { TAGAN_V3B_D(16, 1) } else if (LG == 32) { TAGAN_V3B_D(32, 1) }
+        else if (WPH == 1) { TAGAN_V3B_D(64, 1) } else { TAGAN_V3B_D(64, 2) }
 #undef TAGAN_V3B_D
 #undef TAGAN_V3B
         TAGAN_CHECK_LAUNCH("temporal_attn_bwd_v3");
