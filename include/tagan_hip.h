@@ -108,6 +108,21 @@ int tagan_graph_chunks(const int32_t* seg_ptr, int64_t n_segments, int32_t chunk
                        int32_t* multi_seg, int32_t* counts,
                        void* workspace, size_t workspace_bytes, void* stream);
 
+/* Processing order of the chunks (a permutation of [0, n_chunks)): chunks stay
+ * grouped by window of 2^window_bits consecutive segments (keeps the gathers of
+ * one window of rows / snapshots together in the caches) and, inside a window,
+ * run longest first (counting sort, one workgroup per window).  The edge
+ * kernels run up to 64/lanes-per-chunk chunks side by side in one wave and
+ * loop to the longest of them: on a power-law graph consecutive chunks differ
+ * wildly in length (C2: 47 % of the lane slots busy in row order, 92 % in this
+ * order).  Ties run in any order and no result depends on the order (each
+ * chunk's output and partial slot are fixed by its index), so every kernel
+ * stays bitwise deterministic.  order[] needs n_chunks (<= chunk capacity)
+ * entries; chunk < 256.  No workspace. */
+int tagan_chunk_order(const int32_t* seg_ptr, int64_t n_segments, const int32_t* chunk_ptr,
+                      const int32_t* chunk_seg, const int32_t* chunk_beg, int32_t chunk, int32_t window_bits,
+                      int32_t* order, void* stream);
+
 /* A built snapshot-batch graph (all device pointers).  Filled by the host from
  * tagan_csr_build + two tagan_graph_chunks calls (rows over the CSR, columns
  * over the CSC). */
@@ -133,6 +148,8 @@ typedef struct tagan_graph {
     const int32_t* col_chunk_part;
     const int32_t* col_multi;
     const int32_t* col_counts;
+    const int32_t* row_chunk_order;  /* [chunk_cap] processing order (tagan_chunk_order); NULL = identity */
+    const int32_t* col_chunk_order;
 } tagan_graph;
 
 /* ---------------------------------------------------------------------------

@@ -288,10 +288,72 @@ __global__ void __launch_bounds__(BLK) k_chunk_fill(const int32_t* __restrict__ 
     }
 }
 
+// One workgroup per window of 2^wbits consecutive segments (a contiguous chunk range): counting
+// sort of the window's chunks by entry count, longest first, in LDS.  Positions inside a count
+// bucket come from LDS atomics, so ties may run in any order; no result depends on the order.
+constexpr int ORDER_BINS = 256;
+
+__global__ void __launch_bounds__(BLK) k_chunk_order_window(const int32_t* __restrict__ ptr, int64_t n,
+                                                            const int32_t* __restrict__ chunk_ptr,
+                                                            const int32_t* __restrict__ seg,
+                                                            const int32_t* __restrict__ beg, int chunk, int wbits,
+                                                            int32_t* __restrict__ order) {
+    __shared__ int hist[ORDER_BINS];
+    __shared__ int base[ORDER_BINS];
+    const int64_t s0 = (int64_t)blockIdx.x << wbits;
+    const int64_t s1 = min(n, s0 + ((int64_t)1 << wbits));
+    const int c0 = chunk_ptr[s0], c1 = chunk_ptr[s1];
+    for (int i = threadIdx.x; i < ORDER_BINS; i += BLK) hist[i] = 0;
+    __syncthreads();
+    for (int c = c0 + threadIdx.x; c < c1; c += BLK) {
+        const int cnt = min(chunk, ptr[seg[c] + 1] - beg[c]);
+        atomicAdd(&hist[ORDER_BINS - 1 - cnt], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < WAVE) {      // exclusive scan of the bins by one wave, 4 bins per lane
+        const int l = threadIdx.x;
+        int v[4], t = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { v[k] = hist[4 * l + k]; t += v[k]; }
+        int incl = t;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const int y = __shfl_up(incl, o, WAVE);
+            if (l >= o) incl += y;
+        }
+        int run = incl - t;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { base[4 * l + k] = run; run += v[k]; }
+    }
+    __syncthreads();
+    for (int c = c0 + threadIdx.x; c < c1; c += BLK) {
+        const int cnt = min(chunk, ptr[seg[c] + 1] - beg[c]);
+        order[c0 + atomicAdd(&base[ORDER_BINS - 1 - cnt], 1)] = c;
+    }
+}
+
 }  // namespace
 }  // namespace tagan
 
 extern "C" {
+
+int tagan_chunk_order(const int32_t* seg_ptr, int64_t n_segments, const int32_t* chunk_ptr,
+                      const int32_t* chunk_seg, const int32_t* chunk_beg, int32_t chunk, int32_t window_bits,
+                      int32_t* order, void* stream) {
+    using namespace tagan;
+    TAGAN_REQUIRE(n_segments > 0 && chunk > 0 && chunk < ORDER_BINS && window_bits >= 0 && window_bits < 31,
+                  TAGAN_ERR_ARG, "tagan_chunk_order: n=%lld chunk=%d window_bits=%d", (long long)n_segments,
+                  chunk, window_bits);
+    TAGAN_REQUIRE(seg_ptr && chunk_ptr && chunk_seg && chunk_beg && order, TAGAN_ERR_ARG,
+                  "tagan_chunk_order: null pointer");
+    const int64_t windows = ((n_segments - 1) >> window_bits) + 1;
+    TAGAN_REQUIRE(windows <= 0x7fffffff, TAGAN_ERR_ARG, "tagan_chunk_order: too many windows");
+    hipStream_t s = as_stream(stream);
+    k_chunk_order_window<<<(unsigned)windows, BLK, 0, s>>>(seg_ptr, n_segments, chunk_ptr, chunk_seg, chunk_beg,
+                                                           chunk, window_bits, order);
+    TAGAN_CHECK_LAUNCH("chunk_order");
+    return TAGAN_OK;
+}
 
 int64_t tagan_chunk_capacity(int64_t n_segments, int64_t nnz_cap, int32_t chunk) {
     return chunk > 0 ? n_segments + nnz_cap / chunk + 1 : 0;

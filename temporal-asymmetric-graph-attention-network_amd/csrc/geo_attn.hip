@@ -298,6 +298,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
     Lanes<LPR> L;
     const int nchunks = A.g.row_counts[0];
     const bool valid = L.chunk < nchunks;
+    if (valid && A.g.row_chunk_order) L.chunk = A.g.row_chunk_order[L.chunk];   // length-sorted order
     int row = 0, e0 = 0, cnt = 0;
     if (valid) {
         row = A.g.row_chunk_seg[L.chunk];
@@ -408,6 +409,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
     Lanes<LPR> L;
     const int nchunks = A.g.row_counts[0];
     const bool valid = L.chunk < nchunks;
+    if (valid && A.g.row_chunk_order) L.chunk = A.g.row_chunk_order[L.chunk];   // length-sorted order
     int row = 0, e0 = 0, cnt = 0;
     if (valid) {
         row = A.g.row_chunk_seg[L.chunk];
@@ -519,6 +521,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
     Lanes<LPR> L;
     const int nchunks = A.g.col_counts[0];
     const bool valid = L.chunk < nchunks;
+    if (valid && A.g.col_chunk_order) L.chunk = A.g.col_chunk_order[L.chunk];   // length-sorted order
     int colj = 0, e0 = 0, cnt = 0;
     if (valid) {
         colj = A.g.col_chunk_seg[L.chunk];

@@ -11,6 +11,7 @@ Every output and workspace is allocated here from PyTorch's caching allocator;
 kernels are launched on the current HIP stream.
 """
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -27,6 +28,9 @@ def new_seed() -> int:
 
 # ----------------------------------------------------------------------------- graph
 CHUNK = 64   # max CSR/CSC entries per work chunk (power-law hubs are split)
+# Chunks run in windows of 2^ORDER_BITS consecutive rows/columns, longest first inside a window
+# (tagan_chunk_order); TAGAN_CHUNK_ORDER=0 keeps the plain row order (A/B measurements).
+ORDER_BITS = 12
 
 
 @dataclass
@@ -42,6 +46,8 @@ class SnapshotGraph:
     node_counts: Sequence[int]
     row_chunks: Optional[tuple] = None   # (chunk_ptr, seg, beg, part, multi, counts)
     col_chunks: Optional[tuple] = None
+    row_order: Optional[torch.Tensor] = None   # chunk processing order (None = identity)
+    col_order: Optional[torch.Tensor] = None
     chunk: int = CHUNK
     chunk_cap: int = 0
     part_cap: int = 0
@@ -57,7 +63,8 @@ class SnapshotGraph:
             p = lambda t: t.data_ptr()  # noqa: E731
             self._struct = _lib.TaganGraph(self.num_nodes, p(self.rowptr), p(self.col), p(self.csc_ptr),
                                            p(self.csc_row), p(self.csc_eid), self.chunk, self.chunk_cap,
-                                           self.part_cap, *[p(t) for t in r], *[p(t) for t in c])
+                                           self.part_cap, *[p(t) for t in r], *[p(t) for t in c],
+                                           *[None if t is None else p(t) for t in (self.row_order, self.col_order)])
         return ctypes.byref(self._struct)
 
 
@@ -76,12 +83,17 @@ def _chunk_lists(seg_ptr: torch.Tensor, n: int, nnz_cap: int, chunk: int):
     ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
     check(L.tagan_graph_chunks(ptr(seg_ptr), n, chunk, ptr(chunk_ptr), ptr(seg), ptr(beg), ptr(part), ptr(multi),
                                ptr(counts), ptr(ws), wsb, stream_of(seg_ptr)), "tagan_graph_chunks")
-    return (chunk_ptr, seg, beg, part, multi, counts), cap, pcap
+    order = None
+    if os.environ.get("TAGAN_CHUNK_ORDER", "1") != "0":
+        order = buf[o + 3 * cap:o + 4 * cap]
+        check(L.tagan_chunk_order(ptr(seg_ptr), n, ptr(chunk_ptr), ptr(seg), ptr(beg), chunk, ORDER_BITS,
+                                  ptr(order), stream_of(seg_ptr)), "tagan_chunk_order")
+    return (chunk_ptr, seg, beg, part, multi, counts), cap, pcap, order
 
 
 def _finish(g: SnapshotGraph, nnz_cap: int, chunk: int = CHUNK) -> SnapshotGraph:
-    g.row_chunks, g.chunk_cap, g.part_cap = _chunk_lists(g.rowptr, g.num_nodes, nnz_cap, chunk)
-    g.col_chunks, _, _ = _chunk_lists(g.csc_ptr, g.num_nodes, nnz_cap, chunk)
+    g.row_chunks, g.chunk_cap, g.part_cap, g.row_order = _chunk_lists(g.rowptr, g.num_nodes, nnz_cap, chunk)
+    g.col_chunks, _, _, g.col_order = _chunk_lists(g.csc_ptr, g.num_nodes, nnz_cap, chunk)
     g.chunk = chunk
     return g
 

@@ -88,6 +88,8 @@ def test_argument_validation_reports_errors():
     rc = L.tagan_geo_attn_fwd(0, 0, ctypes.byref(g), 4, 16, None, None, None, 64, None, 0.0, 0, None, None, None,
                               None, 0, None)
     assert rc == -1 and b"graph" in L.tagan_last_error()
+    rc = L.tagan_chunk_order(None, 10, None, None, None, 300, 12, None, None)
+    assert rc == -1 and b"chunk_order" in L.tagan_last_error()
     rc = L.tagan_temporal_attn_fwd(7, 10, 4, 2, 8, None, None, None, 0, 0, None, None, 0, None, 0, 0, 0, 0.0, 0,
                                    None, 0, 0, None, None, None)
     assert rc == -2

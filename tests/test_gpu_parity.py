@@ -319,3 +319,41 @@ def test_geo_kernel_dropout_matches_regenerated_mask(dev):
     (ref * gout.double()).sum().backward()
     G.assert_close("out", out, ref, OUT_ATOL, OUT_RTOL)
     G.assert_close("dqkv", x.grad, q64.grad, GRAD_ATOL, GRAD_RTOL)
+
+
+@pytest.mark.parametrize("chunk", [4, 64])
+def test_chunk_order_is_a_length_sorted_permutation_and_results_do_not_depend_on_it(dev, chunk, monkeypatch):
+    """tagan_chunk_order: a permutation of the real chunks, windows of 2^ORDER_BITS segments in order,
+    longest chunk first inside a window; the edge kernels give bitwise-identical outputs and gradients
+    in that order and in plain row order (every chunk's output / partial slot is fixed by its index)."""
+    from tagan_amd import kernels
+    from tagan_amd.kernels import GeoAttnFn, build_graph
+    monkeypatch.setattr(kernels, "ORDER_BITS", 6)     # several windows at this size
+    counts = [300, 257, 190]
+    eis = [_hub_graph(n, 11 + i) for i, n in enumerate(counts)]
+    N, H, heads = sum(counts), 64, 4
+    g = torch.Generator().manual_seed(3)
+    qkv = torch.randn(N, 3 * H, generator=g) * 0.5
+    gout = torch.randn(N, H, generator=g).to(dev)
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TAGAN_CHUNK_ORDER", flag)
+        graph = build_graph([e.to(dev) for e in eis], counts, chunk=chunk)
+        if flag == "1":
+            for chunks, order, ptr_ in ((graph.row_chunks, graph.row_order, graph.rowptr),
+                                        (graph.col_chunks, graph.col_order, graph.csc_ptr)):
+                n_ch = int(chunks[5][0])
+                o = order[:n_ch].cpu().long()
+                assert torch.equal(o.sort().values, torch.arange(n_ch))
+                seg, beg = chunks[1][:n_ch].cpu().long(), chunks[2][:n_ch].cpu().long()
+                cnt = torch.minimum(torch.full_like(seg, chunk), ptr_.cpu().long()[seg + 1] - beg)
+                key = (seg[o] >> 6) * 256 + (255 - cnt[o])
+                assert bool((key[1:] >= key[:-1]).all())
+        else:
+            assert graph.row_order is None
+        x = qkv.to(dev).requires_grad_(True)
+        out = GeoAttnFn.apply(x, None, graph, 0, heads, 0.1, 77)
+        (out * gout).sum().backward()
+        res.append((out.detach(), x.grad))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])

@@ -49,7 +49,8 @@ def main():
     print(prof.key_averages().table(sort_by="device_time_total", row_limit=40))
     for e in prof.key_averages(group_by_input_shape=True):
         if e.key in ("aten::add", "aten::add_", "aten::copy_", "aten::fill_", "aten::zero_", "aten::sum",
-                     "aten::mul", "aten::cat", "aten::clone"):
+                     "aten::mul", "aten::cat", "aten::clone", "aten::mm", "aten::addmm", "aten::bmm",
+                     "aten::linear", "aten::_efficientzerotensor"):
             print("%-14s calls=%3d dev_us=%8.1f shapes=%s" % (e.key, e.count, e.device_time_total, e.input_shapes))
 
 
