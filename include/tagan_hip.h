@@ -237,6 +237,16 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
                             float p_drop, uint64_t seed, const float* gamma, const float* beta,
                             float eps, float* s_out, float* y, int64_t ldy, float* mean, float* rstd,
                             void* stream);
+/* Layer 0 of the geometric stack with the skip branch of model.py:258-262 fused
+ * into its closing LayerNorm: y = LN(dropout(a) + b) + LN_s(b) (b = the layer
+ * input), one pass instead of LN, LN_s and an add.  fp32 only.  mean_s/rstd_s
+ * [M] are LN_s's statistics, for its backward (tagan_layernorm_bwd with s = b,
+ * dres = the LN's own ds, so both gradients of b arrive summed). */
+int tagan_add_layernorm_skip_fwd(int64_t M, int32_t H, const float* a, const float* b, float p_drop,
+                                 uint64_t seed, const float* gamma, const float* beta, float eps,
+                                 const float* gamma_s, const float* beta_s, float eps_s, float* s_out,
+                                 float* y, float* mean, float* rstd, float* mean_s, float* rstd_s,
+                                 void* stream);
 /* Backward: ds = dL/ds (+ dres when given: the gradient of the LN input's other
  * consumer, fused instead of a separate add), da = dL/ds masked/scaled by the same
  * dropout (the projection branch's gradient), dgamma/dbeta [H], dsum_a [H] = column

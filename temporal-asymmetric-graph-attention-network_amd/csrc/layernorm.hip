@@ -44,6 +44,12 @@ struct LnArgs {
     float* part;   // [gridDim.x, 3H]: dgamma | dbeta | column sums of da (projection-bias gradient)
     int want_dsa;  // accumulate the column sums of da
     int64_t ldy;   // forward output row stride (>= H)
+    // forward skip branch (model.py:258-262): y += LN_s(b) with its own gamma/beta/eps/statistics
+    const float* gamma_s;
+    const float* beta_s;
+    float eps_s;
+    float* mean_s;
+    float* rstd_s;
 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -68,17 +74,20 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
     const int64_t row = wave * RPW + lane / LPR;
     if (row >= A.M) return;
     const int H = A.H;
-    float4 v[NV];
-    float sum = 0.f;
+    float4 v[NV], rb[NV];
+    float sum = 0.f, sum_b = 0.f;
 #pragma unroll
     for (int n = 0; n < NV; ++n) {
         const int c = (n * LPR + sl) * 4;
         const int64_t off = row * H + c;
         float4 x = ld4(A.a + off);
         x = drop4(A, x, row, c);
+        rb[n] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (A.b) {
             const float4 r = ld4(A.b + off);
+            rb[n] = r;
             x.x += r.x; x.y += r.y; x.z += r.z; x.w += r.w;
+            sum_b += (r.x + r.y) + (r.z + r.w);
         }
         v[n] = x;
         if (A.s_out) st4(A.s_out + off, x);
@@ -93,6 +102,17 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
     }
     const float var = row_sum<LPR>(sq) / (float)H;
     const float rstd = 1.f / sqrtf(var + A.eps);
+    float mean_s = 0.f, rstd_s = 0.f;
+    if (A.gamma_s) {                     // skip branch: statistics of b alone (two-pass, like the main one)
+        mean_s = row_sum<LPR>(sum_b) / (float)H;
+        float sqb = 0.f;
+#pragma unroll
+        for (int n = 0; n < NV; ++n) {
+            const float dx = rb[n].x - mean_s, dyv = rb[n].y - mean_s, dz = rb[n].z - mean_s, dw = rb[n].w - mean_s;
+            sqb += (dx * dx + dyv * dyv) + (dz * dz + dw * dw);
+        }
+        rstd_s = 1.f / sqrtf(row_sum<LPR>(sqb) / (float)H + A.eps_s);
+    }
 #pragma unroll
     for (int n = 0; n < NV; ++n) {
         const int c = (n * LPR + sl) * 4;
@@ -102,11 +122,22 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
         o.y = (v[n].y - mean) * rstd * g.y + be.y;
         o.z = (v[n].z - mean) * rstd * g.z + be.z;
         o.w = (v[n].w - mean) * rstd * g.w + be.w;
+        if (A.gamma_s) {   // same rounding as the reference's separate  y + LN_s(b)
+            const float4 gs = ld4(A.gamma_s + c), bs = ld4(A.beta_s + c);
+            o.x += (rb[n].x - mean_s) * rstd_s * gs.x + bs.x;
+            o.y += (rb[n].y - mean_s) * rstd_s * gs.y + bs.y;
+            o.z += (rb[n].z - mean_s) * rstd_s * gs.z + bs.z;
+            o.w += (rb[n].w - mean_s) * rstd_s * gs.w + bs.w;
+        }
         Io<S>::st(A.y, row * A.ldy + c, o);     // y in the storage type (bf16 feeds a GEMM)
     }
     if (sl == 0) {
         A.mean[row] = mean;
         A.rstd[row] = rstd;
+        if (A.gamma_s) {
+            A.mean_s[row] = mean_s;
+            A.rstd_s[row] = rstd_s;
+        }
     }
 }
 
@@ -242,6 +273,28 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
     if (dtype == TAGAN_BF16) launch_ln<bf16s, true>(lpr, nv, g, s, A);
     else launch_ln<float, true>(lpr, nv, g, s, A);
     TAGAN_CHECK_LAUNCH("layernorm_fwd");
+    return TAGAN_OK;
+}
+
+int tagan_add_layernorm_skip_fwd(int64_t M, int32_t H, const float* a, const float* b, float p_drop, uint64_t seed,
+                                 const float* gamma, const float* beta, float eps, const float* gamma_s,
+                                 const float* beta_s, float eps_s, float* s_out, float* y, float* mean, float* rstd,
+                                 float* mean_s, float* rstd_s, void* stream) {
+    using namespace tagan;
+    int lpr, nv;
+    TAGAN_REQUIRE(geometry(H, lpr, nv), TAGAN_ERR_UNSUPPORTED, "layernorm: H=%d unsupported", H);
+    TAGAN_REQUIRE(M > 0 && a && b && gamma && beta && gamma_s && beta_s && y && mean && rstd && mean_s && rstd_s,
+                  TAGAN_ERR_ARG, "layernorm_skip_fwd: bad args");
+    TAGAN_REQUIRE(p_drop >= 0.f && p_drop < 1.f, TAGAN_ERR_ARG, "layernorm_skip_fwd: p_drop");
+    LnArgs A{};
+    A.M = M; A.H = H; A.a = a; A.b = b; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
+    A.gamma = gamma; A.beta = beta; A.eps = eps; A.s_out = s_out; A.y = y; A.mean = mean; A.rstd = rstd;
+    A.ldy = H;
+    A.gamma_s = gamma_s; A.beta_s = beta_s; A.eps_s = eps_s; A.mean_s = mean_s; A.rstd_s = rstd_s;
+    const int64_t rpw = WAVE / lpr;
+    const dim3 g((unsigned)(((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE)));
+    launch_ln<float, true>(lpr, nv, g, as_stream(stream), A);
+    TAGAN_CHECK_LAUNCH("layernorm_skip_fwd");
     return TAGAN_OK;
 }
 

@@ -22,7 +22,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import check, lib, ptr, require_hip, stream_of
-from .kernels import TemporalMask, _geo_fwd, colsum, weight_grad
+from .kernels import TemporalMask, _geo_fwd, colsum, split_rows, weight_grad
 
 
 # ----------------------------------------------------------------------------- raw LayerNorm calls
@@ -39,6 +39,20 @@ def ln_fwd(a2, b2, p_drop, seed, gamma, beta, eps, keep_s, y=None, y_dtype=torch
                                         ptr(beta), float(eps), ptr(s), ptr(y), y.stride(0), ptr(mean), ptr(rstd),
                                         stream_of(a2)), "tagan_add_layernorm_fwd")
     return y, s, mean, rstd
+
+
+def ln_skip_fwd(a2, b2, p_drop, seed, gamma, beta, eps, gamma_s, beta_s, eps_s):
+    """LN(dropout(a2) + b2) + LN_s(b2) (fp32); returns y, s, mean, rstd, (mean_s, rstd_s)."""
+    M, H = a2.shape
+    dev = a2.device
+    s = torch.empty_like(a2)
+    y = torch.empty(M, H, device=dev)
+    st = torch.empty(4, M, device=dev)
+    check(lib().tagan_add_layernorm_skip_fwd(M, H, ptr(a2), ptr(b2), float(p_drop), seed, ptr(gamma), ptr(beta),
+                                             float(eps), ptr(gamma_s), ptr(beta_s), float(eps_s), ptr(s), ptr(y),
+                                             ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(st[3]), stream_of(a2)),
+          "tagan_add_layernorm_skip_fwd")
+    return y, s, st[0], st[1], (st[2], st[3])
 
 
 def ln_bwd(s, mean, rstd, gamma, dy2, dres, p_drop, seed, want_ds, want_da, want_sum_a, da_dtype=torch.float32):
@@ -210,6 +224,7 @@ def _wgrad(dy, x, bf, rows: int = 2048):
     N = x.shape[1]
     if K < 4 * rows:
         return torch.mm(dy.t(), x, out_dtype=torch.float32)
+    rows = split_rows(K, rows)
     c = K // rows
     main = c * rows
     dw = torch.bmm(dy[:main].view(c, rows, M).transpose(1, 2), x[:main].view(c, rows, N),
@@ -225,7 +240,7 @@ class AttnBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, p1, p2, ln1_w, ln1_b, w_qkv, b_qkv, w_o, b_o, ln2_w, ln2_b, core, eps1: float,
-                eps2: float, p_out: float, seed_out: int):
+                eps2: float, p_out: float, seed_out: int, lns_w=None, lns_b=None, eps_s: float = 1e-5):
         require_hip(x)
         H = x.shape[-1]
         x2 = x.reshape(-1, H).contiguous()
@@ -239,21 +254,28 @@ class AttnBlockFn(torch.autograd.Function):
         c, saved = core.fwd(qkv, p1, p2)
         cg = _b(c) if bf else c
         o = _addmm(b_o, cg, w_o, bf)
-        y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True)
-        ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w)
-        ctx.inter = (h, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2)
+        skip = None
+        if lns_w is not None:      # y = LN2(drop(o) + x) + LN_s(x) in one pass (model.py:258-262)
+            y, s2, mean2, rstd2, skip = ln_skip_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, lns_w, lns_b, eps_s)
+        else:
+            y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True)
+        ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
+        ctx.inter = (h, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
         ctx.cfg = (core, p_out, seed_out, x.shape, bf, act)
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, ln1_w, w_qkv, w_o, ln2_w = ctx.saved_tensors
-        h, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2 = ctx.inter
+        x2, ln1_w, w_qkv, w_o, ln2_w, lns_w = ctx.saved_tensors
+        h, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip = ctx.inter
         core, p_out, seed_out, shape, bf, act = ctx.cfg
         ng = ctx.needs_input_grad
         dy2 = dy.reshape(-1, shape[-1]).contiguous()
         dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True,
                                          da_dtype=torch.bfloat16 if bf else torch.float32)
+        dgs = dbs = None
+        if skip is not None:       # skip branch: LN_s backward with the residual gradient added in-kernel
+            dres, _, dgs, dbs, _ = ln_bwd(x2, skip[0], skip[1], lns_w, dy2, dres, 0.0, 0, True, False, False)
         dc = _mm(do, w_o, bf, out_bf16=act)
         dw_o = _wgrad(do, cg, bf) if ng[7] else None
         dqkv, dp1, dp2 = core.bwd(qkv, c, saved, dc, ng[1], ng[2])
@@ -267,13 +289,19 @@ class AttnBlockFn(torch.autograd.Function):
         dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
         ctx.inter = None
         return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
-                None, None, None, None, None)
+                None, None, None, None, None, dgs, dbs, None)
 
 
 def attention_block(x, core, p1: Optional[torch.Tensor], p2: Optional[torch.Tensor], ln1, q_lin, k_lin, v_lin,
-                    out_lin, ln2, p_out: float, seed_out: int):
+                    out_lin, ln2, p_out: float, seed_out: int, skip_ln=None):
+    """``skip_ln``: a LayerNorm whose output of the block input is added to the block output
+    (TAGAN's first geometric layer, model.py:258-262), fused into the closing LayerNorm."""
     w_qkv = torch.cat([q_lin.weight, k_lin.weight, v_lin.weight], 0)
     b_qkv = torch.cat([q_lin.bias, k_lin.bias, v_lin.bias], 0)
+    if skip_ln is not None:
+        return AttnBlockFn.apply(x, p1, p2, ln1.weight, ln1.bias, w_qkv, b_qkv, out_lin.weight, out_lin.bias,
+                                 ln2.weight, ln2.bias, core, ln1.eps, ln2.eps, float(p_out), seed_out,
+                                 skip_ln.weight, skip_ln.bias, skip_ln.eps)
     return AttnBlockFn.apply(x, p1, p2, ln1.weight, ln1.bias, w_qkv, b_qkv, out_lin.weight, out_lin.bias,
                              ln2.weight, ln2.bias, core, ln1.eps, ln2.eps, float(p_out), seed_out)
 

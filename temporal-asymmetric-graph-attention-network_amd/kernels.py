@@ -318,6 +318,16 @@ class TemporalAttnFn(torch.autograd.Function):
 
 
 # ----------------------------------------------------------------------------- projections
+def split_rows(K: int, rows: int = 2048) -> int:
+    """Slice height for a split-K weight gradient: a multiple of 64 in [rows/2, 2·rows] that divides K
+    (closest to ``rows`` in ratio), so no remainder GEMM + add is needed (K = 320000 at C2 -> 2560); else ``rows``."""
+    best = None
+    for r in range(64 * max(1, rows // 128), 2 * rows + 1, 64):
+        if K % r == 0 and (best is None or max(r, rows) / min(r, rows) < max(best, rows) / min(best, rows)):
+            best = r
+    return best or rows
+
+
 def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, rows: int = 2048) -> torch.Tensor:
     """dW = dyᵀ·x for K = dy.shape[0] >> M, N: split-K batched GEMM (hipBLASLt) + ordered sum.
 
@@ -329,6 +339,7 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, rows: int = 2048) -> torch.
     N = x2.shape[1]
     if K < 4 * rows:
         return dy2.t() @ x2
+    rows = split_rows(K, rows)
     c = K // rows
     main = c * rows
     dw = torch.bmm(dy2[:main].view(c, rows, M).transpose(1, 2), x2[:main].view(c, rows, N)).sum(0)

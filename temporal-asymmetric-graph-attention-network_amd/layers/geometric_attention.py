@@ -129,15 +129,20 @@ class GeometricAttention(nn.Module):
             return self.distance_param
         return None
 
-    def forward_graph(self, x: torch.Tensor, graph: SnapshotGraph) -> torch.Tensor:
-        """Hot path: x [N, H] (N = all nodes of a snapshot batch), graph = their CSR/CSC."""
+    def forward_graph(self, x: torch.Tensor, graph: SnapshotGraph, skip_ln=None) -> torch.Tensor:
+        """Hot path: x [N, H] (N = all nodes of a snapshot batch), graph = their CSR/CSC.
+        ``skip_ln``: returns layer(x) + skip_ln(x) (model.py:258-262), fused into the last LayerNorm."""
         p = self.attn_dropout.p if self.training else 0.0
         p_out = self.output_dropout.p if self.training else 0.0
+        if skip_ln is not None and x.dtype != torch.float32:
+            return self.forward_graph(x, graph) + layer_norm(x, skip_ln)
         if fusable(x, self.use_layer_norm):   # one autograd node for the whole layer (fused.py)
             core = GeoCore(graph, self.metric_id, self.num_heads, p, new_seed() if p > 0 else 0)
             return attention_block(x, core, self._metric_param(), None, self.layer_norm1, self.q_linear,
                                    self.k_linear, self.v_linear, self.output_proj, self.layer_norm2, p_out,
-                                   new_seed() if p_out > 0 else 0)
+                                   new_seed() if p_out > 0 else 0, skip_ln=skip_ln)
+        if skip_ln is not None:
+            return self.forward_graph(x, graph) + layer_norm(x, skip_ln)
         identity = x
         h = layer_norm(x, self.layer_norm1) if self.use_layer_norm else x
         qkv = fused_qkv(h, self.q_linear, self.k_linear, self.v_linear).contiguous()

@@ -26,8 +26,8 @@ class TAGANGraphAttention(nn.Module):
                                                       use_layer_norm=use_layer_norm,
                                                       learnable_distance=learnable_distance)
 
-    def forward_graph(self, x: torch.Tensor, graph: SnapshotGraph) -> torch.Tensor:
-        return self.geometric_attention.forward_graph(x, graph)
+    def forward_graph(self, x: torch.Tensor, graph: SnapshotGraph, skip_ln=None) -> torch.Tensor:
+        return self.geometric_attention.forward_graph(x, graph, skip_ln)
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor, edge_attr: Optional[torch.Tensor] = None,
                 return_attention_weights: bool = False

@@ -114,9 +114,12 @@ class TAGAN(nn.Module):
         h = linear(x_cat, self.node_embedding.weight, self.node_embedding.bias)
         skip = h
         for i, layer in enumerate(self.geometric_attention_layers):
-            h = layer.forward_graph(h, graph)
-            if i == 0:
-                h = h + (layer_norm(skip, self.skip_layer_norm) if self.skip_layer_norm is not None else skip)
+            if i == 0 and self.skip_layer_norm is not None:
+                h = layer.forward_graph(h, graph, skip_ln=self.skip_layer_norm)   # + LN_skip(skip), fused
+            else:
+                h = layer.forward_graph(h, graph)
+                if i == 0:
+                    h = h + skip
         weights = [{"node_attention": None} for _ in graph_sequence] if return_attention_weights else []
         return h, counts, weights
 
