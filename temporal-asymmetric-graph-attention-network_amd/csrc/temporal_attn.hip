@@ -868,6 +868,437 @@ __global__ void __launch_bounds__(V3_BLK * WPH) k_tattn_bwd_v3(TArgs A, const fl
     }
 }
 
+// =================================================================== v4: matrix-core kernels (T <= 64)
+// One wave per (node row, head) unit; every product of the layer runs on v_mfma_f32_16x16x4_f32
+// (fp32 in, fp32 accumulate: the same numbers as the fp32 VALU dots, in another summation order),
+// with 16x16 tiles over steps (T padded to TP = 16*TT) and head features (d = 16*DT):
+//   Sᵀ = K·Qᵀ       A = K rows (lane = key j), B = Q rows (lane = query i)
+//   Oᵀ = Vᵀ·Pᵀ      B = Pᵀ straight from Sᵀ's accumulator registers (the sum runs over the
+//                   accumulator's row index j), A = V read transposed (one element per lane)
+// so the softmax over j is in-lane over the registers plus two cross-lane steps (xor 16, 32),
+// and the output tile holds 4 consecutive features of one step per lane (one 16-B store).
+// Backward: Sᵀ and dPᵀ = V·dOᵀ the same way, dQᵀ = Kᵀ·dSᵀ from the accumulators, and dKᵀ = Qᵀ·dS,
+// dVᵀ = dOᵀ·P' with dS / P' transposed through a per-wave LDS tile (row stride TP+4); the
+// bias-table gradient is a fixed-order diagonal sum over that tile (bitwise deterministic).
+// Each wave keeps one head (wave stride = a multiple of heads), so its bias-table slice is staged
+// in LDS once.  MFMA work per unit: 8·TT²·DT instructions forward, 20·TT²·DT backward.
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <typename S>
+__device__ __forceinline__ f4v ld4v(const void* p, int64_t i, bool ok) {
+    if (!ok) return f4v{0.f, 0.f, 0.f, 0.f};
+    const float4 t = Io<S>::ld(p, i);
+    return f4v{t.x, t.y, t.z, t.w};
+}
+
+template <typename S>
+__device__ __forceinline__ float ld1v(const void* p, int64_t i, bool ok) {
+    return ok ? Io<S>::ld1(p, i) : 0.f;
+}
+
+template <typename S>
+__device__ __forceinline__ void st4v(void* p, int64_t i, f4v v, float scale) {
+    Io<S>::st(p, i, make_float4(v[0] * scale, v[1] * scale, v[2] * scale, v[3] * scale));
+}
+
+constexpr int v4_nbp(int TP) { return (2 * TP - 1 + 3) & ~3; }
+// Row stride of the transposed LDS tiles.  A 16-B read at Xt[row c][4g] (lane = 16g + c) is served in
+// ds_read_b128's 16-lane groups {c 0-3,12-15 of g} + {c 4-11 of g+1}; with stride 4m dwords those
+// lanes start on 4-dword bank slots c*m + g (mod 16), all distinct iff m = 2 (mod 4): TP + 8
+// (m = 6 at TP = 16, 10 at TP = 32).  TP + 4 (m = 5, 9) gives 2-way conflicts.
+constexpr int v4_ld(int TP) { return TP + 8; }
+// per-wave LDS: fwd Vt [D][LD]; bwd X [TP][LD] | Kt, Qt, dOt [D][LD]
+size_t v4_fwd_lds(int TT, int DT) { return (size_t)(16 * DT * v4_ld(16 * TT)) * 4; }
+size_t v4_bwd_lds(int TT, int DT) { return (size_t)(16 * TT * v4_ld(16 * TT) + 3 * 16 * DT * v4_ld(16 * TT)) * 4; }
+
+// The unit-invariant part of the score of the lane's elements (i = it*16 + c, j = jt*16 + 4g + e):
+// the head's bias-table value, or -inf outside [0, T)² and above the diagonal when causal.  A wave
+// keeps one head, so this lives in registers for the whole kernel (no per-element table lookup).
+template <int TT>
+__device__ __forceinline__ void v4_static_bias(const TArgs& A, int h, int c, int g, float (&bst)[TT][TT][4]) {
+    const int T = A.T, NB = 2 * T - 1;
+#pragma unroll
+    for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+        for (int it = 0; it < TT; ++it)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int i = it * 16 + c, j = jt * 16 + 4 * g + e;
+                const bool ok = i < T && j < T && !(A.causal && j > i);
+                bst[jt][it][e] = ok ? (A.bias_table ? A.bias_table[h * NB + i - j + T - 1] : 0.f) : -INFINITY;
+            }
+}
+
+// score of (i, j) from the raw dot product and the static part; -inf where masked
+__device__ __forceinline__ float v4_score(const TArgs& A, float bst, int64_t r, int h, int i, int j, float dot) {
+    if (bst == -INFINITY) return -INFINITY;
+    if (A.mask && !A.mask[r * A.mask_bstride + (int64_t)h * A.mask_hstride + (int64_t)i * A.T + j]) return -INFINITY;
+    float s = fmaf(dot, A.inv_sqrt_d, bst);
+    if (A.bias_dense) s += A.bias_dense[r * A.bias_bstride + (((int64_t)h * A.T + i) * A.T + j)];
+    return s;
+}
+
+// Transposed staging of a row tile held as lane (c, g): X[row = t*16 + c][dt*16 + 4g .. +3]
+// into Xt[feature][row] (row stride LT), so a lane can read Xt[dt*16 + c][t*16 + 4g .. +3] -- the
+// A operand of a product that sums over rows -- as one 16-B LDS read.
+template <int TT, int DT, int LT>
+__device__ __forceinline__ void v4_stage_t(float* Xt, const f4v (&x)[TT][DT], int c, int g) {
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Xt[(dt * 16 + 4 * g + e) * LT + t * 16 + c] = x[t][dt][e];
+}
+
+__device__ __forceinline__ f4v lds4(const float* p) { return *(const f4v*)p; }
+
+template <int TT, int DT, typename S>
+__global__ void __launch_bounds__(WAVE) k_tattn_fwd_v4(TArgs A, const float* __restrict__ q,
+                                                       const float* __restrict__ k,
+                                                       const float* __restrict__ v) {
+    constexpr int TP = 16 * TT, LT = v4_ld(TP);
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int T = A.T, d = A.d;
+    const int lane = threadIdx.x, c = lane & 15, g = lane >> 4;
+    const int h = (int)(blockIdx.x % A.heads);
+    float* Vt = sm;    // [16*DT][LT]
+    float bst[TT][TT][4];
+    v4_static_bias<TT>(A, h, c, g, bst);
+    const int64_t units = A.rows * A.heads;
+    f4v qv[TT][DT], kv[TT][DT], vv[TT][DT];
+    auto load = [&](int64_t uu) {
+        const int64_t hb = (uu / A.heads) * A.s_row + (int64_t)h * d;
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            const int i = t * 16 + c;
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                const int64_t off = hb + (int64_t)i * A.s_t + dt * 16 + 4 * g;
+                qv[t][dt] = ld4v<S>(q, off, i < T);
+                kv[t][dt] = ld4v<S>(k, off, i < T);
+                vv[t][dt] = ld4v<S>(v, off, i < T);
+            }
+        }
+    };
+    int64_t u = blockIdx.x;
+    if (u < units) load(u);
+    for (; u < units; u += gridDim.x) {
+        const int64_t r = u / A.heads;
+        f4v s[TT][TT];   // [jt][it]: Sᵀ tiles
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it) s[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int it = 0; it < TT; ++it) s[jt][it] = mfma4(kv[jt][dt][e], qv[it][dt][e], s[jt][it]);
+        wave_sync();   // the previous unit's reads of Vt are done
+        v4_stage_t<TT, DT, LT>(Vt, vv, c, g);
+        if (u + gridDim.x < units) load(u + gridDim.x);   // next unit's rows in flight during this one
+        wave_sync();
+        const uint32_t drk = tkey(A, r, h);
+        float inv_l[TT];
+#pragma unroll
+        for (int it = 0; it < TT; ++it) {
+            const int i = it * 16 + c;
+            float mx = -INFINITY;
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float sc = v4_score(A, bst[jt][it][e], r, h, i, jt * 16 + 4 * g + e, s[jt][it][e]);
+                    s[jt][it][e] = sc;
+                    mx = fmaxf(mx, sc);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, WAVE));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, WAVE));
+            float l = 0.f;
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float sc = s[jt][it][e];
+                    const float p = (sc == -INFINITY) ? 0.f : __expf(sc - mx);
+                    l += p;
+                    s[jt][it][e] = p * drop_scale(A, drk, i, jt * 16 + 4 * g + e);
+                }
+            l += __shfl_xor(l, 16, WAVE);
+            l += __shfl_xor(l, 32, WAVE);
+            inv_l[it] = (l > 0.f) ? 1.f / l : NAN;
+            if (g == 0 && i < T) A.lse[(r * A.heads + h) * T + i] = mx + __logf(l);
+        }
+        f4v o[DT][TT];
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it) o[dt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                const f4v va = lds4(Vt + (dt * 16 + c) * LT + jt * 16 + 4 * g);   // V[jt*16+4g+e][dt*16+c]
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int it = 0; it < TT; ++it) o[dt][it] = mfma4(va[e], s[jt][it][e], o[dt][it]);
+            }
+#pragma unroll
+        for (int it = 0; it < TT; ++it) {
+            const int i = it * 16 + c;
+            if (i >= T) continue;
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+                st4v<S>(A.out, r * A.o_row + (int64_t)i * A.o_t + h * d + dt * 16 + 4 * g, o[dt][it], inv_l[it]);
+        }
+    }
+}
+
+template <int TT, int DT, typename S>
+__global__ void __launch_bounds__(WAVE) k_tattn_bwd_v4(TArgs A, const float* __restrict__ q,
+                                                       const float* __restrict__ k,
+                                                       const float* __restrict__ v,
+                                                       const float* __restrict__ dout,
+                                                       const float* __restrict__ lse) {
+    constexpr int TP = 16 * TT, LD = v4_ld(TP), DP = 16 * DT;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int T = A.T, NB = 2 * T - 1, d = A.d;
+    const int lane = threadIdx.x, c = lane & 15, g = lane >> 4;
+    const int h = (int)(blockIdx.x % A.heads);
+    float* X = sm;               // [TP][LD] transpose tile X[j][i] (dS, then P')
+    float* Kt = X + TP * LD;     // [DP][LD] K transposed
+    float* Qt = Kt + DP * LD;    // [DP][LD] Q transposed
+    float* Ot = Qt + DP * LD;    // [DP][LD] dO transposed
+    float bst[TT][TT][4];
+    v4_static_bias<TT>(A, h, c, g, bst);
+    const float msc = A.p_drop > 0.f ? A.inv_keep : 1.f;   // drop_scale of a kept element
+    // Σ of dSᵀ over this wave's units, in unit order: the bias-table gradient before its diagonal
+    // sums, which run once at the end (fixed order: bitwise reproducible)
+    f4v gsum[TT][TT];
+#pragma unroll
+    for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+        for (int it = 0; it < TT; ++it) gsum[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+    const int64_t units = A.rows * A.heads;
+    f4v qv[TT][DT], kv[TT][DT], vv[TT][DT], dov[TT][DT];
+    float lsev[TT];
+    auto load = [&](int64_t uu) {
+        const int64_t rr = uu / A.heads;
+        const int64_t hb = rr * A.s_row + (int64_t)h * d;
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            const int i = t * 16 + c;
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                const int64_t off = hb + (int64_t)i * A.s_t + dt * 16 + 4 * g;
+                qv[t][dt] = ld4v<S>(q, off, i < T);
+                kv[t][dt] = ld4v<S>(k, off, i < T);
+                vv[t][dt] = ld4v<S>(v, off, i < T);
+                dov[t][dt] = ld4v<S>(dout, rr * A.do_row + (int64_t)h * d + (int64_t)i * A.do_t + dt * 16 + 4 * g,
+                                     i < T);
+            }
+            lsev[t] = (i < T) ? lse[(rr * A.heads + h) * T + i] : 0.f;
+        }
+    };
+    int64_t u = blockIdx.x;
+    if (u < units) load(u);
+    for (; u < units; u += gridDim.x) {
+        const int64_t r = u / A.heads;
+        const uint32_t drk = tkey(A, r, h);
+        f4v s[TT][TT], dp[TT][TT];   // [jt][it]: Sᵀ -> P -> P' (dropped P), dPᵀ -> dSᵀ
+        float lse_i[TT];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) lse_i[t] = lsev[t];
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it) {
+                s[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+                dp[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int it = 0; it < TT; ++it) {
+                        s[jt][it] = mfma4(kv[jt][dt][e], qv[it][dt][e], s[jt][it]);
+                        dp[jt][it] = mfma4(vv[jt][dt][e], dov[it][dt][e], dp[jt][it]);
+                    }
+        wave_sync();   // the previous unit's reads of Kt / Qt / Ot / X are done
+        v4_stage_t<TT, DT, LD>(Kt, kv, c, g);
+        v4_stage_t<TT, DT, LD>(Qt, qv, c, g);
+        v4_stage_t<TT, DT, LD>(Ot, dov, c, g);
+        if (u + gridDim.x < units) load(u + gridDim.x);   // next unit's rows in flight during this one
+        // P = exp(S - lse); dP·m (m = drop_scale); delta_i = Σ_j P·dP·m (= Σ_c dO∘O, so O is not read);
+        // dS = P·(dP·m - delta); P' = P·m
+        uint32_t keep = 0;   // bit (jt*TT + it)*4 + e: element kept by the dropout
+#pragma unroll
+        for (int it = 0; it < TT; ++it) {
+            const int i = it * 16 + c;
+            float dl = 0.f;
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int j = jt * 16 + 4 * g + e;
+                    const float sc = v4_score(A, bst[jt][it][e], r, h, i, j, s[jt][it][e]);
+                    const float p = (sc == -INFINITY) ? 0.f : __expf(sc - lse_i[it]);
+                    const float m = drop_scale(A, drk, i, j);
+                    keep |= (m != 0.f ? 1u : 0u) << ((jt * TT + it) * 4 + e);
+                    s[jt][it][e] = p;
+                    dp[jt][it][e] *= m;
+                    dl = fmaf(p, dp[jt][it][e], dl);
+                }
+            dl += __shfl_xor(dl, 16, WAVE);
+            dl += __shfl_xor(dl, 32, WAVE);
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int j = jt * 16 + 4 * g + e;
+                    const float p = s[jt][it][e];
+                    const float dsv = p * (dp[jt][it][e] - dl);
+                    dp[jt][it][e] = dsv;
+                    s[jt][it][e] = ((keep >> ((jt * TT + it) * 4 + e)) & 1u) ? p * msc : 0.f;
+                    if (A.dbias_dense && i < T && j < T)
+                        A.dbias_dense[((r * A.heads + h) * T + i) * (int64_t)T + j] = dsv;
+                }
+        }
+        if (A.part) {
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int it = 0; it < TT; ++it) gsum[jt][it] += dp[jt][it];
+        }
+        // dSᵀ -> X[j][i]
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g + e) * LD + it * 16 + c] = dp[jt][it][e];
+        wave_sync();
+        // dQᵀ = Kᵀ·dSᵀ: A = K[jt*16+4g+e][dt*16+c] (Kt), B = dSᵀ accumulators
+        {
+            f4v acc[DT][TT];
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+                for (int it = 0; it < TT; ++it) acc[dt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int dt = 0; dt < DT; ++dt) {
+                    const f4v ka = lds4(Kt + (dt * 16 + c) * LD + jt * 16 + 4 * g);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int it = 0; it < TT; ++it) acc[dt][it] = mfma4(ka[e], dp[jt][it][e], acc[dt][it]);
+                }
+#pragma unroll
+            for (int it = 0; it < TT; ++it) {
+                const int i = it * 16 + c;
+                if (i >= T) continue;
+#pragma unroll
+                for (int dt = 0; dt < DT; ++dt)
+                    st4v<S>(A.dq, r * A.d_row + (int64_t)i * A.d_t + h * d + dt * 16 + 4 * g, acc[dt][it],
+                            A.inv_sqrt_d);
+            }
+        }
+        // dKᵀ = Qᵀ·dS (A = Qt, B = X), then dVᵀ = dOᵀ·P' (A = Ot, B = X after P' replaces dS)
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+            if (pass == 1) {
+                wave_sync();   // dK's reads of X are done
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int it = 0; it < TT; ++it)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g + e) * LD + it * 16 + c] = s[jt][it][e];
+                wave_sync();
+            }
+            const float* At = pass == 0 ? Qt : Ot;
+            f4v acc[DT][TT];
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt) acc[dt][jt] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int it = 0; it < TT; ++it) {
+                f4v xa[DT], xb[TT];
+#pragma unroll
+                for (int dt = 0; dt < DT; ++dt) xa[dt] = lds4(At + (dt * 16 + c) * LD + it * 16 + 4 * g);
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt) xb[jt] = lds4(X + (jt * 16 + c) * LD + it * 16 + 4 * g);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                        for (int dt = 0; dt < DT; ++dt) acc[dt][jt] = mfma4(xa[dt][e], xb[jt][e], acc[dt][jt]);
+            }
+            float* dst = pass == 0 ? A.dk : A.dv;
+            const float sc = pass == 0 ? A.inv_sqrt_d : 1.f;
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt) {
+                const int j = jt * 16 + c;
+                if (j >= T) continue;
+#pragma unroll
+                for (int dt = 0; dt < DT; ++dt)
+                    st4v<S>(dst, r * A.d_row + (int64_t)j * A.d_t + h * d + dt * 16 + 4 * g, acc[dt][jt], sc);
+            }
+        }
+    }
+    if (A.part) {
+        // diagonal sums (t = i - j + T - 1) of the summed dS tile in j order; partial row
+        // blockIdx / heads holds head h's columns: part[row][h][t]
+        wave_sync();   // the last unit's reads of X are done
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g + e) * LD + it * 16 + c] = gsum[jt][it][e];
+        wave_sync();
+        float* prow = A.part + (int64_t)(blockIdx.x / A.heads) * A.heads * NB + (int64_t)h * NB;
+        for (int t = lane; t < NB; t += WAVE) {
+            const int off = t - (T - 1);
+            const int j0 = off < 0 ? -off : 0, j1 = off < 0 ? T : T - off;
+            float a = 0.f;
+            for (int j = j0; j < j1; ++j) a += X[j * LD + j + off];
+            prow[t] = a;
+        }
+    }
+}
+
+// T <= 32 (TT <= 2); at TT = 4 the backward needs > 256 VGPRs (spills) and T in (32, 128] keeps v3
+int v4_tiles(int T) { return T <= 16 ? 1 : T <= 32 ? 2 : 0; }
+
+#ifndef TAGAN_TATTN_V4
+#define TAGAN_TATTN_V4 1
+#endif
+bool v4_enabled() {   // TAGAN_TATTN_V4=0 selects the v3 kernels (A/B runs, v3-vs-v4 parity test)
+    const char* e = getenv("TAGAN_TATTN_V4");
+    return (e && e[0] == '0') ? false : TAGAN_TATTN_V4 != 0;
+}
+bool v4_ok(int T, int d) { return v4_enabled() && v4_tiles(T) != 0 && (d == 16 || d == 32); }
+
+// waves: G partial rows x heads (G <= grid_rows(rows), the bias-gradient workspace rows)
+int64_t v4_groups(int64_t rows) { return std::min<int64_t>(rows, 1024); }
+
 int v3_lanes(int T) { return T <= 16 ? 16 : T <= 32 ? 32 : T <= 128 ? 64 : 0; }
 int v3_wph(int T) { return T > 64 ? 2 : 1; }
 
@@ -951,8 +1382,20 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     const float* vf = (const float*)v;
     const bool al4 = s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0;
     const bool bf = dtype == TAGAN_BF16;
-    TAGAN_REQUIRE(!bf || (al4 && !attn && v3_ok(T, head_dim)), TAGAN_ERR_UNSUPPORTED,
+    TAGAN_REQUIRE(!bf || (al4 && !attn && (v3_ok(T, head_dim) || v4_ok(T, head_dim))), TAGAN_ERR_UNSUPPORTED,
                   "temporal_attn_fwd: bf16 storage needs the v3 kernels (T <= 128, head_dim 8..64, no attn output)");
+    if (al4 && !attn && v4_ok(T, head_dim)) {
+        const int TT = v4_tiles(T);
+        const dim3 g4((unsigned)(v4_groups(rows) * heads));
+        const size_t lds = v4_fwd_lds(TT, head_dim / 16);
+#define TAGAN_V4F(TTT, DDT) (bf ? k_tattn_fwd_v4<TTT, DDT, bf16s> : k_tattn_fwd_v4<TTT, DDT, float>)<<<g4, WAVE, lds, s>>>(A, qf, kf, vf)
+#define TAGAN_V4F_D(TTT) if (head_dim == 16) { TAGAN_V4F(TTT, 1); } else { TAGAN_V4F(TTT, 2); }
+        if (TT == 1) { TAGAN_V4F_D(1) } else { TAGAN_V4F_D(2) }
+#undef TAGAN_V4F_D
+#undef TAGAN_V4F
+        TAGAN_CHECK_LAUNCH("temporal_attn_fwd_v4");
+        return TAGAN_OK;
+    }
     if (al4 && !attn && v3_ok(T, head_dim)) {
         const int LG = v3_lanes(T), HPW = WAVE / LG, n_hg = (heads + HPW - 1) / HPW, WPH = v3_wph(T);
         const dim3 g3((unsigned)(grid_rows(rows) * n_hg));
@@ -1043,8 +1486,26 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     const bool al4 = s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0 && do_t % 4 == 0 &&
                      do_row % 4 == 0 && d_t % 4 == 0 && d_row % 4 == 0;
     const bool bf = dtype == TAGAN_BF16;
-    TAGAN_REQUIRE(!bf || (al4 && v3_ok(T, head_dim)), TAGAN_ERR_UNSUPPORTED,
+    TAGAN_REQUIRE(!bf || (al4 && (v3_ok(T, head_dim) || v4_ok(T, head_dim))), TAGAN_ERR_UNSUPPORTED,
                   "temporal_attn_bwd: bf16 storage needs the v3 kernels (T <= 128, head_dim 8..64)");
+    if (al4 && v4_ok(T, head_dim)) {
+        // grid = nblk partial rows x heads; block b keeps head b % heads
+        const int TT = v4_tiles(T);
+        const dim3 g4((unsigned)(nblk * heads));
+        const size_t lds = v4_bwd_lds(TT, head_dim / 16);
+#define TAGAN_V4B(TTT, DDT) (bf ? k_tattn_bwd_v4<TTT, DDT, bf16s> : k_tattn_bwd_v4<TTT, DDT, float>)<<<g4, WAVE, lds, s>>>(A, qf, kf, vf, df, lse)
+#define TAGAN_V4B_D(TTT) if (head_dim == 16) { TAGAN_V4B(TTT, 1); } else { TAGAN_V4B(TTT, 2); }
+        if (TT == 1) { TAGAN_V4B_D(1) } else { TAGAN_V4B_D(2) }
+#undef TAGAN_V4B_D
+#undef TAGAN_V4B
+        TAGAN_CHECK_LAUNCH("temporal_attn_bwd_v4");
+        if (dbias_table) {
+            const int n = heads * (2 * T - 1);
+            launch_colsum(A.part, nblk, n, dbias_table, nullptr, n, s);
+            TAGAN_CHECK_LAUNCH("temporal_attn_bwd_sum");
+        }
+        return TAGAN_OK;
+    }
     if (al4 && v3_ok(T, head_dim)) {
         // grid = nblk partial rows x n_hg head groups; block b keeps head group b % n_hg
         const int LG = v3_lanes(T), HPW = WAVE / LG, n_hg = (heads + HPW - 1) / HPW, WPH = v3_wph(T);

@@ -34,6 +34,8 @@ def _layer(H, heads, causal, dev, seed):
 
 
 @pytest.mark.parametrize("T,H,heads,causal", [
+    (1, 64, 4, False), (10, 64, 4, False), (16, 128, 4, False), (20, 64, 4, True), (32, 128, 8, False),
+    (32, 128, 4, True),                                  # matrix-core (v4) range: T <= 32, d in {16, 32}
     (8, 64, 4, False), (33, 128, 8, False), (64, 128, 8, True), (65, 256, 16, False),
     (100, 128, 8, False), (128, 256, 16, False), (128, 128, 4, True),
 ])
