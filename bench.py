@@ -44,6 +44,11 @@ def parse():
                          "kernels, fp32 math (BASELINE's C2 dtype)")
     ap.add_argument("--no-alt-precision", action="store_true",
                     help="skip the extra bf16-activation measurement reported as alt_precision")
+    ap.add_argument("--no-tuned-gemms", action="store_true",
+                    help="library-default GEMM solutions instead of the shipped TunableOp table (gemm_tuning.py)")
+    ap.add_argument("--tune-gemms", action="store_true",
+                    help="time every GEMM solution of the shapes missing from the table; write the table at exit")
+    ap.add_argument("--gemm-table", default=None, help="TunableOp table path (default: the shipped one)")
     ap.add_argument("--shard", action="store_true",
                     help="one sequence sharded by snapshot over all ranks (strong scaling; C5 mode) instead of "
                          "one sequence per rank (data parallel, weak scaling)")
@@ -124,7 +129,10 @@ def roofline(model, seq, cfg, reps=20):
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "algorithmic_bytes": int(bf + bb), "edges": E, "nodes": N,
-            "ms_fwd": round(tf * 1e3, 4), "ms_bwd": round(tb * 1e3, 4)}
+            "ms_fwd": round(tf * 1e3, 4), "ms_bwd": round(tb * 1e3, 4),
+            "note": "achieved = algorithmic bytes / kernel time; at C2 the L2 and Infinity Cache serve part of "
+                    "the gathered K|V rows (traffic = PMC HBM bytes), so achieved can pass the HBM peak; C4 is "
+                    "the cache-cold case (DESIGN.md section 4)"}
 
 
 def breakdown(model, seq, fwd, bwd, opt, cfg, reps=5):
@@ -198,6 +206,8 @@ def main():
     import tagan_amd
     from tagan_amd import TAGAN, synthetic
     from tagan_amd.distributed import GradBucket, broadcast_parameters
+    from tagan_amd.gemm_tuning import use_tuned_gemms
+    gemm_table = None if args.no_tuned_gemms else use_tuned_gemms(args.gemm_table, tune=args.tune_gemms)
     os.environ["TAGAN_BENCH_CONFIG"] = args.config
     cfg = synthetic.config_for(args.config)
     N, E, T, H, heads = synthetic.CONFIGS[args.config][:5]
@@ -286,6 +296,8 @@ def main():
                    "parallelism": ("snapshot-shard%d" % world) if args.shard else ("dp%d" % world)},
     }
     rec["config"]["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
+    rec["config"]["gemms"] = ("hipBLASLt/rocBLAS solutions from the TunableOp table %s" % os.path.basename(gemm_table)
+                              if gemm_table else "library-default heuristic")
     rec["breakdown"] = breakdown(model, seq, fwd, bwd, opt, cfg)
     if args.precision == "fp32" and not args.no_alt_precision:
         # the same step with bf16 activations between kernels (BASELINE's C2 dtype), fp32 math inside

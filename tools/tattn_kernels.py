@@ -5,7 +5,7 @@
 Layout as in the model: Q|K|V of the time-major [T, N, 3H] projection (row stride 3H,
 step stride N*3H), the folded [heads, 2T-1] bias table, bias-table gradient on.
 Algorithmic bytes: fwd reads Q,K,V and writes O (+ LSE); bwd reads Q,K,V,O,dO (+ LSE)
-and writes dQ,dK,dV.  TAGAN_LIB=<path> selects an alternative build.
+and writes dQ,dK,dV (the matrix-core v4 path does not read O).  TAGAN_LIB=<path> selects an alternative build.
 """
 import argparse
 import ctypes
@@ -78,7 +78,8 @@ def main():
     tf, tb = tf / a.reps, tb / a.reps
     unit = N * T * H * 4
     bf = 4 * unit + N * heads * T * 4
-    bb = 8 * unit + N * heads * T * 4
+    v4 = os.environ.get("TAGAN_TATTN_V4", "1") != "0" and T <= 32 and d in (16, 32)
+    bb = (7 if v4 else 8) * unit + N * heads * T * 4   # v4 takes delta from P·dP and never reads O
     chk = [float(out.double().abs().sum()), float(dqkv.double().abs().sum()), float(dtable.double().abs().sum())]
     print(json.dumps({"lib": os.environ.get("TAGAN_LIB", "default"), "config": a.config, "rows": N, "T": T,
                       "heads": heads, "d": d, "p": a.p, "ms_fwd": round(tf, 4), "ms_bwd": round(tb, 4),
