@@ -884,6 +884,27 @@ __global__ void __launch_bounds__(V3_BLK * WPH) k_tattn_bwd_v3(TArgs A, const fl
 // in LDS once.  MFMA work per unit: 8·TT²·DT instructions forward, 20·TT²·DT backward.
 typedef float f4v __attribute__((ext_vector_type(4)));
 
+// Build-time knobs (A/B builds, tools/runs/build_v4_variants.sh + v4_variants.sh).  Measured at C2 / C4
+// (fwd, bwd ms): register prefetch of the next row (PREFETCH=1, 2 waves/SIMD in the backward) vs
+// loads at the row's start with the backward held to 3 waves/SIMD (PREFETCH=0, WPE_B=3) are within
+// run-to-run noise (+-3 %); the default is the lighter one.  NOHOIST re-derives the lane indices per
+// row (no hoisted per-element constants); SPLIT prefetches only Q, K, LSE in the backward.
+#ifndef TAGAN_V4_PREFETCH
+#define TAGAN_V4_PREFETCH 0
+#endif
+#ifndef TAGAN_V4_WPE_F
+#define TAGAN_V4_WPE_F 1
+#endif
+#ifndef TAGAN_V4_NOHOIST
+#define TAGAN_V4_NOHOIST 1
+#endif
+#ifndef TAGAN_V4_SPLIT
+#define TAGAN_V4_SPLIT 0
+#endif
+#ifndef TAGAN_V4_WPE_B
+#define TAGAN_V4_WPE_B 3
+#endif
+
 __device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -957,22 +978,41 @@ __device__ __forceinline__ void v4_stage_t(float* Xt, const f4v (&x)[TT][DT], in
 
 __device__ __forceinline__ f4v lds4(const float* p) { return *(const f4v*)p; }
 
+// Wave -> (row group rg, head h); the wave runs rows rg, rg + G, ... (G = gridDim.x / heads) of head h.
+// Consecutive workgroups go to different XCDs (b % 8), so the heads of one node row go to
+// workgroups b, b+8, b+16, ... -- ONE XCD -- and a row's Q|K|V|dO lines (a 128-B line holds the
+// 64-B slices of two heads at d = 16) are fetched into one L2 once instead of into several.
+// Needs gridDim.x % (8 * heads) == 0 (the host grid guarantees it when rows >= 8), else the plain map.
+__device__ __forceinline__ void v4_wave_map(int heads, int& h, int64_t& rg) {
+    const int b = blockIdx.x, nb = gridDim.x;
+    if (nb % (8 * heads) == 0) {
+        const int y = b >> 3;
+        h = y % heads;
+        rg = (int64_t)(y / heads) * 8 + (b & 7);
+    } else {
+        h = b % heads;
+        rg = b / heads;
+    }
+}
+
 template <int TT, int DT, typename S>
-__global__ void __launch_bounds__(WAVE) k_tattn_fwd_v4(TArgs A, const float* __restrict__ q,
+__global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_F) k_tattn_fwd_v4(TArgs A, const float* __restrict__ q,
                                                        const float* __restrict__ k,
                                                        const float* __restrict__ v) {
     constexpr int TP = 16 * TT, LT = v4_ld(TP);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int T = A.T, d = A.d;
-    const int lane = threadIdx.x, c = lane & 15, g = lane >> 4;
-    const int h = (int)(blockIdx.x % A.heads);
+    const int lane = threadIdx.x, c0 = lane & 15, g0 = lane >> 4;
+    int h;
+    int64_t rg;
+    v4_wave_map(A.heads, h, rg);
+    const int64_t G = gridDim.x / A.heads;
     float* Vt = sm;    // [16*DT][LT]
     float bst[TT][TT][4];
-    v4_static_bias<TT>(A, h, c, g, bst);
-    const int64_t units = A.rows * A.heads;
+    v4_static_bias<TT>(A, h, c0, g0, bst);
     f4v qv[TT][DT], kv[TT][DT], vv[TT][DT];
-    auto load = [&](int64_t uu) {
-        const int64_t hb = (uu / A.heads) * A.s_row + (int64_t)h * d;
+    auto load = [&](int64_t rr, int c, int g) {
+        const int64_t hb = rr * A.s_row + (int64_t)h * d;
 #pragma unroll
         for (int t = 0; t < TT; ++t) {
             const int i = t * 16 + c;
@@ -985,10 +1025,14 @@ __global__ void __launch_bounds__(WAVE) k_tattn_fwd_v4(TArgs A, const float* __r
             }
         }
     };
-    int64_t u = blockIdx.x;
-    if (u < units) load(u);
-    for (; u < units; u += gridDim.x) {
-        const int64_t r = u / A.heads;
+    if (TAGAN_V4_PREFETCH && rg < A.rows) load(rg, c0, g0);
+    for (int64_t r = rg; r < A.rows; r += G) {
+        // The lane indices are re-derived per row behind an empty asm: otherwise the compiler hoists
+        // every per-element constant built from them (mask / dropout counters, store offsets) out of
+        // the row loop into dozens of live registers, and occupancy drops.
+        int c = c0, g = g0;
+        if (TAGAN_V4_NOHOIST) asm volatile("" : "+v"(c), "+v"(g));
+        if (!TAGAN_V4_PREFETCH) load(r, c, g);
         f4v s[TT][TT];   // [jt][it]: Sᵀ tiles
 #pragma unroll
         for (int jt = 0; jt < TT; ++jt)
@@ -1004,7 +1048,7 @@ __global__ void __launch_bounds__(WAVE) k_tattn_fwd_v4(TArgs A, const float* __r
                     for (int it = 0; it < TT; ++it) s[jt][it] = mfma4(kv[jt][dt][e], qv[it][dt][e], s[jt][it]);
         wave_sync();   // the previous unit's reads of Vt are done
         v4_stage_t<TT, DT, LT>(Vt, vv, c, g);
-        if (u + gridDim.x < units) load(u + gridDim.x);   // next unit's rows in flight during this one
+        if (TAGAN_V4_PREFETCH && r + G < A.rows) load(r + G, c, g);   // next unit's rows in flight during this one
         wave_sync();
         const uint32_t drk = tkey(A, r, h);
         float inv_l[TT];
@@ -1064,7 +1108,7 @@ __global__ void __launch_bounds__(WAVE) k_tattn_fwd_v4(TArgs A, const float* __r
 }
 
 template <int TT, int DT, typename S>
-__global__ void __launch_bounds__(WAVE) k_tattn_bwd_v4(TArgs A, const float* __restrict__ q,
+__global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, const float* __restrict__ q,
                                                        const float* __restrict__ k,
                                                        const float* __restrict__ v,
                                                        const float* __restrict__ dout,
@@ -1072,14 +1116,17 @@ __global__ void __launch_bounds__(WAVE) k_tattn_bwd_v4(TArgs A, const float* __r
     constexpr int TP = 16 * TT, LD = v4_ld(TP), DP = 16 * DT;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int T = A.T, NB = 2 * T - 1, d = A.d;
-    const int lane = threadIdx.x, c = lane & 15, g = lane >> 4;
-    const int h = (int)(blockIdx.x % A.heads);
+    const int lane = threadIdx.x, c0 = lane & 15, g0 = lane >> 4;
+    int h;
+    int64_t rg;
+    v4_wave_map(A.heads, h, rg);
+    const int64_t G = gridDim.x / A.heads;
     float* X = sm;               // [TP][LD] transpose tile X[j][i] (dS, then P')
     float* Kt = X + TP * LD;     // [DP][LD] K transposed
     float* Qt = Kt + DP * LD;    // [DP][LD] Q transposed
     float* Ot = Qt + DP * LD;    // [DP][LD] dO transposed
     float bst[TT][TT][4];
-    v4_static_bias<TT>(A, h, c, g, bst);
+    v4_static_bias<TT>(A, h, c0, g0, bst);
     const float msc = A.p_drop > 0.f ? A.inv_keep : 1.f;   // drop_scale of a kept element
     // Σ of dSᵀ over this wave's units, in unit order: the bias-table gradient before its diagonal
     // sums, which run once at the end (fixed order: bitwise reproducible)
@@ -1088,11 +1135,10 @@ __global__ void __launch_bounds__(WAVE) k_tattn_bwd_v4(TArgs A, const float* __r
     for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
         for (int it = 0; it < TT; ++it) gsum[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
-    const int64_t units = A.rows * A.heads;
     f4v qv[TT][DT], kv[TT][DT], vv[TT][DT], dov[TT][DT];
     float lsev[TT];
-    auto load = [&](int64_t uu) {
-        const int64_t rr = uu / A.heads;
+    // The next row's Q, K, LSE (and, unless TAGAN_V4_SPLIT, V and dO) are prefetched during this one.
+    auto load_qk = [&](int64_t rr, int c, int g) {
         const int64_t hb = rr * A.s_row + (int64_t)h * d;
 #pragma unroll
         for (int t = 0; t < TT; ++t) {
@@ -1102,17 +1148,35 @@ __global__ void __launch_bounds__(WAVE) k_tattn_bwd_v4(TArgs A, const float* __r
                 const int64_t off = hb + (int64_t)i * A.s_t + dt * 16 + 4 * g;
                 qv[t][dt] = ld4v<S>(q, off, i < T);
                 kv[t][dt] = ld4v<S>(k, off, i < T);
-                vv[t][dt] = ld4v<S>(v, off, i < T);
-                dov[t][dt] = ld4v<S>(dout, rr * A.do_row + (int64_t)h * d + (int64_t)i * A.do_t + dt * 16 + 4 * g,
-                                     i < T);
             }
             lsev[t] = (i < T) ? lse[(rr * A.heads + h) * T + i] : 0.f;
         }
     };
-    int64_t u = blockIdx.x;
-    if (u < units) load(u);
-    for (; u < units; u += gridDim.x) {
-        const int64_t r = u / A.heads;
+    auto load_vd = [&](int64_t rr, int c, int g) {
+        const int64_t hb = rr * A.s_row + (int64_t)h * d;
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            const int i = t * 16 + c;
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                vv[t][dt] = ld4v<S>(v, hb + (int64_t)i * A.s_t + dt * 16 + 4 * g, i < T);
+                dov[t][dt] = ld4v<S>(dout, rr * A.do_row + (int64_t)h * d + (int64_t)i * A.do_t + dt * 16 + 4 * g,
+                                     i < T);
+            }
+        }
+    };
+    if (TAGAN_V4_PREFETCH && rg < A.rows) {
+        load_qk(rg, c0, g0);
+        if (!TAGAN_V4_SPLIT) load_vd(rg, c0, g0);
+    }
+    for (int64_t r = rg; r < A.rows; r += G) {
+        // The lane indices are re-derived per row behind an empty asm: otherwise the compiler hoists
+        // every per-element constant built from them (mask / dropout counters, store offsets) out of
+        // the row loop into dozens of live registers, and occupancy drops.
+        int c = c0, g = g0;
+        if (TAGAN_V4_NOHOIST) asm volatile("" : "+v"(c), "+v"(g));
+        if (!TAGAN_V4_PREFETCH) load_qk(r, c, g);
+        if (!TAGAN_V4_PREFETCH || TAGAN_V4_SPLIT) load_vd(r, c, g);
         const uint32_t drk = tkey(A, r, h);
         f4v s[TT][TT], dp[TT][TT];   // [jt][it]: Sᵀ -> P -> P' (dropped P), dPᵀ -> dSᵀ
         float lse_i[TT];
@@ -1132,15 +1196,23 @@ __global__ void __launch_bounds__(WAVE) k_tattn_bwd_v4(TArgs A, const float* __r
 #pragma unroll
                 for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
-                    for (int it = 0; it < TT; ++it) {
-                        s[jt][it] = mfma4(kv[jt][dt][e], qv[it][dt][e], s[jt][it]);
-                        dp[jt][it] = mfma4(vv[jt][dt][e], dov[it][dt][e], dp[jt][it]);
-                    }
+                    for (int it = 0; it < TT; ++it) s[jt][it] = mfma4(kv[jt][dt][e], qv[it][dt][e], s[jt][it]);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int it = 0; it < TT; ++it) dp[jt][it] = mfma4(vv[jt][dt][e], dov[it][dt][e], dp[jt][it]);
         wave_sync();   // the previous unit's reads of Kt / Qt / Ot / X are done
         v4_stage_t<TT, DT, LD>(Kt, kv, c, g);
         v4_stage_t<TT, DT, LD>(Qt, qv, c, g);
         v4_stage_t<TT, DT, LD>(Ot, dov, c, g);
-        if (u + gridDim.x < units) load(u + gridDim.x);   // next unit's rows in flight during this one
+        if (TAGAN_V4_PREFETCH && r + G < A.rows) {
+            load_qk(r + G, c, g);
+            if (!TAGAN_V4_SPLIT) load_vd(r + G, c, g);
+        }   // next unit's rows in flight during this one
         // P = exp(S - lse); dP·m (m = drop_scale); delta_i = Σ_j P·dP·m (= Σ_c dO∘O, so O is not read);
         // dS = P·(dP·m - delta); P' = P·m
         uint32_t keep = 0;   // bit (jt*TT + it)*4 + e: element kept by the dropout
@@ -1264,16 +1336,16 @@ __global__ void __launch_bounds__(WAVE) k_tattn_bwd_v4(TArgs A, const float* __r
     }
     if (A.part) {
         // diagonal sums (t = i - j + T - 1) of the summed dS tile in j order; partial row
-        // blockIdx / heads holds head h's columns: part[row][h][t]
+        // rg holds head h's columns: part[rg][h][t]
         wave_sync();   // the last unit's reads of X are done
 #pragma unroll
         for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
             for (int it = 0; it < TT; ++it)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g + e) * LD + it * 16 + c] = gsum[jt][it][e];
+                for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g0 + e) * LD + it * 16 + c0] = gsum[jt][it][e];
         wave_sync();
-        float* prow = A.part + (int64_t)(blockIdx.x / A.heads) * A.heads * NB + (int64_t)h * NB;
+        float* prow = A.part + rg * A.heads * NB + (int64_t)h * NB;
         for (int t = lane; t < NB; t += WAVE) {
             const int off = t - (T - 1);
             const int j0 = off < 0 ? -off : 0, j1 = off < 0 ? T : T - off;
@@ -1297,7 +1369,8 @@ bool v4_enabled() {   // TAGAN_TATTN_V4=0 selects the v3 kernels (A/B runs, v3-v
 bool v4_ok(int T, int d) { return v4_enabled() && v4_tiles(T) != 0 && (d == 16 || d == 32); }
 
 // waves: G partial rows x heads (G <= grid_rows(rows), the bias-gradient workspace rows)
-int64_t v4_groups(int64_t rows) { return std::min<int64_t>(rows, 1024); }
+// (a multiple of 8 from 8 rows up, for the XCD-aware wave map)
+int64_t v4_groups(int64_t rows) { return rows >= 8 ? std::min<int64_t>(rows, 1024) & ~(int64_t)7 : rows; }
 
 int v3_lanes(int T) { return T <= 16 ? 16 : T <= 32 ? 32 : T <= 128 ? 64 : 0; }
 int v3_wph(int T) { return T > 64 ? 2 : 1; }
@@ -1489,9 +1562,10 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     TAGAN_REQUIRE(!bf || (al4 && (v3_ok(T, head_dim) || v4_ok(T, head_dim))), TAGAN_ERR_UNSUPPORTED,
                   "temporal_attn_bwd: bf16 storage needs the v3 kernels (T <= 128, head_dim 8..64)");
     if (al4 && v4_ok(T, head_dim)) {
-        // grid = nblk partial rows x heads; block b keeps head b % heads
+        // grid = G4 partial rows x heads; each block keeps one head (v4_wave_map)
         const int TT = v4_tiles(T);
-        const dim3 g4((unsigned)(nblk * heads));
+        const int64_t G4 = v4_groups(rows);   // <= nblk: the workspace rows
+        const dim3 g4((unsigned)(G4 * heads));
         const size_t lds = v4_bwd_lds(TT, head_dim / 16);
 #define TAGAN_V4B(TTT, DDT) (bf ? k_tattn_bwd_v4<TTT, DDT, bf16s> : k_tattn_bwd_v4<TTT, DDT, float>)<<<g4, WAVE, lds, s>>>(A, qf, kf, vf, df, lse)
 #define TAGAN_V4B_D(TTT) if (head_dim == 16) { TAGAN_V4B(TTT, 1); } else { TAGAN_V4B(TTT, 2); }
@@ -1501,7 +1575,7 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
         TAGAN_CHECK_LAUNCH("temporal_attn_bwd_v4");
         if (dbias_table) {
             const int n = heads * (2 * T - 1);
-            launch_colsum(A.part, nblk, n, dbias_table, nullptr, n, s);
+            launch_colsum(A.part, (int)G4, n, dbias_table, nullptr, n, s);
             TAGAN_CHECK_LAUNCH("temporal_attn_bwd_sum");
         }
         return TAGAN_OK;
