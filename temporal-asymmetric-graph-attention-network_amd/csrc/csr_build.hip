@@ -1,9 +1,9 @@
 // Snapshot CSR/CSC builder: the sparse form of graph_attention.py:96-105
 //   adj = zeros(N,N); adj[edge_index[0], edge_index[1]] = 1; adj += eye(N)
 // for a block-diagonal batch of snapshots.  Integer/byte work: HBM-bound,
-// no MFMA.  Keys (global src << LB | local dst), LB = bits of the largest
-// snapshot, are radix-sorted with rocPRIM over only LB + bits(N) bits (33 at
-// C2 instead of 64), de-duplicated, scattered into CSR.  The CSC (with CSR edge
+// no MFMA.  Keys global_src * NL + local_dst (NL = the largest snapshot) are
+// radix-sorted with rocPRIM over only the bits of N * NL -- 32-bit keys when that
+// fits (32 bits at C2 instead of a 33-bit key in 64), de-duplicated, scattered into CSR.  The CSC (with CSR edge
 // ids) is a STABLE 32-bit key-value sort of the CSR entries by dst alone: the CSR
 // order is by src, so stability keeps src ascending within each column.
 #include <cstring>
@@ -32,14 +32,19 @@ __device__ __forceinline__ int64_t node_base(const int64_t* __restrict__ node_pt
     return node_ptr[find_graph(node_ptr, G, n)];
 }
 
+// Sort key of the pair (global src s, local dst d): s * NL + d with NL = the largest snapshot's node
+// count, so ascending keys are the CSR order (src-major, dst-minor); the key N * NL marks a dropped
+// (out-of-range) edge.  K = uint32_t whenever N * NL < 2^32 (C1, C2: 320k x 10k = 3.2e9): half the key
+// bytes of the 64-bit form and one radix pass fewer.
+template <typename K>
 __global__ void __launch_bounds__(BLK) k_make_keys(const int64_t* __restrict__ ei, int64_t ld_ei, int64_t E,
                                                    const int64_t* __restrict__ edge_ptr,
                                                    const int64_t* __restrict__ node_ptr, int G,
-                                                   int64_t N, int LB, uint64_t* __restrict__ keys,
+                                                   int64_t N, int64_t NL, K* __restrict__ keys,
                                                    int32_t* __restrict__ err) {
-    const uint64_t sentinel = (uint64_t)N << LB;
+    const K sentinel = (K)N * (K)NL;
     for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < E + N; p += (int64_t)gridDim.x * BLK) {
-        uint64_t key;
+        K key;
         if (p < E) {
             const int g = find_graph(edge_ptr, G, p);
             const int64_t base = node_ptr[g];
@@ -51,35 +56,36 @@ __global__ void __launch_bounds__(BLK) k_make_keys(const int64_t* __restrict__ e
                 atomicOr(err, 1);
                 key = sentinel;
             } else {
-                key = ((uint64_t)(base + s) << LB) | (uint64_t)d;
+                key = (K)(base + s) * (K)NL + (K)d;
             }
         } else {
             const int64_t i = p - E;                // self-loop of global node i (the "+ eye")
-            key = ((uint64_t)i << LB) | (uint64_t)(i - node_base(node_ptr, G, i));
+            key = (K)i * (K)NL + (K)(i - node_base(node_ptr, G, i));
         }
         keys[p] = key;
     }
 }
 
-__global__ void __launch_bounds__(BLK) k_unique_flags(const uint64_t* __restrict__ keys, int64_t M, int64_t N,
-                                                      int LB, int32_t* __restrict__ flags) {
-    const uint64_t sentinel = (uint64_t)N << LB;
+template <typename K>
+__global__ void __launch_bounds__(BLK) k_unique_flags(const K* __restrict__ keys, int64_t M, int64_t N, int64_t NL,
+                                                      int32_t* __restrict__ flags) {
+    const K sentinel = (K)N * (K)NL;
     for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
-        const uint64_t k = keys[p];
+        const K k = keys[p];
         flags[p] = (k < sentinel && (p == 0 || keys[p - 1] != k)) ? 1 : 0;
     }
 }
 
 // Scatter unique keys into CSR; emit CSC keys (global dst) with value = CSR position and the
 // row of every CSR position (srcq) for the CSC scatter.
-__global__ void __launch_bounds__(BLK) k_scatter_csr(const uint64_t* __restrict__ keys,
-                                                     const int32_t* __restrict__ flags,
-                                                     const int32_t* __restrict__ pos, int64_t M, int64_t N, int LB,
-                                                     const int64_t* __restrict__ node_ptr, int G,
+template <typename K>
+__global__ void __launch_bounds__(BLK) k_scatter_csr(const K* __restrict__ keys, const int32_t* __restrict__ flags,
+                                                     const int32_t* __restrict__ pos, int64_t M, int64_t N,
+                                                     int64_t NL, const int64_t* __restrict__ node_ptr, int G,
                                                      int32_t* __restrict__ rowptr, int32_t* __restrict__ col,
                                                      uint32_t* __restrict__ ckeys, int32_t* __restrict__ cvals,
                                                      int32_t* __restrict__ srcq, int64_t* __restrict__ nnz_out) {
-    const uint64_t lmask = ((uint64_t)1 << LB) - 1;
+    const K nl = (K)NL;
     for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
         if (p == M - 1) {
             const int64_t nnz = (int64_t)pos[p] + flags[p];
@@ -87,12 +93,13 @@ __global__ void __launch_bounds__(BLK) k_scatter_csr(const uint64_t* __restrict_
             rowptr[N] = (int32_t)nnz;
         }
         if (!flags[p]) continue;
-        const uint64_t k = keys[p];
-        const int64_t r = (int64_t)(k >> LB);
-        const int32_t c = (int32_t)(node_base(node_ptr, G, r) + (int64_t)(k & lmask));
+        const K k = keys[p];
+        const K rk = k / nl;
+        const int64_t r = (int64_t)rk;
+        const int32_t c = (int32_t)(node_base(node_ptr, G, r) + (int64_t)(k - rk * nl));
         const int32_t q = pos[p];
         col[q] = c;
-        if (p == 0 || (int64_t)(keys[p - 1] >> LB) != r) rowptr[r] = q;   // every row has its self-loop
+        if (p == 0 || keys[p - 1] / nl != rk) rowptr[r] = q;   // every row has its self-loop
         ckeys[q] = (uint32_t)c;
         cvals[q] = q;
         srcq[q] = (int32_t)r;
@@ -150,7 +157,10 @@ CsrWs plan(int64_t E, int64_t N) {
     w.pos = take(M * 4);
     const int bits = key_bits(N);
     size_t t1 = 0, t2 = 0, t3 = 0;
-    (void)rocprim::radix_sort_keys(nullptr, t1, (uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)M, 0, 32 + bits);
+    size_t t1b = 0;
+    (void)rocprim::radix_sort_keys(nullptr, t1, (uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)M, 0, 64);
+    (void)rocprim::radix_sort_keys(nullptr, t1b, (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)M, 0, 32);
+    t1 = std::max(t1, t1b);
     (void)rocprim::radix_sort_pairs(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
                               (int32_t*)nullptr, (size_t)M, 0, bits);
     (void)rocprim::exclusive_scan(nullptr, t3, (int32_t*)nullptr, (int32_t*)nullptr, 0, (size_t)M,
@@ -165,6 +175,34 @@ int grid_for(int64_t n) {
     int64_t g = (n + BLK - 1) / BLK;
     if (g > 256 * 16) g = 256 * 16;
     return (int)(g < 1 ? 1 : g);
+}
+
+// Key build, key sort, de-duplication and CSR scatter with K-wide keys; writes the unsorted CSC
+// keys/values (ckeys_a aliases the unsorted key buffer, free once the key sort is done).
+template <typename K>
+int csr_keys(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, const int64_t* edge_ptr,
+             const int64_t* node_ptr, int32_t n_graphs, int64_t n_nodes, int64_t NL, int sort_bits, char* ws,
+             const CsrWs& w, int32_t* rowptr, int32_t* col, uint32_t* ckeys_a, int32_t* cvals_a, int32_t* srcq,
+             int32_t* flags, int32_t* pos, int64_t* nnz_out, int32_t* err_out, hipStream_t s) {
+    const int64_t M = n_edges + n_nodes;
+    K* keys_a = (K*)(ws + w.keys_a);
+    K* keys_b = (K*)(ws + w.keys_b);
+    void* temp = ws + w.temp;
+    k_make_keys<K><<<grid_for(M), BLK, 0, s>>>(edge_index, ld_ei, n_edges, edge_ptr, node_ptr, n_graphs, n_nodes, NL,
+                                               keys_a, err_out);
+    TAGAN_CHECK_LAUNCH("csr_build.make_keys");
+    size_t tb = w.temp_bytes;
+    TAGAN_CHECK_HIP(rocprim::radix_sort_keys(temp, tb, keys_a, keys_b, (size_t)M, 0, sort_bits, s),
+                    "csr_build radix_sort_keys");
+    k_unique_flags<K><<<grid_for(M), BLK, 0, s>>>(keys_b, M, n_nodes, NL, flags);
+    TAGAN_CHECK_LAUNCH("csr_build.unique_flags");
+    tb = w.temp_bytes;
+    TAGAN_CHECK_HIP(rocprim::exclusive_scan(temp, tb, flags, pos, 0, (size_t)M, rocprim::plus<int32_t>(), s),
+                    "csr_build exclusive_scan");
+    k_scatter_csr<K><<<grid_for(M), BLK, 0, s>>>(keys_b, flags, pos, M, n_nodes, NL, node_ptr, n_graphs, rowptr, col,
+                                                 ckeys_a, cvals_a, srcq, nnz_out);
+    TAGAN_CHECK_LAUNCH("csr_build.scatter_csr");
+    return TAGAN_OK;
 }
 
 }  // namespace
@@ -196,8 +234,6 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
                   "tagan_csr_build: workspace %zu < %zu", workspace_bytes, w.total);
     hipStream_t s = as_stream(stream);
     char* ws = (char*)workspace;
-    uint64_t* keys_a = (uint64_t*)(ws + w.keys_a);
-    uint64_t* keys_b = (uint64_t*)(ws + w.keys_b);
     uint32_t* ckeys_b = (uint32_t*)(ws + w.ckeys_b);
     int32_t* cvals_b = (int32_t*)(ws + w.cvals_b);
     int32_t* srcq = (int32_t*)(ws + w.srcq);
@@ -207,27 +243,23 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     const int64_t M = n_edges + n_nodes;
     const int bits = key_bits(n_nodes);
     TAGAN_REQUIRE(max_graph_nodes <= n_nodes, TAGAN_ERR_ARG, "tagan_csr_build: max_graph_nodes > n_nodes");
-    const int LB = key_bits(max_graph_nodes > 0 ? max_graph_nodes : n_nodes);   // local ids 0..max-1 fit
-    const int sort_bits = LB + bits;
+    const int64_t NL = max_graph_nodes > 0 ? max_graph_nodes : n_nodes;   // local ids 0..NL-1
+    const uint64_t sentinel = (uint64_t)n_nodes * (uint64_t)NL;
+    int sort_bits = 0;
+    while (sort_bits < 64 && (sentinel >> sort_bits) != 0) ++sort_bits;   // keys 0..sentinel
 
     TAGAN_CHECK_HIP(hipMemsetAsync(err_out, 0, sizeof(int32_t), s), "csr_build memset");
-    k_make_keys<<<grid_for(M), BLK, 0, s>>>(edge_index, ld_ei, n_edges, edge_ptr, node_ptr, n_graphs, n_nodes,
-                                            LB, keys_a, err_out);
-    TAGAN_CHECK_LAUNCH("csr_build.make_keys");
-    size_t tb = w.temp_bytes;
-    TAGAN_CHECK_HIP(rocprim::radix_sort_keys(temp, tb, keys_a, keys_b, (size_t)M, 0, sort_bits, s),
-                    "csr_build radix_sort_keys");
-    k_unique_flags<<<grid_for(M), BLK, 0, s>>>(keys_b, M, n_nodes, LB, flags);
-    TAGAN_CHECK_LAUNCH("csr_build.unique_flags");
-    tb = w.temp_bytes;
-    TAGAN_CHECK_HIP(rocprim::exclusive_scan(temp, tb, flags, pos, 0, (size_t)M, rocprim::plus<int32_t>(), s),
-                    "csr_build exclusive_scan");
-    // keys_a is free now: reuse it as the unsorted CSC key buffer; cvals via csc_eid scratch? use csc_row.
-    uint32_t* ckeys_a = (uint32_t*)keys_a;
+    uint32_t* ckeys_a = (uint32_t*)(ws + w.keys_a);   // unsorted CSC keys (the key buffer is free by then)
     int32_t* cvals_a = csc_row;   // staging only; overwritten by the final CSC scatter
-    k_scatter_csr<<<grid_for(M), BLK, 0, s>>>(keys_b, flags, pos, M, n_nodes, LB, node_ptr, n_graphs, rowptr, col,
-                                              ckeys_a, cvals_a, srcq, nnz_out);
-    TAGAN_CHECK_LAUNCH("csr_build.scatter_csr");
+    const int rc = sentinel <= 0xFFFFFFFFull
+                       ? csr_keys<uint32_t>(edge_index, ld_ei, n_edges, edge_ptr, node_ptr, n_graphs, n_nodes, NL,
+                                            sort_bits, ws, w, rowptr, col, ckeys_a, cvals_a, srcq, flags, pos,
+                                            nnz_out, err_out, s)
+                       : csr_keys<uint64_t>(edge_index, ld_ei, n_edges, edge_ptr, node_ptr, n_graphs, n_nodes, NL,
+                                            sort_bits, ws, w, rowptr, col, ckeys_a, cvals_a, srcq, flags, pos,
+                                            nnz_out, err_out, s);
+    if (rc) return rc;
+    size_t tb = 0;
     k_fill_tail<<<grid_for(M), BLK, 0, s>>>(ckeys_a, cvals_a, nnz_out, M, n_nodes);
     TAGAN_CHECK_LAUNCH("csr_build.fill_tail");
     tb = w.temp_bytes;

@@ -29,19 +29,11 @@ def _load(module, sd, dev):
 
 
 # ----------------------------------------------------------------------------- CSR builder
-@pytest.mark.parametrize("seed", [0, 1, 2])
-def test_csr_build_matches_oracle(dev, seed):
+def _check_csr(dev, counts, eis):
     from tagan_amd.kernels import build_graph
-    g = torch.Generator().manual_seed(seed)
-    counts = [1, 7, 50, 3, 200]
-    eis = []
-    for n in counts:
-        E = int(torch.randint(0, 4 * n + 1, (1,), generator=g))
-        ei = torch.randint(-n, n, (2, E), generator=g)      # negatives wrap like torch indexing
-        eis.append(ei)
     graph = build_graph([e.to(dev) for e in eis], counts)
     nnz = graph.nnz_host()
-    rows, cols, off = [], [], 0
+    cols, off = [], 0
     rp_all = [0]
     for n, ei in zip(counts, eis):
         rp, c = oracle.csr_from_edge_index(ei, n)
@@ -52,16 +44,36 @@ def test_csr_build_matches_oracle(dev, seed):
     assert nnz == want_col.numel()
     assert graph.rowptr.cpu().tolist() == rp_all
     assert torch.equal(graph.col[:nnz].cpu().long(), want_col)
-    # CSC is the transpose with edge ids pointing back into the CSR
+    # CSC is the transpose with edge ids pointing back into the CSR, rows ascending in each column
     src = torch.repeat_interleave(torch.arange(off), torch.tensor(rp_all).diff())
     eid = graph.csc_eid[:nnz].cpu().long()
     crow = graph.csc_row[:nnz].cpu().long()
     assert torch.equal(src[eid], crow)
-    cptr = graph.csc_ptr.cpu().long()
-    for j in range(off):
-        seg = eid[cptr[j]:cptr[j + 1]]
-        assert torch.all(want_col[seg] == j)
-        assert torch.all(crow[cptr[j]:cptr[j + 1]].diff() > 0)
+    ccol = torch.repeat_interleave(torch.arange(off), graph.csc_ptr.cpu().long().diff())
+    assert torch.equal(want_col[eid], ccol)
+    same = ccol[1:] == ccol[:-1]
+    assert torch.all(crow.diff()[same] > 0)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_csr_build_matches_oracle(dev, seed):
+    g = torch.Generator().manual_seed(seed)
+    counts = [1, 7, 50, 3, 200]
+    eis = []
+    for n in counts:
+        E = int(torch.randint(0, 4 * n + 1, (1,), generator=g))
+        eis.append(torch.randint(-n, n, (2, E), generator=g))      # negatives wrap like torch indexing
+    _check_csr(dev, counts, eis)
+
+
+def test_csr_build_wide_keys(dev):
+    """N x (largest snapshot) >= 2^32 takes the 64-bit sort keys (a 70,000-node snapshot); the other CSR
+    tests (and C1/C2) run on 32-bit keys."""
+    g = torch.Generator().manual_seed(5)
+    counts = [70_000, 3, 5_000]
+    eis = [torch.randint(-n, n, (2, 4 * n), generator=g) for n in counts]
+    assert sum(counts) * max(counts) >= 2 ** 32
+    _check_csr(dev, counts, eis)
 
 
 def test_csr_build_rejects_out_of_range(dev):
