@@ -228,8 +228,9 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
  *   y = (s - mean) / sqrt(var + eps) * gamma + beta       (biased var, as torch)
  * dtype = storage of y (TAGAN_BF16: y feeds a bf16 GEMM); a, b, s, statistics fp32.
  * s_out (optional) keeps s for the backward pass; mean/rstd: [M].  y has row stride
- * ldy (0 = H; a wider stride leaves room for a ones column that turns the next
- * weight-gradient GEMM into weight + bias gradient).
+ * ldy (0 = H).  With ldy >= H + 4, columns H..H+3 of every y row are written as
+ * (1, 0, 0, 0): the next projection then takes its bias as an extra weight column
+ * (one GEMM over K = H + 4 without a bias epilogue).
  * Supported H: tagan_layernorm_supported(H) (32, 64, 128, 256, 512).
  * ------------------------------------------------------------------------- */
 int tagan_layernorm_supported(int32_t H);

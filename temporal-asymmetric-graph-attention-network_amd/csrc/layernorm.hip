@@ -44,6 +44,7 @@ struct LnArgs {
     float* part;   // [gridDim.x, 3H]: dgamma | dbeta | column sums of da (projection-bias gradient)
     int want_dsa;  // accumulate the column sums of da
     int64_t ldy;   // forward output row stride (>= H)
+    int ones_col;  // ldy >= H + 4: write (1, 0, 0, 0) at columns H..H+3 of y (bias folded into the next GEMM)
     // forward skip branch (model.py:258-262): y += LN_s(b) with its own gamma/beta/eps/statistics
     const float* gamma_s;
     const float* beta_s;
@@ -131,6 +132,7 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
         }
         Io<S>::st(A.y, row * A.ldy + c, o);     // y in the storage type (bf16 feeds a GEMM)
     }
+    if (A.ones_col && sl == 0) Io<S>::st(A.y, row * A.ldy + H, make_float4(1.f, 0.f, 0.f, 0.f));
     if (sl == 0) {
         A.mean[row] = mean;
         A.rstd[row] = rstd;
@@ -267,6 +269,7 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
     A.gamma = gamma; A.beta = beta; A.eps = eps; A.s_out = s_out; A.y = y; A.mean = mean; A.rstd = rstd;
     A.ldy = ldy > 0 ? ldy : H;
     TAGAN_REQUIRE(A.ldy >= H && A.ldy % 4 == 0, TAGAN_ERR_ARG, "layernorm_fwd: ldy %lld", (long long)ldy);
+    A.ones_col = A.ldy >= H + 4;
     const int64_t rpw = WAVE / lpr;
     const dim3 g((unsigned)(((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE)));
     hipStream_t s = as_stream(stream);

@@ -15,6 +15,7 @@ autograd nodes of host overhead per layer.  Here the backward is written out onc
 
 Cores: ``GeoCore`` (tagan_geo_attn_*) and ``TemporalCore`` (tagan_temporal_attn_*).
 """
+import os
 from typing import Optional
 
 import torch
@@ -227,7 +228,8 @@ def _wgrad(dy, x, bf, rows: int = 2048):
     rows = split_rows(K, rows)
     c = K // rows
     main = c * rows
-    dw = torch.bmm(dy[:main].view(c, rows, M).transpose(1, 2), x[:main].view(c, rows, N),
+    xs = x.as_strided((c, rows, N), (rows * x.stride(0), x.stride(0), 1))   # x may be a column view
+    dw = torch.bmm(dy[:main].view(c, rows, M).transpose(1, 2), xs,
                    out_dtype=torch.float32).sum(0)
     if main < K:
         dw = dw + torch.mm(dy[main:].t(), x[main:], out_dtype=torch.float32)
@@ -235,6 +237,9 @@ def _wgrad(dy, x, bf, rows: int = 2048):
 
 
 # ----------------------------------------------------------------------------- the fused block
+# TAGAN_QKV_AUG=0: QKV GEMM with the hipBLASLt bias epilogue instead of the bias-as-weight-column form (A/B)
+QKV_AUG = os.environ.get("TAGAN_QKV_AUG", "1") != "0"
+
 class AttnBlockFn(torch.autograd.Function):
     """y = LN2(dropout(out_proj(core(QKV(LN1(x))))) + x) with LayerNorm on both sides (use_layer_norm=True)."""
 
@@ -246,11 +251,21 @@ class AttnBlockFn(torch.autograd.Function):
         x2 = x.reshape(-1, H).contiguous()
         bf = _PREC != "fp32"          # bf16 GEMM operands
         act = _PREC == "bf16"         # bf16 activations between kernels
-        h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False,
-                                    y_dtype=torch.bfloat16 if act else torch.float32)
-        if bf:
-            h = _b(h)          # only the GEMMs read h: keep it in bf16
-        qkv = _addmm(b_qkv, h, w_qkv, bf, out_bf16=act)
+        if QKV_AUG and not bf:
+            # fp32: LN1 writes [h | 1 0 0 0] (row stride H + 4) and the QKV bias rides in the GEMM as a weight
+            # column -- one GEMM over K = H + 4 without the bias epilogue, ≈1 % of the C2 step faster on
+            # hipBLASLt (tools/runs/qkv_aug.sh); with bf16 operands the epilogue form is the faster one
+            h_aug = torch.empty(x2.shape[0], H + 4, device=x2.device)
+            _, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False, y=h_aug)
+            w_aug = torch.cat([w_qkv, b_qkv[:, None], w_qkv.new_zeros(w_qkv.shape[0], 3)], 1)
+            qkv = h_aug @ w_aug.t()
+            h = h_aug[:, :H]
+        else:
+            h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False,
+                                        y_dtype=torch.bfloat16 if act else torch.float32)
+            if bf:
+                h = _b(h)
+            qkv = _addmm(b_qkv, h, w_qkv, bf, out_bf16=act)
         c, saved = core.fwd(qkv, p1, p2)
         cg = _b(c) if bf else c
         o = _addmm(b_o, cg, w_o, bf)

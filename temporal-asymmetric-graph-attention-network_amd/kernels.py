@@ -342,7 +342,8 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, rows: int = 2048) -> torch.
     rows = split_rows(K, rows)
     c = K // rows
     main = c * rows
-    dw = torch.bmm(dy2[:main].view(c, rows, M).transpose(1, 2), x2[:main].view(c, rows, N)).sum(0)
+    xs = x2.as_strided((c, rows, N), (rows * x2.stride(0), x2.stride(0), 1))   # x2 may be a column view
+    dw = torch.bmm(dy2[:main].view(c, rows, M).transpose(1, 2), xs).sum(0)
     if main < K:
         dw = dw + dy2[main:].t() @ x2[main:]
     return dw
