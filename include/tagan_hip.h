@@ -224,7 +224,9 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
  * Row LayerNorm with fused residual + dropout.  Replaces the ATen chain
  * output_dropout(proj) + identity -> layer_norm2 (geometric_attention.py:586-596,
  * temporal_attention.py:1190-1200) and plain layer_norm1 (b = NULL, p_drop = 0).
- *   s = dropout(a; p_drop, seed) + b     (element (r,c): stream r, counter c)
+ *   s = dropout(a + a_bias; p_drop, seed) + b     (element (r,c): stream r, counter c)
+ * a_bias (optional, [H]) is the producing projection's bias, added here instead of in the GEMM
+ * epilogue (its gradient is dsum_a of the backward).
  *   y = (s - mean) / sqrt(var + eps) * gamma + beta       (biased var, as torch)
  * dtype = storage of y (TAGAN_BF16: y feeds a bf16 GEMM); a, b, s, statistics fp32.
  * s_out (optional) keeps s for the backward pass; mean/rstd: [M].  y has row stride
@@ -234,8 +236,8 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
  * Supported H: tagan_layernorm_supported(H) (32, 64, 128, 256, 512).
  * ------------------------------------------------------------------------- */
 int tagan_layernorm_supported(int32_t H);
-int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, const float* b,
-                            float p_drop, uint64_t seed, const float* gamma, const float* beta,
+int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, const float* a_bias,
+                            const float* b, float p_drop, uint64_t seed, const float* gamma, const float* beta,
                             float eps, float* s_out, float* y, int64_t ldy, float* mean, float* rstd,
                             void* stream);
 /* Layer 0 of the geometric stack with the skip branch of model.py:258-262 fused
@@ -243,7 +245,8 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
  * input), one pass instead of LN, LN_s and an add.  fp32 only.  mean_s/rstd_s
  * [M] are LN_s's statistics, for its backward (tagan_layernorm_bwd with s = b,
  * dres = the LN's own ds, so both gradients of b arrive summed). */
-int tagan_add_layernorm_skip_fwd(int64_t M, int32_t H, const float* a, const float* b, float p_drop,
+int tagan_add_layernorm_skip_fwd(int64_t M, int32_t H, const float* a, const float* a_bias, const float* b,
+                                 float p_drop,
                                  uint64_t seed, const float* gamma, const float* beta, float eps,
                                  const float* gamma_s, const float* beta_s, float eps_s, float* s_out,
                                  float* y, float* mean, float* rstd, float* mean_s, float* rstd_s,

@@ -63,9 +63,9 @@ _SIGNATURES = {
                                            _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,
                                            _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p, _sz, _p]),
     "tagan_layernorm_supported": (_c.c_int, [_i32]),
-    "tagan_add_layernorm_fwd": (_c.c_int, [_c.c_int, _i64, _i32, _p, _p, _f32, _u64, _p, _p, _f32, _p, _p, _i64,
+    "tagan_add_layernorm_fwd": (_c.c_int, [_c.c_int, _i64, _i32, _p, _p, _p, _f32, _u64, _p, _p, _f32, _p, _p, _i64,
                                            _p, _p, _p]),
-    "tagan_add_layernorm_skip_fwd": (_c.c_int, [_i64, _i32, _p, _p, _f32, _u64, _p, _p, _f32, _p, _p, _f32, _p, _p,
+    "tagan_add_layernorm_skip_fwd": (_c.c_int, [_i64, _i32, _p, _p, _p, _f32, _u64, _p, _p, _f32, _p, _p, _f32, _p, _p,
                                                 _p, _p, _p, _p, _p]),
     "tagan_layernorm_bwd_workspace": (_sz, [_i64, _i32]),
     "tagan_layernorm_bwd": (_c.c_int, [_c.c_int, _i64, _i32, _p, _p, _p, _p, _p, _p, _f32, _u64, _p, _p, _p, _p,

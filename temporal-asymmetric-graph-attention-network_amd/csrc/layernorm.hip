@@ -25,6 +25,7 @@ struct LnArgs {
     int64_t M;
     int H;
     const float* a;
+    const float* a_bias;   // optional [H] added to a before the dropout (the projection's bias)
     const float* b;
     float p_drop, inv_keep;
     uint64_t seed;
@@ -82,6 +83,10 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
         const int c = (n * LPR + sl) * 4;
         const int64_t off = row * H + c;
         float4 x = ld4(A.a + off);
+        if (A.a_bias) {
+            const float4 ab = ld4(A.a_bias + c);
+            x.x += ab.x; x.y += ab.y; x.z += ab.z; x.w += ab.w;
+        }
         x = drop4(A, x, row, c);
         rb[n] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (A.b) {
@@ -255,7 +260,8 @@ int tagan_layernorm_supported(int32_t H) {
     return tagan::geometry(H, l, n) ? 1 : 0;
 }
 
-int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, const float* b, float p_drop,
+int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, const float* a_bias, const float* b,
+                            float p_drop,
                             uint64_t seed, const float* gamma, const float* beta, float eps, float* s_out, float* y,
                             int64_t ldy, float* mean, float* rstd, void* stream) {
     using namespace tagan;
@@ -265,7 +271,7 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
     TAGAN_REQUIRE(M > 0 && a && gamma && beta && y && mean && rstd, TAGAN_ERR_ARG, "layernorm_fwd: bad args");
     TAGAN_REQUIRE(p_drop >= 0.f && p_drop < 1.f, TAGAN_ERR_ARG, "layernorm_fwd: p_drop");
     LnArgs A{};
-    A.M = M; A.H = H; A.a = a; A.b = b; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
+    A.M = M; A.H = H; A.a = a; A.a_bias = a_bias; A.b = b; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
     A.gamma = gamma; A.beta = beta; A.eps = eps; A.s_out = s_out; A.y = y; A.mean = mean; A.rstd = rstd;
     A.ldy = ldy > 0 ? ldy : H;
     TAGAN_REQUIRE(A.ldy >= H && A.ldy % 4 == 0, TAGAN_ERR_ARG, "layernorm_fwd: ldy %lld", (long long)ldy);
@@ -279,7 +285,8 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
     return TAGAN_OK;
 }
 
-int tagan_add_layernorm_skip_fwd(int64_t M, int32_t H, const float* a, const float* b, float p_drop, uint64_t seed,
+int tagan_add_layernorm_skip_fwd(int64_t M, int32_t H, const float* a, const float* a_bias, const float* b,
+                                 float p_drop, uint64_t seed,
                                  const float* gamma, const float* beta, float eps, const float* gamma_s,
                                  const float* beta_s, float eps_s, float* s_out, float* y, float* mean, float* rstd,
                                  float* mean_s, float* rstd_s, void* stream) {
@@ -290,7 +297,7 @@ int tagan_add_layernorm_skip_fwd(int64_t M, int32_t H, const float* a, const flo
                   TAGAN_ERR_ARG, "layernorm_skip_fwd: bad args");
     TAGAN_REQUIRE(p_drop >= 0.f && p_drop < 1.f, TAGAN_ERR_ARG, "layernorm_skip_fwd: p_drop");
     LnArgs A{};
-    A.M = M; A.H = H; A.a = a; A.b = b; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
+    A.M = M; A.H = H; A.a = a; A.a_bias = a_bias; A.b = b; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
     A.gamma = gamma; A.beta = beta; A.eps = eps; A.s_out = s_out; A.y = y; A.mean = mean; A.rstd = rstd;
     A.ldy = H;
     A.gamma_s = gamma_s; A.beta_s = beta_s; A.eps_s = eps_s; A.mean_s = mean_s; A.rstd_s = rstd_s;

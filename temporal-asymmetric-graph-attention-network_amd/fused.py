@@ -27,8 +27,8 @@ from .kernels import TemporalMask, _geo_fwd, colsum, split_rows, weight_grad
 
 
 # ----------------------------------------------------------------------------- raw LayerNorm calls
-def ln_fwd(a2, b2, p_drop, seed, gamma, beta, eps, keep_s, y=None, y_dtype=torch.float32):
-    """LN(dropout(a2) + b2); ``y`` may be a wider row-strided buffer ([M, ld], first H columns written);
+def ln_fwd(a2, b2, p_drop, seed, gamma, beta, eps, keep_s, y=None, y_dtype=torch.float32, a_bias=None):
+    """LN(dropout(a2 + a_bias) + b2); ``y`` may be a wider row-strided buffer ([M, ld], first H columns written);
     y is stored in ``y_dtype`` (bf16 when it only feeds a bf16 GEMM)."""
     M, H = a2.shape
     s = torch.empty_like(a2) if keep_s else None
@@ -36,20 +36,22 @@ def ln_fwd(a2, b2, p_drop, seed, gamma, beta, eps, keep_s, y=None, y_dtype=torch
         y = torch.empty(M, H, device=a2.device, dtype=y_dtype)
     mean = torch.empty(M, device=a2.device)
     rstd = torch.empty(M, device=a2.device)
-    check(lib().tagan_add_layernorm_fwd(_lib.dtype_code(y), M, H, ptr(a2), ptr(b2), float(p_drop), seed, ptr(gamma),
+    check(lib().tagan_add_layernorm_fwd(_lib.dtype_code(y), M, H, ptr(a2), ptr(a_bias), ptr(b2), float(p_drop), seed,
+                                        ptr(gamma),
                                         ptr(beta), float(eps), ptr(s), ptr(y), y.stride(0), ptr(mean), ptr(rstd),
                                         stream_of(a2)), "tagan_add_layernorm_fwd")
     return y, s, mean, rstd
 
 
-def ln_skip_fwd(a2, b2, p_drop, seed, gamma, beta, eps, gamma_s, beta_s, eps_s):
-    """LN(dropout(a2) + b2) + LN_s(b2) (fp32); returns y, s, mean, rstd, (mean_s, rstd_s)."""
+def ln_skip_fwd(a2, b2, p_drop, seed, gamma, beta, eps, gamma_s, beta_s, eps_s, a_bias=None):
+    """LN(dropout(a2 + a_bias) + b2) + LN_s(b2) (fp32); returns y, s, mean, rstd, (mean_s, rstd_s)."""
     M, H = a2.shape
     dev = a2.device
     s = torch.empty_like(a2)
     y = torch.empty(M, H, device=dev)
     st = torch.empty(4, M, device=dev)
-    check(lib().tagan_add_layernorm_skip_fwd(M, H, ptr(a2), ptr(b2), float(p_drop), seed, ptr(gamma), ptr(beta),
+    check(lib().tagan_add_layernorm_skip_fwd(M, H, ptr(a2), ptr(a_bias), ptr(b2), float(p_drop), seed, ptr(gamma),
+                                             ptr(beta),
                                              float(eps), ptr(gamma_s), ptr(beta_s), float(eps_s), ptr(s), ptr(y),
                                              ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(st[3]), stream_of(a2)),
           "tagan_add_layernorm_skip_fwd")
@@ -239,6 +241,8 @@ def _wgrad(dy, x, bf, rows: int = 2048):
 # ----------------------------------------------------------------------------- the fused block
 # TAGAN_QKV_AUG=0: QKV GEMM with the hipBLASLt bias epilogue instead of the bias-as-weight-column form (A/B)
 QKV_AUG = os.environ.get("TAGAN_QKV_AUG", "1") != "0"
+# TAGAN_OUT_BIAS_LN=0: out-projection bias in the GEMM epilogue instead of the closing LayerNorm (A/B)
+OUT_BIAS_LN = os.environ.get("TAGAN_OUT_BIAS_LN", "1") != "0"
 
 class AttnBlockFn(torch.autograd.Function):
     """y = LN2(dropout(out_proj(core(QKV(LN1(x))))) + x) with LayerNorm on both sides (use_layer_norm=True)."""
@@ -268,12 +272,16 @@ class AttnBlockFn(torch.autograd.Function):
             qkv = _addmm(b_qkv, h, w_qkv, bf, out_bf16=act)
         c, saved = core.fwd(qkv, p1, p2)
         cg = _b(c) if bf else c
-        o = _addmm(b_o, cg, w_o, bf)
+        if OUT_BIAS_LN:   # out-projection bias added in the closing LayerNorm (no GEMM epilogue)
+            o, b_o_ln = _mm(cg, w_o.t(), bf), b_o
+        else:
+            o, b_o_ln = _addmm(b_o, cg, w_o, bf), None
         skip = None
         if lns_w is not None:      # y = LN2(drop(o) + x) + LN_s(x) in one pass (model.py:258-262)
-            y, s2, mean2, rstd2, skip = ln_skip_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, lns_w, lns_b, eps_s)
+            y, s2, mean2, rstd2, skip = ln_skip_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, lns_w, lns_b, eps_s,
+                                                    a_bias=b_o_ln)
         else:
-            y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True)
+            y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True, a_bias=b_o_ln)
         ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
         ctx.inter = (h, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
         ctx.cfg = (core, p_out, seed_out, x.shape, bf, act)

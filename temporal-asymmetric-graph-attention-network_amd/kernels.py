@@ -411,7 +411,7 @@ class AddLayerNormFn(torch.autograd.Function):
         y = torch.empty_like(a2)
         mean = torch.empty(M, device=a.device)
         rstd = torch.empty(M, device=a.device)
-        check(lib().tagan_add_layernorm_fwd(_lib.TAGAN_F32, M, H, ptr(a2), ptr(b2), float(p_drop), seed,
+        check(lib().tagan_add_layernorm_fwd(_lib.TAGAN_F32, M, H, ptr(a2), None, ptr(b2), float(p_drop), seed,
                                             ptr(gamma), ptr(beta), float(eps), ptr(s), ptr(y), 0, ptr(mean),
                                             ptr(rstd), stream_of(a2)), "tagan_add_layernorm_fwd")
         ctx.save_for_backward(s if keep_s else a2, mean, rstd, gamma)
