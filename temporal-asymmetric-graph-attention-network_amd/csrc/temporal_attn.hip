@@ -1370,7 +1370,15 @@ bool v4_ok(int T, int d) { return v4_enabled() && v4_tiles(T) != 0 && (d == 16 |
 
 // waves: G partial rows x heads (G <= grid_rows(rows), the bias-gradient workspace rows)
 // (a multiple of 8 from 8 rows up, for the XCD-aware wave map)
-int64_t v4_groups(int64_t rows) { return rows >= 8 ? std::min<int64_t>(rows, 1024) & ~(int64_t)7 : rows; }
+// TAGAN_V4_G=<n> overrides the 1024 row groups (grid-size sweeps; capped at 1024 = the workspace rows)
+int64_t v4_groups(int64_t rows) {
+    static const int64_t cap = [] {
+        const char* e = getenv("TAGAN_V4_G");
+        const int64_t v = e ? atoll(e) : 0;
+        return (v >= 8 && v <= 1024) ? v : (int64_t)1024;
+    }();
+    return rows >= 8 ? std::min<int64_t>(rows, cap) & ~(int64_t)7 : rows;
+}
 
 int v3_lanes(int T) { return T <= 16 ? 16 : T <= 32 ? 32 : T <= 128 ? 64 : 0; }
 int v3_wph(int T) { return T > 64 ? 2 : 1; }
