@@ -243,6 +243,9 @@ def _wgrad(dy, x, bf, rows: int = 2048):
 QKV_AUG = os.environ.get("TAGAN_QKV_AUG", "1") != "0"
 # TAGAN_OUT_BIAS_LN=0: out-projection bias in the GEMM epilogue instead of the closing LayerNorm (A/B)
 OUT_BIAS_LN = os.environ.get("TAGAN_OUT_BIAS_LN", "1") != "0"
+# split-K slice height of the QKV weight gradient (3H outputs): taller slices than the out-projection's
+# 2048 (-> 2560 at C2) measured faster for N_out = 384 (tools/wgrad_probe.py); TAGAN_WGRAD_ROWS_QKV overrides
+WGRAD_ROWS_QKV = int(os.environ.get("TAGAN_WGRAD_ROWS_QKV", "8192"))
 
 class AttnBlockFn(torch.autograd.Function):
     """y = LN2(dropout(out_proj(core(QKV(LN1(x))))) + x) with LayerNorm on both sides (use_layer_norm=True)."""
@@ -307,7 +310,7 @@ class AttnBlockFn(torch.autograd.Function):
         if bf:
             dqkv = _b(dqkv)
         dh = _mm(dqkv, w_qkv, bf)
-        dw_qkv = _wgrad(dqkv, h, bf) if ng[5] else None
+        dw_qkv = _wgrad(dqkv, h, bf, WGRAD_ROWS_QKV) if ng[5] else None
         del dqkv
         dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
         ctx.inter = None
