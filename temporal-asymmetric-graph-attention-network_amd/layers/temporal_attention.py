@@ -297,15 +297,30 @@ class AsymmetricTemporalAttention(TemporalAttention):
         vals = self.asymmetric_kernel[torch.clamp(rel + W, 0, 2 * W)]
         return vals * ((rel >= -W) & (rel <= W)).unsqueeze(-1).float()
 
+    def _selectors(self, T, device, dtype):
+        """0/1 matrices that gather the two tables by diagonal: A[t, k] = [k == clamp(t-T+1+W)]·[|t-T+1| <= W],
+        Rsel[t, k] = [k == clamp(t-T+1+m)].  A gather as a GEMM: its backward is a GEMM too (deterministic, two
+        small launches) instead of the sort-based index_put of advanced-indexing backward.  Cached per (T, device)."""
+        key = (T, str(device), dtype)
+        cache = self.__dict__.setdefault("_sel_cache", {})
+        if key not in cache:
+            delta = torch.arange(-(T - 1), T, device=device)
+            W = self.asymmetric_window_size
+            a = torch.nn.functional.one_hot(torch.clamp(delta + W, 0, 2 * W), 2 * W + 1).to(dtype)
+            a = a * ((delta >= -W) & (delta <= W)).unsqueeze(-1).to(dtype)
+            r = None
+            if self.relative_position_bias:
+                m = self.max_relative_position
+                r = torch.nn.functional.one_hot(torch.clamp(delta + m, 0, 2 * m), 2 * m + 1).to(dtype)
+            cache[key] = (a, r)
+        return cache[key]
+
     def _bias_table(self, T, device):
         """[heads, 2T-1] table, entry [h][i-j+T-1] = R[clamp(i-j+32)] + K[clamp(i-j+W)]·[|i-j|<=W] (:1010-1027)."""
-        delta = torch.arange(-(T - 1), T, device=device)
-        W = self.asymmetric_window_size
-        tab = self.asymmetric_kernel[torch.clamp(delta + W, 0, 2 * W)] * \
-            ((delta >= -W) & (delta <= W)).unsqueeze(-1).to(self.asymmetric_kernel.dtype)
-        if self.relative_position_bias:
-            m = self.max_relative_position
-            tab = self.relative_pos_table[torch.clamp(delta + m, 0, 2 * m)] + tab
+        a, r = self._selectors(T, device, self.asymmetric_kernel.dtype)
+        tab = a @ self.asymmetric_kernel                   # exact: one nonzero (1.0) term per row
+        if r is not None:
+            tab = r @ self.relative_pos_table + tab
         return tab.t().contiguous()
 
     def _time_bias(self, time_stamps: torch.Tensor, B: int, T: int) -> torch.Tensor:
