@@ -207,8 +207,12 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
 
 /* Backward.  dbias_table: [heads, 2T-1] (reduced over rows, deterministic) or NULL.
  * dbias_dense: [rows, heads, T, T] per-row score gradients (caller reduces a
- * shared bias) or NULL.  dq/dk/dv element (r,t,f) at d*[r*d_row + t*d_t + f]. */
-size_t tagan_temporal_attn_bwd_workspace(int64_t rows, int32_t T, int32_t heads);
+ * shared bias) or NULL.  dq/dk/dv element (r,t,f) at d*[r*d_row + t*d_t + f].
+ * dsum_qkv (optional): [3 * heads * head_dim] = column sums of dq | dk | dv over all rows and
+ * steps (the QKV projection's bias gradient), summed inside the matrix-core kernel in a fixed
+ * order; only that path (T <= 32, head_dim 16 or 32, 16-B aligned strides) provides it — otherwise
+ * the call returns TAGAN_ERR_UNSUPPORTED before launching anything. */
+size_t tagan_temporal_attn_bwd_workspace(int64_t rows, int32_t T, int32_t heads, int32_t head_dim);
 int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim,
                             const void* q, const void* k, const void* v, int64_t s_row, int64_t s_t,
                             const float* bias_table, const float* bias_dense, int64_t bias_bstride,
@@ -217,7 +221,7 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
                             const void* out, int64_t o_row, int64_t o_t, const float* lse,
                             const void* dout, int64_t do_row, int64_t do_t,
                             void* dq, void* dk, void* dv, int64_t d_row, int64_t d_t,
-                            float* dbias_table, float* dbias_dense,
+                            float* dbias_table, float* dbias_dense, float* dsum_qkv,
                             void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------

@@ -16,6 +16,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tagan_hip.h")
 
 TAGAN_F32 = 0
 TAGAN_BF16 = 1
+TAGAN_ERR_UNSUPPORTED = -2   # tagan_status (include/tagan_hip.h)
 
 
 def dtype_code(t) -> int:
@@ -58,10 +59,10 @@ _SIGNATURES = {
     "tagan_temporal_attn_fwd": (_c.c_int, [_c.c_int, _i64, _i32, _i32, _i32, _p, _p, _p, _i64, _i64, _p, _p,
                                            _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,
                                            _p]),
-    "tagan_temporal_attn_bwd_workspace": (_sz, [_i64, _i32, _i32]),
+    "tagan_temporal_attn_bwd_workspace": (_sz, [_i64, _i32, _i32, _i32]),
     "tagan_temporal_attn_bwd": (_c.c_int, [_c.c_int, _i64, _i32, _i32, _i32, _p, _p, _p, _i64, _i64, _p, _p,
                                            _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,
-                                           _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p, _sz, _p]),
+                                           _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p, _p, _sz, _p]),
     "tagan_layernorm_supported": (_c.c_int, [_i32]),
     "tagan_add_layernorm_fwd": (_c.c_int, [_c.c_int, _i64, _i32, _p, _p, _p, _f32, _u64, _p, _p, _f32, _p, _p, _i64,
                                            _p, _p, _p]),

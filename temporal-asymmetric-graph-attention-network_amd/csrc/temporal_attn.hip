@@ -55,6 +55,7 @@ struct TArgs {
     int64_t d_row, d_t;
     float* dbias_dense;
     float* part;   // [gridDim.x, heads, 2T-1] block partials of dbias_table
+    float* qkv_part;   // v4: [row groups, 3H] partial column sums of dq | dk | dv (QKV bias gradient)
 };
 
 __device__ __forceinline__ bool keep_ij(const TArgs& A, int64_t r, int h, int i, int j) {
@@ -1135,6 +1136,13 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
     for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
         for (int it = 0; it < TT; ++it) gsum[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+    // Σ over this wave's rows and steps of the stored dq | dk | dv (lane: features 16dt + 4g + e), reduced over
+    // the step lanes at the end: the QKV projection's bias gradient without a pass over dqkv
+    f4v bsum[3][DT];
+#pragma unroll
+    for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) bsum[t3][dt] = f4v{0.f, 0.f, 0.f, 0.f};
     f4v qv[TT][DT], kv[TT][DT], vv[TT][DT], dov[TT][DT];
     float lsev[TT];
     // The next row's Q, K, LSE (and, unless TAGAN_V4_SPLIT, V and dO) are prefetched during this one.
@@ -1288,6 +1296,12 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
                     st4v<S>(A.dq, r * A.d_row + (int64_t)i * A.d_t + h * d + dt * 16 + 4 * g, acc[dt][it],
                             A.inv_sqrt_d);
             }
+            if (A.qkv_part) {   // padded steps contribute exact zeros (dS = 0 there)
+#pragma unroll
+                for (int it = 0; it < TT; ++it)
+#pragma unroll
+                    for (int dt = 0; dt < DT; ++dt) bsum[0][dt] += acc[dt][it] * A.inv_sqrt_d;
+            }
         }
         // dKᵀ = Qᵀ·dS (A = Qt, B = X), then dVᵀ = dOᵀ·P' (A = Ot, B = X after P' replaces dS)
 #pragma unroll
@@ -1332,7 +1346,30 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
                 for (int dt = 0; dt < DT; ++dt)
                     st4v<S>(dst, r * A.d_row + (int64_t)j * A.d_t + h * d + dt * 16 + 4 * g, acc[dt][jt], sc);
             }
+            if (A.qkv_part) {
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int dt = 0; dt < DT; ++dt) bsum[1 + pass][dt] += acc[dt][jt] * sc;
+            }
         }
+    }
+    if (A.qkv_part) {
+        // reduce over the 16 step lanes (fixed butterfly order), lanes c == 0 write features 16dt + 4g + e
+        float* prow = A.qkv_part + rg * 3 * (int64_t)A.H + (int64_t)h * d;
+#pragma unroll
+        for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float v = bsum[t3][dt][e];
+                    v += __shfl_xor(v, 1, WAVE);
+                    v += __shfl_xor(v, 2, WAVE);
+                    v += __shfl_xor(v, 4, WAVE);
+                    v += __shfl_xor(v, 8, WAVE);
+                    if (c0 == 0) prow[t3 * (int64_t)A.H + dt * 16 + 4 * g0 + e] = v;
+                }
     }
     if (A.part) {
         // diagonal sums (t = i - j + T - 1) of the summed dS tile in j order; partial row
@@ -1516,10 +1553,11 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     return TAGAN_OK;
 }
 
-size_t tagan_temporal_attn_bwd_workspace(int64_t rows, int32_t T, int32_t heads) {
+size_t tagan_temporal_attn_bwd_workspace(int64_t rows, int32_t T, int32_t heads, int32_t head_dim) {
     using namespace tagan;
-    if (rows <= 0 || T <= 0 || heads <= 0) return 0;
-    return align_up((size_t)grid_rows(rows) * heads * (2 * T - 1) * sizeof(float), 256);
+    if (rows <= 0 || T <= 0 || heads <= 0 || head_dim <= 0) return 0;
+    return align_up((size_t)grid_rows(rows) * heads * (2 * T - 1) * sizeof(float), 256) +
+           align_up((size_t)grid_rows(rows) * 3 * heads * head_dim * sizeof(float), 256);
 }
 
 int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim, const void* q,
@@ -1528,8 +1566,8 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
                             int64_t mask_bstride, int64_t mask_hstride, int causal, float p_drop, uint64_t seed,
                             const void* out, int64_t o_row, int64_t o_t, const float* lse, const void* dout,
                             int64_t do_row, int64_t do_t, void* dq, void* dk, void* dv, int64_t d_row, int64_t d_t,
-                            float* dbias_table, float* dbias_dense, void* workspace, size_t workspace_bytes,
-                            void* stream) {
+                            float* dbias_table, float* dbias_dense, float* dsum_qkv, void* workspace,
+                            size_t workspace_bytes, void* stream) {
     using namespace tagan;
     int rc = check(dtype, rows, T, heads, head_dim, p_drop);
     if (rc) return rc;
@@ -1552,11 +1590,20 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     A.d_t = d_t;
     A.dbias_dense = dbias_dense;
     const int nblk = grid_rows(rows);
-    if (dbias_table) {
-        const size_t need = tagan_temporal_attn_bwd_workspace(rows, T, heads);
+    {
+        const bool al4_ = s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0 && do_t % 4 == 0 &&
+                          do_row % 4 == 0 && d_t % 4 == 0 && d_row % 4 == 0;
+        TAGAN_REQUIRE(!dsum_qkv || (al4_ && v4_ok(T, head_dim)), TAGAN_ERR_UNSUPPORTED,
+                      "temporal_attn_bwd: dsum_qkv needs the matrix-core path (T <= 32, head_dim 16/32, aligned)");
+    }
+    if (dbias_table || dsum_qkv) {
+        const size_t need = tagan_temporal_attn_bwd_workspace(rows, T, heads, head_dim);
         TAGAN_REQUIRE(workspace && workspace_bytes >= need, TAGAN_ERR_WORKSPACE,
                       "temporal_attn_bwd: workspace %zu < %zu", workspace_bytes, need);
-        A.part = (float*)workspace;
+        if (dbias_table) A.part = (float*)workspace;
+        if (dsum_qkv)
+            A.qkv_part = (float*)((char*)workspace +
+                                  align_up((size_t)nblk * heads * (2 * T - 1) * sizeof(float), 256));
     }
     hipStream_t s = as_stream(stream);
     const dim3 g(nblk);
@@ -1585,6 +1632,11 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
             const int n = heads * (2 * T - 1);
             launch_colsum(A.part, (int)G4, n, dbias_table, nullptr, n, s);
             TAGAN_CHECK_LAUNCH("temporal_attn_bwd_sum");
+        }
+        if (dsum_qkv) {
+            const int n = 3 * heads * head_dim;
+            launch_colsum(A.qkv_part, (int)G4, n, dsum_qkv, nullptr, n, s);
+            TAGAN_CHECK_LAUNCH("temporal_attn_bwd_qkv_sum");
         }
         return TAGAN_OK;
     }

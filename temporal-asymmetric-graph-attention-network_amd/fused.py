@@ -90,7 +90,7 @@ class GeoCore:
         _geo_fwd(qkv2, self.graph, self.metric, self.heads, prm, self.p_drop, self.seed, out, lse, None)
         return out, (lse, prm)
 
-    def bwd(self, qkv2, out, saved, dctx, want_p1, want_p2):
+    def bwd(self, qkv2, out, saved, dctx, want_p1, want_p2, want_bias_sum=False):
         lse, prm = saved
         N, H3 = qkv2.shape
         H = H3 // 3
@@ -106,7 +106,7 @@ class GeoCore:
                                    ptr(prm), float(self.p_drop), self.seed, ptr(out), ptr(lse), ptr(dctx), db,
                                    db + H * es, db + 2 * H * es, H3, ptr(dprm), ptr(ws), wsb, stream_of(qkv2)),
               "tagan_geo_attn_bwd")
-        return dqkv, dprm, None
+        return (dqkv, dprm, None, None) if want_bias_sum else (dqkv, dprm, None)
 
 
 class TemporalCore:
@@ -142,7 +142,9 @@ class TemporalCore:
                                             ptr(lse), None, stream_of(qkv2)), "tagan_temporal_attn_fwd")
         return out, (lse, bt, bd, bd_stride)
 
-    def bwd(self, qkv2, out, saved, dctx, want_p1, want_p2):
+    def bwd(self, qkv2, out, saved, dctx, want_p1, want_p2, want_bias_sum=False):
+        """``want_bias_sum``: also return the column sums of dq|dk|dv (the QKV bias gradient) when the
+        matrix-core kernel can sum them in place (else None: the caller reduces dqkv itself)."""
         lse, bt, bd, bd_stride = saved
         T, R, heads = self.T, self.R, self.heads
         H = qkv2.shape[1] // 3
@@ -153,19 +155,25 @@ class TemporalCore:
         dbt = torch.empty(heads, 2 * T - 1, device=dev) if (bt is not None and want_p1) else None
         dbd = torch.empty(R, heads, T, T, device=dev) if (bd is not None and want_p2) else None
         L = lib()
-        wsb = L.tagan_temporal_attn_bwd_workspace(R, T, heads)
+        wsb = L.tagan_temporal_attn_bwd_workspace(R, T, heads, d)
         ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
         m = self.mask
+        dsum = torch.empty(3 * H, device=dev) if want_bias_sum else None
         b, db, es = qkv2.data_ptr(), dqkv.data_ptr(), qkv2.element_size()
-        check(L.tagan_temporal_attn_bwd(_lib.dtype_code(qkv2), R, T, heads, d, b, b + H * es, b + 2 * H * es, s_row, s_t,
-                                        ptr(bt), ptr(bd), bd_stride, ptr(m.keep), m.bstride, m.hstride,
-                                        int(m.causal), float(self.p_drop), self.seed, ptr(out), o_row, o_t, ptr(lse),
-                                        ptr(dctx), o_row, o_t, db, db + H * es, db + 2 * H * es, s_row, s_t,
-                                        ptr(dbt), ptr(dbd), ptr(ws), wsb, stream_of(qkv2)),
-              "tagan_temporal_attn_bwd")
+        def call(ds):
+            return L.tagan_temporal_attn_bwd(_lib.dtype_code(qkv2), R, T, heads, d, b, b + H * es, b + 2 * H * es,
+                                             s_row, s_t, ptr(bt), ptr(bd), bd_stride, ptr(m.keep), m.bstride,
+                                             m.hstride, int(m.causal), float(self.p_drop), self.seed, ptr(out), o_row,
+                                             o_t, ptr(lse), ptr(dctx), o_row, o_t, db, db + H * es, db + 2 * H * es,
+                                             s_row, s_t, ptr(dbt), ptr(dbd), ptr(ds), ptr(ws), wsb, stream_of(qkv2))
+        rc = call(dsum)
+        if rc == _lib.TAGAN_ERR_UNSUPPORTED and dsum is not None:   # rejected before any launch: not this path
+            dsum = None
+            rc = call(None)
+        check(rc, "tagan_temporal_attn_bwd")
         if dbd is not None and bd.shape[0] == 1:
             dbd = dbd.sum(0, keepdim=True)
-        return dqkv, dbt, dbd
+        return (dqkv, dbt, dbd, dsum) if want_bias_sum else (dqkv, dbt, dbd)
 
 
 # ----------------------------------------------------------------------------- precision modes
@@ -304,9 +312,9 @@ class AttnBlockFn(torch.autograd.Function):
             dres, _, dgs, dbs, _ = ln_bwd(x2, skip[0], skip[1], lns_w, dy2, dres, 0.0, 0, True, False, False)
         dc = _mm(do, w_o, bf, out_bf16=act)
         dw_o = _wgrad(do, cg, bf) if ng[7] else None
-        dqkv, dp1, dp2 = core.bwd(qkv, c, saved, dc, ng[1], ng[2])
+        dqkv, dp1, dp2, db_core = core.bwd(qkv, c, saved, dc, ng[1], ng[2], want_bias_sum=bool(ng[6]))
         del dc, do
-        db_qkv = colsum(dqkv) if ng[6] else None
+        db_qkv = (db_core if db_core is not None else colsum(dqkv)) if ng[6] else None
         if bf:
             dqkv = _b(dqkv)
         dh = _mm(dqkv, w_qkv, bf)

@@ -300,7 +300,7 @@ class TemporalAttnFn(torch.autograd.Function):
         L = lib()
         dbt = torch.empty(heads, 2 * T - 1, device=qkv.device) if (ctx.need_bt and ctx.needs_input_grad[1]) else None
         dbd = torch.empty(R, heads, T, T, device=qkv.device) if (ctx.need_bd and ctx.needs_input_grad[2]) else None
-        ws_bytes = L.tagan_temporal_attn_bwd_workspace(R, T, heads)
+        ws_bytes = L.tagan_temporal_attn_bwd_workspace(R, T, heads, d)
         ws = torch.empty(int(ws_bytes), dtype=torch.uint8, device=qkv.device)
         base, es = qkv.data_ptr(), qkv.element_size()
         dbase = dqkv.data_ptr()
@@ -308,7 +308,7 @@ class TemporalAttnFn(torch.autograd.Function):
                                         s_row, s_t, ptr(bt), ptr(bd), bd_stride, ptr(mask.keep), mask.bstride,
                                         mask.hstride, int(mask.causal), float(p_drop), seed, ptr(out), o_row, o_t,
                                         ptr(lse), ptr(dout), o_row, o_t, dbase, dbase + H * es, dbase + 2 * H * es,
-                                        s_row, s_t, ptr(dbt), ptr(dbd), ptr(ws), ws_bytes, stream_of(qkv)),
+                                        s_row, s_t, ptr(dbt), ptr(dbd), None, ptr(ws), ws_bytes, stream_of(qkv)),
               "tagan_temporal_attn_bwd")
         if dbd is not None and bd is not None and bd.shape[0] == 1:
             dbd = dbd.sum(0, keepdim=True)

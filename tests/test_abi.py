@@ -73,7 +73,7 @@ def test_workspace_queries_are_host_only():
     assert g.chunk_cap == 1000 + 12000 // 128 + 1 and g.part_cap == 2 * (12000 // 128) + 2
     assert L.tagan_geo_attn_bwd_workspace(ctypes.byref(g), 8, 16) >= 1000 * 8 * 4
     assert L.tagan_geo_attn_fwd_workspace(ctypes.byref(g), 8, 16) >= g.part_cap * (16 + 128) * 4
-    assert L.tagan_temporal_attn_bwd_workspace(100, 32, 8) >= 8 * 63 * 4
+    assert L.tagan_temporal_attn_bwd_workspace(100, 32, 8, 16) >= 100 * 8 * 63 * 4 + 100 * 3 * 128 * 4
     g.n_nodes = 0
     assert L.tagan_geo_attn_bwd_workspace(ctypes.byref(g), 8, 16) == 0
 

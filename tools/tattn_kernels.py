@@ -42,7 +42,7 @@ def main():
     table = torch.randn(heads, 2 * T - 1, device=dev, generator=g) * 0.1
     dtable = torch.empty_like(table)
     L = _lib.lib()
-    wsb = L.tagan_temporal_attn_bwd_workspace(N, T, heads)
+    wsb = L.tagan_temporal_attn_bwd_workspace(N, T, heads, d)
     ws = torch.empty(max(int(wsb), 1), dtype=torch.uint8, device=dev)
     sp = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     b, db, es = qkv.data_ptr(), dqkv.data_ptr(), 4
@@ -57,7 +57,7 @@ def main():
         _lib.check(L.tagan_temporal_attn_bwd(0, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, st,
                                              _lib.ptr(table), None, 0, None, 0, 0, a.causal, a.p, 99,
                                              _lib.ptr(out), H, N * H, _lib.ptr(lse), _lib.ptr(dout), H, N * H,
-                                             db, db + H * es, db + 2 * H * es, sr, st, _lib.ptr(dtable), None,
+                                             db, db + H * es, db + 2 * H * es, sr, st, _lib.ptr(dtable), None, None,
                                              _lib.ptr(ws), wsb, sp), "bwd")
 
     for _ in range(3):
