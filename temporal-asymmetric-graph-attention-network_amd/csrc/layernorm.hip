@@ -7,6 +7,8 @@
 // XOR-butterfly reductions inside the group, two-pass in registers (no Welford
 // round-off), rstd = 1/sqrt(var+eps).  Backward recomputes x̂ from the saved LN
 // input and (mean, rstd); dγ/dβ are per-block partials summed in block order.
+#include <stdlib.h>
+
 #include "common.cuh"
 
 namespace tagan {
@@ -68,87 +70,111 @@ __device__ __forceinline__ float4 drop4(const LnArgs& A, float4 v, int64_t row, 
     return v;
 }
 
-template <int LPR, int NV, typename S>
+// U row groups per wave: all U rows' loads are issued before the first reduction, so one
+// wave keeps U x NV x (1 or 2) KB in flight instead of one load's worth.  At C2's H = 128 a
+// single row pair per wave left the LN passes latency-bound at ~50 % of the HBM roofline.
+template <int LPR, int NV, int U, typename S>
 __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
     constexpr int RPW = WAVE / LPR;
     const int lane = threadIdx.x & (WAVE - 1), sl = lane % LPR;
     const int64_t wave = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6);
-    const int64_t row = wave * RPW + lane / LPR;
-    if (row >= A.M) return;
+    const int64_t row0 = wave * (RPW * U) + lane / LPR;
+    if (row0 >= A.M) return;   // whole row groups leave together (the butterflies stay inside a group)
     const int H = A.H;
-    float4 v[NV], rb[NV];
-    float sum = 0.f, sum_b = 0.f;
+    float4 v[U][NV], rb[U][NV];
+    float sum[U], sum_b[U];
 #pragma unroll
-    for (int n = 0; n < NV; ++n) {
-        const int c = (n * LPR + sl) * 4;
-        const int64_t off = row * H + c;
-        float4 x = ld4(A.a + off);
-        if (A.a_bias) {
-            const float4 ab = ld4(A.a_bias + c);
-            x.x += ab.x; x.y += ab.y; x.z += ab.z; x.w += ab.w;
-        }
-        x = drop4(A, x, row, c);
-        rb[n] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (A.b) {
-            const float4 r = ld4(A.b + off);
-            rb[n] = r;
-            x.x += r.x; x.y += r.y; x.z += r.z; x.w += r.w;
-            sum_b += (r.x + r.y) + (r.z + r.w);
-        }
-        v[n] = x;
-        if (A.s_out) st4(A.s_out + off, x);
-        sum += (x.x + x.y) + (x.z + x.w);
-    }
-    const float mean = row_sum<LPR>(sum) / (float)H;
-    float sq = 0.f;
-#pragma unroll
-    for (int n = 0; n < NV; ++n) {
-        const float dx = v[n].x - mean, dyv = v[n].y - mean, dz = v[n].z - mean, dw = v[n].w - mean;
-        sq += (dx * dx + dyv * dyv) + (dz * dz + dw * dw);
-    }
-    const float var = row_sum<LPR>(sq) / (float)H;
-    const float rstd = 1.f / sqrtf(var + A.eps);
-    float mean_s = 0.f, rstd_s = 0.f;
-    if (A.gamma_s) {                     // skip branch: statistics of b alone (two-pass, like the main one)
-        mean_s = row_sum<LPR>(sum_b) / (float)H;
-        float sqb = 0.f;
+    for (int u = 0; u < U; ++u) {
+        const int64_t row = row0 + u * RPW;
+        const int64_t r = row < A.M ? row : A.M - 1;   // dead rows reload the last row; never stored
+        sum[u] = 0.f; sum_b[u] = 0.f;
 #pragma unroll
         for (int n = 0; n < NV; ++n) {
-            const float dx = rb[n].x - mean_s, dyv = rb[n].y - mean_s, dz = rb[n].z - mean_s, dw = rb[n].w - mean_s;
-            sqb += (dx * dx + dyv * dyv) + (dz * dz + dw * dw);
+            const int c = (n * LPR + sl) * 4;
+            v[u][n] = ld4(A.a + r * H + c);
+            rb[u][n] = A.b ? ld4(A.b + r * H + c) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        rstd_s = 1.f / sqrtf(row_sum<LPR>(sqb) / (float)H + A.eps_s);
     }
 #pragma unroll
-    for (int n = 0; n < NV; ++n) {
-        const int c = (n * LPR + sl) * 4;
-        const float4 g = ld4(A.gamma + c), be = ld4(A.beta + c);
-        float4 o;
-        o.x = (v[n].x - mean) * rstd * g.x + be.x;
-        o.y = (v[n].y - mean) * rstd * g.y + be.y;
-        o.z = (v[n].z - mean) * rstd * g.z + be.z;
-        o.w = (v[n].w - mean) * rstd * g.w + be.w;
-        if (A.gamma_s) {   // same rounding as the reference's separate  y + LN_s(b)
-            const float4 gs = ld4(A.gamma_s + c), bs = ld4(A.beta_s + c);
-            o.x += (rb[n].x - mean_s) * rstd_s * gs.x + bs.x;
-            o.y += (rb[n].y - mean_s) * rstd_s * gs.y + bs.y;
-            o.z += (rb[n].z - mean_s) * rstd_s * gs.z + bs.z;
-            o.w += (rb[n].w - mean_s) * rstd_s * gs.w + bs.w;
+    for (int u = 0; u < U; ++u) {
+        const int64_t row = row0 + u * RPW;
+        const bool live = row < A.M;
+#pragma unroll
+        for (int n = 0; n < NV; ++n) {
+            const int c = (n * LPR + sl) * 4;
+            float4 x = v[u][n];
+            if (A.a_bias) {
+                const float4 ab = ld4(A.a_bias + c);
+                x.x += ab.x; x.y += ab.y; x.z += ab.z; x.w += ab.w;
+            }
+            x = drop4(A, x, row, c);
+            if (A.b) {
+                const float4 rr = rb[u][n];
+                x.x += rr.x; x.y += rr.y; x.z += rr.z; x.w += rr.w;
+                sum_b[u] += (rr.x + rr.y) + (rr.z + rr.w);
+            }
+            v[u][n] = x;
+            if (A.s_out && live) st4(A.s_out + row * H + c, x);
+            sum[u] += (x.x + x.y) + (x.z + x.w);
         }
-        Io<S>::st(A.y, row * A.ldy + c, o);     // y in the storage type (bf16 feeds a GEMM)
     }
-    if (A.ones_col && sl == 0) Io<S>::st(A.y, row * A.ldy + H, make_float4(1.f, 0.f, 0.f, 0.f));
-    if (sl == 0) {
-        A.mean[row] = mean;
-        A.rstd[row] = rstd;
-        if (A.gamma_s) {
-            A.mean_s[row] = mean_s;
-            A.rstd_s[row] = rstd_s;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t row = row0 + u * RPW;
+        const bool live = row < A.M;
+        const float mean = row_sum<LPR>(sum[u]) / (float)H;
+        float sq = 0.f;
+#pragma unroll
+        for (int n = 0; n < NV; ++n) {
+            const float dx = v[u][n].x - mean, dyv = v[u][n].y - mean, dz = v[u][n].z - mean, dw = v[u][n].w - mean;
+            sq += (dx * dx + dyv * dyv) + (dz * dz + dw * dw);
+        }
+        const float var = row_sum<LPR>(sq) / (float)H;
+        const float rstd = 1.f / sqrtf(var + A.eps);
+        float mean_s = 0.f, rstd_s = 0.f;
+        if (A.gamma_s) {                     // skip branch: statistics of b alone (two-pass, like the main one)
+            mean_s = row_sum<LPR>(sum_b[u]) / (float)H;
+            float sqb = 0.f;
+#pragma unroll
+            for (int n = 0; n < NV; ++n) {
+                const float dx = rb[u][n].x - mean_s, dyv = rb[u][n].y - mean_s, dz = rb[u][n].z - mean_s,
+                            dw = rb[u][n].w - mean_s;
+                sqb += (dx * dx + dyv * dyv) + (dz * dz + dw * dw);
+            }
+            rstd_s = 1.f / sqrtf(row_sum<LPR>(sqb) / (float)H + A.eps_s);
+        }
+        if (!live) continue;
+#pragma unroll
+        for (int n = 0; n < NV; ++n) {
+            const int c = (n * LPR + sl) * 4;
+            const float4 g = ld4(A.gamma + c), be = ld4(A.beta + c);
+            float4 o;
+            o.x = (v[u][n].x - mean) * rstd * g.x + be.x;
+            o.y = (v[u][n].y - mean) * rstd * g.y + be.y;
+            o.z = (v[u][n].z - mean) * rstd * g.z + be.z;
+            o.w = (v[u][n].w - mean) * rstd * g.w + be.w;
+            if (A.gamma_s) {   // same rounding as the reference's separate  y + LN_s(b)
+                const float4 gs = ld4(A.gamma_s + c), bs = ld4(A.beta_s + c);
+                o.x += (rb[u][n].x - mean_s) * rstd_s * gs.x + bs.x;
+                o.y += (rb[u][n].y - mean_s) * rstd_s * gs.y + bs.y;
+                o.z += (rb[u][n].z - mean_s) * rstd_s * gs.z + bs.z;
+                o.w += (rb[u][n].w - mean_s) * rstd_s * gs.w + bs.w;
+            }
+            Io<S>::st(A.y, row * A.ldy + c, o);     // y in the storage type (bf16 feeds a GEMM)
+        }
+        if (A.ones_col && sl == 0) Io<S>::st(A.y, row * A.ldy + H, make_float4(1.f, 0.f, 0.f, 0.f));
+        if (sl == 0) {
+            A.mean[row] = mean;
+            A.rstd[row] = rstd;
+            if (A.gamma_s) {
+                A.mean_s[row] = mean_s;
+                A.rstd_s[row] = rstd_s;
+            }
         }
     }
 }
 
-template <int LPR, int NV, typename S>
+template <int LPR, int NV, int U, typename S>
 __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
     constexpr int RPW = WAVE / LPR;
     __shared__ float red[BLK / WAVE][RPW][3 * 4 * NV * LPR];
@@ -162,48 +188,65 @@ __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
         dsa[n] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const int64_t nwaves = (int64_t)gridDim.x * (BLK / WAVE);
-    for (int64_t wave = blockIdx.x * (int64_t)(BLK / WAVE) + w; wave * RPW < A.M; wave += nwaves) {
-        const int64_t row = wave * RPW + sub;
-        const bool live = row < A.M;
-        const int64_t r = live ? row : 0;
-        const float mean = A.mean[r], rstd = A.rstd[r];
-        float4 xh[NV], gd[NV];
-        float c1 = 0.f, c2 = 0.f;
+    for (int64_t wave = blockIdx.x * (int64_t)(BLK / WAVE) + w; wave * (RPW * U) < A.M; wave += nwaves) {
+        float4 sv[U][NV], dv[U][NV], ev[U][NV];
+        float mean[U], rstd[U];
 #pragma unroll
-        for (int n = 0; n < NV; ++n) {
-            const int c = (n * LPR + sl) * 4;
-            const float4 s = ld4(A.s_in + r * H + c), d = ld4(A.dy + r * H + c), g = ld4(A.gamma + c);
-            xh[n] = make_float4((s.x - mean) * rstd, (s.y - mean) * rstd, (s.z - mean) * rstd, (s.w - mean) * rstd);
-            gd[n] = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
-            c1 += (gd[n].x * xh[n].x + gd[n].y * xh[n].y) + (gd[n].z * xh[n].z + gd[n].w * xh[n].w);
-            c2 += (gd[n].x + gd[n].y) + (gd[n].z + gd[n].w);
-            if (live) {
-                dg[n].x += d.x * xh[n].x; dg[n].y += d.y * xh[n].y; dg[n].z += d.z * xh[n].z; dg[n].w += d.w * xh[n].w;
-                db[n].x += d.x; db[n].y += d.y; db[n].z += d.z; db[n].w += d.w;
+        for (int u = 0; u < U; ++u) {        // every load of the U row groups first
+            const int64_t row = wave * (RPW * U) + u * RPW + sub;
+            const int64_t r = row < A.M ? row : A.M - 1;
+            mean[u] = A.mean[r];
+            rstd[u] = A.rstd[r];
+#pragma unroll
+            for (int n = 0; n < NV; ++n) {
+                const int c = (n * LPR + sl) * 4;
+                sv[u][n] = ld4(A.s_in + r * H + c);
+                dv[u][n] = ld4(A.dy + r * H + c);
+                ev[u][n] = (A.ds && A.dres) ? ld4(A.dres + r * H + c) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
-        c1 = row_sum<LPR>(c1) / (float)H;
-        c2 = row_sum<LPR>(c2) / (float)H;
-        if (!live) continue;
 #pragma unroll
-        for (int n = 0; n < NV; ++n) {
-            const int c = (n * LPR + sl) * 4;
-            float4 o;
-            o.x = rstd * (gd[n].x - c1 * xh[n].x - c2);
-            o.y = rstd * (gd[n].y - c1 * xh[n].y - c2);
-            o.z = rstd * (gd[n].z - c1 * xh[n].z - c2);
-            o.w = rstd * (gd[n].w - c1 * xh[n].w - c2);
-            if (A.da || A.want_dsa) {
-                const float4 a = drop4(A, o, row, c);
-                if (A.da) Io<S>::st(A.da, row * H + c, a);   // da in the storage type
-                dsa[n].x += a.x; dsa[n].y += a.y; dsa[n].z += a.z; dsa[n].w += a.w;
-            }
-            if (A.ds) {
-                if (A.dres) {
-                    const float4 e = ld4(A.dres + row * H + c);
-                    o.x += e.x; o.y += e.y; o.z += e.z; o.w += e.w;
+        for (int u = 0; u < U; ++u) {
+            const int64_t row = wave * (RPW * U) + u * RPW + sub;
+            const bool live = row < A.M;
+            float4 xh[NV], gd[NV];
+            float c1 = 0.f, c2 = 0.f;
+#pragma unroll
+            for (int n = 0; n < NV; ++n) {
+                const int c = (n * LPR + sl) * 4;
+                const float4 s = sv[u][n], d = dv[u][n], g = ld4(A.gamma + c);
+                const float m = mean[u], rs = rstd[u];
+                xh[n] = make_float4((s.x - m) * rs, (s.y - m) * rs, (s.z - m) * rs, (s.w - m) * rs);
+                gd[n] = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
+                c1 += (gd[n].x * xh[n].x + gd[n].y * xh[n].y) + (gd[n].z * xh[n].z + gd[n].w * xh[n].w);
+                c2 += (gd[n].x + gd[n].y) + (gd[n].z + gd[n].w);
+                if (live) {
+                    dg[n].x += d.x * xh[n].x; dg[n].y += d.y * xh[n].y; dg[n].z += d.z * xh[n].z; dg[n].w += d.w * xh[n].w;
+                    db[n].x += d.x; db[n].y += d.y; db[n].z += d.z; db[n].w += d.w;
                 }
-                st4(A.ds + row * H + c, o);
+            }
+            c1 = row_sum<LPR>(c1) / (float)H;
+            c2 = row_sum<LPR>(c2) / (float)H;
+            if (!live) continue;
+            const float rs = rstd[u];
+#pragma unroll
+            for (int n = 0; n < NV; ++n) {
+                const int c = (n * LPR + sl) * 4;
+                float4 o;
+                o.x = rs * (gd[n].x - c1 * xh[n].x - c2);
+                o.y = rs * (gd[n].y - c1 * xh[n].y - c2);
+                o.z = rs * (gd[n].z - c1 * xh[n].z - c2);
+                o.w = rs * (gd[n].w - c1 * xh[n].w - c2);
+                if (A.da || A.want_dsa) {
+                    const float4 a = drop4(A, o, row, c);
+                    if (A.da) Io<S>::st(A.da, row * H + c, a);   // da in the storage type
+                    dsa[n].x += a.x; dsa[n].y += a.y; dsa[n].z += a.z; dsa[n].w += a.w;
+                }
+                if (A.ds) {
+                    const float4 e = ev[u][n];
+                    o.x += e.x; o.y += e.y; o.z += e.z; o.w += e.w;
+                    st4(A.ds + row * H + c, o);
+                }
             }
         }
     }
@@ -239,14 +282,34 @@ bool geometry(int H, int& lpr, int& nv) {
 
 constexpr int LN_BWD_BLOCKS = 1024;
 
+// Row groups per wave (U).  Default 2 (best of 1/2/4 at C2 in tools/ln_probe.py); TAGAN_LN_ROWS = 1|2|4 overrides it
+// for A/B probes (read once).
+int ln_rows(int nv) {
+    static const int env = [] {
+        const char* e = getenv("TAGAN_LN_ROWS");
+        const int v = e ? atoi(e) : 0;
+        return (v == 1 || v == 2 || v == 4) ? v : 0;
+    }();
+    const int u = env ? env : 2;
+    return nv == 2 && u > 2 ? 2 : u;
+}
+
 template <typename S, bool FWD>
-void launch_ln(int lpr, int nv, dim3 g, hipStream_t s, const LnArgs& A) {
-#define TAGAN_LN_K(L, N) (FWD ? k_ln_fwd<L, N, S> : k_ln_bwd<L, N, S>)<<<g, BLK, 0, s>>>(A)
-    if (lpr == 8) TAGAN_LN_K(8, 1);
-    else if (lpr == 16) TAGAN_LN_K(16, 1);
-    else if (lpr == 32) TAGAN_LN_K(32, 1);
-    else if (nv == 1) TAGAN_LN_K(64, 1);
-    else TAGAN_LN_K(64, 2);
+void launch_ln(int lpr, int nv, int u, dim3 g, hipStream_t s, const LnArgs& A) {
+#define TAGAN_LN_K(L, N, U) (FWD ? k_ln_fwd<L, N, U, S> : k_ln_bwd<L, N, U, S>)<<<g, BLK, 0, s>>>(A)
+#define TAGAN_LN_U(L, N)                          \
+    do {                                          \
+        if (u == 1) TAGAN_LN_K(L, N, 1);          \
+        else if (u == 2) TAGAN_LN_K(L, N, 2);     \
+        else TAGAN_LN_K(L, N, 4);                 \
+    } while (0)
+    if (lpr == 8) TAGAN_LN_U(8, 1);
+    else if (lpr == 16) TAGAN_LN_U(16, 1);
+    else if (lpr == 32) TAGAN_LN_U(32, 1);
+    else if (nv == 1) TAGAN_LN_U(64, 1);
+    else if (u == 1) TAGAN_LN_K(64, 2, 1);
+    else TAGAN_LN_K(64, 2, 2);
+#undef TAGAN_LN_U
 #undef TAGAN_LN_K
 }
 
@@ -276,11 +339,12 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
     A.ldy = ldy > 0 ? ldy : H;
     TAGAN_REQUIRE(A.ldy >= H && A.ldy % 4 == 0, TAGAN_ERR_ARG, "layernorm_fwd: ldy %lld", (long long)ldy);
     A.ones_col = A.ldy >= H + 4;
-    const int64_t rpw = WAVE / lpr;
+    const int u = ln_rows(nv);
+    const int64_t rpw = (WAVE / lpr) * u;
     const dim3 g((unsigned)(((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE)));
     hipStream_t s = as_stream(stream);
-    if (dtype == TAGAN_BF16) launch_ln<bf16s, true>(lpr, nv, g, s, A);
-    else launch_ln<float, true>(lpr, nv, g, s, A);
+    if (dtype == TAGAN_BF16) launch_ln<bf16s, true>(lpr, nv, u, g, s, A);
+    else launch_ln<float, true>(lpr, nv, u, g, s, A);
     TAGAN_CHECK_LAUNCH("layernorm_fwd");
     return TAGAN_OK;
 }
@@ -301,9 +365,10 @@ int tagan_add_layernorm_skip_fwd(int64_t M, int32_t H, const float* a, const flo
     A.gamma = gamma; A.beta = beta; A.eps = eps; A.s_out = s_out; A.y = y; A.mean = mean; A.rstd = rstd;
     A.ldy = H;
     A.gamma_s = gamma_s; A.beta_s = beta_s; A.eps_s = eps_s; A.mean_s = mean_s; A.rstd_s = rstd_s;
-    const int64_t rpw = WAVE / lpr;
+    const int u = ln_rows(nv);
+    const int64_t rpw = (WAVE / lpr) * u;
     const dim3 g((unsigned)(((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE)));
-    launch_ln<float, true>(lpr, nv, g, as_stream(stream), A);
+    launch_ln<float, true>(lpr, nv, u, g, as_stream(stream), A);
     TAGAN_CHECK_LAUNCH("layernorm_skip_fwd");
     return TAGAN_OK;
 }
@@ -330,12 +395,13 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, cons
     A.dres = dres; A.ds = ds; A.da = da; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
     A.part = want ? (float*)workspace : nullptr;
     A.want_dsa = dsum_a != nullptr;
-    const int64_t rpw = WAVE / lpr;
+    const int u = ln_rows(nv);
+    const int64_t rpw = (WAVE / lpr) * u;
     const int64_t need = ((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE);
     const int nblk = (int)std::min<int64_t>(need, LN_BWD_BLOCKS);
     hipStream_t s = as_stream(stream);
-    if (dtype == TAGAN_BF16) launch_ln<bf16s, false>(lpr, nv, dim3(nblk), s, A);
-    else launch_ln<float, false>(lpr, nv, dim3(nblk), s, A);
+    if (dtype == TAGAN_BF16) launch_ln<bf16s, false>(lpr, nv, u, dim3(nblk), s, A);
+    else launch_ln<float, false>(lpr, nv, u, dim3(nblk), s, A);
     TAGAN_CHECK_LAUNCH("layernorm_bwd");
     if (dgamma || dbeta) {
         launch_colsum(A.part, nblk, 2 * H, dgamma, dbeta, H, s, 1.f, 3 * H);
