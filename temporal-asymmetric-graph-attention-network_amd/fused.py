@@ -254,6 +254,9 @@ OUT_BIAS_LN = os.environ.get("TAGAN_OUT_BIAS_LN", "1") != "0"
 # split-K slice height of the QKV weight gradient (3H outputs): taller slices than the out-projection's
 # 2048 (-> 2560 at C2) measured faster for N_out = 384 (tools/wgrad_probe.py); TAGAN_WGRAD_ROWS_QKV overrides
 WGRAD_ROWS_QKV = int(os.environ.get("TAGAN_WGRAD_ROWS_QKV", "8192"))
+# TAGAN_WGRAD_BIAS_AUG=0: QKV bias gradient by a column-sum pass over dqkv instead of the ones column of
+# LN1's augmented output riding through the weight-gradient GEMM (fp32 QKV_AUG form only; A/B)
+WGRAD_BIAS_AUG = os.environ.get("TAGAN_WGRAD_BIAS_AUG", "1") != "0"
 
 class AttnBlockFn(torch.autograd.Function):
     """y = LN2(dropout(out_proj(core(QKV(LN1(x))))) + x) with LayerNorm on both sides (use_layer_norm=True)."""
@@ -276,6 +279,7 @@ class AttnBlockFn(torch.autograd.Function):
             qkv = h_aug @ w_aug.t()
             h = h_aug[:, :H]
         else:
+            h_aug = None
             h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False,
                                         y_dtype=torch.bfloat16 if act else torch.float32)
             if bf:
@@ -294,14 +298,14 @@ class AttnBlockFn(torch.autograd.Function):
         else:
             y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True, a_bias=b_o_ln)
         ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
-        ctx.inter = (h, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
+        ctx.inter = (h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
         ctx.cfg = (core, p_out, seed_out, x.shape, bf, act)
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, ln1_w, w_qkv, w_o, ln2_w, lns_w = ctx.saved_tensors
-        h, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip = ctx.inter
+        h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip = ctx.inter
         core, p_out, seed_out, shape, bf, act = ctx.cfg
         ng = ctx.needs_input_grad
         dy2 = dy.reshape(-1, shape[-1]).contiguous()
@@ -314,11 +318,20 @@ class AttnBlockFn(torch.autograd.Function):
         dw_o = _wgrad(do, cg, bf) if ng[7] else None
         dqkv, dp1, dp2, db_core = core.bwd(qkv, c, saved, dc, ng[1], ng[2], want_bias_sum=bool(ng[6]))
         del dc, do
-        db_qkv = (db_core if db_core is not None else colsum(dqkv)) if ng[6] else None
+        H = shape[-1]
+        if db_core is None and ng[5] and ng[6] and h_aug is not None and WGRAD_BIAS_AUG:
+            # dqkvᵀ·[h | 1 0 0 0]: column H of the product is the column sum of dqkv (the bias gradient)
+            # -- 4 more GEMM columns instead of a 491 MB column-sum pass at C2
+            dw_aug = _wgrad(dqkv, h_aug, bf, WGRAD_ROWS_QKV)
+            dw_qkv, db_qkv = dw_aug[:, :H].contiguous(), dw_aug[:, H].contiguous()
+        else:
+            db_qkv = (db_core if db_core is not None else colsum(dqkv)) if ng[6] else None
+            dw_qkv = None
         if bf:
             dqkv = _b(dqkv)
         dh = _mm(dqkv, w_qkv, bf)
-        dw_qkv = _wgrad(dqkv, h, bf, WGRAD_ROWS_QKV) if ng[5] else None
+        if dw_qkv is None and ng[5]:
+            dw_qkv = _wgrad(dqkv, h, bf, WGRAD_ROWS_QKV)
         del dqkv
         dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
         ctx.inter = None
