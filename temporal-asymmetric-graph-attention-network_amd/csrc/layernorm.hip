@@ -280,7 +280,16 @@ bool geometry(int H, int& lpr, int& nv) {
     }
 }
 
-constexpr int LN_BWD_BLOCKS = 1024;
+// Backward grid (persistent blocks, one [3H] partial row each); TAGAN_LN_BWD_BLOCKS overrides it for
+// A/B probes (read once; 256..8192).
+int ln_bwd_blocks() {
+    static const int n = [] {
+        const char* e = getenv("TAGAN_LN_BWD_BLOCKS");
+        const int v = e ? atoi(e) : 0;
+        return (v >= 256 && v <= 8192) ? v : 1024;
+    }();
+    return n;
+}
 
 // Row groups per wave (U).  Default 2 (best of 1/2/4 at C2 in tools/ln_probe.py); TAGAN_LN_ROWS = 1|2|4 overrides it
 // for A/B probes (read once).
@@ -375,7 +384,7 @@ int tagan_add_layernorm_skip_fwd(int64_t M, int32_t H, const float* a, const flo
 
 size_t tagan_layernorm_bwd_workspace(int64_t M, int32_t H) {
     (void)M;
-    return (size_t)tagan::LN_BWD_BLOCKS * 3 * H * sizeof(float);
+    return (size_t)tagan::ln_bwd_blocks() * 3 * H * sizeof(float);
 }
 
 int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, const float* mean, const float* rstd,
@@ -398,7 +407,7 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, cons
     const int u = ln_rows(nv);
     const int64_t rpw = (WAVE / lpr) * u;
     const int64_t need = ((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE);
-    const int nblk = (int)std::min<int64_t>(need, LN_BWD_BLOCKS);
+    const int nblk = (int)std::min<int64_t>(need, ln_bwd_blocks());
     hipStream_t s = as_stream(stream);
     if (dtype == TAGAN_BF16) launch_ln<bf16s, false>(lpr, nv, u, dim3(nblk), s, A);
     else launch_ln<float, false>(lpr, nv, u, dim3(nblk), s, A);
