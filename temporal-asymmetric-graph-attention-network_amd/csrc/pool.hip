@@ -4,7 +4,7 @@
 //   gf[t] = mean(out.view(T, -1, H)[t]) = mean of node-major flat rows [t*N, (t+1)*N)
 // (flat row f = n*T + t'), which mixes nodes and steps.  Here the output is time-major
 // [T, N, H]; flat row f lives at time-major row (f % T)*N + f / T.  HBM-bound gather:
-// a group of H/4 lanes (float4) owns one row; block (t, s) sums slice s of chunk t
+// a group of H/4 lanes (float4) owns one row, 4 row loads in flight per lane; block (t, s) sums slice s of chunk t
 // into a partial, and the ordered column sum (k_colsum_parts) folds the slices —
 // deterministic.  Backward broadcasts g[t]/N back to the rows of chunk t.
 #include "common.cuh"
@@ -13,25 +13,52 @@ namespace tagan {
 namespace {
 
 constexpr int BLK = 256;
-constexpr int SLICES = 16;   // partial slices per chunk (T * 16 blocks: >= 512 at T = 32)
+constexpr int SLICES = 64;   // partial slices per chunk (T * 64 blocks: 2048 at T = 32, 8 waves per CU)
+constexpr int PU = 4;        // independent row loads in flight per thread
 
+// IDX = int32_t whenever T * N * H fits (every config here): the flat-row -> (step, node) split is a
+// 32-bit divide instead of a ~40-instruction 64-bit one per row.
+template <typename IDX>
 __global__ void __launch_bounds__(BLK) k_pool_fwd(const float* __restrict__ x, int T, int64_t N, int H,
                                                   int64_t ld_row, int64_t ld_t, float* __restrict__ part) {
     __shared__ float red[4 * BLK];   // rpb * H = 4 * BLK floats
     const int t = blockIdx.x / SLICES, sl = blockIdx.x % SLICES;
     const int lpr = H / 4, rpb = BLK / lpr;          // lanes per row, rows per block-iteration
     const int lane = threadIdx.x % lpr, rsub = threadIdx.x / lpr;
-    const int64_t f_beg = (int64_t)t * N, per = (N + SLICES - 1) / SLICES;
-    const int64_t a = f_beg + sl * per, b = f_beg + min<int64_t>(N, (int64_t)(sl + 1) * per);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t f = a + rsub; f < b; f += rpb) {
-        const int64_t tp = f % T, n = f / T;
-        const float4 v = *(const float4*)(x + tp * ld_t + n * ld_row + lane * 4);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    const IDX n_ = (IDX)N, t_ = (IDX)T;
+    const IDX f_beg = (IDX)t * n_, per = (n_ + SLICES - 1) / SLICES;
+    const IDX a = f_beg + (IDX)sl * per, b = f_beg + ((IDX)(sl + 1) * per < n_ ? (IDX)(sl + 1) * per : n_);
+    float4 acc[PU];
+#pragma unroll
+    for (int u = 0; u < PU; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    IDX f = a + rsub;
+    for (; f + (PU - 1) * rpb < b; f += PU * rpb) {
+        float4 v[PU];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            const IDX ff = f + u * rpb, tp = ff % t_, n = ff / t_;
+            v[u] = *(const float4*)(x + (int64_t)tp * ld_t + (int64_t)n * ld_row + lane * 4);
+        }
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+        }
     }
+#pragma unroll
+    for (int u = 0; u < PU - 1; ++u) {               // tail: fewer than PU rows left for this thread
+        const IDX ff = f + u * rpb;
+        if (ff < b) {
+            const IDX tp = ff % t_, n = ff / t_;
+            const float4 v = *(const float4*)(x + (int64_t)tp * ld_t + (int64_t)n * ld_row + lane * 4);
+            acc[u].x += v.x; acc[u].y += v.y; acc[u].z += v.z; acc[u].w += v.w;
+        }
+    }
+    float4 tot = acc[0];
+#pragma unroll
+    for (int u = 1; u < PU; ++u) { tot.x += acc[u].x; tot.y += acc[u].y; tot.z += acc[u].z; tot.w += acc[u].w; }
     // fixed-order block reduction over the rpb row groups
     float* r = red;
-    *(float4*)(r + (size_t)rsub * H + lane * 4) = acc;
+    *(float4*)(r + (size_t)rsub * H + lane * 4) = tot;
     __syncthreads();
     for (int c = threadIdx.x; c < H; c += BLK) {
         float s = 0.f;
@@ -40,18 +67,20 @@ __global__ void __launch_bounds__(BLK) k_pool_fwd(const float* __restrict__ x, i
     }
 }
 
+template <typename IDX>
 __global__ void __launch_bounds__(BLK) k_pool_bwd(const float* __restrict__ g, int T, int64_t N, int H,
                                                   float inv_n, float* __restrict__ dx, int64_t ld_row,
                                                   int64_t ld_t) {
-    const int lpr = H / 4;
-    const int64_t rows = (int64_t)T * N;
-    for (int64_t i = blockIdx.x * (int64_t)BLK + threadIdx.x; i < rows * lpr; i += (int64_t)gridDim.x * BLK) {
-        const int64_t row = i / lpr;            // time-major row = t'*N + n
-        const int c = (int)(i % lpr) * 4;
-        const int64_t tp = row / N, n = row % N;
-        const int64_t chunk = (n * T + tp) / N;
-        const float4 v = *(const float4*)(g + chunk * H + c);
-        *(float4*)(dx + tp * ld_t + n * ld_row + c) = make_float4(v.x * inv_n, v.y * inv_n, v.z * inv_n, v.w * inv_n);
+    const IDX lpr = H / 4, n_ = (IDX)N, t_ = (IDX)T;
+    const IDX total = t_ * n_ * lpr;
+    for (IDX i = blockIdx.x * (IDX)BLK + threadIdx.x; i < total; i += (IDX)gridDim.x * BLK) {
+        const IDX row = i / lpr;                // time-major row = t'*N + n
+        const int c = (int)(i - row * lpr) * 4;
+        const IDX tp = row / n_, n = row - tp * n_;
+        const IDX chunk = (n * t_ + tp) / n_;
+        const float4 v = *(const float4*)(g + (int64_t)chunk * H + c);
+        *(float4*)(dx + (int64_t)tp * ld_t + (int64_t)n * ld_row + c) =
+            make_float4(v.x * inv_n, v.y * inv_n, v.z * inv_n, v.w * inv_n);
     }
 }
 
@@ -72,7 +101,8 @@ int tagan_pool_fwd(int dtype, int32_t T, int64_t N, int32_t H, const float* x, i
     TAGAN_REQUIRE(workspace && workspace_bytes >= tagan_pool_workspace(T, H), TAGAN_ERR_WORKSPACE, "pool: ws");
     hipStream_t s = as_stream(stream);
     float* part = (float*)workspace;
-    k_pool_fwd<<<T * SLICES, BLK, 0, s>>>(x, T, N, H, ld_row, ld_t, part);
+    if ((int64_t)T * N * H < ((int64_t)1 << 31)) k_pool_fwd<int32_t><<<T * SLICES, BLK, 0, s>>>(x, T, N, H, ld_row, ld_t, part);
+    else k_pool_fwd<int64_t><<<T * SLICES, BLK, 0, s>>>(x, T, N, H, ld_row, ld_t, part);
     TAGAN_CHECK_LAUNCH("pool_fwd");
     // ordered sum over slices, times the 1/N of the mean
     launch_colsum(part, SLICES, T * H, out, nullptr, T * H, s, 1.f / (float)N);
@@ -87,7 +117,9 @@ int tagan_pool_bwd(int dtype, int32_t T, int64_t N, int32_t H, const float* g, f
     TAGAN_REQUIRE(T > 0 && N > 0 && H % 4 == 0 && g && dx, TAGAN_ERR_ARG, "pool_bwd: bad args");
     const int64_t work = (int64_t)T * N * (H / 4);
     const int grid = (int)std::min<int64_t>((work + BLK - 1) / BLK, 256 * 64);
-    k_pool_bwd<<<grid, BLK, 0, as_stream(stream)>>>(g, T, N, H, 1.f / (float)N, dx, ld_row, ld_t);
+    if ((int64_t)T * N * H < ((int64_t)1 << 31))
+        k_pool_bwd<int32_t><<<grid, BLK, 0, as_stream(stream)>>>(g, T, N, H, 1.f / (float)N, dx, ld_row, ld_t);
+    else k_pool_bwd<int64_t><<<grid, BLK, 0, as_stream(stream)>>>(g, T, N, H, 1.f / (float)N, dx, ld_row, ld_t);
     TAGAN_CHECK_LAUNCH("pool_bwd");
     return TAGAN_OK;
 }
