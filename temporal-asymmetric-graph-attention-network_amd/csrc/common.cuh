@@ -135,40 +135,44 @@ struct Io<bf16s> {
 };
 
 // Deterministic column sums of a [nblk, n] (row stride ld) partials table (per-block dγ/dβ, bias-table
-// grads): one 1024-thread block per 64 columns, wave w sums rows w, w+16, ... with four
-// independent accumulators (loads in flight), then a fixed-order LDS tree.  Column x < split
-// goes to out0[x], the rest to out1[x - split] (either may be null), times ``scale``.
+// grads): one 1024-thread block per CS_CW = 16 columns (a wave-instruction reads 4 rows x 64 B), so a
+// 256-column table spreads over 16 CUs instead of 4; lane (w, rsub) sums rows w*4+rsub, +64, ... with
+// four independent accumulators (loads in flight), then one fixed-order LDS pass per column.
+// Column x < split goes to out0[x], the rest to out1[x - split] (either may be null), times ``scale``.
 constexpr int COLSUM_BLK = 1024;
+constexpr int CS_CW = 16;
 namespace {
 __global__ void __launch_bounds__(COLSUM_BLK) k_colsum_parts(const float* __restrict__ part, int nblk, int n,
                                                             float* __restrict__ out0, float* __restrict__ out1,
                                                             int split, float scale, int64_t ld) {
-    constexpr int NW = COLSUM_BLK / WAVE;
-    __shared__ float red[NW][WAVE];
+    constexpr int RPI = WAVE / CS_CW;                 // rows per wave-instruction
+    constexpr int NR = (COLSUM_BLK / WAVE) * RPI;     // row lanes per block
+    __shared__ float red[NR][CS_CW];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x >> 6;
-    const int x = blockIdx.x * WAVE + lane;
+    const int col = lane % CS_CW, r0 = w * RPI + lane / CS_CW;
+    const int x = blockIdx.x * CS_CW + col;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (x < n) {
-        int b = w;
-        for (; b + 3 * NW < nblk; b += 4 * NW) {
+        int b = r0;
+        for (; b + 3 * NR < nblk; b += 4 * NR) {
             s0 += part[(int64_t)b * ld + x];
-            s1 += part[(int64_t)(b + NW) * ld + x];
-            s2 += part[(int64_t)(b + 2 * NW) * ld + x];
-            s3 += part[(int64_t)(b + 3 * NW) * ld + x];
+            s1 += part[(int64_t)(b + NR) * ld + x];
+            s2 += part[(int64_t)(b + 2 * NR) * ld + x];
+            s3 += part[(int64_t)(b + 3 * NR) * ld + x];
         }
-        for (; b < nblk; b += NW) s0 += part[(int64_t)b * ld + x];
+        for (; b < nblk; b += NR) s0 += part[(int64_t)b * ld + x];
     }
-    red[w][lane] = (s0 + s1) + (s2 + s3);
+    red[r0][col] = (s0 + s1) + (s2 + s3);
     __syncthreads();
-#pragma unroll
-    for (int half = NW / 2; half > 0; half >>= 1) {
-        if (w < half) red[w][lane] += red[w + half][lane];
-        __syncthreads();
-    }
-    if (w == 0 && x < n) {
-        const float v = scale == 1.f ? red[0][lane] : red[0][lane] * scale;
-        if (x < split) { if (out0) out0[x] = v; }
-        else if (out1) out1[x - split] = v;
+    if (threadIdx.x < CS_CW) {
+        const int xo = blockIdx.x * CS_CW + threadIdx.x;
+        float v = 0.f;
+        for (int r = 0; r < NR; ++r) v += red[r][threadIdx.x];
+        if (xo < n) {
+            if (scale != 1.f) v *= scale;
+            if (xo < split) { if (out0) out0[xo] = v; }
+            else if (out1) out1[xo - split] = v;
+        }
     }
 }
 
@@ -177,7 +181,7 @@ __global__ void __launch_bounds__(COLSUM_BLK) k_colsum_parts(const float* __rest
 // ld = row stride of the partials table (default n)
 static inline void launch_colsum(const float* part, int nblk, int n, float* out0, float* out1, int split,
                                  hipStream_t s, float scale = 1.f, int64_t ld = -1) {
-    k_colsum_parts<<<(n + WAVE - 1) / WAVE, COLSUM_BLK, 0, s>>>(part, nblk, n, out0, out1, split, scale,
+    k_colsum_parts<<<(n + CS_CW - 1) / CS_CW, COLSUM_BLK, 0, s>>>(part, nblk, n, out0, out1, split, scale,
                                                                 ld < 0 ? n : ld);
 }
 
