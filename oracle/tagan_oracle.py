@@ -222,7 +222,7 @@ def time_basis_bias(time_stamps, P, name, num_heads, hidden_dim):
         tn = torch.zeros_like(diffs)
     mu = P[name + ".time_encoding.basis_mu"]
     sigma = P[name + ".time_encoding.basis_sigma"]
-    if float(sigma.min()) < 1e-7:
+    if float(sigma.detach().min()) < 1e-7:
         sigma = torch.clamp(sigma, min=1e-7)
     expo = torch.clamp(-(((tn.unsqueeze(-1) - mu) ** 2) / (2 * sigma ** 2)), -88.0, 88.0)
     basis = torch.nan_to_num(torch.exp(expo), nan=0.0)
