@@ -1,6 +1,6 @@
 """TAGAN training-step benchmark on MI355X (graph-snapshots/s, fwd+bwd+optimizer).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--shard] [--roofline-only]
   (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N ... bench.py --gpus N)
 
 One step = one TAGAN sequence (all T snapshots) per rank: forward, BCE loss,
@@ -9,11 +9,19 @@ the reference trainer's step (trainer.py:295-311).  Inputs are synthetic, seeded
 per rank and resident in HBM before timing; the snapshot CSR is rebuilt inside
 every step.  Prints ONE JSON line on rank 0.
 
-roofline: the edge-softmax + aggregate kernels (tagan_geo_attn fwd, bwd-row,
-bwd-col) re-launched on the benchmark's own graph and Q/K/V, timed with HIP
-events on the launch stream; achieved = algorithmic bytes ÷
-time, peak = 8.0 TB/s.  cpu_baseline: the CPU oracle (oracle/, sparse CSR
-restatement of the reference algorithm) on a bounded sample, rank 0, N=1 only.
+``--gpus N`` with N > 1 outside torchrun re-launches itself under ``torch.distributed.run`` with N ranks
+(before anything touches the GPU); under torchrun (the driver's form) WORLD_SIZE must equal N.
+
+roofline: the edge-softmax + aggregate kernels (tagan_geo_attn fwd, bwd-row, bwd-col;
+geometric_attention.py:332-516 + :579-583) on a cache-cold C4 snapshot (SURVEY §8(d)'s roofline
+configuration: 1M nodes, 20M uniform edges, H=128, 4 heads, fp32), timed with HIP events on the launch
+stream; achieved = SURVEY §8(d)'s algorithmic bytes ÷ time, peak = 8.0 TB/s; traffic = the PMC HBM bytes
+of the same launches (profiles/pmc_c4.json).  The same kernels on the bench's own C2 graph are reported
+beside it as ``cache_assisted`` (C2's gathers are served partly by L2 / Infinity Cache).
+cpu_baseline: the CPU oracle (oracle/, restatements of the reference algorithm) on bounded samples,
+rank 0, N=1 only: sparse CSR at C2 (the headline ratio), and at C1 both sparse and dense_faithful (the
+reference's own dense N×N mask + per-(head, node) loop, cross-checked against the literal reference in
+profiles/r2_cpu_crosscheck.json), next to a GPU C1 step measured here.
 """
 import argparse
 import json
@@ -49,90 +57,139 @@ def parse():
     ap.add_argument("--tune-gemms", action="store_true",
                     help="time every GEMM solution of the shapes missing from the table; write the table at exit")
     ap.add_argument("--gemm-table", default=None, help="TunableOp table path (default: the shipped one)")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the C4 roofline launches (for rocprofv3 kernel-trace / PMC passes of the same kernels)")
+    ap.add_argument("--roofline-reps", type=int, default=10)
+    ap.add_argument("--no-c1", action="store_true", help="skip the GPU C1 line beside the C1 CPU baselines")
     ap.add_argument("--shard", action="store_true",
                     help="one sequence sharded by snapshot over all ranks (strong scaling; C5 mode) instead of "
                          "one sequence per rank (data parallel, weak scaling)")
     return ap.parse_args()
 
 
-def geo_bytes(E, N, H, heads, s=4):
-    """Algorithmic HBM bytes of one geometric-attention layer pass (fwd, bwd) over N nodes / E CSR entries."""
-    fwd = s * H * (2 * E + 2 * N) + 4 * (E + N) + 4 * heads * N
-    bwd_row = s * H * (2 * E + 4 * N) + 4 * (E + N) + 8 * heads * N
-    bwd_col = s * H * (2 * E + 4 * N) + 8 * E + 4 * N + 8 * heads * E
-    return fwd, bwd_row + bwd_col
+def geo_bytes(E, N, H, heads=None, s=4):
+    """SURVEY §8(d)'s algorithmic HBM bytes of one geometric layer over N nodes / E' CSR entries:
+    B_fwd = s·H·(2E' + 2N) + 4(E' + N) (K_j, V_j gathered per edge; Q_i read, O_i written; CSR col + rowptr);
+    B_bwd = s·H·(4E' + 8N) + 8(E' + N) (CSR pass gathers K_j, V_j; CSC pass gathers Q_i, dO_i; per node Q, K, V,
+    O, dO read and dQ, dK, dV written; CSR + CSC indices)."""
+    fwd = s * H * (2 * E + 2 * N) + 4 * (E + N)
+    bwd = s * H * (4 * E + 8 * N) + 8 * (E + N)
+    return fwd, bwd
 
 
-def roofline(model, seq, cfg, reps=20):
-    """Time the three edge kernels on the benchmark graph with HIP events on the launch stream."""
-    import ctypes
-    import tagan_amd
-    from tagan_amd import _lib
-    from tagan_amd.kernels import build_graph
-    dev = seq[0][0].device
-    counts = [int(x.shape[0]) for x, _, _, _ in seq]
-    graph = build_graph([ei for _, ei, _, _ in seq], counts)
-    N, H, heads = graph.num_nodes, cfg.hidden_dim, cfg.num_heads
-    d = H // heads
-    E = graph.nnz_host()
-    g = torch.Generator(device=dev).manual_seed(7)
-    qkv = torch.randn(N, 3 * H, device=dev, generator=g)
-    dout = torch.randn(N, H, device=dev, generator=g)
-    out = torch.empty(N, H, device=dev)
-    lse = torch.empty(N, heads, device=dev)
-    dqkv = torch.empty_like(qkv)
-    L = _lib.lib()
-    gs = graph.struct()
-    fwb = L.tagan_geo_attn_fwd_workspace(gs, heads, d)
-    fws = torch.empty(max(int(fwb), 1), dtype=torch.uint8, device=dev)
-    wsb = L.tagan_geo_attn_bwd_workspace(gs, heads, d)
-    ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sp = ctypes.c_void_p(stream.cuda_stream)
-    b, es = qkv.data_ptr(), 4
-    db = dqkv.data_ptr()
-    metric = 6 if cfg.learnable_distance else 0
-    p = float(cfg.dropout)
+class EdgeKernels:
+    """The edge-softmax + aggregate launches of one geometric layer (fwd; bwd row + col passes) through the
+    C-ABI on a graph, random Q|K|V and dO, launched on the current stream."""
 
-    def fwd():
-        _lib.check(L.tagan_geo_attn_fwd(0, metric, gs, heads, d, b, b + H * es, b + 2 * H * es, 3 * H, None, p,
-                                        1234, _lib.ptr(out), _lib.ptr(lse), None, _lib.ptr(fws), fwb, sp), "fwd")
+    def __init__(self, graph, H, heads, p_drop, metric=0):
+        import ctypes
+        from tagan_amd import _lib
+        dev = graph.rowptr.device
+        self.graph, self.H, self.heads, self.p, self.metric = graph, H, heads, float(p_drop), metric
+        self.N, self.d = graph.num_nodes, H // heads
+        self.E = graph.nnz_host()
+        g = torch.Generator(device=dev).manual_seed(7)
+        self.qkv = torch.randn(self.N, 3 * H, device=dev, generator=g)
+        self.dout = torch.randn(self.N, H, device=dev, generator=g)
+        self.out = torch.empty(self.N, H, device=dev)
+        self.lse = torch.empty(self.N, heads, device=dev)
+        self.dqkv = torch.empty_like(self.qkv)
+        L = self.L = _lib.lib()
+        self.gs = graph.struct()
+        self.fwb = L.tagan_geo_attn_fwd_workspace(self.gs, heads, self.d)
+        self.fws = torch.empty(max(int(self.fwb), 1), dtype=torch.uint8, device=dev)
+        self.wsb = L.tagan_geo_attn_bwd_workspace(self.gs, heads, self.d)
+        self.ws = torch.empty(max(int(self.wsb), 1), dtype=torch.uint8, device=dev)
+        self.stream = torch.cuda.current_stream(dev)
+        self.sp = ctypes.c_void_p(self.stream.cuda_stream)
 
-    def bwd():
-        _lib.check(L.tagan_geo_attn_bwd(0, metric, gs, heads, d, b, b + H * es, b + 2 * H * es, 3 * H, None, p,
-                                        1234, _lib.ptr(out), _lib.ptr(lse), _lib.ptr(dout), db, db + H * es,
-                                        db + 2 * H * es, 3 * H, None, _lib.ptr(ws), wsb, sp), "bwd")
+    def fwd(self):
+        from tagan_amd import _lib
+        b, es, H = self.qkv.data_ptr(), 4, self.H
+        _lib.check(self.L.tagan_geo_attn_fwd(0, self.metric, self.gs, self.heads, self.d, b, b + H * es, b + 2 * H * es,
+                                             3 * H, None, self.p, 1234, _lib.ptr(self.out), _lib.ptr(self.lse), None,
+                                             _lib.ptr(self.fws), self.fwb, self.sp), "fwd")
 
-    for _ in range(3):
-        fwd()
-        bwd()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    tf = tb = 0.0
-    for _ in range(reps):
-        ev[0].record(stream)
-        fwd()
-        ev[1].record(stream)
-        bwd()
-        ev[2].record(stream)
-        ev[2].synchronize()
-        tf += ev[0].elapsed_time(ev[1])
-        tb += ev[1].elapsed_time(ev[2])
-    tf, tb = tf / reps * 1e-3, tb / reps * 1e-3
-    bf, bb = geo_bytes(E, N, H, heads)
-    achieved = (bf + bb) / (tf + tb) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % os.environ.get("TAGAN_BENCH_CONFIG", "c2"))
+    def bwd(self):
+        from tagan_amd import _lib
+        b, db, es, H = self.qkv.data_ptr(), self.dqkv.data_ptr(), 4, self.H
+        _lib.check(self.L.tagan_geo_attn_bwd(0, self.metric, self.gs, self.heads, self.d, b, b + H * es, b + 2 * H * es,
+                                             3 * H, None, self.p, 1234, _lib.ptr(self.out), _lib.ptr(self.lse),
+                                             _lib.ptr(self.dout), db, db + H * es, db + 2 * H * es, 3 * H, None,
+                                             _lib.ptr(self.ws), self.wsb, self.sp), "bwd")
+
+    def time(self, reps):
+        """Mean fwd / bwd launch-group durations (s), HIP events on the launch stream, after 2 warm-ups."""
+        for _ in range(2):
+            self.fwd()
+            self.bwd()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        tf = tb = 0.0
+        for _ in range(reps):
+            ev[0].record(self.stream)
+            self.fwd()
+            ev[1].record(self.stream)
+            self.bwd()
+            ev[2].record(self.stream)
+            ev[2].synchronize()
+            tf += ev[0].elapsed_time(ev[1])
+            tb += ev[1].elapsed_time(ev[2])
+        return tf / reps * 1e-3, tb / reps * 1e-3
+
+
+def _pmc_traffic(config):
+    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % config)
     if os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch_group")
-    return {"kernel": "tagan_geo_attn fwd+bwd_row+bwd_col (edge-softmax + aggregate, one layer)",
-            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "algorithmic_bytes": int(bf + bb), "edges": E, "nodes": N,
-            "ms_fwd": round(tf * 1e3, 4), "ms_bwd": round(tb * 1e3, 4),
-            "note": "achieved = algorithmic bytes / kernel time; at C2 the L2 and Infinity Cache serve part of "
-                    "the gathered K|V rows (traffic = PMC HBM bytes), so achieved can pass the HBM peak; C4 is "
-                    "the cache-cold case (DESIGN.md section 4)"}
+            return json.load(f).get("hbm_bytes_per_launch_group")
+    return None
+
+
+def roofline_c4(reps=10):
+    """The ≥40 %-of-HBM gate configuration: one C4 snapshot, 1M nodes, 20M uniform-random edges
+    (worst-case gather locality; Q|K|V = 1.5 GB, far beyond the 256 MB Infinity Cache), H=128, 4 heads, fp32,
+    dropout 0.1, euclidean metric."""
+    from tagan_amd import synthetic
+    from tagan_amd.kernels import build_graph
+    dev = torch.device("cuda", torch.cuda.current_device())
+    N, E, _T, H, heads = synthetic.CONFIGS["c4"][:5]
+    seq = synthetic.make_sequence("c4", dev, seed=4000, snapshots=1)
+    graph = build_graph([seq[0][1]], [N])
+    del seq
+    k = EdgeKernels(graph, H, heads, 0.1)
+    tf, tb = k.time(reps)
+    bf, bb = geo_bytes(k.E, k.N, H)
+    achieved = (bf + bb) / (tf + tb) / 1e9
+    traffic = _pmc_traffic("c4")
+    rec = {"kernel": "tagan_geo_attn fwd (k_geo_fwd_chunk + merge) + bwd (k_geo_bwd_row_chunk + k_geo_bwd_col_chunk "
+                     "+ 2 k_geo_sum_parts): edge-softmax + aggregate of one layer, one C4 snapshot",
+           "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+           "algorithmic_bytes": int(bf + bb), "bytes_fwd": int(bf), "bytes_bwd": int(bb),
+           "edges": k.E, "nodes": k.N, "H": H, "heads": heads, "dtype": "fp32",
+           "ms_fwd": round(tf * 1e3, 4), "ms_bwd": round(tb * 1e3, 4), "reps": reps,
+           "formula": "SURVEY 8(d): B_fwd = s*H*(2E'+2N) + 4(E'+N), B_bwd = s*H*(4E'+8N) + 8(E'+N), s = 4",
+           "config": "c4 (1M nodes, 20M uniform edges, cache-cold)"}
+    if traffic:
+        rec["traffic_frac"] = round(traffic / (tf + tb) / 1e9 / HBM_PEAK_GBS, 4)
+    del k, graph
+    torch.cuda.empty_cache()
+    return rec
+
+
+def roofline_cache_assisted(seq, cfg, reps=20):
+    """The same launches on the bench's own C2 graph (all 32 snapshots): L2 / Infinity Cache serve part of the
+    gathered K|V rows, so algorithmic bytes / time can pass the HBM peak -- an effective bandwidth, not a
+    roofline fraction."""
+    from tagan_amd.kernels import build_graph
+    graph = build_graph([ei for _, ei, _, _ in seq], [int(x.shape[0]) for x, _, _, _ in seq])
+    k = EdgeKernels(graph, cfg.hidden_dim, cfg.num_heads, cfg.dropout, 6 if cfg.learnable_distance else 0)
+    tf, tb = k.time(reps)
+    bf, bb = geo_bytes(k.E, k.N, cfg.hidden_dim)
+    eff = (bf + bb) / (tf + tb) / 1e9
+    return {"effective_gbs": round(eff, 1), "effective_over_peak": round(eff / HBM_PEAK_GBS, 4),
+            "traffic": _pmc_traffic("c2"), "algorithmic_bytes": int(bf + bb), "edges": k.E, "nodes": k.N,
+            "ms_fwd": round(tf * 1e3, 4), "ms_bwd": round(tb * 1e3, 4)}
 
 
 def breakdown(model, seq, fwd, bwd, opt, cfg, reps=5):
@@ -166,47 +223,167 @@ def breakdown(model, seq, fwd, bwd, opt, cfg, reps=5):
     return res
 
 
-def cpu_baseline(cfg, name, model_state, n_snap, min_seconds=10.0):
-    """CPU oracle (sparse CSR restatement of the reference) on a bounded sample of the same workload:
-    whole sequences of ``n_snap`` snapshots, fwd+bwd, repeated until ``min_seconds`` of CPU work."""
+def _host_cores():
+    """Threads for the CPU legs: the box's CPU share (OMP_NUM_THREADS, 16 per GPU on the pool) or the affinity
+    mask, whichever is smaller; plus what the host reports (nproc, CPU model) for the record."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(aff, omp) if omp > 0 else aff
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return threads, {"nproc": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": omp or None,
+                     "cpu_model": model}
+
+
+def _oracle_rate(P, c, seq, lab, mode, min_seconds, max_reps=1000):
     import oracle
+    n = len(seq)
+    done, t0 = 0, time.perf_counter()
+    reps = 0
+    while True:
+        out = oracle.tagan_forward(P, c, seq, lab, mode=mode)
+        out["loss"].backward()
+        done += n
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= min_seconds or reps >= max_reps:
+            return done / dt, done, dt
+
+
+def cpu_baseline(cfg, name, model_state, n_snap, gpu_c1=None, gpu_value=None, min_seconds=8.0):
+    """CPU oracle on bounded samples of the workloads, fwd+bwd (no optimizer), fp32, on the host's cores:
+
+    * ``value``: sparse CSR restatement on ``n_snap``-snapshot sequences of the bench's own config (C2) — the
+      strong CPU baseline of the headline;
+    * ``c1.dense_faithful``: the reference's own algorithm and cost model (dense N×N mask, per-(head, node)
+      distance loop; geometric_attention.py:386-401, graph_attention.py:96-105) on one whole C1 sequence —
+      matched to the literal reference within 10 % in this container (profiles/r2_cpu_crosscheck.json);
+    * ``c1.sparse``: the sparse restatement on the same C1 sequence.
+    """
     from tagan_amd import synthetic
-    threads = min(16, os.cpu_count() or 1)
+    threads, host = _host_cores()
     torch.set_num_threads(threads)
+    lab = torch.tensor([1.0])
     seq = synthetic.make_sequence(name, "cpu", seed=42, snapshots=n_snap)
     P = {k: v.detach().cpu().clone().requires_grad_(v.is_floating_point()) for k, v in model_state.items()}
     c = cfg.to_dict()
-    lab = torch.tensor([1.0])
     small = synthetic.make_sequence(name, "cpu", seed=1, snapshots=1, nodes=500, edges=2000)
+    import oracle
     oracle.tagan_forward(P, c, small, lab)["loss"].backward()            # warm-up
-    done, t0 = 0, time.perf_counter()
-    while True:
-        out = oracle.tagan_forward(P, c, seq, lab)
-        out["loss"].backward()
-        done += n_snap
-        dt = time.perf_counter() - t0
-        if dt >= min_seconds:
-            break
-    return {"value": round(done / dt, 4), "unit": "graph-snapshots/s", "cores": threads, "kind": "port",
-            "sample": "oracle sparse-CSR restatement, fwd+bwd (no optimizer), %s shape, %d-snapshot sequences "
-                      "x %d (%d snapshots) in %.1f s, fp32" % (name, n_snap, done // n_snap, done, dt)}
+    rate, done, dt = _oracle_rate(P, c, seq, lab, "sparse", min_seconds)
+    rec = {"value": round(rate, 4), "unit": "graph-snapshots/s", "cores": threads, "kind": "port",
+           "sample": "oracle sparse-CSR restatement, fwd+bwd (no optimizer), %s shape, %d-snapshot sequences "
+                     "x %d (%d snapshots) in %.1f s, fp32, %d threads" % (name, n_snap, done // n_snap, done, dt, threads),
+           "host": host}
+    if gpu_value:
+        rec["gpu_over_cpu"] = round(gpu_value / rate, 1)
+    # C1: the reference's own configuration (example.py), the only one the literal reference runs in full
+    c1cfg = synthetic.config_for("c1")
+    torch.manual_seed(0)
+    from tagan_amd import TAGAN
+    m1 = TAGAN(c1cfg)
+    P1 = {k: v.detach().clone().requires_grad_(v.is_floating_point()) for k, v in m1.state_dict().items()}
+    seq1 = synthetic.make_sequence("c1", "cpu", seed=42)
+    c1 = c1cfg.to_dict()
+    oracle.tagan_forward(P1, c1, seq1[:2], lab, mode="dense_faithful")["loss"].backward()   # warm-up
+    df_rate, df_done, df_dt = _oracle_rate(P1, c1, seq1, lab, "dense_faithful", 0.0, max_reps=1)
+    sp_rate, sp_done, sp_dt = _oracle_rate(P1, c1, seq1, lab, "sparse", 2.0)
+    c1rec = {"dense_faithful": {"value": round(df_rate, 4), "unit": "graph-snapshots/s", "kind": "port",
+                                "sample": "one C1 sequence (10 snapshots of 500 nodes) in %.1f s" % df_dt},
+             "sparse": {"value": round(sp_rate, 4), "unit": "graph-snapshots/s", "kind": "port",
+                        "sample": "%d C1 sequences in %.1f s" % (sp_done // 10, sp_dt)},
+             "literal_reference_crosscheck": "profiles/r2_cpu_crosscheck.json (container, 8 threads)"}
+    if gpu_c1:
+        c1rec["gpu"] = gpu_c1
+        c1rec["gpu_over_dense_faithful"] = round(gpu_c1["value"] / df_rate, 1)
+        c1rec["gpu_over_sparse"] = round(gpu_c1["value"] / sp_rate, 1)
+    rec["c1"] = c1rec
+    return rec
+
+
+def make_step(model, opt, cfg, fwd, bwd):
+    def step():
+        opt.zero_grad(set_to_none=True)
+        out = fwd()
+        bwd(out)
+        torch.nn.utils.clip_grad_norm_(model.parameters(), cfg.gradient_clip_val)
+        opt.step()
+        return out["loss"]
+    return step
+
+
+def gpu_c1_line(dev, precision, steps=20, warmup=5):
+    """The same training step on C1 (example.py: 500 nodes, 1000 edges, 10 snapshots, H=64, 4 heads) on this GPU,
+    beside the C1 CPU baselines (host-launch-bound at this size)."""
+    from tagan_amd import TAGAN, synthetic
+    cfg = synthetic.config_for("c1")
+    torch.manual_seed(0)
+    model = TAGAN(cfg, precision=precision).to(dev).train()
+    opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay)
+    seq = synthetic.make_sequence("c1", dev, seed=1000)
+    labels = torch.tensor([1.0], device=dev)
+    step = make_step(model, opt, cfg, lambda: model(seq, labels=labels), lambda out: out["loss"].backward())
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    T = len(seq)
+    return {"value": round(T * steps / el, 3), "unit": "graph-snapshots/s", "ms_per_step": round(el / steps * 1e3, 3),
+            "steps": steps, "dtype": precision}
+
+
+def _relaunch(n):
+    """``--gpus N`` outside torchrun: run this script under torch.distributed.run with N ranks (no GPU call has
+    happened in this process) and exit with its status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_relaunch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     import tagan_amd
     from tagan_amd import TAGAN, synthetic
     from tagan_amd.distributed import GradBucket, broadcast_parameters
     from tagan_amd.gemm_tuning import use_tuned_gemms
+    if args.roofline_only:
+        print(json.dumps({"roofline": roofline_c4(args.roofline_reps)}), flush=True)
+        return
     gemm_table = None if args.no_tuned_gemms else use_tuned_gemms(args.gemm_table, tune=args.tune_gemms)
     os.environ["TAGAN_BENCH_CONFIG"] = args.config
     cfg = synthetic.config_for(args.config)
@@ -245,17 +422,7 @@ def main():
             out["loss"].backward()
             bucket.allreduce_mean()
 
-    def forward_backward():
-        out = fwd()
-        bwd(out)
-        return out
-
-    def step():
-        opt.zero_grad(set_to_none=True)
-        out = forward_backward()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), cfg.gradient_clip_val)
-        opt.step()
-        return out["loss"]
+    step = make_step(model, opt, cfg, fwd, bwd)
 
     def timed(steps, warmup):
         """W untimed steps, then exactly K steps between barrier + sync; max over ranks."""
@@ -294,6 +461,9 @@ def main():
                                % (args.config, N, E, T, H, heads, cfg.dropout),
                    "sequences_per_step": seqs_per_step, "snapshots_per_sequence": T,
                    "parallelism": ("snapshot-shard%d" % world) if args.shard else ("dp%d" % world)},
+        "backend": "nccl (RCCL over xGMI)" if world > 1 else "none (single rank)",
+        "n_ranks_rccl": world if world > 1 else 0,
+        "parallelism": ("snapshot-shard%d" % world) if args.shard else ("dp%d" % world),
     }
     rec["config"]["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
     rec["config"]["gemms"] = ("hipBLASLt/rocBLAS solutions from the TunableOp table %s" % os.path.basename(gemm_table)
@@ -309,9 +479,13 @@ def main():
                                 "ms_per_step": round(alt / args.steps * 1e3, 3),
                                 "dtype": "bf16 (activations; fp32 math and accumulation)"}
     if rank == 0 and not args.no_roofline:
-        rec["roofline"] = roofline(model, seq, cfg)
+        roof = roofline_c4(args.roofline_reps)
+        roof["cache_assisted"] = dict(roofline_cache_assisted(seq, cfg), config=args.config)
+        rec["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline(cfg, args.config, init_state, args.cpu_sample_snapshots)
+        c1 = None if args.no_c1 else gpu_c1_line(dev, args.precision)
+        rec["cpu_baseline"] = cpu_baseline(cfg, args.config, init_state, args.cpu_sample_snapshots, gpu_c1=c1,
+                                           gpu_value=value)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -16,29 +16,51 @@ import torch.distributed as dist
 
 
 class GradBucket:
+    """ONE flat all-reduce of every trainable parameter's gradient plus a has-grad flag per parameter.
+
+    The buffer layout is the same on every rank whatever grads exist locally (a missing grad is packed as
+    zeros), so the collective always matches across ranks; after the reduction a parameter whose grad was
+    None on EVERY rank keeps grad None (dead in the shipped forward, as in the reference), one that had a
+    grad on some rank gets the mean.  The flags ride in the same buffer: no second collective.
+    """
+
     def __init__(self, params: Iterable[torch.nn.Parameter]):
         self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
+        self.n = sum(p.numel() for p in self.params)
         self.flat = None
 
     def allreduce_mean(self, group=None) -> None:
         if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
             return
-        live = [p for p in self.params if p.grad is not None]
-        n = sum(p.numel() for p in live)
-        if self.flat is None or self.flat.numel() != n or self.flat.device != live[0].grad.device:
-            self.flat = torch.empty(n, dtype=torch.float32, device=live[0].grad.device)
+        if not self.params:
+            return
+        dev = self.params[0].device
+        k = len(self.params)
+        if self.flat is None or self.flat.device != dev:
+            self.flat = torch.empty(self.n + k, dtype=torch.float32, device=dev)
+        flags = self.flat[self.n:]
         off = 0
-        for p in live:
-            k = p.numel()
-            self.flat[off:off + k].copy_(p.grad.reshape(-1))
-            off += k
+        for i, p in enumerate(self.params):
+            m = p.numel()
+            if p.grad is not None:
+                self.flat[off:off + m].copy_(p.grad.reshape(-1))
+            else:
+                self.flat[off:off + m].zero_()
+            off += m
+        flags.copy_(torch.tensor([p.grad is not None for p in self.params], dtype=torch.float32), non_blocking=True)
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
-        self.flat.div_(dist.get_world_size(group))
+        self.flat[:self.n].div_(dist.get_world_size(group))
+        has = (flags > 0).tolist()
         off = 0
-        for p in live:
-            k = p.numel()
-            p.grad.copy_(self.flat[off:off + k].view_as(p.grad))
-            off += k
+        for i, p in enumerate(self.params):
+            m = p.numel()
+            if has[i]:
+                g = self.flat[off:off + m].view_as(p)
+                if p.grad is None:
+                    p.grad = g.clone()
+                else:
+                    p.grad.copy_(g)
+            off += m
 
 
 def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None) -> None:

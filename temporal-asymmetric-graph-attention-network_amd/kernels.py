@@ -21,9 +21,25 @@ from . import _lib
 from ._lib import check, lib, ptr, require_hip, stream_of
 
 
+def _mix64(x: int) -> int:
+    """splitmix64 finaliser (host side)."""
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
 def new_seed() -> int:
-    """Dropout seed drawn from torch's default CPU generator (reproducible under manual_seed, no device sync)."""
-    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    """Dropout seed drawn from torch's default CPU generator (reproducible under manual_seed, no device sync).
+
+    Under torch.distributed the rank is mixed in: ranks that seed their generators identically (the usual
+    ``manual_seed`` before building the model) still draw independent dropout masks for their shards of
+    the global batch instead of the same mask row for row."""
+    s = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    dist = torch.distributed
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        s = _mix64(s ^ (_mix64(dist.get_rank() + 1) & 0x3FFFFFFFFFFFFFFF)) & 0x3FFFFFFFFFFFFFFF
+    return s
 
 
 # ----------------------------------------------------------------------------- graph

@@ -174,13 +174,15 @@ class SnapshotShardedTAGAN:
         out_rows = self.temporal(xt_rows) if n1 > n0 else xt_rows
         pooled = _SumAcrossRanks.apply(pool_partial(out_rows, n0, n_max), self.group) / n_max
         self.step += 1
-        # same head-dropout mask on every rank: reseed the generator the head draws from (the HIP
-        # kernels take their seeds from kernels.new_seed, not from this generator)
-        if pooled.is_cuda:
-            torch.cuda.manual_seed(self.head_seed + self.step)
-        else:
-            torch.manual_seed(self.head_seed + self.step)
-        return self.head(pooled, labels)
+        # same head-dropout mask on every rank: the head draws from a generator seeded from a per-step
+        # counter shared by all ranks, inside fork_rng so the caller's generators are left as they were
+        devices = [pooled.device] if pooled.is_cuda else []
+        with torch.random.fork_rng(devices=devices):
+            if pooled.is_cuda:
+                torch.cuda.manual_seed(self.head_seed + self.step)
+            else:
+                torch.manual_seed(self.head_seed + self.step)
+            return self.head(pooled, labels)
 
     __call__ = forward
 

@@ -196,18 +196,33 @@ class NodeMemoryBank:
                 "max_inactivity_limit": self.max_inactivity, "decay_factor": self.decay_factor,
                 "hidden_dim": self.hidden_dim}
 
-    def save(self, filepath: str):
-        """Same content as memory_bank.py:246-272, written with torch.save (load with weights_only=True)."""
+    def save(self, filepath: str, legacy_pickle: bool = False):
+        """Same content as memory_bank.py:246-272.  Default: torch.save (zip; readable with weights_only=True).
+        ``legacy_pickle=True`` writes the reference's own format (a plain ``pickle.dump`` of the dict,
+        memory_bank.py:271-272), so the reference's loader can read the file."""
         import os
         os.makedirs(os.path.dirname(os.path.abspath(filepath)), exist_ok=True)
-        torch.save({"hidden_dim": self.hidden_dim, "decay_factor": self.decay_factor,
-                    "max_inactivity": self.max_inactivity, "node_states": self.node_states,
-                    "inactivity_counter": self.inactivity_counter}, filepath)
+        d = {"hidden_dim": self.hidden_dim, "decay_factor": self.decay_factor,
+             "max_inactivity": self.max_inactivity,
+             "node_states": {k: v.detach().cpu() for k, v in self.node_states.items()},
+             "inactivity_counter": dict(self.inactivity_counter)}
+        if legacy_pickle:
+            import pickle
+            with open(filepath, "wb") as f:
+                pickle.dump(d, f)
+        else:
+            torch.save(d, filepath)
 
     @classmethod
     def load(cls, filepath: str, device=None) -> "NodeMemoryBank":
-        """memory_bank.py:299-332 (classmethod form): states and counters only."""
-        d = torch.load(filepath, weights_only=True)
+        """memory_bank.py:299-332 (classmethod form): states and counters only.  Reads both this class's
+        torch.save files and the reference's plain-pickle files; the latter through a restricted unpickler
+        that rebuilds only tensors, dicts and scalars (``_read_legacy``) — nothing else in the file runs."""
+        import zipfile
+        if zipfile.is_zipfile(filepath):
+            d = torch.load(filepath, weights_only=True)
+        else:
+            d = _read_legacy(filepath)
         bank = cls(d["hidden_dim"], d["decay_factor"], d["max_inactivity"], device=device)
         if d["node_states"]:
             ids = list(d["node_states"].keys())
@@ -220,6 +235,33 @@ class NodeMemoryBank:
     def __repr__(self):
         return (f"NodeMemoryBank(hidden_dim={self.hidden_dim}, decay_factor={self.decay_factor}, "
                 f"max_inactivity={self.max_inactivity}, active_nodes={self.size})")
+
+
+def _read_legacy(filepath: str):
+    """The reference's bank file (``pickle.dump`` of a dict of scalars, {id: tensor} and {id: int}) read by an
+    unpickler whose only globals are the tensor rebuild path, with storages loaded weights_only."""
+    import collections
+    import io
+    import pickle
+
+    def load_storage(b):
+        return torch.load(io.BytesIO(b), weights_only=True)
+
+    allowed = {("torch._utils", "_rebuild_tensor_v2"): torch._utils._rebuild_tensor_v2,
+               ("torch.storage", "_load_from_bytes"): load_storage,
+               ("collections", "OrderedDict"): collections.OrderedDict}
+
+    class _Restricted(pickle.Unpickler):
+        def find_class(self, module, name):
+            if (module, name) in allowed:
+                return allowed[(module, name)]
+            raise pickle.UnpicklingError("refusing global %s.%s in a memory-bank file" % (module, name))
+
+    with open(filepath, "rb") as f:
+        d = _Restricted(f).load()
+    if not isinstance(d, dict) or not {"hidden_dim", "node_states", "inactivity_counter"} <= set(d):
+        raise ValueError("%s is not a NodeMemoryBank file" % filepath)
+    return d
 
 
 def _pow2(n: int) -> int:

@@ -44,12 +44,36 @@ def labels(meta, t, device="cpu"):
     return lab.to(device) if lab is not None else None
 
 
+# Observed errors of every assert_close, keyed by test id (written by conftest.py to $TAGAN_PARITY_LOG at the
+# end of the session): {test: {check: [max_abs, max_rel_where_|want|>atol, normwise_rel, atol, rtol]}}.
+ERRORS = {}
+
+
+def _record(name, diff, want, atol, rtol):
+    test = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+    finite = torch.isfinite(diff)
+    d = diff[finite]
+    w = want.abs()[finite]
+    big = w > atol
+    max_rel = float((d[big] / w[big]).max()) if bool(big.any()) else 0.0
+    wn = float(w.norm())
+    norm_rel = float(d.norm()) / wn if wn > 0 else float(d.norm())
+    ERRORS.setdefault(test, {})[name] = [float(d.max()) if d.numel() else 0.0, max_rel, norm_rel, atol, rtol]
+
+
+def normwise_rel(got, want):
+    got = got.detach().to("cpu", torch.float64)
+    want = want.detach().to("cpu", torch.float64)
+    return float((got - want).norm()) / max(float(want.norm()), 1e-300)
+
+
 def assert_close(name, got, want, atol, rtol=0.0):
     got = got.detach().to("cpu", torch.float64)
     want = want.detach().to("cpu", torch.float64)
     assert got.shape == want.shape, "%s: shape %s vs %s" % (name, tuple(got.shape), tuple(want.shape))
     both_nan = torch.isnan(got) & torch.isnan(want)
     diff = torch.where(both_nan, torch.zeros_like(got), (got - want).abs())
+    _record(name, diff, want, atol, rtol)
     tol = atol + rtol * want.abs()
     bad = ~(diff <= torch.where(both_nan, torch.ones_like(tol), tol))
     if bad.any():

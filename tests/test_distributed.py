@@ -56,3 +56,42 @@ def test_grad_bucket_allreduce_world2():
     assert torch.allclose(res["avg0"], want, atol=1e-7)
     assert torch.equal(res["avg0"], res["avg1"])
     assert res["none0"] == res["none1"] == [False, False, False, False, True, True]
+
+
+def _worker_uneven(rank, world, port, results):
+    """A parameter with a grad on rank 0 only: same bucket layout on both ranks, mean over ranks."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import tagan_amd  # noqa: F401
+    from tagan_amd.distributed import GradBucket
+    from tagan_amd.kernels import new_seed
+    torch.manual_seed(0)
+    a, b = torch.nn.Linear(3, 2), torch.nn.Linear(2, 2)
+    x = torch.ones(1, 3) * (rank + 1)
+    y = a(x)
+    if rank == 0:
+        y = b(y)
+    y.sum().backward()
+    results["b%d" % rank] = b.weight.grad.clone() if b.weight.grad is not None else None
+    GradBucket(list(a.parameters()) + list(b.parameters())).allreduce_mean()
+    results["a_avg%d" % rank] = a.weight.grad.clone()
+    results["b_avg%d" % rank] = b.weight.grad.clone()
+    torch.manual_seed(5)                      # identical generators on every rank ...
+    results["seed%d" % rank] = new_seed()     # ... still give per-rank dropout seeds
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_bucket_grad_on_one_rank_only():
+    port = _free_port()
+    with mp.Manager() as m:
+        res = m.dict()
+        mp.spawn(_worker_uneven, args=(2, port, res), nprocs=2, join=True)
+        res = dict(res)
+    assert res["b1"] is None and res["b0"] is not None
+    assert torch.allclose(res["b_avg0"], res["b0"] / 2) and torch.equal(res["b_avg0"], res["b_avg1"])
+    assert torch.equal(res["a_avg0"], res["a_avg1"])
+    assert res["seed0"] != res["seed1"]

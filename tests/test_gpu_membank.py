@@ -98,3 +98,18 @@ def test_membank_get_state_and_checkpoint(dev, tmp_path):
     assert sorted(again.node_states) == [7, 9]
     assert torch.equal(again.node_states[9], bank.node_states[9])
     assert again.inactivity_counter == bank.inactivity_counter
+
+
+def test_membank_legacy_pickle_round_trip(dev, tmp_path):
+    """The reference's file format (memory_bank.py:246-272 pickle.dump) written and read back."""
+    from tagan_amd import NodeMemoryBank
+    bank = NodeMemoryBank(4, device=dev)
+    bank.update([3, 11, 5], torch.randn(3, 4).to(dev), 0)
+    bank.update([3], torch.randn(1, 4).to(dev), 1)
+    path = str(tmp_path / "bank.pkl")
+    bank.save(path, legacy_pickle=True)
+    again = NodeMemoryBank.load(path, device=dev)
+    assert sorted(again.node_states) == sorted(bank.node_states)
+    for k in bank.node_states:
+        assert torch.equal(again.node_states[k].cpu(), bank.node_states[k].cpu())
+    assert again.inactivity_counter == bank.inactivity_counter

@@ -12,7 +12,7 @@ import oracle
 pytestmark = pytest.mark.gpu
 
 OUT_ATOL, OUT_RTOL = 1e-4, 1e-4      # forward values
-GRAD_ATOL, GRAD_RTOL = 1e-4, 1e-3    # gradients (longer fp32 reduction chains)
+GRAD_ATOL, GRAD_RTOL = 1e-4, 1e-4    # north_star: 1e-4 fp32 (observed errors: profiles/parity_errors_r02.json)
 
 
 @pytest.fixture(scope="module")

@@ -78,4 +78,4 @@ def test_sharded_hip_matches_unsharded():
         assert sorted(got) == sorted(ref)
         for k, g in ref.items():
             err = float((got[k] - g).abs().max())
-            assert err <= 1e-4 + 1e-3 * float(g.abs().max()), (r, k, err)
+            assert err <= 1e-4 + 1e-4 * float(g.abs().max()), (r, k, err)   # north_star 1e-4

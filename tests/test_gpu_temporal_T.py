@@ -11,7 +11,7 @@ import oracle
 pytestmark = pytest.mark.gpu
 
 OUT_ATOL, OUT_RTOL = 1e-4, 1e-4
-GRAD_ATOL, GRAD_RTOL = 1e-4, 1e-3
+GRAD_ATOL, GRAD_RTOL = 1e-4, 1e-4    # north_star: 1e-4 fp32 (observed errors: profiles/parity_errors_r02.json)
 
 
 @pytest.fixture(scope="module")

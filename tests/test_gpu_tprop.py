@@ -12,7 +12,7 @@ from oracle.tagan_oracle import _lin, _ln, bce_loss, classification_head, graph_
 pytestmark = pytest.mark.gpu
 
 OUT_ATOL, OUT_RTOL = 1e-4, 1e-4
-GRAD_ATOL, GRAD_RTOL = 1e-4, 1e-3
+GRAD_ATOL, GRAD_RTOL = 1e-4, 1e-4    # north_star: 1e-4 fp32 (observed errors: profiles/parity_errors_r02.json)
 
 
 @pytest.fixture(scope="module")
