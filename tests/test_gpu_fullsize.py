@@ -38,6 +38,12 @@ NORM_REL = 1e-4
 # analytically zero gradients (fp32 noise against fp64 noise): scaled-dot attention is invariant to a shift
 # of k by a per-head constant, so d(k bias) = 0 exactly (temporal_attention.py:1006 scores = q·kᵀ/√d)
 ZERO_GRADS = ("temporal_attention.k_linear.bias",)
+# ill-conditioned in ANY fp32 implementation (written exception): the attention-pool bias gradient
+# is Σ_t dscore_t·(1 - tanh²)·w₂ where the softmax backward makes Σ_t dscore_t = 0 (classification.py:856-966),
+# so it is a small difference of larger terms.  The CPU fp32 oracle itself lands at 1.72e-4 normwise vs fp64 on
+# this exact tensor at C2 (tools/fp32_conditioning.py -> profiles/r2_fp32_conditioning.json); the HIP path is
+# held to 2x that in norm and to the full 1e-4 element-wise bound.
+COND_GRADS = {"classification_head.classification_head.attention.0.bias": 3.5e-4}
 SAMPLE = 2048
 
 
@@ -51,8 +57,19 @@ def dev():
 
 def _free():
     import gc
+    import sys
+    # a failed test's traceback (sys.last_traceback, kept by pytest) pins its frames and their 10-100 GB of
+    # device tensors: drop it so one failure does not turn every later full-size test into an OOM
+    sys.last_type = sys.last_value = sys.last_traceback = None
     gc.collect()
     torch.cuda.empty_cache()
+
+
+@pytest.fixture(autouse=True)
+def _clean_device():
+    _free()
+    yield
+    _free()
 
 
 def _p64(module, prefix=""):
@@ -65,7 +82,17 @@ def _close_grad(name, got, want):
     if any(name.endswith(z) for z in ZERO_GRADS):
         return
     nr = G.normwise_rel(got, want)
-    assert nr <= NORM_REL, "%s: normwise rel %.3e" % (name, nr)
+    bound = next((b for k, b in COND_GRADS.items() if name.endswith(k)), NORM_REL)
+    assert nr <= bound, "%s: normwise rel %.3e" % (name, nr)
+
+
+def _unit_grad(shape, gen, dev):
+    """Upstream gradient on the sampled rows, normalised to unit Frobenius norm -- the scale of a mean-reduced
+    loss over those rows.  With an O(1)-per-element randn upstream gradient summed over 10^5 rows x T, every
+    parameter gradient is ~10^2-10^3 in size and an absolute 1e-4 bound becomes a 10^-7 relative one, tighter
+    than fp32 rounding of the result itself; the normwise check (scale-free) is unchanged by this."""
+    g = torch.randn(*shape, generator=gen, dtype=torch.float64)
+    return (g / g.norm()).float().to(dev)
 
 
 def _segments(rp, rows):
@@ -200,7 +227,7 @@ def test_fullsize_csr_softmax_and_geometric_rows(dev, name):
     h0.requires_grad_(True)
     y = layer.forward_graph(h0, graph, skip_ln=model.skip_layer_norm)
     gy = torch.zeros_like(y)
-    gy[rows] = torch.randn(rows.numel(), H, generator=gen).to(dev)
+    gy[rows] = _unit_grad((rows.numel(), H), gen, dev)
     (y * gy).sum().backward()
     U, loc, rowptr_l, col_l = _local_csr(graph, rows)
     P = _p64(model)
@@ -237,7 +264,7 @@ def test_fullsize_temporal_rows(dev, name):
     rows = torch.unique(torch.randint(0, N, (SAMPLE - 1,), generator=gen).to(dev))
     rows = torch.unique(torch.cat([rows, torch.tensor([N - 1], device=dev)]))
     gy = torch.zeros_like(out)
-    gy[:, rows] = torch.randn(T, rows.numel(), H, generator=gen).to(dev)
+    gy[:, rows] = _unit_grad((T, rows.numel(), H), gen, dev)
     (out * gy).sum().backward()
     P = _p64(ta, "temporal_attention.")
     x64 = xt.detach()[:, rows].permute(1, 0, 2).cpu().double().requires_grad_(True)
