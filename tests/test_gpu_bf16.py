@@ -29,7 +29,7 @@ def test_reduced_precision_tracks_fp32(mode, loss_tol, grad_tol):
         m = TAGAN(cfg, precision=prec).to(dev)
         r = m(seq, labels)
         r["loss"].backward()
-        out[prec] = (float(r["loss"]), {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
+        out[prec] = (float(r["loss"].detach()), {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
     l32, g32 = out["fp32"]
     l16, g16 = out[mode]
     assert abs(l16 - l32) <= loss_tol * abs(l32)
