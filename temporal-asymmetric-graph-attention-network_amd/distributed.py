@@ -29,8 +29,11 @@ class GradBucket:
         self.n = sum(p.numel() for p in self.params)
         self.flat = None
 
-    def allreduce_mean(self, group=None) -> None:
-        if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+    def allreduce_mean(self, group=None, force: bool = False) -> None:
+        """``force``: run the collective even at world size 1 (exercises the RCCL path on one GPU)."""
+        if not dist.is_available() or not dist.is_initialized():
+            return
+        if dist.get_world_size(group) == 1 and not force:
             return
         if not self.params:
             return

@@ -201,9 +201,10 @@ class ShardGradSync:
         self.replicated = [any(n.startswith(x) for x in replicated_prefixes) for n, _ in self.items]
         self.group = group
 
-    def sync(self):
+    def sync(self, force: bool = False):
+        """``force``: run the collective even at world size 1 (exercises the RCCL path on one GPU)."""
         P, _ = _world(self.group)
-        if P == 1:
+        if P == 1 and not (force and dist.is_available() and dist.is_initialized()):
             return
         ref = self.items[0][1]
         n = sum(p.numel() for _, p in self.items)

@@ -1,0 +1,81 @@
+"""The RCCL code path (backend "nccl") executed on one MI355X at world size 1.
+
+The driver's 8-GPU runs are the only place several RCCL ranks meet; every other multi-rank test uses gloo.
+This test makes the RCCL calls themselves run once on the device — the snapshot-shard all-to-all
+(`sharded._all_to_all`, all_to_all_single on device buffers), the pooling all-reduce, and both gradient
+buckets (`GradBucket.allreduce_mean`, `ShardGradSync.sync`, forced at world size 1) — and checks that a
+one-rank collective leaves every value exactly as the unsharded model computed it (sum over one rank = identity).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+COUNTS = [40, 57, 33, 57, 49, 21]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _setup(dev):
+    from tagan_amd import TAGAN, TAGANConfig
+    cfg = TAGANConfig(node_feature_dim=8, edge_feature_dim=0, hidden_dim=64, num_heads=4, num_layers=2,
+                      dropout=0.0, output_dim=1, window_size=3)
+    torch.manual_seed(21)
+    model = TAGAN(cfg).to(dev)
+    g = torch.Generator().manual_seed(4)
+    seq = [(torch.randn(n, 8, generator=g).to(dev), torch.randint(0, n, (2, 4 * n), generator=g).to(dev), None,
+            list(range(n))) for n in COUNTS]
+    return model, seq
+
+
+def test_rccl_world1_shard_and_buckets():
+    import tagan_amd  # noqa: F401
+    from tagan_amd.distributed import GradBucket
+    from tagan_amd.sharded import ShardGradSync, SnapshotShardedTAGAN, _all_to_all
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1)
+    try:
+        assert dist.get_backend() == "nccl"
+        # raw all_to_all_single over device buffers
+        a = torch.arange(12, dtype=torch.float32, device=dev).view(3, 4)
+        (b,) = _all_to_all([a], [(3, 4)], None)
+        assert torch.equal(a, b)
+
+        labels = torch.tensor([1.0], device=dev)
+        ref_model, seq = _setup(dev)
+        ref = ref_model(seq, labels)
+        ref["loss"].backward()
+        ref_grads = {k: p.grad.clone() for k, p in ref_model.named_parameters() if p.grad is not None}
+
+        model, seq = _setup(dev)
+        out = SnapshotShardedTAGAN.for_model(model)(seq, COUNTS, labels)
+        out["loss"].backward()
+        ShardGradSync(list(model.named_parameters())).sync(force=True)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(out["loss"], ref["loss"], rtol=1e-5, atol=1e-6)
+        for k, p in model.named_parameters():
+            if k in ref_grads:
+                torch.testing.assert_close(p.grad, ref_grads[k], rtol=1e-4, atol=1e-5, msg=k)
+            else:
+                assert p.grad is None, k
+        before = {k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None}
+        GradBucket(model.parameters()).allreduce_mean(force=True)
+        torch.cuda.synchronize()
+        for k, p in model.named_parameters():
+            if k in before:
+                assert torch.equal(p.grad, before[k]), k
+            else:
+                assert p.grad is None, k
+    finally:
+        dist.destroy_process_group()
