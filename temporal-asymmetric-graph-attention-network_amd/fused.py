@@ -257,6 +257,75 @@ WGRAD_ROWS_QKV = int(os.environ.get("TAGAN_WGRAD_ROWS_QKV", "8192"))
 # TAGAN_WGRAD_BIAS_AUG=0: QKV bias gradient by a column-sum pass over dqkv instead of the ones column of
 # LN1's augmented output riding through the weight-gradient GEMM (fp32 QKV_AUG form only; A/B)
 WGRAD_BIAS_AUG = os.environ.get("TAGAN_WGRAD_BIAS_AUG", "1") != "0"
+# Fused matrix-core projection kernels of csrc/proj_gemm.hip (fp32, H = 128), per GEMM of the block:
+#   "qkv": LN1 as the QKV GEMM's prologue;  "out": dropout + residual + LN2 as the out-projection's epilogue;
+#   "dc":  the out-projection's input gradient;  "dh": LN1's backward as the epilogue of the QKV input gradient.
+# TAGAN_PROJ = comma list of those, "all", or "0"/"none" (default).  Interleaved C2 A/B on one MI355X
+# (tools/runs/ab_proj.sh, profiles/r2_proj_ab.txt): none 8.40-8.42 ms, "out,dc" 8.48-8.52, all 8.66-8.73 — at
+# C2 each fused kernel is bound by HBM traffic and MFMA issue that its two waves per SIMD do not overlap, so it
+# lands at parity with the TunableOp-tuned hipBLASLt GEMM + the standalone LayerNorm kernel it replaces and the
+# default keeps the latter.
+_PROJ_ENV = os.environ.get("TAGAN_PROJ", "0").strip().lower()
+PROJ_SET = (set() if _PROJ_ENV in ("0", "none", "") else
+            {"qkv", "out", "dc", "dh"} if _PROJ_ENV in ("1", "all") else set(_PROJ_ENV.split(",")))
+PROJ = bool(PROJ_SET)
+
+
+def _proj_ok(H: int, bf: bool) -> bool:
+    return PROJ and not bf and bool(lib().tagan_proj_supported(H))
+
+
+def proj_ln_qkv(x2, ln1_w, ln1_b, eps1, w_qkv, b_qkv, want_h: bool):
+    """LN1 + QKV projection in one kernel: qkv [M, 3H], h_aug [M, H + 4] (LN1 output + ones column) or None."""
+    M, H = x2.shape
+    dev = x2.device
+    qkv = torch.empty(M, 3 * H, device=dev)
+    st = torch.empty(2, M, device=dev)
+    h_aug = torch.empty(M, H + 4, device=dev) if want_h else None
+    check(lib().tagan_ln_qkv_fwd(M, H, 3 * H, ptr(x2), ptr(ln1_w), ptr(ln1_b), float(eps1), ptr(w_qkv), ptr(b_qkv),
+                                 ptr(qkv), 3 * H, ptr(h_aug), H + 4 if want_h else 0, ptr(st[0]), ptr(st[1]),
+                                 stream_of(x2)), "tagan_ln_qkv_fwd")
+    return qkv, h_aug, st[0], st[1]
+
+
+def proj_ln_out(c, w_o, b_o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, lns_w=None, lns_b=None, eps_s=1e-5):
+    """y = LN2(dropout(c·w_oᵀ + b_o) + x2) [+ LN_s(x2)] in one kernel; returns y, s, mean, rstd, skip stats."""
+    M, H = x2.shape
+    dev = x2.device
+    y = torch.empty(M, H, device=dev)
+    s2 = torch.empty(M, H, device=dev)
+    st = torch.empty(4 if lns_w is not None else 2, M, device=dev)
+    skip = (st[2], st[3]) if lns_w is not None else None
+    check(lib().tagan_proj_ln_fwd(M, H, ptr(c), ptr(w_o), ptr(b_o), ptr(x2), float(p_out), seed_out, ptr(ln2_w),
+                                  ptr(ln2_b), float(eps2), ptr(lns_w), ptr(lns_b), float(eps_s), ptr(s2), ptr(y),
+                                  ptr(st[0]), ptr(st[1]), ptr(skip[0]) if skip else None,
+                                  ptr(skip[1]) if skip else None, stream_of(x2)), "tagan_proj_ln_fwd")
+    return y, s2, st[0], st[1], skip
+
+
+def proj_mm(a, w, kmajor: bool):
+    """a[M, K] · (w if kmajor else wᵀ) -> [M, H] on the matrix-core kernel (K = H or 3H)."""
+    M, K = a.shape
+    H = w.shape[1] if kmajor else w.shape[0]
+    out = torch.empty(M, H, device=a.device)
+    check(lib().tagan_proj_gemm(M, H, K, ptr(a), a.stride(0), ptr(w), int(kmajor), ptr(out), H, stream_of(a)),
+          "tagan_proj_gemm")
+    return out
+
+
+def proj_ln_bwd(da, w, x2, mean, rstd, gamma, dres):
+    """dx = LNᵀ(da·w) + dres with dgamma, dbeta (w [K, H] = the projection's nn.Linear weight)."""
+    M, K = da.shape
+    H = x2.shape[1]
+    dev = da.device
+    dx = torch.empty(M, H, device=dev)
+    dgb = torch.empty(2, H, device=dev)
+    L = lib()
+    wsb = L.tagan_proj_ln_bwd_workspace(M, H)
+    ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
+    check(L.tagan_proj_ln_bwd(M, H, K, ptr(da), ptr(w), ptr(x2), ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), ptr(dx),
+                              ptr(dgb[0]), ptr(dgb[1]), ptr(ws), wsb, stream_of(da)), "tagan_proj_ln_bwd")
+    return dx, dgb[0], dgb[1]
 
 class AttnBlockFn(torch.autograd.Function):
     """y = LN2(dropout(out_proj(core(QKV(LN1(x))))) + x) with LayerNorm on both sides (use_layer_norm=True)."""
@@ -269,7 +338,13 @@ class AttnBlockFn(torch.autograd.Function):
         x2 = x.reshape(-1, H).contiguous()
         bf = _PREC != "fp32"          # bf16 GEMM operands
         act = _PREC == "bf16"         # bf16 activations between kernels
-        if QKV_AUG and not bf:
+        proj = _proj_ok(H, bf)
+        if proj and "qkv" in PROJ_SET:
+            w_qkv, b_qkv = w_qkv.contiguous(), b_qkv.contiguous()
+            qkv, h_aug, mean1, rstd1 = proj_ln_qkv(x2, ln1_w, ln1_b, eps1, w_qkv, b_qkv,
+                                                   want_h=any(ctx.needs_input_grad))
+            h = h_aug[:, :H] if h_aug is not None else None
+        elif QKV_AUG and not bf:
             # fp32: LN1 writes [h | 1 0 0 0] (row stride H + 4) and the QKV bias rides in the GEMM as a weight
             # column -- one GEMM over K = H + 4 without the bias epilogue, ≈1 % of the C2 step faster on
             # hipBLASLt (tools/runs/qkv_aug.sh); with bf16 operands the epilogue form is the faster one
@@ -287,6 +362,13 @@ class AttnBlockFn(torch.autograd.Function):
             qkv = _addmm(b_qkv, h, w_qkv, bf, out_bf16=act)
         c, saved = core.fwd(qkv, p1, p2)
         cg = _b(c) if bf else c
+        if proj and "out" in PROJ_SET:
+            y, s2, mean2, rstd2, skip = proj_ln_out(c, w_o.contiguous(), b_o, x2, p_out, seed_out, ln2_w, ln2_b, eps2,
+                                                    lns_w, lns_b, eps_s)
+            ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
+            ctx.inter = (h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
+            ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, proj)
+            return y.view(x.shape)
         if OUT_BIAS_LN:   # out-projection bias added in the closing LayerNorm (no GEMM epilogue)
             o, b_o_ln = _mm(cg, w_o.t(), bf), b_o
         else:
@@ -299,14 +381,14 @@ class AttnBlockFn(torch.autograd.Function):
             y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True, a_bias=b_o_ln)
         ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
         ctx.inter = (h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
-        ctx.cfg = (core, p_out, seed_out, x.shape, bf, act)
+        ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, False)
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, ln1_w, w_qkv, w_o, ln2_w, lns_w = ctx.saved_tensors
         h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip = ctx.inter
-        core, p_out, seed_out, shape, bf, act = ctx.cfg
+        core, p_out, seed_out, shape, bf, act, proj = ctx.cfg
         ng = ctx.needs_input_grad
         dy2 = dy.reshape(-1, shape[-1]).contiguous()
         dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True,
@@ -314,7 +396,7 @@ class AttnBlockFn(torch.autograd.Function):
         dgs = dbs = None
         if skip is not None:       # skip branch: LN_s backward with the residual gradient added in-kernel
             dres, _, dgs, dbs, _ = ln_bwd(x2, skip[0], skip[1], lns_w, dy2, dres, 0.0, 0, True, False, False)
-        dc = _mm(do, w_o, bf, out_bf16=act)
+        dc = proj_mm(do, w_o.contiguous(), True) if (proj and "dc" in PROJ_SET) else _mm(do, w_o, bf, out_bf16=act)
         dw_o = _wgrad(do, cg, bf) if ng[7] else None
         dqkv, dp1, dp2, db_core = core.bwd(qkv, c, saved, dc, ng[1], ng[2], want_bias_sum=bool(ng[6]))
         del dc, do
@@ -327,6 +409,13 @@ class AttnBlockFn(torch.autograd.Function):
         else:
             db_qkv = (db_core if db_core is not None else colsum(dqkv)) if ng[6] else None
             dw_qkv = None
+        if proj and "dh" in PROJ_SET:
+            if dw_qkv is None and ng[5]:
+                dw_qkv = _wgrad(dqkv, h, bf, WGRAD_ROWS_QKV)
+            dx, dg1, db1 = proj_ln_bwd(dqkv, w_qkv, x2, mean1, rstd1, ln1_w, dres)
+            ctx.inter = None
+            return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
+                    None, None, None, None, None, dgs, dbs, None)
         if bf:
             dqkv = _b(dqkv)
         dh = _mm(dqkv, w_qkv, bf)

@@ -7,7 +7,6 @@ buckets (`GradBucket.allreduce_mean`, `ShardGradSync.sync`, forced at world size
 one-rank collective leaves every value exactly as the unsharded model computed it (sum over one rank = identity).
 """
 import os
-import socket
 
 import pytest
 import torch
@@ -16,14 +15,6 @@ import torch.distributed as dist
 pytestmark = pytest.mark.gpu
 
 COUNTS = [40, 57, 33, 57, 49, 21]
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def _setup(dev):
@@ -44,7 +35,9 @@ def test_rccl_world1_shard_and_buckets():
     from tagan_amd.sharded import ShardGradSync, SnapshotShardedTAGAN, _all_to_all
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1)
+    import tempfile
+    store = os.path.join(tempfile.mkdtemp(prefix="tagan_rccl_"), "store")   # file rendezvous: no TCP port race
+    dist.init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1)
     try:
         assert dist.get_backend() == "nccl"
         # raw all_to_all_single over device buffers

@@ -1,7 +1,6 @@
 """Snapshot-sharded sequence on the HIP path: two ranks sharing cuda:0 (gloo, host-staged collectives)
 against the unsharded HIP model on the same sequence and weights (fp32, dropout 0)."""
 import os
-import socket
 
 import pytest
 import torch
@@ -11,14 +10,6 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 COUNTS = [40, 57, 33, 57, 49, 21]
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def _setup(dev):
@@ -36,10 +27,9 @@ def _setup(dev):
     return model, seq
 
 
-def _worker(rank, world, port, results):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, store_path, results):
+    # a file rendezvous: no TCP port to race for with another test's lingering store
+    dist.init_process_group("gloo", init_method="file://" + store_path, rank=rank, world_size=world)
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     from tagan_amd.sharded import ShardGradSync, SnapshotShardedTAGAN, blocks
@@ -66,10 +56,11 @@ def _worker(rank, world, port, results):
 def test_sharded_hip_matches_unsharded():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    port = _free_port()
+    import tempfile
+    store_path = os.path.join(tempfile.mkdtemp(prefix="tagan_shard_"), "store")
     with mp.Manager() as m:
         res = m.dict()
-        mp.spawn(_worker, args=(2, port, res), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, store_path, res), nprocs=2, join=True)
         res = dict(res)
     ref = res["ref_grads"]
     for r in range(2):

@@ -13,6 +13,7 @@ FAMILIES = [
     ("geo", r"k_geo_"),
     ("temporal", r"k_tattn"),
     ("layernorm", r"k_ln_"),
+    ("proj (fused MFMA)", r"k_proj"),
     ("csr", r"rocprim|k_scatter|k_fill_tail|k_keys|k_chunk|k_tri|csr|k_count"),
     ("colsum/pool", r"k_colsum|k_pool"),
     ("torch elementwise", r"elementwise|CatArray|index|gather|scatter"),
