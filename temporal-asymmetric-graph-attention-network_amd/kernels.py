@@ -68,6 +68,16 @@ class SnapshotGraph:
     chunk_cap: int = 0
     part_cap: int = 0
     _struct: object = None
+    pending_err: object = None     # (pinned int32 flag, event) of a deferred index validation
+
+    def check_valid(self) -> None:
+        """Raise the deferred IndexError of ``build_graph(validate="deferred")`` (waits for the CSR build only)."""
+        if self.pending_err is not None:
+            host, ev = self.pending_err
+            self.pending_err = None
+            ev.synchronize()
+            if int(host[0]) != 0:
+                raise IndexError("edge_index contains an index out of range for its snapshot's node count")
 
     def nnz_host(self) -> int:
         return int(self.nnz.item())
@@ -114,29 +124,42 @@ def _finish(g: SnapshotGraph, nnz_cap: int, chunk: int = CHUNK) -> SnapshotGraph
     return g
 
 
-def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], validate: bool = True,
+def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], validate=True,
                 chunk: int = CHUNK) -> SnapshotGraph:
     """CSR/CSC of the block-diagonal union of snapshot adjacencies (+ self-loops, de-duplicated).
 
     ``edge_indices[g]`` is snapshot g's [2, E_g] edge_index with local node ids.
-    With ``validate`` an out-of-range index raises IndexError like the reference's
-    ``adj[edge_index[0], edge_index[1]] = 1`` (costs one device sync).
+    ``validate``: True raises IndexError for an out-of-range index like the reference's
+    ``adj[edge_index[0], edge_index[1]] = 1`` (one device sync, here); "deferred" records the flag and
+    ``SnapshotGraph.check_valid()`` raises later (waits only for the CSR build, not the stream); False skips
+    it.  An out-of-range edge never enters the CSR either way (tagan_csr_build drops it), so the kernels
+    that follow are safe to launch before the check.
     """
-    dev = edge_indices[0].device
     require_hip(*edge_indices)
     eis = [e.to(torch.int64) for e in edge_indices]
     ei = torch.cat(eis, dim=1) if len(eis) > 1 else eis[0]
-    ei = ei.contiguous()
-    E = int(ei.shape[1])
-    N = int(sum(node_counts))
     e_ptr = [0]
     for e in eis:
         e_ptr.append(e_ptr[-1] + int(e.shape[1]))
+    return build_graph_cat(ei, e_ptr, node_counts, validate, chunk)
+
+
+def build_graph_cat(ei: torch.Tensor, e_ptr: Sequence[int], node_counts: Sequence[int], validate=True,
+                    chunk: int = CHUNK) -> SnapshotGraph:
+    """``build_graph`` on already-concatenated edges: ei [2, ΣE_g] int64 (local ids), snapshot g's edges in
+    columns [e_ptr[g], e_ptr[g+1]) (the layout of ``ingest.SnapshotBatch``)."""
+    require_hip(ei)
+    dev = ei.device
+    ei = ei.to(torch.int64).contiguous()
+    E = int(ei.shape[1])
+    G = len(node_counts)
+    assert len(e_ptr) == G + 1 and e_ptr[0] == 0 and e_ptr[-1] == E
+    N = int(sum(node_counts))
     n_ptr = [0]
     for n in node_counts:
         n_ptr.append(n_ptr[-1] + int(n))
-    meta = torch.tensor(e_ptr + n_ptr, dtype=torch.int64).to(dev)   # a few hundred bytes; no pinned alloc per call
-    edge_ptr, node_ptr = meta[:len(e_ptr)], meta[len(e_ptr):]
+    meta = torch.tensor(list(e_ptr) + n_ptr, dtype=torch.int64).to(dev)   # a few hundred bytes
+    edge_ptr, node_ptr = meta[:G + 1], meta[G + 1:]
     cap = E + N
     buf = torch.empty(2 * (N + 1) + 3 * cap, dtype=torch.int32, device=dev)
     rowptr, csc_ptr = buf[:N + 1], buf[N + 1:2 * (N + 1)]
@@ -148,13 +171,20 @@ def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], va
     L = lib()
     ws_bytes = L.tagan_csr_build_workspace(E, N)
     ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=dev)
-    check(L.tagan_csr_build(ptr(ei), E, E, ptr(edge_ptr), ptr(node_ptr), len(eis), N, max(n_ptr[i + 1] - n_ptr[i]
-                            for i in range(len(eis))), ptr(rowptr), ptr(col),
+    check(L.tagan_csr_build(ptr(ei), E, E, ptr(edge_ptr), ptr(node_ptr), G, N,
+                            max(n_ptr[i + 1] - n_ptr[i] for i in range(G)), ptr(rowptr), ptr(col),
                             ptr(csc_ptr), ptr(csc_row), ptr(csc_eid), ptr(nnz), ptr(err), ptr(ws), ws_bytes,
                             stream_of(ei)), "tagan_csr_build")
-    if validate and int(err.item()) != 0:
+    g = SnapshotGraph(N, rowptr, col, csc_ptr, csc_row, csc_eid, nnz, list(node_counts))
+    if validate == "deferred":
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(err, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        g.pending_err = (host, ev)
+    elif validate and int(err.item()) != 0:
         raise IndexError("edge_index contains an index out of range for its snapshot's node count")
-    return _finish(SnapshotGraph(N, rowptr, col, csc_ptr, csc_row, csc_eid, nnz, list(node_counts)), cap, chunk)
+    return _finish(g, cap, chunk)
 
 
 def graph_from_dense_mask(mask: torch.Tensor) -> SnapshotGraph:

@@ -25,7 +25,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .fused import precision as precision_ctx
-from .kernels import build_graph, layer_norm, linear, pool_time_major
+from .ingest import SnapshotBatch, unpack as _unpack
+from .kernels import build_graph, build_graph_cat, layer_norm, linear, pool_time_major
 from .layers.classification import ClassificationModule, TemporalLossModule
 from .layers.graph_attention import TAGANGraphAttention
 from .layers.temporal_attention import AsymmetricTemporalAttention, MaskBroadcastError
@@ -34,16 +35,6 @@ from .utils.config import TAGANConfig
 from .utils.memory_bank import NodeMemoryBank
 
 Snapshot = Union[Dict[str, Any], Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor], List[int]]]
-
-
-def _unpack(snapshot):
-    if isinstance(snapshot, dict):
-        return snapshot["x"], snapshot["edge_index"], snapshot.get("edge_attr"), snapshot["node_ids"]
-    if isinstance(snapshot, tuple):
-        if len(snapshot) < 4:
-            raise ValueError(f"Snapshot tuple has incorrect format. Expected at least 4 elements, got {len(snapshot)}")
-        return snapshot[0], snapshot[1], snapshot[2], snapshot[3]
-    raise ValueError(f"Unsupported snapshot type: {type(snapshot)}")
 
 
 class TAGAN(nn.Module):
@@ -59,6 +50,9 @@ class TAGAN(nn.Module):
             raise ValueError("temporal_propagation must be 'shipped' or 'intended'")
         precision_ctx(precision)   # validates
         self.temporal_propagation_mode = temporal_propagation
+        # index validation of the edge lists: "deferred" (checked after the geometric stage is launched, waiting
+        # only for the CSR build), True (immediate device sync), False (off: HIP-graph capture)
+        self.validate_edges = "deferred"
         self.precision = precision
         self.config = config
         self.memory_bank = NodeMemoryBank(hidden_dim=config.hidden_dim, decay_factor=0.8,
@@ -103,14 +97,19 @@ class TAGAN(nn.Module):
         (model.py:236-239, never consumed) and its parameters get no gradient there either.
         """
         device = next(self.parameters()).device
-        xs, eis, counts = [], [], []
-        for snap in graph_sequence:
-            x, ei, _ea, _ids = _unpack(snap)
-            xs.append(x.to(device))
-            eis.append(ei.to(device))
-            counts.append(int(x.shape[0]))
-        x_cat = torch.cat(xs, 0) if len(xs) > 1 else xs[0]
-        graph = build_graph(eis, counts)
+        if isinstance(graph_sequence, SnapshotBatch):      # pre-ingested (ingest.py): one packed batch
+            batch = graph_sequence if graph_sequence.x.device == device else graph_sequence.to(device)
+            x_cat, counts = batch.x, list(batch.node_counts)
+            graph = build_graph_cat(batch.edge_index, batch.edge_ptr, counts, validate=self.validate_edges)
+        else:
+            xs, eis, counts = [], [], []
+            for snap in graph_sequence:
+                x, ei, _ea, _ids = _unpack(snap)
+                xs.append(x.to(device))
+                eis.append(ei.to(device))
+                counts.append(int(x.shape[0]))
+            x_cat = torch.cat(xs, 0) if len(xs) > 1 else xs[0]
+            graph = build_graph(eis, counts, validate=self.validate_edges)
         h = linear(x_cat, self.node_embedding.weight, self.node_embedding.bias)
         skip = h
         for i, layer in enumerate(self.geometric_attention_layers):
@@ -120,7 +119,8 @@ class TAGAN(nn.Module):
                 h = layer.forward_graph(h, graph)
                 if i == 0:
                     h = h + skip
-        weights = [{"node_attention": None} for _ in graph_sequence] if return_attention_weights else []
+        graph.check_valid()   # the reference's IndexError for an out-of-range edge (deferred: no stream stall)
+        weights = [{"node_attention": None} for _ in range(len(counts))] if return_attention_weights else []
         return h, counts, weights
 
     @staticmethod
@@ -156,14 +156,20 @@ class TAGAN(nn.Module):
         node_major = out_tm.transpose(0, 1).reshape(T, N, H)   # == out.view(T, -1, H) of the reference
         return node_major.mean(1)
 
+    def ingest(self, graph_sequence: List[Snapshot]) -> SnapshotBatch:
+        """Pack a snapshot sequence (dicts or tuples, host or device tensors) into one device batch
+        (ingest.py); ``forward`` accepts the result in place of the list."""
+        return SnapshotBatch.from_sequence(graph_sequence, next(self.parameters()).device)
+
     def forward(self, graph_sequence: List[Snapshot], labels: Optional[torch.Tensor] = None,
                 return_attention_weights: bool = False) -> Dict[str, Any]:
         with precision_ctx(self.precision):
             return self._forward(graph_sequence, labels, return_attention_weights)
 
     def _forward(self, graph_sequence, labels, return_attention_weights):
-        for snap in graph_sequence:
-            _unpack(snap)   # format validation of model.py:187-200
+        if not isinstance(graph_sequence, SnapshotBatch):
+            for snap in graph_sequence:
+                _unpack(snap)   # format validation of model.py:187-200
         x_cat, counts, geo_w = self.encode_snapshots(graph_sequence, return_attention_weights)
         # TemporalPropagation never returns in the shipped code: identity (model.py:276-309).
         xt = self._time_major(x_cat, counts)

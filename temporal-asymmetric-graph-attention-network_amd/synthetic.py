@@ -9,6 +9,18 @@ reproduced instead:
                         edges parent-author -> reply-author with Zipf(1.1) user
                         activity (power-law degrees), same user set every snapshot.
 Generated directly on the target device (inputs resident in HBM before timing).
+
+``make_social_snapshots`` is the ingestion-shaped variant: the reference's snapshot DICTS
+(preprocess_social_media.py:297-315, 374-389; model.py:187-230) with global user ids, a variable
+active-user count per snapshot, local edge indices and optional edge_attr.
+
+Degree law and unique edges (``social``): both endpoints of each reply edge are drawn from the same
+Zipf(alpha = 1.1) user-activity law p(u) ∝ rank(u)^-1.1, so in- and out-degrees are power-law and hub pairs
+repeat; the reference's adjacency is a SET (graph_attention.py:96-105), so what the kernels see is the
+unique (src, dst) count plus one self-loop per node.  At C2 (10,000 users, 100,000 edges per snapshot)
+that is 52.8k unique edges + 10k self-loops = 62.8k CSR entries per snapshot (2,011,143 over the 32
+snapshots, measured on the GPU by tagan_csr_build; ``unique_edges`` computes it on the host);
+``uniform`` (C3-C5) keeps ≈ E unique edges (E/N² ≪ 1).
 """
 from typing import List, Sequence, Tuple
 
@@ -55,3 +67,51 @@ def config_for(name: str, **over):
               output_dim=1, loss_type="bce", dropout=0.1, device="cuda")
     kw.update(over)
     return TAGANConfig(**kw)
+
+
+def unique_edges(edge_index: torch.Tensor, num_nodes: int) -> int:
+    """|unique (src, dst)| of one snapshot (the reference's set adjacency, before self-loops)."""
+    key = edge_index[0].to(torch.int64) * num_nodes + edge_index[1].to(torch.int64)
+    return int(torch.unique(key).numel())
+
+
+def make_social_snapshots(T: int, users: int, edges: int, seed: int = 42, alpha: float = 1.1,
+                          active: Tuple[float, float] = (0.6, 0.9), feature_dim: int = 27,
+                          with_edge_attr: bool = True, device="cpu") -> List[dict]:
+    """Reference-shaped snapshot dicts {x, edge_index, edge_attr, node_ids, timestep}.
+
+    Per snapshot t: a Zipf(alpha)-weighted sample (without replacement) of round(users * U(active)) active
+    users, their GLOBAL ids (user ids 1000 + permuted rank, as the preprocessing's user_id column) in
+    node_ids, x = [activity, age/100, post_count/10, 16-d text embedding, 8-d interest one-hot]
+    (feature_dim = 27, preprocess_social_media.py:297-309), ``edges`` reply edges parent-author ->
+    reply-author drawn from the active users' activity law (LOCAL indices into x; duplicates and self
+    replies allowed), edge_attr [E, 2] = (controversial flag, 1.0) (:312-315), timestep = t * 3600.0."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    rank = torch.randperm(users, generator=g).to(torch.float64) + 1.0
+    activity = rank.pow(-alpha)
+    user_id = 1000 + torch.randperm(users, generator=g)
+    age = torch.randint(18, 70, (users,), generator=g).to(torch.float32)
+    seq = []
+    for t in range(T):
+        frac = active[0] + (active[1] - active[0]) * float(torch.rand(1, generator=g))
+        n = max(2, int(round(users * frac)))
+        act = torch.multinomial(activity, n, replacement=False, generator=g)       # active users this window
+        w = activity[act]
+        src = torch.multinomial(w, edges, replacement=True, generator=g)
+        dst = torch.multinomial(w, edges, replacement=True, generator=g)
+        posts = torch.bincount(src, minlength=n).to(torch.float32)
+        x = torch.zeros(n, feature_dim)
+        x[:, 0] = (w / w.max()).to(torch.float32)
+        x[:, 1] = age[act] / 100.0
+        x[:, 2] = posts / 10.0
+        emb = torch.randn(n, 16, generator=g)
+        x[:, 3:19] = emb / emb.norm(dim=1, keepdim=True)
+        x[torch.arange(n), 19 + torch.randint(0, feature_dim - 19, (n,), generator=g)] = 1.0
+        snap = {"x": x.to(device), "edge_index": torch.stack([src, dst]).to(device),
+                "node_ids": user_id[act].tolist(), "timestep": t * 3600.0}
+        if with_edge_attr:
+            ea = torch.ones(edges, 2)
+            ea[:, 0] = (torch.rand(edges, generator=g) < 0.2).to(torch.float32)
+            snap["edge_attr"] = ea.to(device)
+        seq.append(snap)
+    return seq

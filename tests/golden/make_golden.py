@@ -21,6 +21,9 @@ Cases (SURVEY.md §8c G1–G5):
   geo_*        GeometricAttention standalone (dense mask, no mask, geometric_bias).
   tatt_*       AsymmetricTemporalAttention / TemporalAttention (temporal_attention.py).
   membank_*    NodeMemoryBank.update/get_states/update_state/decay_all traces.
+  ingest_dict_* TAGAN.forward on the reference's snapshot DICTS (model.py:187-230; the format of
+               preprocess_social_media.py:374-389): global user ids, a variable node count per snapshot,
+               edge_attr absent or present, timestep keys — inputs from tagan_amd.synthetic.make_social_snapshots.
   tprop_*      TemporalPropagation's intended compute (G6): TemporalEvolutionLayer (GRU over T,
                time-aware / bidirectional), TemporalSkipConnection (mean/max/sum windows),
                TemporalGatingUnit, and the full forward with tensor masks — reachable only with a
@@ -450,6 +453,12 @@ def main(prefixes):
     cases.append(("e2e_attnw", lambda: e2e_case(R, "e2e_attnw", base, [16, 19, 17, 15, 18], 109, lab1,
                                                 with_attn=True)))
     cases.append(("e2e_nolabels", lambda: e2e_case_nolabel(R)))
+    # ingestion: dict snapshots with global ids, variable N, edge_attr absent / present
+    soc = dict(base, node_feature_dim=27, edge_feature_dim=2)
+    cases.append(("ingest_dict_social", lambda: ingest_dict_case(R, "ingest_dict_social", soc, 6, 60, 150, 120,
+                                                                 False)))
+    cases.append(("ingest_dict_social_ea", lambda: ingest_dict_case(
+        R, "ingest_dict_social_ea", dict(soc, hidden_dim=128, num_heads=8), 5, 80, 240, 121, True)))
     # G3
     for m in METRICS:
         for learn in (False, True):
@@ -500,6 +509,47 @@ def main(prefixes):
             continue
         print(name)
         fn()
+
+
+def ingest_dict_case(R, case, cfg_kw, T, users, edges, seed, with_edge_attr):
+    """TAGAN.forward + backward on dict snapshots (model.py:187-230) — the ingestion golden."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from tagan_amd.synthetic import make_social_snapshots   # our generator (CPU only, no GPU code)
+    cfg_kw = dict(cfg_kw, device="cpu", dropout=0.0)
+    torch.manual_seed(seed)
+    cfg = quiet(R["TAGANConfig"], **cfg_kw)
+    model = quiet(R["TAGAN"], cfg)
+    model.train()
+    seq = make_social_snapshots(T, users, edges, seed=seed + 1, with_edge_attr=with_edge_attr)
+    for snap in seq:
+        snap["x"] = snap["x"].clone().requires_grad_(True)
+    labels = torch.tensor([1.0])
+    out = quiet(model, seq, labels=labels)
+    quiet(out["loss"].backward)
+    t = {}
+    for i, snap in enumerate(seq):
+        t[f"in.x.{i}"] = snap["x"].detach()
+        t[f"in.edge_index.{i}"] = snap["edge_index"]
+        t[f"in.node_ids.{i}"] = torch.tensor(snap["node_ids"], dtype=torch.int64)
+        if "edge_attr" in snap:
+            t[f"in.edge_attr.{i}"] = snap["edge_attr"]
+        t[f"grad.x.{i}"] = snap["x"].grad
+    t["in.timestep"] = torch.tensor([snap["timestep"] for snap in seq], dtype=torch.float64)
+    t["in.labels"] = labels
+    for k, v in model.state_dict().items():
+        t["sd." + k] = v
+    for name, p in model.named_parameters():
+        if p.grad is not None:
+            t["grad." + name] = p.grad
+    t["out.logits"] = out["logits"]
+    t["out.predictions"] = out["predictions"]
+    t["out.loss"] = out["loss"].detach().reshape(1)
+    n_list = [int(snap["x"].shape[0]) for snap in seq]
+    meta = dict(kind="e2e", format="dict", config=cfg_kw, n_list=n_list, seed=seed, T=T, users=users,
+                edges=edges, with_edge_attr=with_edge_attr, labels=[1.0], labels_dtype=str(labels.dtype),
+                anchors=["src/tagan/model.py:158-473 (dict snapshots :187-230)",
+                         "preprocess_social_media.py:297-315, 374-389"])
+    save(case, t, meta)
 
 
 def e2e_case_nolabel(R):

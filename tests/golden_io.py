@@ -39,6 +39,18 @@ def sequence(meta, t, device="cpu"):
     return seq
 
 
+def dict_sequence(meta, t, device="cpu"):
+    """The reference's snapshot dicts of an ingest_dict_* case (model.py:187-230): edge_attr only when stored."""
+    seq = []
+    for i in range(meta["T"]):
+        d = {"x": t["in.x.%d" % i].to(device), "edge_index": t["in.edge_index.%d" % i].to(device),
+             "node_ids": t["in.node_ids.%d" % i].tolist(), "timestep": float(t["in.timestep"][i])}
+        if ("in.edge_attr.%d" % i) in t:
+            d["edge_attr"] = t["in.edge_attr.%d" % i].to(device)
+        seq.append(d)
+    return seq
+
+
 def labels(meta, t, device="cpu"):
     lab = t.get("in.labels")
     return lab.to(device) if lab is not None else None
