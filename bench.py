@@ -61,6 +61,10 @@ def parse():
                     help="only the C4 roofline launches (for rocprofv3 kernel-trace / PMC passes of the same kernels)")
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--no-c1", action="store_true", help="skip the GPU C1 line beside the C1 CPU baselines")
+    ap.add_argument("--launch", default="auto", choices=("auto", "graph", "eager"),
+                    help="graph: replay the step as a HIP graph (graph_step.py); eager: launch every kernel from "
+                         "Python; auto (default): time a short trial of both and keep the faster (--shard: eager)")
+    ap.add_argument("--no-graph", action="store_true", help="same as --launch eager")
     ap.add_argument("--shard", action="store_true",
                     help="one sequence sharded by snapshot over all ranks (strong scaling; C5 mode) instead of "
                          "one sequence per rank (data parallel, weak scaling)")
@@ -322,17 +326,45 @@ def make_step(model, opt, cfg, fwd, bwd):
     return step
 
 
-def gpu_c1_line(dev, precision, steps=20, warmup=5):
+def graphed(model, opt, cfg, fwd, world=1, bucket=None, warmup=3):
+    """The bench step as a replayable HIP graph (graph_step.GraphedStep): forward, backward, clip, Adam in one
+    graph at N = 1; at N > 1 the RCCL gradient all-reduce runs eagerly between two captured segments."""
+    from tagan_amd.graph_step import GraphedStep
+
+    def fb():
+        out = fwd()
+        out["loss"].backward()
+        return out["loss"]
+
+    def post():
+        torch.nn.utils.clip_grad_norm_(model.parameters(), cfg.gradient_clip_val)
+        opt.step()
+
+    if world == 1:
+        def whole():
+            loss = fb()
+            post()
+            return loss
+        return GraphedStep(model, whole, optimizer=opt, warmup=warmup)
+    return GraphedStep(model, fb, optimizer=opt, warmup=warmup, between=lambda: bucket.allreduce_mean(static=True),
+                       post=post)
+
+
+def gpu_c1_line(dev, precision, steps=20, warmup=5, graph=True):
     """The same training step on C1 (example.py: 500 nodes, 1000 edges, 10 snapshots, H=64, 4 heads) on this GPU,
     beside the C1 CPU baselines (host-launch-bound at this size)."""
     from tagan_amd import TAGAN, synthetic
     cfg = synthetic.config_for("c1")
     torch.manual_seed(0)
     model = TAGAN(cfg, precision=precision).to(dev).train()
-    opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay)
+    opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay, capturable=graph,
+                           fused=True)
     seq = synthetic.make_sequence("c1", dev, seed=1000)
     labels = torch.tensor([1.0], device=dev)
     step = make_step(model, opt, cfg, lambda: model(seq, labels=labels), lambda out: out["loss"].backward())
+    g = graphed(model, opt, cfg, lambda: model(seq, labels=labels)) if graph else None
+    if g is not None:
+        step = g
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -342,8 +374,10 @@ def gpu_c1_line(dev, precision, steps=20, warmup=5):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     T = len(seq)
+    if g is not None:
+        g.close()
     return {"value": round(T * steps / el, 3), "unit": "graph-snapshots/s", "ms_per_step": round(el / steps * 1e3, 3),
-            "steps": steps, "dtype": precision}
+            "steps": steps, "dtype": precision, "launch": "hip-graph" if graph else "eager"}
 
 
 def _relaunch(n):
@@ -388,10 +422,15 @@ def main():
     os.environ["TAGAN_BENCH_CONFIG"] = args.config
     cfg = synthetic.config_for(args.config)
     N, E, T, H, heads = synthetic.CONFIGS[args.config][:5]
+    launch = "eager" if (args.no_graph or args.shard) else args.launch
+    use_graph = launch != "eager"   # capturable optimizer whenever a graph may be captured
     torch.manual_seed(0)
     model = TAGAN(cfg, precision=args.precision).to(dev).train()
     broadcast_parameters(model)
-    opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay)
+    # the reference trainer's Adam (trainer.py); fused=True: the same update as ONE multi-tensor kernel
+    # (capturable into the step graph), instead of ~15 foreach launches
+    opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay,
+                           capturable=use_graph, fused=True)
     init_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
     if args.shard:
         from tagan_amd.sharded import ShardGradSync, SnapshotShardedTAGAN, blocks
@@ -420,9 +459,39 @@ def main():
 
         def bwd(out):
             out["loss"].backward()
-            bucket.allreduce_mean()
+            bucket.allreduce_mean(static=use_graph)
 
     step = make_step(model, opt, cfg, fwd, bwd)
+    eager_step = step
+
+    def trial(fn, n=5):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)   # every rank takes the same decision
+        return float(t.item()) / n
+
+    launch_trial = None
+    gstep = None
+    if use_graph:
+        gstep = graphed(model, opt, cfg, fwd, world, None if args.shard else bucket)
+        if launch == "auto":
+            tg = trial(gstep)
+            gstep.close()
+            te = trial(eager_step)
+            launch_trial = {"graph_ms": round(tg * 1e3, 3), "eager_ms": round(te * 1e3, 3)}
+            if tg < te:
+                gstep = graphed(model, opt, cfg, fwd, world, None if args.shard else bucket)
+            else:
+                gstep = None
+    if gstep is not None:
+        step = gstep
 
     def timed(steps, warmup):
         """W untimed steps, then exactly K steps between barrier + sync; max over ranks."""
@@ -468,22 +537,45 @@ def main():
     rec["config"]["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
     rec["config"]["gemms"] = ("hipBLASLt/rocBLAS solutions from the TunableOp table %s" % os.path.basename(gemm_table)
                               if gemm_table else "library-default heuristic")
+    rec["launch"] = ("hip-graph (one replay per step)" if world == 1 else
+                     "hip-graph (fwd+bwd and clip+Adam replays, RCCL all-reduce between)") if gstep is not None \
+        else "eager"
+    if launch_trial:
+        rec["launch_trial"] = dict(launch_trial, note="5-step trial of both launch modes; the faster one is timed")
+    if gstep is not None:
+        gstep.close()
+        step = make_step(model, opt, cfg, fwd, bwd)
     rec["breakdown"] = breakdown(model, seq, fwd, bwd, opt, cfg)
     if args.precision == "fp32" and not args.no_alt_precision:
         # the same step with bf16 activations between kernels (BASELINE's C2 dtype), fp32 math inside
         # every kernel; held to the fp32 mode by tests/test_gpu_bf16.py (loss 2e-2, gradients 8e-2)
         model.precision = "bf16"
+        gstep = graphed(model, opt, cfg, fwd, world, None if args.shard else bucket) if use_graph else None
+        if gstep is not None and launch == "auto":
+            tg = trial(gstep)
+            gstep.close()
+            te = trial(eager_step)
+            gstep = graphed(model, opt, cfg, fwd, world, None if args.shard else bucket) if tg < te else None
+            alt_launch = {"graph_ms": round(tg * 1e3, 3), "eager_ms": round(te * 1e3, 3)}
+        else:
+            alt_launch = None
+        if gstep is not None:
+            step = gstep
         alt = timed(args.steps, args.warmup)
+        if gstep is not None:
+            gstep.close()
+            step = make_step(model, opt, cfg, fwd, bwd)
         model.precision = args.precision
         rec["alt_precision"] = {"precision": "bf16", "value": round(seqs_per_step * T * args.steps / alt, 3),
                                 "ms_per_step": round(alt / args.steps * 1e3, 3),
+                                "launch": "hip-graph" if gstep is not None else "eager", "launch_trial": alt_launch,
                                 "dtype": "bf16 (activations; fp32 math and accumulation)"}
     if rank == 0 and not args.no_roofline:
         roof = roofline_c4(args.roofline_reps)
         roof["cache_assisted"] = dict(roofline_cache_assisted(seq, cfg), config=args.config)
         rec["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        c1 = None if args.no_c1 else gpu_c1_line(dev, args.precision)
+        c1 = None if args.no_c1 else gpu_c1_line(dev, args.precision, graph=launch != "eager")
         rec["cpu_baseline"] = cpu_baseline(cfg, args.config, init_state, args.cpu_sample_snapshots, gpu_c1=c1,
                                            gpu_value=value)
     if rank == 0:

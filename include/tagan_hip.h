@@ -63,6 +63,14 @@ int tagan_device_arch(char* buf, int len);   /* e.g. "gfx950"; needs a device */
  * (seed, stream) by four lowbias32 rounds, then u = lowbias32(counter ^ key) >> 8 / 2^24. */
 float tagan_uniform(uint64_t seed, uint64_t stream, uint32_t counter);
 
+/* HIP-graph replay of a training step.  tagan_set_seed_counter registers a device uint64 counter (NULL to
+ * clear; process-wide, read by the launches that follow): every kernel that draws a dropout mask then uses
+ * seed ^ (counter · 0x9E3779B97F4A7C15) with the counter's value AT RUN TIME, so the seeds baked into a captured
+ * graph still give fresh masks per replay once the graph advances the counter with tagan_seed_counter_step
+ * (one tiny launch, capturable).  With no counter registered every seed is used as passed. */
+void tagan_set_seed_counter(const uint64_t* counter);
+int tagan_seed_counter_step(uint64_t* counter, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Snapshot CSR builder.  Replaces graph_attention.py:96-105
  *   adj = zeros(N,N); adj[edge_index[0], edge_index[1]] = 1; adj += eye(N)
@@ -305,6 +313,31 @@ size_t tagan_proj_ln_bwd_workspace(int64_t M, int32_t H);
 int tagan_proj_ln_bwd(int64_t M, int32_t H, int32_t K, const float* da, const float* w, const float* x,
                       const float* mean, const float* rstd, const float* gamma, const float* dres, float* dx,
                       float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused classification head + loss (csrc/head.hip).  Replaces model.py:377-459 after the pooling:
+ * graph_features [B, T, H] (row 0 = x0 [T, H], rows 1..B-1 zero, model.py:382-394) ->
+ * attention pooling over T (classification.py:912-925: s_t = w2·tanh(W1 x_t + b1), softmax over T,
+ * Σ_t a_t x_t) -> Linear(Wc1, bc1) -> LayerNorm(ln_w, ln_b, eps) -> ReLU -> Dropout(p_drop; stream =
+ * batch row, counter = feature) -> Linear(Wc2, bc2) = logits [B, C]; preds = sigmoid (C = 1) or
+ * softmax; loss_kind 1 = BCE-with-logits mean over B·C (labels [B·C]), 2 = cross entropy mean over B
+ * (labels [B] class indices stored as float), 0 = none.  saved: tagan_head_saved_floats(B, T, H) floats
+ * kept for the backward.  One workgroup per call.  Backward: any of g_loss [1] / g_logits [B, C] /
+ * g_preds [B, C] (the incoming gradients) may be NULL; writes dx0 [T, H] and every parameter gradient.
+ * Supported: tagan_head_supported(T, H, C) (H <= 256, H % 4 == 0, T <= 128, C <= 16, T·H <= 8192).
+ * ------------------------------------------------------------------------- */
+int tagan_head_supported(int32_t T, int32_t H, int32_t C);
+size_t tagan_head_saved_floats(int32_t B, int32_t T, int32_t H);
+int tagan_head_fwd(int32_t B, int32_t T, int32_t H, int32_t C, const float* x0, const float* W1, const float* b1,
+                   const float* w2, const float* Wc1, const float* bc1, const float* ln_w, const float* ln_b,
+                   float eps, const float* Wc2, const float* bc2, float p_drop, uint64_t seed, const float* labels,
+                   int loss_kind, float* logits, float* preds, float* loss, float* saved, void* stream);
+int tagan_head_bwd(int32_t B, int32_t T, int32_t H, int32_t C, const float* x0, const float* W1, const float* w2,
+                   const float* Wc1, const float* ln_w, const float* ln_b, const float* Wc2, float p_drop,
+                   uint64_t seed, const float* labels, int loss_kind, const float* logits, const float* preds,
+                   const float* saved, const float* g_loss, const float* g_logits, const float* g_preds,
+                   float* dx0, float* dW1, float* db1, float* dw2, float* dWc1, float* dbc1, float* dln_w,
+                   float* dln_b, float* dWc2, float* dbc2, void* stream);
 
 /* ---------------------------------------------------------------------------
  * NodeMemoryBank on the device.  Replaces src/tagan/utils/memory_bank.py:14-360

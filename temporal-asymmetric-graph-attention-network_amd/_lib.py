@@ -37,6 +37,8 @@ _SIGNATURES = {
     "tagan_version": (_c.c_int, []),
     "tagan_device_arch": (_c.c_int, [_c.c_char_p, _c.c_int]),
     "tagan_uniform": (_f32, [_u64, _u64, _c.c_uint32]),
+    "tagan_set_seed_counter": (None, [_p]),
+    "tagan_seed_counter_step": (_c.c_int, [_p, _p]),
     "tagan_csr_build_workspace": (_sz, [_i64, _i64]),
     "tagan_pool_workspace": (_sz, [_i32, _i32]),
     "tagan_colsum_workspace": (_sz, [_i64, _i32]),
@@ -78,6 +80,11 @@ _SIGNATURES = {
     "tagan_proj_gemm": (_c.c_int, [_i64, _i32, _i32, _p, _i64, _p, _c.c_int, _p, _i64, _p]),
     "tagan_proj_ln_bwd_workspace": (_sz, [_i64, _i32]),
     "tagan_proj_ln_bwd": (_c.c_int, [_i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
+    "tagan_head_supported": (_c.c_int, [_i32, _i32, _i32]),
+    "tagan_head_saved_floats": (_sz, [_i32, _i32, _i32]),
+    "tagan_head_fwd": (_c.c_int, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _f32, _p, _p, _f32, _u64,
+                                  _p, _c.c_int, _p, _p, _p, _p, _p]),
+    "tagan_head_bwd": (_c.c_int, [_i32] * 4 + [_p] * 7 + [_f32, _u64, _p, _c.c_int] + [_p] * 6 + [_p] * 10 + [_p]),
     "tagan_membank_init": (_c.c_int, [_p, _p]),
     "tagan_membank_lookup": (_c.c_int, [_p, _p, _i64, _c.c_int, _i32, _p, _p, _p]),
     "tagan_membank_update": (_c.c_int, [_p, _p, _i64, _p, _i64, _i64, _c.c_double, _i32, _i32, _u64, _p, _p, _p]),

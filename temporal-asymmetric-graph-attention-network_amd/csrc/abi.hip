@@ -5,6 +5,15 @@
 
 namespace tagan {
 static thread_local char g_err[512] = "";
+static const uint64_t* g_seed_ctr = nullptr;
+
+const uint64_t* seed_counter() { return g_seed_ctr; }
+
+namespace {
+__global__ void k_counter_step(uint64_t* c) {
+    if (threadIdx.x == 0) c[0] = c[0] + 1;
+}
+}  // namespace
 
 void set_error(const char* fmt, ...) {
     va_list ap;
@@ -27,6 +36,15 @@ int tagan_device_arch(char* buf, int len) {
     hipDeviceProp_t p;
     TAGAN_CHECK_HIP(hipGetDeviceProperties(&p, dev), "hipGetDeviceProperties");
     snprintf(buf, (size_t)len, "%s", p.gcnArchName);
+    return TAGAN_OK;
+}
+
+void tagan_set_seed_counter(const uint64_t* counter) { tagan::g_seed_ctr = counter; }
+
+int tagan_seed_counter_step(uint64_t* counter, void* stream) {
+    TAGAN_REQUIRE(counter != nullptr, TAGAN_ERR_ARG, "seed_counter_step: null counter");
+    tagan::k_counter_step<<<1, 64, 0, tagan::as_stream(stream)>>>(counter);
+    TAGAN_CHECK_LAUNCH("seed_counter_step");
     return TAGAN_OK;
 }
 

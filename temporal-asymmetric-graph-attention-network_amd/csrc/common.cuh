@@ -66,6 +66,16 @@ __host__ __device__ __forceinline__ uint32_t drop_key(uint64_t seed, uint64_t st
     return lowbias32(k ^ (uint32_t)(stream >> 32));
 }
 
+// Graph-replay seed source.  When the host registered a device counter (tagan_set_seed_counter), every kernel
+// that draws a dropout mask mixes the counter's CURRENT value into its seed when it starts (TAGAN_LIVE_SEED), so
+// a captured HIP graph whose first node advances the counter (tagan_seed_counter_step) draws fresh masks on
+// every replay.  Null (the default) = the seed as passed: eager calls are unchanged.
+const uint64_t* seed_counter();
+#define TAGAN_LIVE_SEED(A)                                                          \
+    do {                                                                            \
+        if ((A).seed_ctr) (A).seed ^= *(A).seed_ctr * 0x9E3779B97F4A7C15ull;        \
+    } while (0)
+
 // uniform in [0,1) with 24-bit resolution
 __host__ __device__ __forceinline__ float drop_u(uint32_t key, uint32_t counter) {
     return (float)(lowbias32(counter ^ key) >> 8) * (1.0f / 16777216.0f);

@@ -183,6 +183,7 @@ struct GeoArgs {
     const float* mparam;
     float p_drop, inv_keep;
     uint64_t seed;
+    const uint64_t* seed_ctr;   // graph-replay seed source (tagan_set_seed_counter) or null
     const float* o;
     const float* lse_in;
     const float* dout;
@@ -294,6 +295,7 @@ __device__ __forceinline__ float dotf(const float (&a)[F], const float (&b)[F]) 
 // ------------------------------------------------------------------ forward
 template <int METRIC, int LPR, int FPL, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
+    TAGAN_LIVE_SEED(A);
     constexpr int UN = Unroll<FPL>::v;
     Lanes<LPR> L;
     const int nchunks = A.g.row_counts[0];
@@ -370,6 +372,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
 // lane owns 4 features (H <= 256).
 template <typename S>
 __global__ void __launch_bounds__(BLK) k_geo_fwd_merge(GeoArgs A) {
+    TAGAN_LIVE_SEED(A);
     using IO = Io<S>;
     const int64_t k = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6);
     if (k >= A.g.row_counts[1]) return;
@@ -404,6 +407,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_merge(GeoArgs A) {
 // ------------------------------------------------------------------ backward, row pass (CSR chunks)
 template <int METRIC, int LPR, int FPL, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
+    TAGAN_LIVE_SEED(A);
     constexpr int UN = Unroll<FPL>::v;
     __shared__ float red[BLK];
     Lanes<LPR> L;
@@ -517,6 +521,7 @@ __global__ void __launch_bounds__(BLK) k_geo_sum_parts(const int32_t* __restrict
 // ------------------------------------------------------------------ backward, column pass (CSC chunks)
 template <int METRIC, int LPR, int FPL, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
+    TAGAN_LIVE_SEED(A);
     constexpr int UN = Unroll<FPL>::v;
     Lanes<LPR> L;
     const int nchunks = A.g.col_counts[0];
@@ -625,6 +630,7 @@ __global__ void __launch_bounds__(BLK) k_reduce_partials(const float* __restrict
 // used only when the fast path's lane geometry does not fit.
 template <int METRIC>
 __global__ void __launch_bounds__(BLK) k_geo_alpha(GeoArgs A, float* __restrict__ alpha) {
+    TAGAN_LIVE_SEED(A);
     const int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x;
     if (t >= A.N * A.heads) return;
     const int64_t row = t / A.heads;
@@ -652,6 +658,7 @@ __global__ void __launch_bounds__(BLK) k_geo_alpha(GeoArgs A, float* __restrict_
 
 template <int METRIC>
 __global__ void __launch_bounds__(BLK) k_geo_fwd_generic(GeoArgs A) {
+    TAGAN_LIVE_SEED(A);
     const int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x;
     if (t >= A.N * A.heads) return;
     const int64_t row = t / A.heads;
@@ -690,6 +697,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_generic(GeoArgs A) {
 
 template <int METRIC>
 __global__ void __launch_bounds__(BLK) k_geo_bwd_row_generic(GeoArgs A) {
+    TAGAN_LIVE_SEED(A);
     const int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x;
     if (t >= A.N * A.heads) return;
     const int64_t row = t / A.heads;
@@ -739,6 +747,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_generic(GeoArgs A) {
 
 template <int METRIC>
 __global__ void __launch_bounds__(BLK) k_geo_bwd_col_generic(GeoArgs A) {
+    TAGAN_LIVE_SEED(A);
     const int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x;
     if (t >= A.N * A.heads) return;
     const int64_t colj = t / A.heads;
@@ -921,7 +930,7 @@ GeoArgs make_args(const tagan_graph* g, int heads, int d, const void* q, const v
     A.mparam = mparam;
     A.p_drop = p_drop;
     A.inv_keep = 1.f / (1.f - p_drop);
-    A.seed = seed;
+    A.seed = seed; A.seed_ctr = seed_counter();
     A.inv_sqrt_d = 1.f / sqrtf((float)d);
     return A;
 }

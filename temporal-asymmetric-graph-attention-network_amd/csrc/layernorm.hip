@@ -31,6 +31,7 @@ struct LnArgs {
     const float* b;
     float p_drop, inv_keep;
     uint64_t seed;
+    const uint64_t* seed_ctr;   // graph-replay seed source (tagan_set_seed_counter) or null
     const float* gamma;
     const float* beta;
     float eps;
@@ -75,6 +76,7 @@ __device__ __forceinline__ float4 drop4(const LnArgs& A, float4 v, int64_t row, 
 // single row pair per wave left the LN passes latency-bound at ~50 % of the HBM roofline.
 template <int LPR, int NV, int U, typename S>
 __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
+    TAGAN_LIVE_SEED(A);
     constexpr int RPW = WAVE / LPR;
     const int lane = threadIdx.x & (WAVE - 1), sl = lane % LPR;
     const int64_t wave = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6);
@@ -176,6 +178,7 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
 
 template <int LPR, int NV, int U, typename S>
 __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
+    TAGAN_LIVE_SEED(A);
     constexpr int RPW = WAVE / LPR;
     __shared__ float red[BLK / WAVE][RPW][3 * 4 * NV * LPR];
     const int lane = threadIdx.x & (WAVE - 1), sl = lane % LPR, sub = lane / LPR, w = threadIdx.x >> 6;
@@ -343,7 +346,7 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
     TAGAN_REQUIRE(M > 0 && a && gamma && beta && y && mean && rstd, TAGAN_ERR_ARG, "layernorm_fwd: bad args");
     TAGAN_REQUIRE(p_drop >= 0.f && p_drop < 1.f, TAGAN_ERR_ARG, "layernorm_fwd: p_drop");
     LnArgs A{};
-    A.M = M; A.H = H; A.a = a; A.a_bias = a_bias; A.b = b; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
+    A.M = M; A.H = H; A.a = a; A.a_bias = a_bias; A.b = b; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed; A.seed_ctr = seed_counter();
     A.gamma = gamma; A.beta = beta; A.eps = eps; A.s_out = s_out; A.y = y; A.mean = mean; A.rstd = rstd;
     A.ldy = ldy > 0 ? ldy : H;
     TAGAN_REQUIRE(A.ldy >= H && A.ldy % 4 == 0, TAGAN_ERR_ARG, "layernorm_fwd: ldy %lld", (long long)ldy);
@@ -370,7 +373,7 @@ int tagan_add_layernorm_skip_fwd(int64_t M, int32_t H, const float* a, const flo
                   TAGAN_ERR_ARG, "layernorm_skip_fwd: bad args");
     TAGAN_REQUIRE(p_drop >= 0.f && p_drop < 1.f, TAGAN_ERR_ARG, "layernorm_skip_fwd: p_drop");
     LnArgs A{};
-    A.M = M; A.H = H; A.a = a; A.a_bias = a_bias; A.b = b; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
+    A.M = M; A.H = H; A.a = a; A.a_bias = a_bias; A.b = b; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed; A.seed_ctr = seed_counter();
     A.gamma = gamma; A.beta = beta; A.eps = eps; A.s_out = s_out; A.y = y; A.mean = mean; A.rstd = rstd;
     A.ldy = H;
     A.gamma_s = gamma_s; A.beta_s = beta_s; A.eps_s = eps_s; A.mean_s = mean_s; A.rstd_s = rstd_s;
@@ -401,7 +404,7 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, cons
                   TAGAN_ERR_WORKSPACE, "layernorm_bwd: workspace");
     LnArgs A{};
     A.M = M; A.H = H; A.gamma = gamma; A.s_in = s_in; A.mean = (float*)mean; A.rstd = (float*)rstd; A.dy = dy;
-    A.dres = dres; A.ds = ds; A.da = da; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
+    A.dres = dres; A.ds = ds; A.da = da; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed; A.seed_ctr = seed_counter();
     A.part = want ? (float*)workspace : nullptr;
     A.want_dsa = dsum_a != nullptr;
     const int u = ln_rows(nv);

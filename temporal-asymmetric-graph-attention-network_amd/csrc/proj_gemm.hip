@@ -80,6 +80,7 @@ struct PgArgs {
     const float* res;
     float p_drop, inv_keep;
     uint64_t seed;
+    const uint64_t* seed_ctr;   // graph-replay seed source (tagan_set_seed_counter) or null
     const float* g2;
     const float* b2;
     float eps2;
@@ -442,6 +443,7 @@ __device__ __forceinline__ void block_partials(const PgArgs& P, float* lds, floa
 // One workgroup per 128 rows; KCH weight chunks staged per output chunk (the K = 3H input gradient).
 template <int PRO, int EPI, bool KMAJOR, bool SKIP, int KCH, int NCH>
 __global__ void __launch_bounds__(PG_BLK, 2) k_proj(PgArgs P) {
+    TAGAN_LIVE_SEED(P);
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x >> 6, h = lane >> 5, cl = lane & 31;
     const int64_t row_w = (int64_t)blockIdx.x * PG_ROWS + 32 * w;          // first row of this wave
@@ -483,6 +485,7 @@ __global__ void __launch_bounds__(PG_BLK, 2) k_proj(PgArgs P) {
 // for the second and third chunk type).
 template <int PRO, int EPI, bool KMAJOR, bool SKIP>
 __global__ void __launch_bounds__(PG_BLK, 2) k_proj_res(PgArgs P, int nslots) {
+    TAGAN_LIVE_SEED(P);
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x >> 6, h = lane >> 5, cl = lane & 31;
     const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
@@ -552,6 +555,7 @@ constexpr int PP_BLK = 512;
 
 template <int PRO, int EPI, bool KMAJOR, bool SKIP>
 __global__ void __launch_bounds__(PP_BLK, 1) k_proj_pp(PgArgs P, int nslots) {
+    TAGAN_LIVE_SEED(P);
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x >> 6, half = w >> 2, h = lane >> 5, cl = lane & 31;
     const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
@@ -725,7 +729,7 @@ int tagan_proj_ln_fwd(int64_t M, int32_t H, const float* a, const float* w, cons
     TAGAN_REQUIRE(aligned16(a) && aligned16(w), TAGAN_ERR_ARG, "proj_ln_fwd: operands must be 16-byte aligned");
     PgArgs P{};
     P.M = M; P.kch = 1; P.nch = 1; P.a = a; P.lda = H; P.w = w; P.ldw = H; P.bias = bias; P.out = y; P.ldo = H;
-    P.res = res; P.p_drop = p_drop; P.inv_keep = 1.f / (1.f - p_drop); P.seed = seed; P.g2 = gamma; P.b2 = beta;
+    P.res = res; P.p_drop = p_drop; P.inv_keep = 1.f / (1.f - p_drop); P.seed = seed; P.seed_ctr = seed_counter(); P.g2 = gamma; P.b2 = beta;
     P.eps2 = eps; P.s_out = s_out; P.mean2 = mean; P.rstd2 = rstd; P.gs = gamma_s; P.bs = beta_s; P.eps_s = eps_s;
     P.mean_s = mean_s; P.rstd_s = rstd_s;
     hipStream_t s = as_stream(stream);

@@ -40,6 +40,7 @@ struct TArgs {
     int causal;
     float p_drop, inv_keep, inv_sqrt_d;
     uint64_t seed;
+    const uint64_t* seed_ctr;   // graph-replay seed source (tagan_set_seed_counter) or null
     float* out;
     int64_t o_row, o_t;
     float* lse;
@@ -90,6 +91,7 @@ __device__ __forceinline__ void load_row(const float* __restrict__ p, int d, flo
 template <int D>
 __global__ void __launch_bounds__(BLK) k_tattn_fwd(TArgs A, const float* __restrict__ q,
                                                    const float* __restrict__ k, const float* __restrict__ v) {
+    TAGAN_LIVE_SEED(A);
     const int lane = threadIdx.x & (WAVE - 1);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int T = A.T, d = A.d;
@@ -160,6 +162,7 @@ template <int D>
 __global__ void __launch_bounds__(BLK) k_tattn_bwd(TArgs A, const float* __restrict__ q,
                                                    const float* __restrict__ k, const float* __restrict__ v,
                                                    const float* __restrict__ dout, const float* __restrict__ lse) {
+    TAGAN_LIVE_SEED(A);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & (WAVE - 1);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -337,6 +340,7 @@ template <int D>
 __global__ void __launch_bounds__(BLK) k_tattn_fwd_v2(TArgs A, const float* __restrict__ q,
                                                       const float* __restrict__ k, const float* __restrict__ v,
                                                       int G) {
+    TAGAN_LIVE_SEED(A);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int T = A.T, NB = 2 * T - 1;
     float* Qs = sm;
@@ -415,6 +419,7 @@ __global__ void __launch_bounds__(BLK) k_tattn_bwd_v2(TArgs A, const float* __re
                                                       const float* __restrict__ k, const float* __restrict__ v,
                                                       const float* __restrict__ dout, const float* __restrict__ lse,
                                                       int G) {
+    TAGAN_LIVE_SEED(A);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int T = A.T, NB = 2 * T - 1;
     float* Qs = sm;
@@ -686,6 +691,7 @@ template <int D, int LG, typename S, int WPH>
 __global__ void __launch_bounds__(V3_BLK * WPH) k_tattn_fwd_v3(TArgs A, const float* __restrict__ q,
                                                                const float* __restrict__ k,
                                                                const float* __restrict__ v, int n_hg) {
+    TAGAN_LIVE_SEED(A);
     constexpr int HPW = WAVE / LG;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int T = A.T, NB = 2 * T - 1, NBp = (NB + 3) & ~3;
@@ -746,6 +752,7 @@ __global__ void __launch_bounds__(V3_BLK * WPH) k_tattn_bwd_v3(TArgs A, const fl
                                                                const float* __restrict__ v,
                                                                const float* __restrict__ dout,
                                                                const float* __restrict__ lse, int n_hg) {
+    TAGAN_LIVE_SEED(A);
     constexpr int HPW = WAVE / LG;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int T = A.T, NB = 2 * T - 1, NBp = (NB + 3) & ~3;
@@ -1000,6 +1007,7 @@ template <int TT, int DT, typename S>
 __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_F) k_tattn_fwd_v4(TArgs A, const float* __restrict__ q,
                                                        const float* __restrict__ k,
                                                        const float* __restrict__ v) {
+    TAGAN_LIVE_SEED(A);
     constexpr int TP = 16 * TT, LT = v4_ld(TP);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int T = A.T, d = A.d;
@@ -1114,6 +1122,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
                                                        const float* __restrict__ v,
                                                        const float* __restrict__ dout,
                                                        const float* __restrict__ lse) {
+    TAGAN_LIVE_SEED(A);
     constexpr int TP = 16 * TT, LD = v4_ld(TP), DP = 16 * DT;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int T = A.T, NB = 2 * T - 1, d = A.d;
@@ -1468,7 +1477,7 @@ TArgs make(int64_t rows, int T, int heads, int d, int64_t s_row, int64_t s_t, co
     A.p_drop = p_drop;
     A.inv_keep = 1.f / (1.f - p_drop);
     A.inv_sqrt_d = 1.f / sqrtf((float)d);
-    A.seed = seed;
+    A.seed = seed; A.seed_ctr = seed_counter();
     return A;
 }
 

@@ -29,13 +29,32 @@ class GradBucket:
         self.n = sum(p.numel() for p in self.params)
         self.flat = None
 
-    def allreduce_mean(self, group=None, force: bool = False) -> None:
-        """``force``: run the collective even at world size 1 (exercises the RCCL path on one GPU)."""
+    def allreduce_mean(self, group=None, force: bool = False, static: bool = False) -> None:
+        """``force``: run the collective even at world size 1 (exercises the RCCL path on one GPU).
+        ``static``: the capturable form (HIP graphs): no flags and no host read-back — the grads present
+        locally are packed, reduced and written back; every rank must have the same grads present (the
+        flagged form, used by the eager warm-up before a capture, establishes that)."""
         if not dist.is_available() or not dist.is_initialized():
             return
         if dist.get_world_size(group) == 1 and not force:
             return
         if not self.params:
+            return
+        if static:
+            live = [p for p in self.params if p.grad is not None]
+            if not live:
+                return
+            n = sum(p.numel() for p in live)
+            if self.flat is None or self.flat.device != live[0].device or self.flat.numel() < n:
+                self.flat = torch.empty(max(n, self.n + len(self.params)), dtype=torch.float32, device=live[0].device)
+            torch.cat([p.grad.reshape(-1) for p in live], out=self.flat[:n])
+            dist.all_reduce(self.flat[:n], op=dist.ReduceOp.SUM, group=group)
+            self.flat[:n].div_(dist.get_world_size(group))
+            off = 0
+            for p in live:
+                m = p.numel()
+                p.grad.copy_(self.flat[off:off + m].view_as(p))
+                off += m
             return
         dev = self.params[0].device
         k = len(self.params)

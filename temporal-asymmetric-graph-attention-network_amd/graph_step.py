@@ -1,0 +1,84 @@
+"""A whole TAGAN training step as ONE replayable HIP graph.
+
+The reference trainer's step (trainer.py:295-311: forward, loss, backward, clip_grad_norm_, optimizer step)
+issues ~300 launches per C2 sequence from Python: at C2 bf16 and at C1 the host, not the GPU, sets the pace
+(DESIGN.md §4).  ``GraphedStep`` captures the step once with ``torch.cuda.graph`` and replays it: the CSR
+build, both attention stacks, the fused head + loss, their backward passes, the gradient all-reduce (N > 1,
+RCCL captures into the graph), clipping and Adam all run from one ``hipGraphLaunch``.
+
+What capture needs from the hot path, and how it gets it:
+* fresh dropout masks per replay — the seeds drawn at capture time are constants in the graph, so the step
+  first advances a device counter (``tagan_seed_counter_step``) that every dropout kernel mixes into its seed
+  at run time (``tagan_set_seed_counter``, include/tagan_hip.h);
+* no host synchronisation inside the step — the edge-index validation is switched off for the captured step
+  (``model.validate_edges = False``; the inputs are static and were validated by the eager warm-up), and the
+  gradient bucket runs in its static form (``GradBucket.allreduce_mean(static=True)``);
+* static inputs — the replay re-runs the step on the same input tensors (the bench's resident sequence);
+  a caller feeding new data copies it into those tensors before ``__call__``;
+* a capturable optimizer (``torch.optim.Adam(..., capturable=True)``).
+"""
+import ctypes
+from typing import Callable, Optional
+
+import torch
+
+from ._lib import check, lib, ptr
+
+
+class GraphedStep:
+    """``step_fn()`` (no ``zero_grad`` inside: gradients are written, not accumulated, by the captured backward)
+    captured after ``warmup`` eager calls on a side stream; ``__call__`` replays it and returns the static loss.
+
+    ``between`` / ``post``: an optional eager call (e.g. the RCCL gradient all-reduce of a multi-GPU step, kept out
+    of the graph) and a second captured segment after it (clipping + optimizer): ``__call__`` then replays
+    ``step_fn``'s graph, runs ``between()`` eagerly and replays ``post``'s graph."""
+
+    def __init__(self, model: torch.nn.Module, step_fn: Callable[[], torch.Tensor], optimizer=None, warmup: int = 3,
+                 between: Optional[Callable[[], None]] = None, post: Optional[Callable[[], None]] = None):
+        dev = next(model.parameters()).device
+        self.model, self.dev, self.between = model, dev, between
+        self.prev_validate = getattr(model, "validate_edges", None)
+        if self.prev_validate is not None:
+            model.validate_edges = False
+        self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        lib().tagan_set_seed_counter(ptr(self.counter))
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                if optimizer is not None:
+                    optimizer.zero_grad(set_to_none=True)
+                step_fn()
+                if between is not None:
+                    between()
+                if post is not None:
+                    post()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        if optimizer is not None:
+            optimizer.zero_grad(set_to_none=True)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            s = torch.cuda.current_stream(dev)
+            check(lib().tagan_seed_counter_step(ptr(self.counter), ctypes.c_void_p(s.cuda_stream)),
+                  "tagan_seed_counter_step")
+            self.loss = step_fn()
+        self.post_graph = None
+        if post is not None:
+            self.post_graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.post_graph, pool=self.graph.pool()):
+                post()
+
+    def __call__(self) -> torch.Tensor:
+        self.graph.replay()
+        if self.between is not None:
+            self.between()
+        if self.post_graph is not None:
+            self.post_graph.replay()
+        return self.loss
+
+    def close(self) -> None:
+        """Unregister the seed counter (eager launches use their seeds as passed again)."""
+        lib().tagan_set_seed_counter(None)
+        if self.prev_validate is not None:
+            self.model.validate_edges = self.prev_validate
+        self.graph = self.post_graph = None

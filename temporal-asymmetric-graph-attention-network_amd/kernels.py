@@ -12,6 +12,7 @@ kernels are launched on the current HIP stream.
 """
 import ctypes
 import os
+from collections import OrderedDict
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -124,6 +125,24 @@ def _finish(g: SnapshotGraph, nnz_cap: int, chunk: int = CHUNK) -> SnapshotGraph
     return g
 
 
+_PTR_TABLES = OrderedDict()
+
+
+def _ptr_table(dev, values):
+    """Device copy of the snapshot edge/node offset table, cached per (device, offsets): a repeated shape (every
+    training step of a sequence, a captured HIP graph) issues no host-to-device copy."""
+    key = (str(dev), tuple(values))
+    t = _PTR_TABLES.get(key)
+    if t is None:
+        t = torch.tensor(values, dtype=torch.int64).to(dev)
+        _PTR_TABLES[key] = t
+        if len(_PTR_TABLES) > 256:
+            _PTR_TABLES.popitem(last=False)
+    else:
+        _PTR_TABLES.move_to_end(key)
+    return t
+
+
 def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], validate=True,
                 chunk: int = CHUNK) -> SnapshotGraph:
     """CSR/CSC of the block-diagonal union of snapshot adjacencies (+ self-loops, de-duplicated).
@@ -158,7 +177,7 @@ def build_graph_cat(ei: torch.Tensor, e_ptr: Sequence[int], node_counts: Sequenc
     n_ptr = [0]
     for n in node_counts:
         n_ptr.append(n_ptr[-1] + int(n))
-    meta = torch.tensor(list(e_ptr) + n_ptr, dtype=torch.int64).to(dev)   # a few hundred bytes
+    meta = _ptr_table(dev, list(e_ptr) + n_ptr)
     edge_ptr, node_ptr = meta[:G + 1], meta[G + 1:]
     cap = E + N
     buf = torch.empty(2 * (N + 1) + 3 * cap, dtype=torch.int32, device=dev)

@@ -195,6 +195,92 @@ class TemporalClassificationHead(nn.Module):
         return self.loss_fn(logits, labels), logits
 
 
+class FusedHeadFn(torch.autograd.Function):
+    """graph_features (row 0 = x0 [T, H], rows 1..B-1 zero) -> logits, predictions, loss in ONE kernel each way
+    (csrc/head.hip, tagan_head_fwd/bwd): attention pooling, Linear -> LN -> ReLU -> Dropout -> Linear, sigmoid or
+    softmax, BCE-with-logits / cross-entropy mean (classification.py:856-966, model.py:430-459)."""
+
+    @staticmethod
+    def forward(ctx, x0, W1, b1, w2, Wc1, bc1, lnw, lnb, Wc2, bc2, B: int, eps: float, p_drop: float, seed: int,
+                labels, loss_kind: int):
+        from .._lib import check, lib, ptr, stream_of
+        T, H = x0.shape
+        C = Wc2.shape[0]
+        dev = x0.device
+        L = lib()
+        logits = torch.empty(B, C, device=dev)
+        preds = torch.empty(B, C, device=dev)
+        loss = torch.empty(1, device=dev) if loss_kind else None
+        saved = torch.empty(int(L.tagan_head_saved_floats(B, T, H)), device=dev)
+        ps = [t.detach().contiguous() for t in (x0, W1, b1, w2, Wc1, bc1, lnw, lnb, Wc2, bc2)]
+        check(L.tagan_head_fwd(B, T, H, C, *[ptr(t) for t in ps[:8]], float(eps), ptr(ps[8]), ptr(ps[9]),
+                               float(p_drop), seed, ptr(labels), int(loss_kind), ptr(logits), ptr(preds), ptr(loss),
+                               ptr(saved), stream_of(x0)), "tagan_head_fwd")
+        ctx.save_for_backward(*ps, logits, preds, saved, labels)
+        ctx.cfg = (B, p_drop, seed, loss_kind)
+        if loss is None:
+            return logits, preds
+        return logits, preds, loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, g_logits, g_preds, g_loss=None):
+        from .._lib import check, lib, ptr, stream_of
+        x0, W1, b1, w2, Wc1, bc1, lnw, lnb, Wc2, bc2, logits, preds, saved, labels = ctx.saved_tensors
+        B, p_drop, seed, loss_kind = ctx.cfg
+        T, H = x0.shape
+        C = Wc2.shape[0]
+        grads = [torch.empty_like(t) for t in (x0, W1, b1, w2, Wc1, bc1, lnw, lnb, Wc2, bc2)]
+        c = lambda g: None if g is None else g.contiguous()  # noqa: E731
+        gl = c(g_loss.reshape(1)) if g_loss is not None else None
+        check(lib().tagan_head_bwd(B, T, H, C, ptr(x0), ptr(W1), ptr(w2), ptr(Wc1), ptr(lnw), ptr(lnb), ptr(Wc2),
+                                   float(p_drop), seed, ptr(labels), int(loss_kind), ptr(logits), ptr(preds),
+                                   ptr(saved), ptr(gl), ptr(c(g_logits)), ptr(c(g_preds)),
+                                   *[ptr(g) for g in grads], stream_of(x0)), "tagan_head_bwd")
+        return (*grads, None, None, None, None, None, None)
+
+
+def fused_head(module: "ClassificationModule", pooled: torch.Tensor, batch_size: int,
+               labels: Optional[torch.Tensor], output_dim: int, seed: Optional[int] = None):
+    """(logits, predictions, loss) of TAGAN.head through FusedHeadFn, or None when this head / loss form is not
+    the one the kernel implements (attention pooling, 2 layers with LayerNorm + ReLU, BCE or CE) — the caller
+    then runs the module path, which also reproduces the reference's errors for unsupported label shapes."""
+    from .._lib import lib
+    from ..kernels import new_seed
+    head = getattr(module, "classification_head", None)
+    if not (pooled.is_cuda and pooled.dtype == torch.float32 and isinstance(head, TemporalClassificationHead)
+            and head.pooling_type == "attention" and head.num_layers == 2 and head.use_layer_norm
+            and head.activation == "relu" and not head.multi_label):
+        return None
+    T, H = pooled.shape
+    C = head.num_classes
+    if not lib().tagan_head_supported(T, H, C):
+        return None
+    lin1, ln, _relu, drop, lin2 = head.classifier
+    att1, _tanh, att2 = head.attention
+    loss_kind, lab = 0, None
+    if labels is not None:
+        if labels.dtype == torch.bool:
+            labels = labels.long()
+        if output_dim > 1 and labels.dim() == 1:                     # model.py:439-441
+            if labels.shape[0] != batch_size or labels.is_floating_point():
+                return None
+            loss_kind, lab = 2, labels.to(torch.float32).contiguous()
+        else:                                                        # TemporalLossModule default: BCE mean
+            ok = labels.is_floating_point() and (
+                (C == 1 and labels.dim() == 1 and labels.shape[0] == batch_size) or
+                (labels.dim() == 2 and tuple(labels.shape) == (batch_size, C)))
+            if not ok:
+                return None
+            loss_kind, lab = 1, labels.to(torch.float32).contiguous()
+    p = drop.p if head.training else 0.0
+    s = (seed if seed is not None else new_seed()) if p > 0 else 0
+    out = FusedHeadFn.apply(pooled, att1.weight, att1.bias, att2.weight.reshape(-1), lin1.weight, lin1.bias,
+                            ln.weight, ln.bias, lin2.weight, lin2.bias, batch_size, ln.eps, p, s, lab, loss_kind)
+    if loss_kind:
+        return out
+    return out[0], out[1], None
+
+
 class ClassificationModule(nn.Module):
     """Single-task form used by TAGAN (classification.py:1069-1231; multi-task head not restated)."""
 

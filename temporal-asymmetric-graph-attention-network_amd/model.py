@@ -18,6 +18,7 @@ MI355X-first:
 
 Parity against the reference (fp32, dropout=0): tests/test_gpu_parity.py.
 """
+import os
 from typing import Any, Dict, List, Optional, Tuple, Union
 
 import torch
@@ -27,12 +28,15 @@ import torch.nn.functional as F
 from .fused import precision as precision_ctx
 from .ingest import SnapshotBatch, unpack as _unpack
 from .kernels import build_graph, build_graph_cat, layer_norm, linear, pool_time_major
-from .layers.classification import ClassificationModule, TemporalLossModule
+from .layers.classification import ClassificationModule, TemporalLossModule, fused_head
 from .layers.graph_attention import TAGANGraphAttention
 from .layers.temporal_attention import AsymmetricTemporalAttention, MaskBroadcastError
 from .layers.temporal_propagation import TemporalPropagation
 from .utils.config import TAGANConfig
 from .utils.memory_bank import NodeMemoryBank
+
+# TAGAN_FUSED_HEAD=0: the classification head + loss as torch modules instead of csrc/head.hip (A/B)
+FUSED_HEAD = os.environ.get("TAGAN_FUSED_HEAD", "1") != "0"
 
 Snapshot = Union[Dict[str, Any], Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor], List[int]]]
 
@@ -184,10 +188,22 @@ class TAGAN(nn.Module):
             outputs["temporal_attention_weights"] = temp_w
         return outputs
 
-    def head(self, pooled: torch.Tensor, labels: Optional[torch.Tensor] = None) -> Dict[str, Any]:
-        """graph_features -> classification head -> loss / predictions (model.py:377-459); pooled [T, H]."""
+    def head(self, pooled: torch.Tensor, labels: Optional[torch.Tensor] = None,
+             dropout_seed: Optional[int] = None) -> Dict[str, Any]:
+        """graph_features -> classification head -> loss / predictions (model.py:377-459); pooled [T, H].
+        On the device the whole head + loss is one kernel each way (csrc/head.hip) when its shape and loss form
+        are the fused ones; ``dropout_seed`` fixes that kernel's dropout mask (replicated heads)."""
         T = pooled.shape[0]
         batch_size = labels.shape[0] if (labels is not None and labels.dim() > 0) else 1
+        if FUSED_HEAD:
+            fused = fused_head(self.classification_head, pooled, batch_size, labels, self.config.output_dim,
+                               dropout_seed)
+            if fused is not None:
+                logits, predictions, loss = fused
+                self.last_predictions = predictions
+                if self.config.output_dim == 1:
+                    self.last_binary_predictions = (predictions > 0.65).float()
+                return {"logits": logits, "predictions": predictions, "loss": loss}
         if batch_size > 1:
             graph_features = torch.cat([pooled.unsqueeze(0), pooled.new_zeros(batch_size - 1, T, pooled.shape[1])])
         else:

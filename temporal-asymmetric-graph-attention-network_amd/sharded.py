@@ -152,7 +152,12 @@ class SnapshotShardedTAGAN:
                 xt = model.temporal_propagation.forward_intended(xt)
             return model._temporal(xt, False)[0]
 
-        return cls(encode, temporal, model.head, group)
+        def head(pooled, labels, step_seed):   # the fused head kernel's dropout mask: same on every rank
+            return model.head(pooled, labels, dropout_seed=step_seed)
+
+        obj = cls(encode, temporal, head, group)
+        obj.head_takes_seed = True
+        return obj
 
     def forward(self, local_snapshots: Sequence, counts_all: Sequence[int], labels: Optional[torch.Tensor] = None):
         P, r = _world(self.group)
@@ -182,6 +187,8 @@ class SnapshotShardedTAGAN:
                 torch.cuda.manual_seed(self.head_seed + self.step)
             else:
                 torch.manual_seed(self.head_seed + self.step)
+            if getattr(self, "head_takes_seed", False):
+                return self.head(pooled, labels, (self.head_seed * 0x9E3779B1 + self.step) & 0x3FFFFFFFFFFFFFFF)
             return self.head(pooled, labels)
 
     __call__ = forward
