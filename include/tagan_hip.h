@@ -340,6 +340,32 @@ int tagan_head_bwd(int32_t B, int32_t T, int32_t H, int32_t C, const float* x0, 
                    float* dln_b, float* dWc2, float* dbc2, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * GRU recurrence of TemporalEvolutionLayer over T (csrc/gru.hip; TemporalPropagation's intended compute,
+ * temporal_propagation.py:402-558 inside :648-755), one launch per direction over all T steps.
+ * gx [T, N, 3hc] = the x-side of the reset | update | candidate gates (LN_x(x)·W_xᵀ + b, one GEMM by the
+ * caller); Wrz [2hc, hc] = the h-side columns of W_reset | W_update; Wc [hc, hc] = the h-side columns of
+ * W_candidate (nn.Linear layout).  Per step: hn = LN_h(h_{t-1})·tscale[t] (h_{-1} = 0, no LayerNorm),
+ * r, z = σ(gx + W·hn), h~ = tanh(gx_c + Wc·(r⊙hn)), u = dropout((1-z)⊙hn + z⊙h~) (stream row·T + t,
+ * counter unit), states[t] = LN_out(u).  LayerNorm pointers NULL = use_layer_norm False; tscale [T, N]
+ * (row t = exp(-clamp(Δt, 0, 10)) of step t) or NULL.  saved: tagan_gru_saved_floats(N, T, hc) floats.
+ * Backward: dstates [T, N, hc] -> dgx [T, N, 3hc] (gate pre-activation gradients; the W_h gradients are
+ * dgxᵀ·hn and dgx_cᵀ·(r⊙hn), hn and r⊙hn being the first two [T, N, hc] blocks of saved) and the four
+ * LayerNorm parameter gradients.  hc in {16, 32, 64, 128, 256} (tagan_gru_supported).
+ * ------------------------------------------------------------------------- */
+int tagan_gru_supported(int32_t hc);
+size_t tagan_gru_saved_floats(int64_t N, int32_t T, int32_t hc);
+int tagan_gru_fwd(int64_t N, int32_t T, int32_t hc, const float* gx, const float* Wrz, const float* Wc,
+                  const float* ln_h_w, const float* ln_h_b, float eps_h, const float* ln_o_w, const float* ln_o_b,
+                  float eps_o, const float* tscale, float p_drop, uint64_t seed, float* states, float* saved,
+                  void* stream);
+size_t tagan_gru_bwd_workspace(int64_t N, int32_t hc);
+int tagan_gru_bwd(int64_t N, int32_t T, int32_t hc, const float* Wrz, const float* Wc, const float* ln_h_w,
+                  const float* ln_h_b, const float* ln_o_w, const float* ln_o_b, const float* tscale, float p_drop,
+                  uint64_t seed, const float* states, const float* saved, const float* dstates, float* dgx,
+                  float* dln_h_w, float* dln_h_b, float* dln_o_w, float* dln_o_b, void* workspace,
+                  size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
  * NodeMemoryBank on the device.  Replaces src/tagan/utils/memory_bank.py:14-360
  * (a dict of per-node CPU tensors):  update (:65-173), get_state(s) (:175-211),
  * update_state (:235-244), decay_all (:222-225).  All arrays are caller-owned

@@ -85,6 +85,12 @@ _SIGNATURES = {
     "tagan_head_fwd": (_c.c_int, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _f32, _p, _p, _f32, _u64,
                                   _p, _c.c_int, _p, _p, _p, _p, _p]),
     "tagan_head_bwd": (_c.c_int, [_i32] * 4 + [_p] * 7 + [_f32, _u64, _p, _c.c_int] + [_p] * 6 + [_p] * 10 + [_p]),
+    "tagan_gru_supported": (_c.c_int, [_i32]),
+    "tagan_gru_saved_floats": (_sz, [_i64, _i32, _i32]),
+    "tagan_gru_fwd": (_c.c_int, [_i64, _i32, _i32, _p, _p, _p, _p, _p, _f32, _p, _p, _f32, _p, _f32, _u64, _p, _p, _p]),
+    "tagan_gru_bwd_workspace": (_sz, [_i64, _i32]),
+    "tagan_gru_bwd": (_c.c_int, [_i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _f32, _u64, _p, _p, _p, _p, _p, _p, _p,
+                                 _p, _p, _sz, _p]),
     "tagan_membank_init": (_c.c_int, [_p, _p]),
     "tagan_membank_lookup": (_c.c_int, [_p, _p, _i64, _c.c_int, _i32, _p, _p, _p]),
     "tagan_membank_update": (_c.c_int, [_p, _p, _i64, _p, _i64, _i64, _c.c_double, _i32, _i32, _u64, _p, _p, _p]),

@@ -15,25 +15,94 @@ raises the same exception types without spending the dead compute.
 masks (pinned by the tprop_* fixtures, G6): GRU evolution
 over T -> windowed skip connection -> output_proj -> dropout -> LayerNorm.  It runs
 time-major ([T, N, H], node rows independent) on the device: the x-side of all three
-GRU gates for all T steps is ONE GEMM, each recurrent step is two GEMMs on the hidden
-state plus gate elementwise work, LayerNorms and the residual tails run on the HIP
-LayerNorm kernels, the window aggregation is one pooling pass over T.  TAGAN uses it
+GRU gates for all T steps is ONE GEMM, the whole recurrence over T (recurrent products,
+gates, both LayerNorms, dropout) is ONE kernel each way (csrc/gru.hip, GRUSeqFn), the
+residual tails run on the HIP LayerNorm kernels, the window aggregation is one pooling
+pass over T.  TAGAN uses it
 when constructed with ``temporal_propagation="intended"`` (default "shipped").
 The submodules keep their reference list-in/list-out forwards (on the same device
 code) for standalone use.
 """
+import os
 from typing import Any, List, Optional
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .._lib import require_hip
-from ..kernels import dropout_add_layer_norm, layer_norm, linear
+from .._lib import check, lib, ptr, require_hip, stream_of
+from ..kernels import dropout_add_layer_norm, layer_norm, linear, new_seed, weight_grad
+
+
+# TAGAN_GRU_KERNEL=0: step the recurrence from Python (two GEMMs + gate ops per step) instead of csrc/gru.hip
+USE_GRU_KERNEL = os.environ.get("TAGAN_GRU_KERNEL", "1") != "0"
 
 
 def _ln(x, mod):
     return layer_norm(x, mod) if mod is not None else x
+
+
+class GRUSeqFn(torch.autograd.Function):
+    """The whole recurrence over T in one kernel each way (csrc/gru.hip): gx [T, N, 3hc] (x-side gates) ->
+    states [T, N, hc]; backward gives d gx, the h-side weight gradients (two split-K GEMMs against the saved
+    hn and r⊙hn) and the two LayerNorms' parameter gradients."""
+
+    @staticmethod
+    def forward(ctx, gx, w_rz, w_c, lnh_w, lnh_b, lno_w, lno_b, tscale, eps_h: float, eps_o: float, p: float,
+                seed: int):
+        T, N, H3 = gx.shape
+        hc = H3 // 3
+        dev = gx.device
+        L = lib()
+        gx = gx.contiguous()
+        states = torch.empty(T, N, hc, device=dev)
+        saved = torch.empty(int(L.tagan_gru_saved_floats(N, T, hc)), device=dev)
+        prm = [None if t is None else t.detach().contiguous() for t in (w_rz, w_c, lnh_w, lnh_b, lno_w, lno_b)]
+        check(L.tagan_gru_fwd(N, T, hc, ptr(gx), ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(prm[3]), float(eps_h),
+                              ptr(prm[4]), ptr(prm[5]), float(eps_o), ptr(tscale), float(p), seed, ptr(states),
+                              ptr(saved), stream_of(gx)), "tagan_gru_fwd")
+        ctx.save_for_backward(states, saved, tscale, *prm)
+        ctx.cfg = (T, N, hc, p, seed)
+        return states
+
+    @staticmethod
+    def backward(ctx, dstates):
+        states, saved, tscale, w_rz, w_c, lnh_w, lnh_b, lno_w, lno_b = ctx.saved_tensors
+        T, N, hc, p, seed = ctx.cfg
+        dev = states.device
+        L = lib()
+        dgx = torch.empty(T, N, 3 * hc, device=dev)
+        d = [torch.empty(hc, device=dev) if t is not None else None for t in (lnh_w, lnh_b, lno_w, lno_b)]
+        wsb = L.tagan_gru_bwd_workspace(N, hc)
+        ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
+        check(L.tagan_gru_bwd(N, T, hc, ptr(w_rz), ptr(w_c), ptr(lnh_w), ptr(lnh_b), ptr(lno_w), ptr(lno_b),
+                              ptr(tscale), float(p), seed, ptr(states), ptr(saved), ptr(dstates.contiguous()),
+                              ptr(dgx), *[ptr(t) for t in d], ptr(ws), wsb, stream_of(states)), "tagan_gru_bwd")
+        S = T * N * hc
+        hn = saved[:S].view(T * N, hc)
+        rh = saved[S:2 * S].view(T * N, hc)
+        g2 = dgx.view(T * N, 3 * hc)
+        dw_rz = weight_grad(g2[:, :2 * hc], hn) if ctx.needs_input_grad[1] else None
+        dw_c = weight_grad(g2[:, 2 * hc:], rh) if ctx.needs_input_grad[2] else None
+        return (dgx, dw_rz, dw_c, *d, None, None, None, None, None)
+
+
+def gru_sequence(cell: "TemporalGRUCell", gx: torch.Tensor, tscale: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """All T recurrent steps of ``cell`` on the device kernel (gx [T, N, 3hc] from ``cell.x_gates``), or None when
+    the cell's width is not one the kernel takes (the caller then steps in Python)."""
+    hc = cell.hidden_dim
+    if not (gx.is_cuda and gx.dtype == torch.float32 and lib().tagan_gru_supported(hc)):
+        return None
+    D = cell.input_dim
+    w_rz = torch.cat([cell.reset_gate.weight[:, D:], cell.update_gate.weight[:, D:]], 0)
+    w_c = cell.candidate.weight[:, D:]
+    ln = cell.use_layer_norm
+    p = cell.dropout_layer.p if cell.training else 0.0
+    seed = new_seed() if p > 0 else 0
+    return GRUSeqFn.apply(gx, w_rz, w_c, cell.layer_norm_h.weight if ln else None,
+                          cell.layer_norm_h.bias if ln else None, cell.layer_norm_out.weight if ln else None,
+                          cell.layer_norm_out.bias if ln else None, tscale,
+                          cell.layer_norm_h.eps if ln else 1e-5, cell.layer_norm_out.eps if ln else 1e-5, p, seed)
 
 
 class TemporalGRUCell(nn.Module):
@@ -127,20 +196,35 @@ class TemporalEvolutionLayer(nn.Module):
         T = xt.shape[0]
         has_time = time_stamps is not None and self.time_aware
         gx = self.forward_cell.x_gates(xt)
-        fwd, h = [], None
-        for t in range(T):
-            td = time_stamps[:, t] - time_stamps[:, t - 1] if (has_time and t > 0) else None
-            h = self.forward_cell.step(gx[t], h, td)
-            fwd.append(h)
-        states = torch.stack(fwd, 0)
+        # time factors exp(-clamp(Δt, 0, 10)) per step (step 0 has no previous state: unused)
+        tsf = tsb = None
+        if has_time:
+            dt = torch.diff(time_stamps.to(torch.float32), dim=1).t()                    # [T-1, N]: t - (t-1)
+            fac = torch.exp(-torch.clamp(dt, min=0.0, max=10.0))
+            one = torch.ones_like(fac[:1])
+            tsf = torch.cat([one, fac], 0).contiguous()
+            tsb = torch.cat([one, fac.flip(0)], 0).contiguous()   # reversed step t' = T-1-t: (t+1) - t
+        states = gru_sequence(self.forward_cell, gx, tsf) if USE_GRU_KERNEL else None
+        if states is None:
+            fwd, h = [], None
+            for t in range(T):
+                td = time_stamps[:, t] - time_stamps[:, t - 1] if (has_time and t > 0) else None
+                h = self.forward_cell.step(gx[t], h, td)
+                fwd.append(h)
+            states = torch.stack(fwd, 0)
         if self.bidirectional:
             gb = self.backward_cell.x_gates(xt)
-            bwd, hb = [None] * T, None
-            for t in range(T - 1, -1, -1):
-                td = time_stamps[:, t + 1] - time_stamps[:, t] if (has_time and t < T - 1) else None
-                hb = self.backward_cell.step(gb[t], hb, td)
-                bwd[t] = hb
-            states = torch.cat([states, torch.stack(bwd, 0)], -1)
+            sb = gru_sequence(self.backward_cell, gb.flip(0), tsb) if USE_GRU_KERNEL else None
+            if sb is not None:
+                sb = sb.flip(0)
+            else:
+                bwd, hb = [None] * T, None
+                for t in range(T - 1, -1, -1):
+                    td = time_stamps[:, t + 1] - time_stamps[:, t] if (has_time and t < T - 1) else None
+                    hb = self.backward_cell.step(gb[t], hb, td)
+                    bwd[t] = hb
+                sb = torch.stack(bwd, 0)
+            states = torch.cat([states, sb], -1)
         y = linear(states, self.output_projection.weight, self.output_projection.bias)
         res = xt if (self.residual and self.input_dim == self.hidden_dim) else None
         if self.use_layer_norm and res is not None:
