@@ -1402,6 +1402,388 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// v5 (T in (16, 128], d in {16, 32}: C3's T = 64, C5's T = 128): one WORKGROUP of TT waves per (node row, head)
+// unit, TP = 16·TT >= T steps (TT in {2, 4, 8}).  Wave w owns query tile w (steps 16w .. 16w+15) in the score,
+// softmax and dQ products and key tile w in the dK / dV products, so no wave holds more than one 16-step
+// column of the T x T score matrix (v4 keeps all of it in one wave: > 256 VGPRs at T = 64).  Per unit the
+// waves stage their K | V rows (row-major, the A operand of Sᵀ = K·Qᵀ and dPᵀ = V·dOᵀ) and Kᵀ, Qᵀ, dOᵀ (the A
+// operands of dQᵀ, dKᵀ, dVᵀ) once into the workgroup's LDS; dSᵀ and then P'ᵀ pass between the query-tile and
+// key-tile phases through one shared [TP][LD] tile.  Five T x T x d products per unit (none recomputed), all on
+// v_mfma_f32_16x16x4_f32; no atomics (every sum has a fixed order), so results are bitwise reproducible.
+// ---------------------------------------------------------------------------------------------------------
+// Row stride of the row-major K | V tiles: lane (c, g) reads 16 B at row c, column 4g, and with stride 4m
+// dwords (m = DP/4 + 2 = 6 or 10, i.e. m = 2 mod 4) the 16-lane groups of ds_read_b128 hit distinct bank slots
+// (the same argument as v4_ld).
+constexpr int v5_lk(int DP) { return DP + 8; }
+size_t v5_fwd_lds(int TT, int DT) { return (size_t)(16 * TT * v5_lk(16 * DT) + 16 * DT * v4_ld(16 * TT) + 32 * TT) * 4; }
+size_t v5_bwd_lds(int TT, int DT) {
+    const int TP = 16 * TT, DP = 16 * DT;
+    return (size_t)(TP * v4_ld(TP) + 3 * DP * v4_ld(TP) + 2 * TP * v5_lk(DP) + 2 * TP) * 4;
+}
+
+// static score part of the lane's elements of query tile it (i = 16·it + c, j = 16·jt + 4g + e): see v4_static_bias
+template <int TT>
+__device__ __forceinline__ void v5_static_bias(const TArgs& A, int h, int it, int c, int g, float (&bst)[TT][4]) {
+    const int T = A.T, NB = 2 * T - 1;
+    const int i = it * 16 + c;
+#pragma unroll
+    for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int j = jt * 16 + 4 * g + e;
+            const bool ok = i < T && j < T && !(A.causal && j > i);
+            bst[jt][e] = ok ? (A.bias_table ? A.bias_table[h * NB + i - j + T - 1] : 0.f) : -INFINITY;
+        }
+}
+
+template <int TT, int DT, typename S>
+__global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float* __restrict__ q,
+                                                            const float* __restrict__ k,
+                                                            const float* __restrict__ v) {
+    TAGAN_LIVE_SEED(A);
+    constexpr int TP = 16 * TT, LT = v4_ld(TP), DP = 16 * DT, LK = v5_lk(DP);
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* Kr = sm;              // [TP][LK] K row-major
+    float* Vt = Kr + TP * LK;    // [DP][LT] V transposed
+    float* Bt = Vt + DP * LT;    // [2TP] the head's bias-table row (BREG false)
+    const int T = A.T, d = A.d;
+    const int w = threadIdx.x / WAVE, lane = threadIdx.x % WAVE, c0 = lane & 15, g0 = lane >> 4;
+    int h;
+    int64_t rg;
+    v4_wave_map(A.heads, h, rg);
+    const int64_t G = gridDim.x / A.heads;
+    constexpr bool BREG = TT <= 4;   // as in k_tattn_bwd_v5: at TT = 8 the table row is read from LDS
+    float bst[BREG ? TT : 1][4];
+    if constexpr (BREG) {
+        v5_static_bias<TT>(A, h, w, c0, g0, bst);
+    } else {
+        for (int t = threadIdx.x; t < 2 * T - 1; t += WAVE * TT) Bt[t] = A.bias_table ? A.bias_table[h * (2 * T - 1) + t] : 0.f;
+    }
+    f4v qv[DT], kv[DT], vv[DT];
+    auto load = [&](int64_t rr) {
+        const int i = w * 16 + c0;
+        const int64_t off = rr * A.s_row + (int64_t)h * d + (int64_t)i * A.s_t + 4 * g0;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+            qv[dt] = ld4v<S>(q, off + dt * 16, i < T);
+            kv[dt] = ld4v<S>(k, off + dt * 16, i < T);
+            vv[dt] = ld4v<S>(v, off + dt * 16, i < T);
+        }
+    };
+    if (rg < A.rows) load(rg);
+    for (int64_t r = rg; r < A.rows; r += G) {
+        int c = c0, g = g0;
+        asm volatile("" : "+v"(c), "+v"(g));   // see k_tattn_fwd_v4
+        const int i = w * 16 + c;
+        __syncthreads();   // the previous unit's reads of Kr / Vt are done
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+            *(f4v*)(Kr + i * LK + dt * 16 + 4 * g) = kv[dt];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Vt[(dt * 16 + 4 * g + e) * LT + i] = vv[dt][e];
+        }
+        f4v qc[DT];
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) qc[dt] = qv[dt];
+        __syncthreads();
+        if (r + G < A.rows) load(r + G);   // the next unit's rows in flight during this one
+        f4v s[TT];   // Sᵀ tiles [jt] of query tile w
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt) {
+            s[jt] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                const f4v ka = lds4(Kr + (jt * 16 + c) * LK + dt * 16 + 4 * g);   // K[16jt + c][16dt + 4g + e]
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s[jt] = mfma4(ka[e], qc[dt][e], s[jt]);
+            }
+        }
+        const uint32_t drk = tkey(A, r, h);
+        float mx = -INFINITY;
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int j = jt * 16 + 4 * g + e;
+                float b0;
+                if constexpr (BREG) {
+                    b0 = bst[jt][e];
+                } else {
+                    b0 = (i < T && j < T && !(A.causal && j > i)) ? Bt[i - j + T - 1] : -INFINITY;
+                }
+                const float sc = v4_score(A, b0, r, h, i, j, s[jt][e]);
+                s[jt][e] = sc;
+                mx = fmaxf(mx, sc);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, WAVE));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, WAVE));
+        float l = 0.f;
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float sc = s[jt][e];
+                const float p = (sc == -INFINITY) ? 0.f : __expf(sc - mx);
+                l += p;
+                s[jt][e] = p * drop_scale(A, drk, i, jt * 16 + 4 * g + e);
+            }
+        l += __shfl_xor(l, 16, WAVE);
+        l += __shfl_xor(l, 32, WAVE);
+        const float inv_l = (l > 0.f) ? 1.f / l : NAN;
+        if (g == 0 && i < T) A.lse[(r * A.heads + h) * T + i] = mx + __logf(l);
+        // Oᵀ = Vᵀ·P'ᵀ, two accumulator chains per feature tile
+        f4v o[DT][2];
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt][0] = o[dt][1] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                const f4v va = lds4(Vt + (dt * 16 + c) * LT + jt * 16 + 4 * g);   // V[16jt + 4g + e][16dt + c]
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[dt][jt & 1] = mfma4(va[e], s[jt][e], o[dt][jt & 1]);
+            }
+        if (i < T) {
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+                st4v<S>(A.out, r * A.o_row + (int64_t)i * A.o_t + h * d + dt * 16 + 4 * g, o[dt][0] + o[dt][1], inv_l);
+        }
+    }
+}
+
+template <int TT, int DT, typename S>
+__global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float* __restrict__ q,
+                                                            const float* __restrict__ k,
+                                                            const float* __restrict__ v,
+                                                            const float* __restrict__ dout,
+                                                            const float* __restrict__ lse) {
+    TAGAN_LIVE_SEED(A);
+    constexpr int TP = 16 * TT, LD = v4_ld(TP), DP = 16 * DT, LK = v5_lk(DP);
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* X = sm;               // [TP][LD]: dSᵀ[j][i], then P'ᵀ[j][i]
+    float* Kt = X + TP * LD;     // [DP][LD] Kᵀ
+    float* Qt = Kt + DP * LD;    // [DP][LD] Qᵀ
+    float* Ot = Qt + DP * LD;    // [DP][LD] dOᵀ
+    float* Kr = Ot + DP * LD;    // [TP][LK] K row-major
+    float* Vr = Kr + TP * LK;    // [TP][LK] V row-major
+    float* Bt = Vr + TP * LK;    // [2TP] the head's bias-table row (BREG false)
+    const int T = A.T, NB = 2 * T - 1, d = A.d;
+    const int w = threadIdx.x / WAVE, lane = threadIdx.x % WAVE, c0 = lane & 15, g0 = lane >> 4;
+    int h;
+    int64_t rg;
+    v4_wave_map(A.heads, h, rg);
+    const int64_t G = gridDim.x / A.heads;
+    // static score part in registers up to TT = 4; at TT = 8 those 32 VGPRs would spill, so the head's
+    // bias-table row is read from LDS per element instead
+    constexpr bool BREG = TT <= 4;
+    float bst[BREG ? TT : 1][4];
+    if constexpr (BREG) {
+        v5_static_bias<TT>(A, h, w, c0, g0, bst);
+    } else {
+        for (int t = threadIdx.x; t < NB; t += WAVE * TT) Bt[t] = A.bias_table ? A.bias_table[h * NB + t] : 0.f;
+        // (visible to all waves after the first unit's staging barrier)
+    }
+    const float msc = A.p_drop > 0.f ? A.inv_keep : 1.f;
+    f4v gsum[TT];   // Σ over units of dSᵀ[jt tiles][query tile w]: the bias-table gradient before its diagonal sums
+#pragma unroll
+    for (int jt = 0; jt < TT; ++jt) gsum[jt] = f4v{0.f, 0.f, 0.f, 0.f};
+    f4v bsum[3][DT];   // Σ of the stored dq (query tile w) | dk | dv (key tile w): the QKV bias gradient
+#pragma unroll
+    for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) bsum[t3][dt] = f4v{0.f, 0.f, 0.f, 0.f};
+    f4v qv[DT], kv[DT], vv[DT], dov[DT];
+    float lsev;
+    auto load = [&](int64_t rr) {
+        const int i = w * 16 + c0;
+        const int64_t off = rr * A.s_row + (int64_t)h * d + (int64_t)i * A.s_t + 4 * g0;
+        const int64_t offd = rr * A.do_row + (int64_t)h * d + (int64_t)i * A.do_t + 4 * g0;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+            qv[dt] = ld4v<S>(q, off + dt * 16, i < T);
+            kv[dt] = ld4v<S>(k, off + dt * 16, i < T);
+            vv[dt] = ld4v<S>(v, off + dt * 16, i < T);
+            dov[dt] = ld4v<S>(dout, offd + dt * 16, i < T);
+        }
+        lsev = (i < T) ? lse[(rr * A.heads + h) * T + i] : 0.f;
+    };
+    if (rg < A.rows) load(rg);
+    for (int64_t r = rg; r < A.rows; r += G) {
+        int c = c0, g = g0;
+        asm volatile("" : "+v"(c), "+v"(g));   // see k_tattn_fwd_v4
+        const int i = w * 16 + c;   // this lane's query step (phase 1) and key step (phase 2)
+        __syncthreads();   // the previous unit's reads of every LDS tile are done
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+            *(f4v*)(Kr + i * LK + dt * 16 + 4 * g) = kv[dt];
+            *(f4v*)(Vr + i * LK + dt * 16 + 4 * g) = vv[dt];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                Kt[(dt * 16 + 4 * g + e) * LD + i] = kv[dt][e];
+                Qt[(dt * 16 + 4 * g + e) * LD + i] = qv[dt][e];
+                Ot[(dt * 16 + 4 * g + e) * LD + i] = dov[dt][e];
+            }
+        }
+        const float lse_i = lsev;
+        __syncthreads();
+        // ---- phase 1, query tile w: Sᵀ, dPᵀ (all key tiles), P, δ, dS, P', dQ
+        f4v s[TT], dp[TT];
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt) {
+            s[jt] = f4v{0.f, 0.f, 0.f, 0.f};
+            dp[jt] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                const f4v ka = lds4(Kr + (jt * 16 + c) * LK + dt * 16 + 4 * g);
+                const f4v va = lds4(Vr + (jt * 16 + c) * LK + dt * 16 + 4 * g);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    s[jt] = mfma4(ka[e], qv[dt][e], s[jt]);
+                    dp[jt] = mfma4(va[e], dov[dt][e], dp[jt]);
+                }
+            }
+        }
+        if (r + G < A.rows) load(r + G);   // the next unit's rows in flight during the rest of this one
+        const uint32_t drk = tkey(A, r, h);
+        uint32_t keep = 0;   // bit jt*4 + e: element kept by the dropout
+        float dl = 0.f;
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int j = jt * 16 + 4 * g + e;
+                float b0;
+                if constexpr (BREG) {
+                    b0 = bst[jt][e];
+                } else {
+                    b0 = (i < T && j < T && !(A.causal && j > i)) ? Bt[i - j + T - 1] : -INFINITY;
+                }
+                const float sc = v4_score(A, b0, r, h, i, j, s[jt][e]);
+                const float p = (sc == -INFINITY) ? 0.f : __expf(sc - lse_i);
+                const float m = drop_scale(A, drk, i, j);
+                keep |= (m != 0.f ? 1u : 0u) << (jt * 4 + e);
+                s[jt][e] = p;
+                dp[jt][e] *= m;
+                dl = fmaf(p, dp[jt][e], dl);
+            }
+        dl += __shfl_xor(dl, 16, WAVE);
+        dl += __shfl_xor(dl, 32, WAVE);
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int j = jt * 16 + 4 * g + e;
+                const float p = s[jt][e];
+                const float dsv = p * (dp[jt][e] - dl);
+                dp[jt][e] = dsv;
+                s[jt][e] = ((keep >> (jt * 4 + e)) & 1u) ? p * msc : 0.f;
+                if (A.dbias_dense && i < T && j < T)
+                    A.dbias_dense[((r * A.heads + h) * T + i) * (int64_t)T + j] = dsv;
+                X[j * LD + i] = dsv;   // dSᵀ[j][i]
+            }
+        if (A.part) {
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt) gsum[jt] += dp[jt];
+        }
+        {   // dQᵀ = Kᵀ·dSᵀ: A = Kᵀ[16dt + c][16jt + 4g + e], B = the dSᵀ accumulators
+            f4v acc[DT][2];
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) acc[dt][0] = acc[dt][1] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int dt = 0; dt < DT; ++dt) {
+                    const f4v ka = lds4(Kt + (dt * 16 + c) * LD + jt * 16 + 4 * g);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[dt][jt & 1] = mfma4(ka[e], dp[jt][e], acc[dt][jt & 1]);
+                }
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                const f4v a = acc[dt][0] + acc[dt][1];
+                if (i < T) st4v<S>(A.dq, r * A.d_row + (int64_t)i * A.d_t + h * d + dt * 16 + 4 * g, a, A.inv_sqrt_d);
+                if (A.qkv_part) bsum[0][dt] += a * A.inv_sqrt_d;   // padded steps add exact zeros (dS = 0)
+            }
+        }
+        __syncthreads();   // dSᵀ complete in X
+        // ---- phase 2, key tile w: dKᵀ = Qᵀ·dS (B = X[16w + c][i]), then dVᵀ = dOᵀ·P' (B = X after P'ᵀ replaces dSᵀ)
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+            if (pass == 1) {
+                __syncthreads();   // dK's reads of X are done
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g + e) * LD + i] = s[jt][e];
+                __syncthreads();
+            }
+            const float* At = pass == 0 ? Qt : Ot;
+            f4v acc[DT][2];
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) acc[dt][0] = acc[dt][1] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int it = 0; it < TT; ++it) {
+                const f4v xb = lds4(X + i * LD + it * 16 + 4 * g);   // B[k = 16it + 4g + e][n = key 16w + c]
+#pragma unroll
+                for (int dt = 0; dt < DT; ++dt) {
+                    const f4v xa = lds4(At + (dt * 16 + c) * LD + it * 16 + 4 * g);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[dt][it & 1] = mfma4(xa[e], xb[e], acc[dt][it & 1]);
+                }
+            }
+            float* dst = pass == 0 ? A.dk : A.dv;
+            const float sc = pass == 0 ? A.inv_sqrt_d : 1.f;
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                const f4v a = acc[dt][0] + acc[dt][1];
+                if (i < T) st4v<S>(dst, r * A.d_row + (int64_t)i * A.d_t + h * d + dt * 16 + 4 * g, a, sc);
+                if (A.qkv_part) bsum[1 + pass][dt] += a * sc;
+            }
+        }
+    }
+    __syncthreads();   // the last unit's reads of X and the staged tiles are done
+    if (A.qkv_part) {
+        // over the 16 step lanes (fixed butterfly), then over the waves in wave order through Kr
+        float* red = Kr;   // [TT][3·DP]
+#pragma unroll
+        for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float x = bsum[t3][dt][e];
+                    x += __shfl_xor(x, 1, WAVE);
+                    x += __shfl_xor(x, 2, WAVE);
+                    x += __shfl_xor(x, 4, WAVE);
+                    x += __shfl_xor(x, 8, WAVE);
+                    if (c0 == 0) red[w * 3 * DP + t3 * DP + dt * 16 + 4 * g0 + e] = x;
+                }
+        __syncthreads();
+        float* prow = A.qkv_part + rg * 3 * (int64_t)A.H + (int64_t)h * d;
+        for (int t = threadIdx.x; t < 3 * DP; t += WAVE * TT) {
+            float x = 0.f;
+            for (int ww = 0; ww < TT; ++ww) x += red[ww * 3 * DP + t];
+            if (t % DP < d) prow[(t / DP) * (int64_t)A.H + t % DP] = x;
+        }
+    }
+    if (A.part) {
+        // diagonal sums (t = i - j + T - 1) of the summed dSᵀ tile in j order: part[rg][h][t]
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g0 + e) * LD + w * 16 + c0] = gsum[jt][e];
+        __syncthreads();
+        float* prow = A.part + rg * A.heads * NB + (int64_t)h * NB;
+        for (int t = threadIdx.x; t < NB; t += WAVE * TT) {
+            const int off = t - (T - 1);
+            const int j0 = off < 0 ? -off : 0, j1 = off < 0 ? T : T - off;
+            float a = 0.f;
+            for (int j = j0; j < j1; ++j) a += X[j * LD + j + off];
+            prow[t] = a;
+        }
+    }
+}
+
 // T <= 32 (TT <= 2); at TT = 4 the backward needs > 256 VGPRs (spills) and T in (32, 128] keeps v3
 int v4_tiles(int T) { return T <= 16 ? 1 : T <= 32 ? 2 : 0; }
 
@@ -1413,6 +1795,28 @@ bool v4_enabled() {   // TAGAN_TATTN_V4=0 selects the v3 kernels (A/B runs, v3-v
     return (e && e[0] == '0') ? false : TAGAN_TATTN_V4 != 0;
 }
 bool v4_ok(int T, int d) { return v4_enabled() && v4_tiles(T) != 0 && (d == 16 || d == 32); }
+
+// v5 (one workgroup of TT waves per unit) for T in (32, 128]; TAGAN_TATTN_V5=2 also takes T in (16, 32]
+// (TT = 2, the A/B against v4), 0 leaves T > 32 on v3
+int v5_tiles(int T) { return T <= 16 ? 0 : T <= 32 ? 2 : T <= 64 ? 4 : T <= 128 ? 8 : 0; }
+int v5_mode() {   // read per call, like TAGAN_TATTN_V4, so a test can switch kernels within one process
+    const char* e = getenv("TAGAN_TATTN_V5");
+    return e ? atoi(e) : 1;
+}
+bool v5_ok(int T, int d) {
+    const int m = v5_mode();
+    return m > 0 && v5_tiles(T) != 0 && (d == 16 || d == 32) && (T > 32 || (m == 2 && v4_enabled()));
+}
+
+// > 64 KB of dynamic LDS needs the per-kernel opt-in (once per instantiation)
+template <typename K>
+int lds_optin(K* kern, size_t bytes) {
+    if (bytes <= 64 * 1024) return TAGAN_OK;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)bytes);
+    TAGAN_REQUIRE(e == hipSuccess, TAGAN_ERR_LAUNCH, "temporal_attn: LDS opt-in %zu B: %s", bytes, hipGetErrorString(e));
+    return TAGAN_OK;
+}
 
 // waves: G partial rows x heads (G <= grid_rows(rows), the bias-gradient workspace rows)
 // (a multiple of 8 from 8 rows up, for the XCD-aware wave map)
@@ -1509,8 +1913,22 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     const float* vf = (const float*)v;
     const bool al4 = s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0;
     const bool bf = dtype == TAGAN_BF16;
-    TAGAN_REQUIRE(!bf || (al4 && !attn && (v3_ok(T, head_dim) || v4_ok(T, head_dim))), TAGAN_ERR_UNSUPPORTED,
+    TAGAN_REQUIRE(!bf || (al4 && !attn && (v3_ok(T, head_dim) || v4_ok(T, head_dim) || v5_ok(T, head_dim))),
+                  TAGAN_ERR_UNSUPPORTED,
                   "temporal_attn_fwd: bf16 storage needs the v3 kernels (T <= 128, head_dim 8..64, no attn output)");
+    if (al4 && !attn && v5_ok(T, head_dim)) {
+        const int TT = v5_tiles(T);
+        const dim3 g5((unsigned)(v4_groups(rows) * heads));
+        const size_t lds = v5_fwd_lds(TT, head_dim / 16);
+#define TAGAN_V5F(TTT, DDT) { auto kern = bf ? k_tattn_fwd_v5<TTT, DDT, bf16s> : k_tattn_fwd_v5<TTT, DDT, float>; \
+                              rc = lds_optin(kern, lds); if (rc) return rc; kern<<<g5, WAVE * TTT, lds, s>>>(A, qf, kf, vf); }
+#define TAGAN_V5F_D(TTT) if (head_dim == 16) TAGAN_V5F(TTT, 1) else TAGAN_V5F(TTT, 2)
+        if (TT == 2) TAGAN_V5F_D(2) else if (TT == 4) TAGAN_V5F_D(4) else TAGAN_V5F_D(8)
+#undef TAGAN_V5F_D
+#undef TAGAN_V5F
+        TAGAN_CHECK_LAUNCH("temporal_attn_fwd_v5");
+        return TAGAN_OK;
+    }
     if (al4 && !attn && v4_ok(T, head_dim)) {
         const int TT = v4_tiles(T);
         const dim3 g4((unsigned)(v4_groups(rows) * heads));
@@ -1602,8 +2020,8 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     {
         const bool al4_ = s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0 && do_t % 4 == 0 &&
                           do_row % 4 == 0 && d_t % 4 == 0 && d_row % 4 == 0;
-        TAGAN_REQUIRE(!dsum_qkv || (al4_ && v4_ok(T, head_dim)), TAGAN_ERR_UNSUPPORTED,
-                      "temporal_attn_bwd: dsum_qkv needs the matrix-core path (T <= 32, head_dim 16/32, aligned)");
+        TAGAN_REQUIRE(!dsum_qkv || (al4_ && (v4_ok(T, head_dim) || v5_ok(T, head_dim))), TAGAN_ERR_UNSUPPORTED,
+                      "temporal_attn_bwd: dsum_qkv needs the matrix-core path (T <= 128, head_dim 16/32, aligned)");
     }
     if (dbias_table || dsum_qkv) {
         const size_t need = tagan_temporal_attn_bwd_workspace(rows, T, heads, head_dim);
@@ -1623,8 +2041,34 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     const bool al4 = s_t % 4 == 0 && s_row % 4 == 0 && o_t % 4 == 0 && o_row % 4 == 0 && do_t % 4 == 0 &&
                      do_row % 4 == 0 && d_t % 4 == 0 && d_row % 4 == 0;
     const bool bf = dtype == TAGAN_BF16;
-    TAGAN_REQUIRE(!bf || (al4 && (v3_ok(T, head_dim) || v4_ok(T, head_dim))), TAGAN_ERR_UNSUPPORTED,
+    TAGAN_REQUIRE(!bf || (al4 && (v3_ok(T, head_dim) || v4_ok(T, head_dim) || v5_ok(T, head_dim))),
+                  TAGAN_ERR_UNSUPPORTED,
                   "temporal_attn_bwd: bf16 storage needs the v3 kernels (T <= 128, head_dim 8..64)");
+    if (al4 && v5_ok(T, head_dim)) {
+        // grid = G5 partial rows x heads; each workgroup keeps one head (v4_wave_map)
+        const int TT = v5_tiles(T);
+        const int64_t G5 = v4_groups(rows);   // <= nblk: the workspace rows
+        const dim3 g5((unsigned)(G5 * heads));
+        const size_t lds = v5_bwd_lds(TT, head_dim / 16);
+#define TAGAN_V5B(TTT, DDT) { auto kern = bf ? k_tattn_bwd_v5<TTT, DDT, bf16s> : k_tattn_bwd_v5<TTT, DDT, float>; \
+                              rc = lds_optin(kern, lds); if (rc) return rc; kern<<<g5, WAVE * TTT, lds, s>>>(A, qf, kf, vf, df, lse); }
+#define TAGAN_V5B_D(TTT) if (head_dim == 16) TAGAN_V5B(TTT, 1) else TAGAN_V5B(TTT, 2)
+        if (TT == 2) TAGAN_V5B_D(2) else if (TT == 4) TAGAN_V5B_D(4) else TAGAN_V5B_D(8)
+#undef TAGAN_V5B_D
+#undef TAGAN_V5B
+        TAGAN_CHECK_LAUNCH("temporal_attn_bwd_v5");
+        if (dbias_table) {
+            const int n = heads * (2 * T - 1);
+            launch_colsum(A.part, (int)G5, n, dbias_table, nullptr, n, s);
+            TAGAN_CHECK_LAUNCH("temporal_attn_bwd_sum");
+        }
+        if (dsum_qkv) {
+            const int n = 3 * heads * head_dim;
+            launch_colsum(A.qkv_part, (int)G5, n, dsum_qkv, nullptr, n, s);
+            TAGAN_CHECK_LAUNCH("temporal_attn_bwd_qkv_sum");
+        }
+        return TAGAN_OK;
+    }
     if (al4 && v4_ok(T, head_dim)) {
         // grid = G4 partial rows x heads; each block keeps one head (v4_wave_map)
         const int TT = v4_tiles(T);

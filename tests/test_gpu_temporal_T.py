@@ -1,5 +1,6 @@
-"""GPU parity of the temporal attention layer over the sequence-length range of the v3 kernels:
-one wave per head group (T <= 64) and two waves per head (64 < T <= 128, BASELINE C5's T = 128).
+"""GPU parity of the temporal attention layer over the whole sequence-length range: the one-wave matrix-core
+kernels (v4, T <= 32), the workgroup-per-unit matrix-core kernels (v5, 32 < T <= 128 with head_dim 16/32: C3's
+T = 64, C5's T = 128) and the VALU v3 kernels (other head widths).
 The layer (AsymmetricTemporalAttention, temporal_attention.py:624-1217) against the fp64 oracle
 (oracle/tagan_oracle.py temporal_attention), forward and every gradient; tolerance 1e-4 fp32."""
 import pytest
@@ -38,6 +39,7 @@ def _layer(H, heads, causal, dev, seed):
     (32, 128, 4, True),                                  # matrix-core (v4) range: T <= 32, d in {16, 32}
     (8, 64, 4, False), (33, 128, 8, False), (64, 128, 8, True), (65, 256, 16, False),
     (100, 128, 8, False), (128, 256, 16, False), (128, 128, 4, True),
+    (48, 256, 8, False), (64, 256, 8, True),            # d = 32 in the 4-wave v5 range (C3: T = 64)
 ])
 def test_temporal_layer_T_sweep(dev, T, H, heads, causal):
     mod = _layer(H, heads, causal, dev, seed=T)

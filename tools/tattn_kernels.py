@@ -5,7 +5,8 @@
 Layout as in the model: Q|K|V of the time-major [T, N, 3H] projection (row stride 3H,
 step stride N*3H), the folded [heads, 2T-1] bias table, bias-table gradient on.
 Algorithmic bytes: fwd reads Q,K,V and writes O (+ LSE); bwd reads Q,K,V,O,dO (+ LSE)
-and writes dQ,dK,dV (the matrix-core v4 path does not read O).  TAGAN_LIB=<path> selects an alternative build.
+and writes dQ,dK,dV (the matrix-core v4/v5 paths do not read O).  FLOPs: 2 (fwd) and 5 (bwd) T x T x d
+products per (row, head).  TAGAN_LIB=<path> selects an alternative build.
 """
 import argparse
 import ctypes
@@ -79,12 +80,15 @@ def main():
     unit = N * T * H * 4
     bf = 4 * unit + N * heads * T * 4
     v4 = os.environ.get("TAGAN_TATTN_V4", "1") != "0" and T <= 32 and d in (16, 32)
-    bb = (7 if v4 else 8) * unit + N * heads * T * 4   # v4 takes delta from P·dP and never reads O
+    v5 = os.environ.get("TAGAN_TATTN_V5", "1") != "0" and 16 < T <= 128 and d in (16, 32)
+    bb = (7 if (v4 or v5) else 8) * unit + N * heads * T * 4   # v4/v5 take delta from P·dP and never read O
+    mm = 2.0 * T * T * d * N * heads   # flops of one T x T x d product over all units
     chk = [float(out.double().abs().sum()), float(dqkv.double().abs().sum()), float(dtable.double().abs().sum())]
     print(json.dumps({"lib": os.environ.get("TAGAN_LIB", "default"), "config": a.config, "rows": N, "T": T,
                       "heads": heads, "d": d, "p": a.p, "ms_fwd": round(tf, 4), "ms_bwd": round(tb, 4),
                       "gbs_fwd": round(bf / tf / 1e6, 1), "gbs_bwd": round(bb / tb / 1e6, 1),
                       "frac_hbm": round((bf + bb) / (tf + tb) / 1e6 / bench.HBM_PEAK_GBS, 4),
+                      "tflops_fwd": round(2 * mm / tf / 1e9, 1), "tflops_bwd": round(5 * mm / tb / 1e9, 1),
                       "checksums": chk}), flush=True)
 
 
