@@ -366,6 +366,16 @@ int tagan_gru_bwd(int64_t N, int32_t T, int32_t hc, const float* Wrz, const floa
                   size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Window aggregation of TemporalSkipConnection over T (csrc/window.hip; temporal_propagation.py:846-946),
+ * time-major: out[t, n, :] = agg over t' in [t-w, t+w] ∩ [0, T) of x[t', n, :].  mode 0 = mean over the
+ * in-range steps (avg_pool1d, count_include_pad False), 1 = max (first maximum in window order, as
+ * max_pool1d), 2 = sum.  x/out/dy/dx [T, N, H] contiguous fp32, H % 4 == 0.  Backward needs x only for max.
+ * ------------------------------------------------------------------------- */
+int tagan_window_fwd(int mode, int32_t T, int64_t N, int32_t H, int32_t w, const float* x, float* out, void* stream);
+int tagan_window_bwd(int mode, int32_t T, int64_t N, int32_t H, int32_t w, const float* x, const float* dy, float* dx,
+                     void* stream);
+
+/* ---------------------------------------------------------------------------
  * NodeMemoryBank on the device.  Replaces src/tagan/utils/memory_bank.py:14-360
  * (a dict of per-node CPU tensors):  update (:65-173), get_state(s) (:175-211),
  * update_state (:235-244), decay_all (:222-225).  All arrays are caller-owned

@@ -91,6 +91,8 @@ _SIGNATURES = {
     "tagan_gru_bwd_workspace": (_sz, [_i64, _i32]),
     "tagan_gru_bwd": (_c.c_int, [_i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _f32, _u64, _p, _p, _p, _p, _p, _p, _p,
                                  _p, _p, _sz, _p]),
+    "tagan_window_fwd": (_c.c_int, [_c.c_int, _i32, _i64, _i32, _i32, _p, _p, _p]),
+    "tagan_window_bwd": (_c.c_int, [_c.c_int, _i32, _i64, _i32, _i32, _p, _p, _p, _p]),
     "tagan_membank_init": (_c.c_int, [_p, _p]),
     "tagan_membank_lookup": (_c.c_int, [_p, _p, _i64, _c.c_int, _i32, _p, _p, _p]),
     "tagan_membank_update": (_c.c_int, [_p, _p, _i64, _p, _i64, _i64, _c.c_double, _i32, _i32, _u64, _p, _p, _p]),

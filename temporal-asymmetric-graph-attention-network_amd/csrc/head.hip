@@ -7,17 +7,21 @@
 //      B·C elements (TemporalLossModule's default, classification.py:453-456) or cross entropy over B
 //      rows (model.py:439-441).
 // The reference runs this as ~25 ATen launches forward and ~40 backward on [1..B, 32, 128] tensors; it is
-// launch-bound, so here it is ONE workgroup (256 threads, thread j <-> feature j) per direction, every
-// intermediate in LDS, reductions in fixed order (bitwise reproducible).  Shapes: H <= 256, T <= 128,
+// launch-bound, so here it is ONE workgroup per direction (1024 threads: HB/H groups of H feature threads, the
+// [T, H] x [H, H] products split over the groups by step), every intermediate in LDS, the H x H weights streamed
+// through LDS in coalesced chunks (all in flight at once, instead of one latency-bound row walk per thread),
+// one wave per output row in the matrix-vector products, reductions in fixed order (bitwise reproducible).  Shapes: H <= 256, T <= 128,
 // C <= 16, T·H <= 8192 (tagan_head_supported); larger heads keep the torch path.
 #include "common.cuh"
 
 namespace tagan {
 namespace {
 
-constexpr int HB = 256;      // threads
-constexpr int HT = 32;       // time-step tile held in registers
+constexpr int HB = 1024;     // threads: NG = HB / H groups of H feature threads
+constexpr int HU = 8;        // steps per thread in the [T, H] products (ceil(T / NG); T·H <= 8192)
 constexpr int HC = 16;       // max classes
+constexpr int KC = 32;       // weight rows / columns staged per LDS chunk
+constexpr int NWV = HB / 64; // waves
 
 struct HeadArgs {
     int B, T, H, C;
@@ -42,123 +46,153 @@ struct HeadArgs {
 
 __host__ __device__ inline int64_t saved_floats(int T, int H) { return (int64_t)T * H + T + 3 * H + 2; }
 
+// sum over the whole block (16 wave sums folded in wave order)
 __device__ float block_sum(float v, float* red) {
     v = wave_sum(v);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     __syncthreads();
     if (lane == 0) red[w] = v;
     __syncthreads();
-    return (red[0] + red[1]) + (red[2] + red[3]);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NWV; ++i) s += red[i];
+    return s;
 }
 
-// LDS: xs[T*H] | zs[T*H] | vec[4*256] (a/da, pooled/dp, u/du, misc) | red[8]
+// LDS layout (floats): xs[T*H] | zs[T*H] | wt[KC*(H+1)] | part[HB] | va[128] | vd[128] | vp, vu, vg, vh [256 each]
+// | vl[16] | red[32]
+struct HeadLds {
+    float *xs, *zs, *wt, *part, *va, *vd, *vp, *vu, *vg, *vh, *vl, *red;
+    __device__ HeadLds(float* sm, int T, int H) {
+        xs = sm; zs = xs + T * H; wt = zs + T * H; part = wt + KC * (H + 1); va = part + HB; vd = va + 128;
+        vp = vd + 128; vu = vp + 256; vg = vu + 256; vh = vg + 256; vl = vh + 256; red = vl + 16;
+    }
+};
+
+// Z[t][j] = Σ_k X[t][k] W[j][k] for the thread's steps t = grp + NG·u (thread (grp, j)); W (nn.Linear [H, H]) is
+// staged through LDS in chunks of KC columns, transposed (row stride H + 1: conflict-free both ways), so every
+// global read is a coalesced run and the H·H weight reads of one workgroup are all in flight together
+__device__ __forceinline__ void xw_t(const float* __restrict__ W, const float* xs, float* wt, int T, int H, int NG,
+                                     bool act, int grp, int j, float (&acc)[HU]) {
+#pragma unroll
+    for (int u = 0; u < HU; ++u) acc[u] = 0.f;
+    for (int kc = 0; kc < H; kc += KC) {
+        const int kn = min(KC, H - kc);
+        __syncthreads();   // the previous chunk's reads are done
+        for (int e = threadIdx.x; e < H * kn; e += HB) {
+            const int jj = e / kn, kk = e % kn;
+            wt[kk * (H + 1) + jj] = W[(int64_t)jj * H + kc + kk];
+        }
+        __syncthreads();
+        if (act) {
+            for (int kk = 0; kk < kn; ++kk) {
+                const float w = wt[kk * (H + 1) + j];
+#pragma unroll
+                for (int u = 0; u < HU; ++u) {
+                    const int t = grp + NG * u;
+                    if (t < T) acc[u] = fmaf(w, xs[t * H + kc + kk], acc[u]);
+                }
+            }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(HB) k_head_fwd(HeadArgs A) {
     TAGAN_LIVE_SEED(A);
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int T = A.T, H = A.H, C = A.C, j = threadIdx.x;
-    float* xs = sm;
-    float* zs = xs + T * H;
-    float* va = zs + T * H;          // a [T]
-    float* vp = va + 256;            // pooled [H]
-    float* vh = vp + 256;            // h2 [H]
-    float* vl = vh + 256;            // logits of this row [C]
-    float* red = vl + 256;
+    const int T = A.T, H = A.H, C = A.C, tid = threadIdx.x;
+    const int NG = HB / H, grp = tid / H, j = tid % H, w = tid >> 6, lane = tid & 63;
+    const bool act = grp < NG;
+    HeadLds L(sm, T, H);
     float lsum = 0.f;
     for (int b = 0; b < A.B; ++b) {
         float* sv = A.saved + (int64_t)b * saved_floats(T, H);
-        for (int i = j; i < T * H; i += HB) xs[i] = b == 0 ? A.x0[i] : 0.f;
-        __syncthreads();
-        // z_t = tanh(W1 x_t + b1): thread j, a tile of HT steps in registers, W1 row j streamed as float4
-        if (j < H) {
-            for (int t0 = 0; t0 < T; t0 += HT) {
-                float acc[HT];
+        for (int i = tid; i < T * H; i += HB) L.xs[i] = b == 0 ? A.x0[i] : 0.f;
+        // z_t = tanh(W1 x_t + b1)
+        float acc[HU];
+        xw_t(A.W1, L.xs, L.wt, T, H, NG, act, grp, j, acc);
+        if (act) {
+            const float bj = A.b1[j];
 #pragma unroll
-                for (int u = 0; u < HT; ++u) acc[u] = 0.f;
-                for (int k = 0; k < H; k += 4) {
-                    const float4 w = *reinterpret_cast<const float4*>(A.W1 + (int64_t)j * H + k);
-#pragma unroll
-                    for (int u = 0; u < HT; ++u) {
-                        if (t0 + u < T) {
-                            const float4 x = *reinterpret_cast<const float4*>(xs + (t0 + u) * H + k);
-                            acc[u] += (w.x * x.x + w.y * x.y) + (w.z * x.z + w.w * x.w);
-                        }
-                    }
-                }
-                const float bj = A.b1[j];
-#pragma unroll
-                for (int u = 0; u < HT; ++u)
-                    if (t0 + u < T) zs[(t0 + u) * H + j] = tanhf(acc[u] + bj);
+            for (int u = 0; u < HU; ++u) {
+                const int t = grp + NG * u;
+                if (t < T) L.zs[t * H + j] = tanhf(acc[u] + bj);
             }
         }
         __syncthreads();
         // s_t = w2 . z_t (one wave per step, fixed-order lane sums)
-        const int w = j >> 6, lane = j & 63;
-        for (int t = w; t < T; t += HB / 64) {
+        for (int t = w; t < T; t += NWV) {
             float s = 0.f;
-            for (int k = lane; k < H; k += 64) s += A.w2[k] * zs[t * H + k];
+            for (int k = lane; k < H; k += 64) s += A.w2[k] * L.zs[t * H + k];
             s = wave_sum(s);
-            if (lane == 0) va[t] = s;
+            if (lane == 0) L.va[t] = s;
         }
         __syncthreads();
         if (w == 0) {   // softmax over T
             float m = -INFINITY;
-            for (int t = lane; t < T; t += 64) m = fmaxf(m, va[t]);
+            for (int t = lane; t < T; t += 64) m = fmaxf(m, L.va[t]);
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
             float e[2], den = 0.f;
             for (int q = 0; q < 2; ++q) {
                 const int t = lane + 64 * q;
-                e[q] = t < T ? expf(va[t] - m) : 0.f;
+                e[q] = t < T ? expf(L.va[t] - m) : 0.f;
                 den += e[q];
             }
             den = wave_sum(den);
             for (int q = 0; q < 2; ++q) {
                 const int t = lane + 64 * q;
-                if (t < T) va[t] = e[q] / den;
+                if (t < T) L.va[t] = e[q] / den;
             }
         }
         __syncthreads();
         // pooled[k] = Σ_t a_t x_t[k]
-        if (j < H) {
+        if (tid < H) {
             float p = 0.f;
-            for (int t = 0; t < T; ++t) p += va[t] * xs[t * H + j];
-            vp[j] = p;
+            for (int t = 0; t < T; ++t) p += L.va[t] * L.xs[t * H + tid];
+            L.vp[tid] = p;
         }
         __syncthreads();
-        // u = Wc1 p + bc1 ; LayerNorm ; ReLU ; dropout
-        float u = 0.f;
-        if (j < H) {
-            u = A.bc1[j];
-            for (int k = 0; k < H; k += 4) {
-                const float4 wv = *reinterpret_cast<const float4*>(A.Wc1 + (int64_t)j * H + k);
-                u += (wv.x * vp[k] + wv.y * vp[k + 1]) + (wv.z * vp[k + 2] + wv.w * vp[k + 3]);
+        // u = Wc1 p + bc1: one wave per output row, lanes over the (coalesced) row
+        for (int jo = w; jo < H; jo += NWV) {
+            float s = 0.f;
+            for (int k = lane * 4; k < H; k += 256) {
+                const float4 wv = *reinterpret_cast<const float4*>(A.Wc1 + (int64_t)jo * H + k);
+                s += (wv.x * L.vp[k] + wv.y * L.vp[k + 1]) + (wv.z * L.vp[k + 2] + wv.w * L.vp[k + 3]);
             }
+            s = wave_sum(s);
+            if (lane == 0) L.vu[jo] = s + A.bc1[jo];
         }
-        const float mean = block_sum(j < H ? u : 0.f, red) / (float)H;
-        const float dv = j < H ? u - mean : 0.f;
-        const float rstd = 1.f / sqrtf(block_sum(dv * dv, red) / (float)H + A.eps);
-        if (j < H) {
-            float n = dv * rstd * A.lng[j] + A.lnb[j];
+        __syncthreads();
+        // LayerNorm ; ReLU ; dropout
+        const float u = tid < H ? L.vu[tid] : 0.f;
+        const float mean = block_sum(u, L.red) / (float)H;
+        const float dv = tid < H ? u - mean : 0.f;
+        const float rstd = 1.f / sqrtf(block_sum(dv * dv, L.red) / (float)H + A.eps);
+        if (tid < H) {
+            float n = dv * rstd * A.lng[tid] + A.lnb[tid];
             n = n > 0.f ? n : 0.f;
             if (A.p_drop > 0.f) {
                 const uint32_t key = drop_key(A.seed, (uint64_t)b);
-                n = drop_u(key, (uint32_t)j) >= A.p_drop ? n * A.inv_keep : 0.f;
+                n = drop_u(key, (uint32_t)tid) >= A.p_drop ? n * A.inv_keep : 0.f;
             }
-            vh[j] = n;
+            L.vh[tid] = n;
         }
         __syncthreads();
-        // logits[c] = Wc2[c] . h2 + bc2[c]
-        for (int c = 0; c < C; ++c) {
-            const float v = block_sum(j < H ? A.Wc2[(int64_t)c * H + j] * vh[j] : 0.f, red);
-            if (j == 0) vl[c] = v + A.bc2[c];
+        // logits[c] = Wc2[c] . h2 + bc2[c]: one wave per class
+        for (int c = w; c < C; c += NWV) {
+            float s = 0.f;
+            for (int k = lane; k < H; k += 64) s += A.Wc2[(int64_t)c * H + k] * L.vh[k];
+            s = wave_sum(s);
+            if (lane == 0) L.vl[c] = s + A.bc2[c];
         }
         __syncthreads();
-        if (j == 0) {
+        if (tid == 0) {
             float m = -INFINITY, den = 0.f;
-            for (int c = 0; c < C; ++c) m = fmaxf(m, vl[c]);
-            for (int c = 0; c < C; ++c) den += expf(vl[c] - m);
+            for (int c = 0; c < C; ++c) m = fmaxf(m, L.vl[c]);
+            for (int c = 0; c < C; ++c) den += expf(L.vl[c] - m);
             for (int c = 0; c < C; ++c) {
-                const float z = vl[c];
+                const float z = L.vl[c];
                 A.logits[b * C + c] = z;
                 A.preds[b * C + c] = C == 1 ? 1.f / (1.f + expf(-z)) : expf(z - m) / den;
                 if (A.loss_kind == 1) {
@@ -168,46 +202,40 @@ __global__ void __launch_bounds__(HB) k_head_fwd(HeadArgs A) {
             }
             if (A.loss_kind == 2) {   // an out-of-range class index poisons the loss (torch would raise)
                 const int y = (int)A.labels[b];
-                lsum += (y >= 0 && y < C) ? (m + logf(den)) - vl[y] : NAN;
+                lsum += (y >= 0 && y < C) ? (m + logf(den)) - L.vl[y] : NAN;
             }
         }
         // saved: z | a | pooled | u | mean, rstd | h2
-        for (int i = j; i < T * H; i += HB) sv[i] = zs[i];
-        for (int t = j; t < T; t += HB) sv[T * H + t] = va[t];
-        if (j < H) {
-            sv[T * H + T + j] = vp[j];
-            sv[T * H + T + H + j] = u;
-            sv[T * H + T + 2 * H + 2 + j] = vh[j];
+        for (int i = tid; i < T * H; i += HB) sv[i] = L.zs[i];
+        for (int t = tid; t < T; t += HB) sv[T * H + t] = L.va[t];
+        if (tid < H) {
+            sv[T * H + T + tid] = L.vp[tid];
+            sv[T * H + T + H + tid] = u;
+            sv[T * H + T + 2 * H + 2 + tid] = L.vh[tid];
         }
-        if (j == 0) { sv[T * H + T + 2 * H] = mean; sv[T * H + T + 2 * H + 1] = rstd; }
+        if (tid == 0) { sv[T * H + T + 2 * H] = mean; sv[T * H + T + 2 * H + 1] = rstd; }
         __syncthreads();
     }
-    if (j == 0 && A.loss_kind && A.loss)
+    if (tid == 0 && A.loss_kind && A.loss)
         A.loss[0] = A.loss_kind == 1 ? lsum / (float)(A.B * C) : lsum / (float)A.B;
 }
 
 __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
     TAGAN_LIVE_SEED(A);
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int T = A.T, H = A.H, C = A.C, j = threadIdx.x;
-    const int w = j >> 6, lane = j & 63;
-    float* xs = sm;
-    float* zs = xs + T * H;          // z, then dpre
-    float* va = zs + T * H;          // a [T]
-    float* vd = va + 256;            // da, then ds [T]
-    float* vp = vd + 256;            // pooled [H]
-    float* vq = vp + 256;            // du [H]
-    float* vg = vq + 256;            // dpooled [H]
-    float* vl = vg + 256;            // dlogits [C]
-    float* red = vl + 256;
+    const int T = A.T, H = A.H, C = A.C, tid = threadIdx.x;
+    const int NG = HB / H, grp = tid / H, j = tid % H, w = tid >> 6, lane = tid & 63;
+    const bool act = grp < NG;
+    HeadLds L(sm, T, H);
+    float* vq = L.vu;    // x̂, then du
     const float gL = A.g_loss ? A.g_loss[0] : 0.f;
     for (int b = 0; b < A.B; ++b) {
         const bool first = b == 0;
         const float* sv = A.saved + (int64_t)b * saved_floats(T, H);
-        for (int i = j; i < T * H; i += HB) { xs[i] = first ? A.x0[i] : 0.f; zs[i] = sv[i]; }
-        for (int t = j; t < T; t += HB) va[t] = sv[T * H + t];
-        if (j < H) vp[j] = sv[T * H + T + j];
-        if (j == 0) {   // dlogits of this row
+        for (int i = tid; i < T * H; i += HB) { L.xs[i] = first ? A.x0[i] : 0.f; L.zs[i] = sv[i]; }
+        for (int t = tid; t < T; t += HB) L.va[t] = sv[T * H + t];
+        if (tid < H) L.vp[tid] = sv[T * H + T + tid];
+        if (tid == 0) {   // dlogits of this row
             float sgp = 0.f;
             if (A.g_preds && C > 1)
                 for (int c = 0; c < C; ++c) sgp += A.g_preds[b * C + c] * A.preds[b * C + c];
@@ -221,110 +249,121 @@ __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
                 }
                 if (A.loss_kind == 2 && A.g_loss)
                     g += gL * (p - (c == (int)A.labels[b] ? 1.f : 0.f)) / (float)A.B;
-                vl[c] = g;
+                L.vl[c] = g;
             }
         }
         __syncthreads();
-        if (j < C) A.dbc2[j] = (first ? 0.f : A.dbc2[j]) + vl[j];
+        if (tid < C) A.dbc2[tid] = (first ? 0.f : A.dbc2[tid]) + L.vl[tid];
         float du = 0.f;
-        if (j < H) {
-            const float u = sv[T * H + T + H + j], mean = sv[T * H + T + 2 * H], rstd = sv[T * H + T + 2 * H + 1];
-            const float h2 = sv[T * H + T + 2 * H + 2 + j];
+        if (tid < H) {
+            const float u = sv[T * H + T + H + tid], mean = sv[T * H + T + 2 * H], rstd = sv[T * H + T + 2 * H + 1];
+            const float h2 = sv[T * H + T + 2 * H + 2 + tid];
             float dh = 0.f;
             for (int c = 0; c < C; ++c) {
-                const int64_t o = (int64_t)c * H + j;
-                A.dWc2[o] = (first ? 0.f : A.dWc2[o]) + vl[c] * h2;
-                dh += vl[c] * A.Wc2[o];
+                const int64_t o = (int64_t)c * H + tid;
+                A.dWc2[o] = (first ? 0.f : A.dWc2[o]) + L.vl[c] * h2;
+                dh += L.vl[c] * A.Wc2[o];
             }
             if (A.p_drop > 0.f) {
                 const uint32_t key = drop_key(A.seed, (uint64_t)b);
-                dh = drop_u(key, (uint32_t)j) >= A.p_drop ? dh * A.inv_keep : 0.f;
+                dh = drop_u(key, (uint32_t)tid) >= A.p_drop ? dh * A.inv_keep : 0.f;
             }
             const float xh = (u - mean) * rstd;
-            const float n = xh * A.lng[j] + A.lnb[j];
+            const float n = xh * A.lng[tid] + A.lnb[tid];
             const float dn = n > 0.f ? dh : 0.f;
-            A.dlng[j] = (first ? 0.f : A.dlng[j]) + dn * xh;
-            A.dlnb[j] = (first ? 0.f : A.dlnb[j]) + dn;
-            du = dn * A.lng[j];           // g·dn, reduced below
-            vq[j] = xh;                   // keep x̂ for the LN backward
+            A.dlng[tid] = (first ? 0.f : A.dlng[tid]) + dn * xh;
+            A.dlnb[tid] = (first ? 0.f : A.dlnb[tid]) + dn;
+            du = dn * A.lng[tid];         // g·dn, reduced below
+            vq[tid] = xh;                 // keep x̂ for the LN backward
         }
-        const float c1 = block_sum(j < H ? du * vq[j] : 0.f, red) / (float)H;
-        const float c2 = block_sum(j < H ? du : 0.f, red) / (float)H;
-        if (j < H) {
+        const float c1 = block_sum(tid < H ? du * vq[tid] : 0.f, L.red) / (float)H;
+        const float c2 = block_sum(tid < H ? du : 0.f, L.red) / (float)H;
+        if (tid < H) {
             const float rstd = sv[T * H + T + 2 * H + 1];
-            du = rstd * (du - c1 * vq[j] - c2);
-            A.dbc1[j] = (first ? 0.f : A.dbc1[j]) + du;
+            du = rstd * (du - c1 * vq[tid] - c2);
+            A.dbc1[tid] = (first ? 0.f : A.dbc1[tid]) + du;
         }
         __syncthreads();
-        if (j < H) vq[j] = du;
+        if (tid < H) vq[tid] = du;
         __syncthreads();
-        if (j < H) {
-            // dWc1[j][k] += du_j p_k ; dpooled[k] = Σ_j du_j Wc1[j][k]
-            for (int k = 0; k < H; ++k) {
-                const int64_t o = (int64_t)j * H + k;
-                A.dWc1[o] = (first ? 0.f : A.dWc1[o]) + vq[j] * vp[k];
-            }
+        // dWc1[j][k] += du_j p_k (coalesced over the flat index)
+        for (int o = tid; o < H * H; o += HB) A.dWc1[o] = (first ? 0.f : A.dWc1[o]) + vq[o / H] * L.vp[o % H];
+        // dpooled[k] = Σ_j du_j Wc1[j][k]: thread (grp, k) over j = grp, grp + NG, ..., then the groups in order
+        if (act) {
             float g = 0.f;
-            for (int jj = 0; jj < H; ++jj) g += vq[jj] * A.Wc1[(int64_t)jj * H + j];
-            vg[j] = g;
+            for (int jj = grp; jj < H; jj += NG) g += vq[jj] * A.Wc1[(int64_t)jj * H + j];
+            L.part[grp * H + j] = g;
+        }
+        __syncthreads();
+        if (tid < H) {
+            float g = 0.f;
+            for (int q = 0; q < NG; ++q) g += L.part[q * H + tid];
+            L.vg[tid] = g;
         }
         __syncthreads();
         // da_t = dpooled . x_t ; ds = a (da - Σ a da)
-        for (int t = w; t < T; t += HB / 64) {
+        for (int t = w; t < T; t += NWV) {
             float s = 0.f;
-            for (int k = lane; k < H; k += 64) s += vg[k] * xs[t * H + k];
+            for (int k = lane; k < H; k += 64) s += L.vg[k] * L.xs[t * H + k];
             s = wave_sum(s);
-            if (lane == 0) vd[t] = s;
+            if (lane == 0) L.vd[t] = s;
         }
         __syncthreads();
         if (w == 0) {
             float s = 0.f;
-            for (int t = lane; t < T; t += 64) s += va[t] * vd[t];
+            for (int t = lane; t < T; t += 64) s += L.va[t] * L.vd[t];
             s = wave_sum(s);
-            for (int t = lane; t < T; t += 64) vd[t] = va[t] * (vd[t] - s);
+            for (int t = lane; t < T; t += 64) L.vd[t] = L.va[t] * (L.vd[t] - s);
         }
         __syncthreads();
         // dw2[j] += Σ_t ds_t z_tj ; dpre_tj = ds_t w2_j (1 - z_tj^2) (overwrites z) ; db1[j] += Σ_t dpre_tj
-        if (j < H) {
+        if (tid < H) {
             float gw = 0.f, gb = 0.f;
-            const float w2j = A.w2[j];
+            const float w2j = A.w2[tid];
             for (int t = 0; t < T; ++t) {
-                const float z = zs[t * H + j], ds = vd[t];
+                const float z = L.zs[t * H + tid], ds = L.vd[t];
                 gw += ds * z;
                 const float dp = ds * w2j * (1.f - z * z);
-                zs[t * H + j] = dp;
+                L.zs[t * H + tid] = dp;
                 gb += dp;
             }
-            A.dw2[j] = (first ? 0.f : A.dw2[j]) + gw;
-            A.db1[j] = (first ? 0.f : A.db1[j]) + gb;
+            A.dw2[tid] = (first ? 0.f : A.dw2[tid]) + gw;
+            A.db1[tid] = (first ? 0.f : A.db1[tid]) + gb;
         }
         __syncthreads();
         if (first) {   // rows >= 1 have x = 0: no dW1 and no dx
-            if (j < H) {
-                // dW1[j][k] = Σ_t dpre_tj x_tk
-                for (int k = 0; k < H; k += 4) {
-                    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-                    for (int t = 0; t < T; ++t) {
-                        const float dp = zs[t * H + j];
-                        const float4 x = *reinterpret_cast<const float4*>(xs + t * H + k);
-                        acc.x += dp * x.x; acc.y += dp * x.y; acc.z += dp * x.z; acc.w += dp * x.w;
+            // dW1[j][k] = Σ_t dpre_tj x_tk (coalesced over the flat index)
+            for (int o = tid; o < H * H; o += HB) {
+                const int jj = o / H, k = o % H;
+                float acc = 0.f;
+                for (int t = 0; t < T; ++t) acc = fmaf(L.zs[t * H + jj], L.xs[t * H + k], acc);
+                A.dW1[o] = acc;
+            }
+            // dx_t[k] = a_t dpooled_k + Σ_jj dpre_t,jj W1[jj][k]: W1 rows staged through LDS in chunks of KC
+            float acc[HU];
+#pragma unroll
+            for (int u = 0; u < HU; ++u) acc[u] = 0.f;
+            for (int jc = 0; jc < H; jc += KC) {
+                const int jn = min(KC, H - jc);
+                __syncthreads();
+                for (int e = tid; e < jn * H; e += HB) L.wt[(e / H) * (H + 1) + e % H] = A.W1[(int64_t)jc * H + e];
+                __syncthreads();
+                if (act) {
+                    for (int kk = 0; kk < jn; ++kk) {
+                        const float wv = L.wt[kk * (H + 1) + j];
+#pragma unroll
+                        for (int u = 0; u < HU; ++u) {
+                            const int t = grp + NG * u;
+                            if (t < T) acc[u] = fmaf(L.zs[t * H + jc + kk], wv, acc[u]);
+                        }
                     }
-                    *reinterpret_cast<float4*>(A.dW1 + (int64_t)j * H + k) = acc;
                 }
-                // dx_t[k=j] = a_t dpooled_j + Σ_jj dpre_t,jj W1[jj][j]
-                for (int t0 = 0; t0 < T; t0 += HT) {
-                    float acc[HT];
+            }
+            if (act) {
 #pragma unroll
-                    for (int u = 0; u < HT; ++u) acc[u] = 0.f;
-                    for (int jj = 0; jj < H; ++jj) {
-                        const float wv = A.W1[(int64_t)jj * H + j];
-#pragma unroll
-                        for (int u = 0; u < HT; ++u)
-                            if (t0 + u < T) acc[u] += zs[(t0 + u) * H + jj] * wv;
-                    }
-#pragma unroll
-                    for (int u = 0; u < HT; ++u)
-                        if (t0 + u < T) A.dx0[(int64_t)(t0 + u) * H + j] = va[t0 + u] * vg[j] + acc[u];
+                for (int u = 0; u < HU; ++u) {
+                    const int t = grp + NG * u;
+                    if (t < T) A.dx0[(int64_t)t * H + j] = L.va[t] * L.vg[j] + acc[u];
                 }
             }
         }
@@ -332,7 +371,21 @@ __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
     }
 }
 
-size_t head_lds(int T, int H) { return (size_t)(2 * T * H + 6 * 256 + 8) * sizeof(float); }
+size_t head_lds(int T, int H) {
+    return (size_t)(2 * T * H + KC * (H + 1) + HB + 2 * 128 + 4 * 256 + 16 + 32) * sizeof(float);
+}
+
+int head_lds_optin(size_t bytes) {
+    static bool done = false;
+    if (done || bytes <= 64 * 1024) return TAGAN_OK;
+    hipError_t e1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_head_fwd),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_head_bwd),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    TAGAN_REQUIRE(e1 == hipSuccess && e2 == hipSuccess, TAGAN_ERR_LAUNCH, "head: LDS opt-in failed");
+    done = true;
+    return TAGAN_OK;
+}
 
 }  // namespace
 }  // namespace tagan
@@ -340,8 +393,8 @@ size_t head_lds(int T, int H) { return (size_t)(2 * T * H + 6 * 256 + 8) * sizeo
 extern "C" {
 
 int tagan_head_supported(int32_t T, int32_t H, int32_t C) {
-    return (H >= 4 && H <= tagan::HB && H % 4 == 0 && T >= 1 && T <= 128 && C >= 1 && C <= tagan::HC &&
-            T * H <= 8192) ? 1 : 0;
+    return (H >= 4 && H <= 256 && H % 4 == 0 && T >= 1 && T <= 128 && C >= 1 && C <= tagan::HC &&
+            T * H <= 8192 && (T + tagan::HB / H - 1) / (tagan::HB / H) <= tagan::HU) ? 1 : 0;
 }
 
 size_t tagan_head_saved_floats(int32_t B, int32_t T, int32_t H) {
@@ -364,6 +417,7 @@ int tagan_head_fwd(int32_t B, int32_t T, int32_t H, int32_t C, const float* x0, 
     A.lng = ln_w; A.lnb = ln_b; A.eps = eps; A.Wc2 = Wc2; A.bc2 = bc2; A.p_drop = p_drop;
     A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed; A.seed_ctr = seed_counter(); A.labels = labels; A.loss_kind = loss_kind;
     A.logits = logits; A.preds = preds; A.loss = loss; A.saved = saved;
+    if (int rc = head_lds_optin(head_lds(T, H))) return rc;
     k_head_fwd<<<1, HB, head_lds(T, H), as_stream(stream)>>>(A);
     TAGAN_CHECK_LAUNCH("head_fwd");
     return TAGAN_OK;
@@ -387,6 +441,7 @@ int tagan_head_bwd(int32_t B, int32_t T, int32_t H, int32_t C, const float* x0, 
     A.loss_kind = loss_kind; A.logits = (float*)logits; A.preds = (float*)preds; A.saved = (float*)saved;
     A.g_loss = g_loss; A.g_logits = g_logits; A.g_preds = g_preds; A.dx0 = dx0; A.dW1 = dW1; A.db1 = db1;
     A.dw2 = dw2; A.dWc1 = dWc1; A.dbc1 = dbc1; A.dlng = dln_w; A.dlnb = dln_b; A.dWc2 = dWc2; A.dbc2 = dbc2;
+    if (int rc = head_lds_optin(head_lds(T, H))) return rc;
     k_head_bwd<<<1, HB, head_lds(T, H), as_stream(stream)>>>(A);
     TAGAN_CHECK_LAUNCH("head_bwd");
     return TAGAN_OK;

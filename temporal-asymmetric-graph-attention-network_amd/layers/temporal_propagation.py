@@ -17,8 +17,8 @@ over T -> windowed skip connection -> output_proj -> dropout -> LayerNorm.  It r
 time-major ([T, N, H], node rows independent) on the device: the x-side of all three
 GRU gates for all T steps is ONE GEMM, the whole recurrence over T (recurrent products,
 gates, both LayerNorms, dropout) is ONE kernel each way (csrc/gru.hip, GRUSeqFn), the
-residual tails run on the HIP LayerNorm kernels, the window aggregation is one pooling
-pass over T.  TAGAN uses it
+residual tails run on the HIP LayerNorm kernels, the window aggregation is one kernel
+pass over T each way (csrc/window.hip, WindowFn).  TAGAN uses it
 when constructed with ``temporal_propagation="intended"`` (default "shipped").
 The submodules keep their reference list-in/list-out forwards (on the same device
 code) for standalone use.
@@ -28,7 +28,6 @@ from typing import Any, List, Optional
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .._lib import check, lib, ptr, require_hip, stream_of
 from ..kernels import dropout_add_layer_norm, layer_norm, linear, new_seed, weight_grad
@@ -103,6 +102,41 @@ def gru_sequence(cell: "TemporalGRUCell", gx: torch.Tensor, tscale: Optional[tor
                           cell.layer_norm_h.bias if ln else None, cell.layer_norm_out.weight if ln else None,
                           cell.layer_norm_out.bias if ln else None, tscale,
                           cell.layer_norm_h.eps if ln else 1e-5, cell.layer_norm_out.eps if ln else 1e-5, p, seed)
+
+
+_AGG_MODE = {"mean": 0, "max": 1}   # anything else sums (temporal_propagation.py:912-925)
+
+
+class WindowFn(torch.autograd.Function):
+    """±w window aggregation over T of a time-major [T, N, H] tensor in one pass each way (csrc/window.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, w: int, mode: int):
+        T, N, H = x.shape
+        x = x.contiguous()
+        out = torch.empty_like(x)
+        check(lib().tagan_window_fwd(mode, T, N, H, w, ptr(x), ptr(out), stream_of(x)), "tagan_window_fwd")
+        ctx.save_for_backward(x if mode == 1 else None)
+        ctx.cfg = (w, mode, T, N, H)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        w, mode, T, N, H = ctx.cfg
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        check(lib().tagan_window_bwd(mode, T, N, H, w, ptr(x), ptr(dy), ptr(dx), stream_of(dy)), "tagan_window_bwd")
+        return dx, None, None
+
+
+def window_aggregate(x: torch.Tensor, w: int, aggregation: str) -> torch.Tensor:
+    """TemporalSkipConnection's windowed aggregation (mean over the in-range steps / max / sum) of x [T, N, H]."""
+    if w <= 0:
+        return x
+    if x.shape[-1] % 4 != 0 or x.dtype != torch.float32:
+        raise ValueError(f"window aggregation kernel takes fp32 with H % 4 == 0, got {x.dtype} H={x.shape[-1]}")
+    return WindowFn.apply(x, int(w), _AGG_MODE.get(aggregation, 2))
 
 
 class TemporalGRUCell(nn.Module):
@@ -268,17 +302,7 @@ class TemporalSkipConnection(nn.Module):
         if self.apply_activation:
             p = self.act_fn(p)
         p = self.dropout_layer(_ln(p, self.layer_norm1 if self.use_layer_norm else None))
-        Hd = p.shape[-1]
-        w = self.window_size
-        seq = p.permute(1, 2, 0).reshape(N * Hd, 1, T)          # pooling runs along T
-        k = 2 * w + 1
-        if self.aggregation == "mean":
-            agg = F.avg_pool1d(seq, k, 1, w, count_include_pad=False) if w > 0 else seq
-        elif self.aggregation == "max":
-            agg = F.max_pool1d(seq, k, 1, w) if w > 0 else seq
-        else:
-            agg = F.avg_pool1d(seq, k, 1, w, count_include_pad=True) * k if w > 0 else seq
-        agg = agg.reshape(N, Hd, T).permute(2, 0, 1)
+        agg = window_aggregate(p, self.window_size, self.aggregation)
         out = linear(self.act_fn(agg), self.output_proj.weight, self.output_proj.bias)
         if self.residual and self.use_layer_norm:
             return dropout_add_layer_norm(out, xt, self.layer_norm2, self.dropout if self.training else 0.0)

@@ -64,6 +64,8 @@ CASES = [  # T, H, C, B, kind, label shape
     (16, 128, 3, 2, "bce", "2d"),
     (5, 64, 2, 1, "none", None),
     (128, 64, 1, 1, "bce", "1d"),
+    (32, 256, 1, 2, "bce", "1d"),     # T·H = 8192: the largest head the kernel takes, 4 step groups
+    (20, 96, 4, 2, "ce", "1d"),       # H not a power of two: 10 step groups, 64 idle threads
 ]
 
 
