@@ -1403,6 +1403,440 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
 }
 
 // ---------------------------------------------------------------------------------------------------------
+// v6 (T <= 32, d in {16, 32}: C1, C2, C4): the v4 per-head products, fed through head-group SLABS.  At d = 16 every
+// (row, step, head) slice of the time-major [T, N, 3H] projection is a 64-B half line, and the v4 lane -> (step,
+// 4 features) loads cap even a compute-free copy of the backward's traffic at 3.3-3.7 TB/s (tools/probes/
+// tattn_copy.hip); 256-B+ runs per step reach 5+ TB/s.  So one workgroup of GH waves takes (node row, group of GH
+// heads): the whole workgroup streams the row's [T, GH·d] slices of Q | K | V (| dO) with flat float4 loads into one
+// LDS slab (issued one unit ahead, held in registers meanwhile), wave w computes head w of the group exactly as v4
+// (operands from the slab: b128 rows for the register operands, four b32 reads for the transposed ones; dS / P'
+// through a private [TP][TP+8] tile), parks its outputs in its own slab columns, and the workgroup stores the slab
+// back as flat float4 runs.
+// ---------------------------------------------------------------------------------------------------------
+// Build knobs: PREFETCH=1 holds the next unit's slab share in registers during this one (else the slab is loaded
+// at the unit's start and the other workgroups on the CU cover the latency); WPE = minimum waves per SIMD.
+#ifndef TAGAN_V6_PREFETCH
+#define TAGAN_V6_PREFETCH 0
+#endif
+#ifndef TAGAN_V6_WPE
+#define TAGAN_V6_WPE 2
+#endif
+#ifndef TAGAN_V6_WPE_B
+#define TAGAN_V6_WPE_B 3
+#endif
+// slab pitch: (4 or 3)·GH·DP + 8 floats = 4m with m = 2 (mod 4): conflict-free ds_read_b128 of lanes (c, g)
+template <int NT, int GH, int DP>
+constexpr int v6_pitch() { return NT * GH * DP + 8; }
+size_t v6_fwd_lds(int TT, int DT, int GH) { return (size_t)(16 * TT) * (3 * GH * 16 * DT + 8) * 4; }
+size_t v6_bwd_lds(int TT, int DT, int GH) {
+    return ((size_t)(16 * TT) * (4 * GH * 16 * DT + 8) + (size_t)GH * 16 * TT * v4_ld(16 * TT)) * 4;
+}
+
+// the workgroup's share of one unit's slab: thread tid holds float4 number tid + n·(64·GH), n < NPF
+template <int TT, int DT, int GH, int NT, typename S>
+struct V6Slab {
+    static constexpr int TP = 16 * TT, DP = 16 * DT, C4 = NT * GH * DP / 4, NPF = TP * C4 / (WAVE * GH);
+    static constexpr int SP = v6_pitch<NT, GH, DP>();
+    f4v pf[NPF];
+    // tensor x of the slab: 0..2 = Q, K, V (row stride s_row, step stride s_t), 3 = dO
+    __device__ __forceinline__ void load(const TArgs& A, const void* q, const void* k, const void* v, const void* dout,
+                                         int64_t r, int hg) {
+#pragma unroll
+        for (int n = 0; n < NPF; ++n) {
+            const int e = threadIdx.x + n * WAVE * GH, t = e / C4, col = 4 * (e % C4);
+            const int x = col / (GH * DP), cc = col % (GH * DP);
+            const bool ok = t < A.T;
+            if (x < 3) {
+                const void* src = x == 0 ? q : x == 1 ? k : v;
+                pf[n] = ld4v<S>(src, r * A.s_row + (int64_t)t * A.s_t + hg * GH * DP + cc, ok);
+            } else {
+                pf[n] = ld4v<S>(dout, r * A.do_row + (int64_t)t * A.do_t + hg * GH * DP + cc, ok);
+            }
+        }
+    }
+    __device__ __forceinline__ void park(float* slab) const {
+#pragma unroll
+        for (int n = 0; n < NPF; ++n) {
+            const int e = threadIdx.x + n * WAVE * GH;
+            *(f4v*)(slab + (e / C4) * SP + 4 * (e % C4)) = pf[n];
+        }
+    }
+};
+
+template <int TT, int DT, int GH, typename S>
+__global__ void __launch_bounds__(WAVE * GH, TAGAN_V6_WPE) k_tattn_fwd_v6(TArgs A, const float* __restrict__ q,
+                                                            const float* __restrict__ k,
+                                                            const float* __restrict__ v) {
+    TAGAN_LIVE_SEED(A);
+    using Slab = V6Slab<TT, DT, GH, 3, S>;
+    constexpr int DP = 16 * DT, SP = Slab::SP;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* slab = sm;   // [TP][SP]: Q | K | V of the group's heads, then O in the Q columns
+    const int T = A.T;
+    const int w = threadIdx.x / WAVE, lane = threadIdx.x % WAVE, c0 = lane & 15, g0 = lane >> 4;
+    const int hgc = A.heads / GH, hg = blockIdx.x % hgc, h = hg * GH + w;
+    const int64_t rg = blockIdx.x / hgc, G = gridDim.x / hgc;
+    float bst[TT][TT][4];
+    v4_static_bias<TT>(A, h, c0, g0, bst);
+    Slab io;
+    if (TAGAN_V6_PREFETCH && rg < A.rows) io.load(A, q, k, v, nullptr, rg, hg);
+    for (int64_t r = rg; r < A.rows; r += G) {
+        int c = c0, g = g0;
+        asm volatile("" : "+v"(c), "+v"(g));   // see k_tattn_fwd_v4
+        if (!TAGAN_V6_PREFETCH) io.load(A, q, k, v, nullptr, r, hg);
+        __syncthreads();   // the previous unit's stores have read the slab
+        io.park(slab);
+        __syncthreads();
+        if (TAGAN_V6_PREFETCH && r + G < A.rows) io.load(A, q, k, v, nullptr, r + G, hg);
+        const float* sq = slab + w * DP;
+        const float* sk = slab + GH * DP + w * DP;
+        const float* sv = slab + 2 * GH * DP + w * DP;
+        f4v s[TT][TT];
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it) s[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+            f4v qv[TT], kv[TT];
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                qv[t] = lds4(sq + (t * 16 + c) * SP + dt * 16 + 4 * g);
+                kv[t] = lds4(sk + (t * 16 + c) * SP + dt * 16 + 4 * g);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int it = 0; it < TT; ++it) s[jt][it] = mfma4(kv[jt][e], qv[it][e], s[jt][it]);
+        }
+        const uint32_t drk = tkey(A, r, h);
+        float inv_l[TT];
+#pragma unroll
+        for (int it = 0; it < TT; ++it) {
+            const int i = it * 16 + c;
+            float mx = -INFINITY;
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float sc = v4_score(A, bst[jt][it][e], r, h, i, jt * 16 + 4 * g + e, s[jt][it][e]);
+                    s[jt][it][e] = sc;
+                    mx = fmaxf(mx, sc);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, WAVE));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, WAVE));
+            float l = 0.f;
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float sc = s[jt][it][e];
+                    const float p = (sc == -INFINITY) ? 0.f : __expf(sc - mx);
+                    l += p;
+                    s[jt][it][e] = p * drop_scale(A, drk, i, jt * 16 + 4 * g + e);
+                }
+            l += __shfl_xor(l, 16, WAVE);
+            l += __shfl_xor(l, 32, WAVE);
+            inv_l[it] = (l > 0.f) ? 1.f / l : NAN;
+            if (g == 0 && i < T) A.lse[(r * A.heads + h) * T + i] = mx + __logf(l);
+        }
+        // Oᵀ = Vᵀ·P'ᵀ: A = V[16jt + 4g + e][16dt + c] (four b32 reads of the slab), B = the P'ᵀ accumulators
+        f4v o[DT][TT];
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it) o[dt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float va = sv[(jt * 16 + 4 * g + e) * SP + dt * 16 + c];
+#pragma unroll
+                    for (int it = 0; it < TT; ++it) o[dt][it] = mfma4(va, s[jt][it][e], o[dt][it]);
+                }
+        __syncthreads();   // every wave is done reading the slab
+#pragma unroll
+        for (int it = 0; it < TT; ++it)
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+                *(f4v*)(slab + (it * 16 + c) * SP + w * DP + dt * 16 + 4 * g) = o[dt][it] * inv_l[it];
+        __syncthreads();
+        // O of the group's heads: the slab's first GH·DP columns, flat float4 runs
+        constexpr int OC4 = GH * DP / 4;
+        for (int e = threadIdx.x; e < T * OC4; e += WAVE * GH) {
+            const int t = e / OC4, col = 4 * (e % OC4);
+            st4v<S>(A.out, r * A.o_row + (int64_t)t * A.o_t + hg * GH * DP + col, lds4(slab + t * SP + col), 1.f);
+        }
+    }
+}
+
+template <int TT, int DT, int GH, typename S>
+__global__ void __launch_bounds__(WAVE * GH, (TT == 2 && DT == 2) ? 2 : TAGAN_V6_WPE_B) k_tattn_bwd_v6(TArgs A, const float* __restrict__ q,
+                                                            const float* __restrict__ k,
+                                                            const float* __restrict__ v,
+                                                            const float* __restrict__ dout,
+                                                            const float* __restrict__ lse) {
+    TAGAN_LIVE_SEED(A);
+    using Slab = V6Slab<TT, DT, GH, 4, S>;
+    constexpr int TP = 16 * TT, LD = v4_ld(TP), DP = 16 * DT, SP = Slab::SP;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* slab = sm;                       // [TP][SP]: Q | K | V | dO, then dQ | dK | dV in the first three
+    const int T = A.T, NB = 2 * T - 1, d = A.d;
+    const int w = threadIdx.x / WAVE, lane = threadIdx.x % WAVE, c0 = lane & 15, g0 = lane >> 4;
+    const int hgc = A.heads / GH, hg = blockIdx.x % hgc, h = hg * GH + w;
+    const int64_t rg = blockIdx.x / hgc, G = gridDim.x / hgc;
+    float* X = sm + TP * SP + w * TP * LD;   // this wave's [TP][LD] transpose tile (dS, then P')
+    float bst[TT][TT][4];
+    v4_static_bias<TT>(A, h, c0, g0, bst);
+    const float msc = A.p_drop > 0.f ? A.inv_keep : 1.f;
+    f4v gsum[TT][TT];
+#pragma unroll
+    for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+        for (int it = 0; it < TT; ++it) gsum[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+    f4v bsum[3][DT];
+#pragma unroll
+    for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) bsum[t3][dt] = f4v{0.f, 0.f, 0.f, 0.f};
+    Slab io;
+    float lsev[TT];
+    auto load_lse = [&](int64_t rr) {
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            const int i = t * 16 + c0;
+            lsev[t] = (i < T) ? lse[(rr * A.heads + h) * T + i] : 0.f;
+        }
+    };
+    if (TAGAN_V6_PREFETCH && rg < A.rows) {
+        io.load(A, q, k, v, dout, rg, hg);
+        load_lse(rg);
+    }
+    for (int64_t r = rg; r < A.rows; r += G) {
+        int c = c0, g = g0;
+        asm volatile("" : "+v"(c), "+v"(g));   // see k_tattn_fwd_v4
+        if (!TAGAN_V6_PREFETCH) {
+            io.load(A, q, k, v, dout, r, hg);
+            load_lse(r);
+        }
+        __syncthreads();   // the previous unit's stores have read the slab
+        io.park(slab);
+        float lse_i[TT];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) lse_i[t] = lsev[t];
+        __syncthreads();
+        if (TAGAN_V6_PREFETCH && r + G < A.rows) {
+            io.load(A, q, k, v, dout, r + G, hg);
+            load_lse(r + G);
+        }
+        const float* sq = slab + w * DP;
+        const float* sk = slab + GH * DP + w * DP;
+        const float* sv = slab + 2 * GH * DP + w * DP;
+        const float* so = slab + 3 * GH * DP + w * DP;
+        const uint32_t drk = tkey(A, r, h);
+        f4v s[TT][TT], dp[TT][TT];
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it) {
+                s[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+                dp[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+            f4v xa[TT], xb[TT];
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                xa[t] = lds4(sk + (t * 16 + c) * SP + dt * 16 + 4 * g);
+                xb[t] = lds4(sq + (t * 16 + c) * SP + dt * 16 + 4 * g);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int it = 0; it < TT; ++it) s[jt][it] = mfma4(xa[jt][e], xb[it][e], s[jt][it]);
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                xa[t] = lds4(sv + (t * 16 + c) * SP + dt * 16 + 4 * g);
+                xb[t] = lds4(so + (t * 16 + c) * SP + dt * 16 + 4 * g);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int it = 0; it < TT; ++it) dp[jt][it] = mfma4(xa[jt][e], xb[it][e], dp[jt][it]);
+        }
+        uint32_t keep = 0;
+#pragma unroll
+        for (int it = 0; it < TT; ++it) {
+            const int i = it * 16 + c;
+            float dl = 0.f;
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int j = jt * 16 + 4 * g + e;
+                    const float sc = v4_score(A, bst[jt][it][e], r, h, i, j, s[jt][it][e]);
+                    const float p = (sc == -INFINITY) ? 0.f : __expf(sc - lse_i[it]);
+                    const float m = drop_scale(A, drk, i, j);
+                    keep |= (m != 0.f ? 1u : 0u) << ((jt * TT + it) * 4 + e);
+                    s[jt][it][e] = p;
+                    dp[jt][it][e] *= m;
+                    dl = fmaf(p, dp[jt][it][e], dl);
+                }
+            dl += __shfl_xor(dl, 16, WAVE);
+            dl += __shfl_xor(dl, 32, WAVE);
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int j = jt * 16 + 4 * g + e;
+                    const float p = s[jt][it][e];
+                    const float dsv = p * (dp[jt][it][e] - dl);
+                    dp[jt][it][e] = dsv;
+                    s[jt][it][e] = ((keep >> ((jt * TT + it) * 4 + e)) & 1u) ? p * msc : 0.f;
+                    if (A.dbias_dense && i < T && j < T)
+                        A.dbias_dense[((r * A.heads + h) * T + i) * (int64_t)T + j] = dsv;
+                }
+        }
+        if (A.part) {
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int it = 0; it < TT; ++it) gsum[jt][it] += dp[jt][it];
+        }
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g + e) * LD + it * 16 + c] = dp[jt][it][e];
+        // dQᵀ = Kᵀ·dSᵀ: A = K[16jt + 4g + e][16dt + c] (four b32 reads), B = the dSᵀ accumulators
+        f4v aq[DT][TT];
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it) aq[dt][it] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float ka = sk[(jt * 16 + 4 * g + e) * SP + dt * 16 + c];
+#pragma unroll
+                    for (int it = 0; it < TT; ++it) aq[dt][it] = mfma4(ka, dp[jt][it][e], aq[dt][it]);
+                }
+        wave_sync();   // X (dSᵀ) written by the whole wave
+        // dKᵀ = Qᵀ·dS (B = X), then dVᵀ = dOᵀ·P' (B = X after P'ᵀ replaces dSᵀ).  Each output is parked in this
+        // head's slab columns as soon as its source columns are dead for this wave (only wave w reads head w's
+        // columns): dK over K (K last read by dQ), then dQ over Q (Q last read by dK), dV over V (V last read by dP).
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+            if (pass == 1) {
+                wave_sync();   // dK's reads of X are done
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int it = 0; it < TT; ++it)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g + e) * LD + it * 16 + c] = s[jt][it][e];
+                wave_sync();
+            }
+            const float* At = pass == 0 ? sq : so;
+            f4v acc[DT][TT];
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt) acc[dt][jt] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int it = 0; it < TT; ++it) {
+                f4v xb[TT];
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt) xb[jt] = lds4(X + (jt * 16 + c) * LD + it * 16 + 4 * g);
+#pragma unroll
+                for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float xa = At[(it * 16 + 4 * g + e) * SP + dt * 16 + c];
+#pragma unroll
+                        for (int jt = 0; jt < TT; ++jt) acc[dt][jt] = mfma4(xa, xb[jt][e], acc[dt][jt]);
+                    }
+            }
+            const float sc = pass == 0 ? A.inv_sqrt_d : 1.f;
+            float* dst = slab + (pass == 0 ? GH * DP : 2 * GH * DP) + w * DP;   // dK over K, dV over V
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int dt = 0; dt < DT; ++dt) {
+                    const f4v vv = acc[dt][t] * sc;
+                    *(f4v*)(dst + (t * 16 + c) * SP + dt * 16 + 4 * g) = vv;
+                    if (A.qkv_part) bsum[1 + pass][dt] += vv;   // padded steps add exact zeros
+                }
+            if (pass == 0) {   // Q is dead for this wave: dQ over Q
+#pragma unroll
+                for (int t = 0; t < TT; ++t)
+#pragma unroll
+                    for (int dt = 0; dt < DT; ++dt) {
+                        const f4v vq = aq[dt][t] * A.inv_sqrt_d;
+                        *(f4v*)(slab + (t * 16 + c) * SP + w * DP + dt * 16 + 4 * g) = vq;
+                        if (A.qkv_part) bsum[0][dt] += vq;
+                    }
+            }
+        }
+        __syncthreads();   // every head's dQ | dK | dV is parked
+        // dQ | dK | dV of the group's heads as flat float4 runs (the layout of Q | K | V)
+        constexpr int OC4 = 3 * GH * DP / 4;
+        for (int e = threadIdx.x; e < T * OC4; e += WAVE * GH) {
+            const int t = e / OC4, col = 4 * (e % OC4);
+            const int x = col / (GH * DP), cc = col % (GH * DP);
+            float* dst = x == 0 ? A.dq : x == 1 ? A.dk : A.dv;
+            st4v<S>(dst, r * A.d_row + (int64_t)t * A.d_t + hg * GH * DP + cc, lds4(slab + t * SP + col), 1.f);
+        }
+    }
+    if (A.qkv_part) {
+        float* prow = A.qkv_part + rg * 3 * (int64_t)A.H + (int64_t)h * d;
+#pragma unroll
+        for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float v = bsum[t3][dt][e];
+                    v += __shfl_xor(v, 1, WAVE);
+                    v += __shfl_xor(v, 2, WAVE);
+                    v += __shfl_xor(v, 4, WAVE);
+                    v += __shfl_xor(v, 8, WAVE);
+                    if (c0 == 0) prow[t3 * (int64_t)A.H + dt * 16 + 4 * g0 + e] = v;
+                }
+    }
+    if (A.part) {
+        wave_sync();   // the last unit's reads of X are done
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g0 + e) * LD + it * 16 + c0] = gsum[jt][it][e];
+        wave_sync();
+        float* prow = A.part + rg * A.heads * NB + (int64_t)h * NB;
+        for (int t = lane; t < NB; t += WAVE) {
+            const int off = t - (T - 1);
+            const int j0 = off < 0 ? -off : 0, j1 = off < 0 ? T : T - off;
+            float a = 0.f;
+            for (int j = j0; j < j1; ++j) a += X[j * LD + j + off];
+            prow[t] = a;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------
 // v5 (T in (16, 128], d in {16, 32}: C3's T = 64, C5's T = 128): one WORKGROUP of TT waves per (node row, head)
 // unit, TP = 16·TT >= T steps (TT in {2, 4, 8}).  Wave w owns query tile w (steps 16w .. 16w+15) in the score,
 // softmax and dQ products and key tile w in the dK / dV products, so no wave holds more than one 16-step
@@ -1808,6 +2242,25 @@ bool v5_ok(int T, int d) {
     return m > 0 && v5_tiles(T) != 0 && (d == 16 || d == 32) && (T > 32 || (m == 2 && v4_enabled()));
 }
 
+// v6 (head-group slabs) for the v4 range; TAGAN_TATTN_V6=0 keeps v4, TAGAN_V6_GH=2|4 forces the group width
+int v6_group(int T, int heads, int d) {
+    const char* e = getenv("TAGAN_TATTN_V6");
+    if (e && e[0] == '0') return 0;
+    if (!v4_ok(T, d)) return 0;
+    const char* f = getenv("TAGAN_V6_GH");
+    const int want = f ? atoi(f) : 4;
+    if (want >= 8 && heads % 8 == 0) return 8;
+    if (want >= 4 && heads % 4 == 0) return 4;
+    return (want >= 2 && heads % 2 == 0) ? 2 : 0;
+}
+// the v6 backward only where it measured faster than v4: head_dim 32 (C4: 12.0 vs 15.9 ms) or T <= 16; at
+// T in (16, 32] with head_dim 16 (C2) its 168+ VGPRs cost a wave per SIMD against v4 (0.43 vs 0.36 ms)
+bool v6_bwd_ok(int T, int d) {
+    const char* e = getenv("TAGAN_TATTN_V6");
+    if (e && e[0] == '2') return true;   // force (A/B runs, parity tests)
+    return d == 32 || v4_tiles(T) == 1;
+}
+
 // > 64 KB of dynamic LDS needs the per-kernel opt-in (once per instantiation)
 template <typename K>
 int lds_optin(K* kern, size_t bytes) {
@@ -1916,6 +2369,21 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     TAGAN_REQUIRE(!bf || (al4 && !attn && (v3_ok(T, head_dim) || v4_ok(T, head_dim) || v5_ok(T, head_dim))),
                   TAGAN_ERR_UNSUPPORTED,
                   "temporal_attn_fwd: bf16 storage needs the v3 kernels (T <= 128, head_dim 8..64, no attn output)");
+    if (al4 && !attn && v6_group(T, heads, head_dim)) {
+        const int TT = v4_tiles(T), GH = v6_group(T, heads, head_dim);
+        const dim3 g6((unsigned)(v4_groups(rows) * (heads / GH)));
+        const size_t lds = v6_fwd_lds(TT, head_dim / 16, GH);
+#define TAGAN_V6F(TTT, DDT, GGH) { auto kern = bf ? k_tattn_fwd_v6<TTT, DDT, GGH, bf16s> : k_tattn_fwd_v6<TTT, DDT, GGH, float>; \
+                                   rc = lds_optin(kern, lds); if (rc) return rc; kern<<<g6, WAVE * GGH, lds, s>>>(A, qf, kf, vf); }
+#define TAGAN_V6F_G(TTT, DDT) if (GH == 8) TAGAN_V6F(TTT, DDT, 8) else if (GH == 4) TAGAN_V6F(TTT, DDT, 4) else TAGAN_V6F(TTT, DDT, 2)
+#define TAGAN_V6F_D(TTT) if (head_dim == 16) { TAGAN_V6F_G(TTT, 1) } else { TAGAN_V6F_G(TTT, 2) }
+        if (TT == 1) { TAGAN_V6F_D(1) } else { TAGAN_V6F_D(2) }
+#undef TAGAN_V6F_D
+#undef TAGAN_V6F_G
+#undef TAGAN_V6F
+        TAGAN_CHECK_LAUNCH("temporal_attn_fwd_v6");
+        return TAGAN_OK;
+    }
     if (al4 && !attn && v5_ok(T, head_dim)) {
         const int TT = v5_tiles(T);
         const dim3 g5((unsigned)(v4_groups(rows) * heads));
@@ -2044,6 +2512,33 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
     TAGAN_REQUIRE(!bf || (al4 && (v3_ok(T, head_dim) || v4_ok(T, head_dim) || v5_ok(T, head_dim))),
                   TAGAN_ERR_UNSUPPORTED,
                   "temporal_attn_bwd: bf16 storage needs the v3 kernels (T <= 128, head_dim 8..64)");
+    if (al4 && v6_group(T, heads, head_dim) && v6_bwd_ok(T, head_dim)) {
+        // grid = G6 partial rows x head groups; workgroup b keeps head group b % (heads / GH)
+        const int TT = v4_tiles(T), GH = v6_group(T, heads, head_dim);
+        const int64_t G6 = v4_groups(rows);   // <= nblk: the workspace rows
+        const dim3 g6((unsigned)(G6 * (heads / GH)));
+        const size_t lds = v6_bwd_lds(TT, head_dim / 16, GH);
+#define TAGAN_V6B(TTT, DDT, GGH) { auto kern = bf ? k_tattn_bwd_v6<TTT, DDT, GGH, bf16s> : k_tattn_bwd_v6<TTT, DDT, GGH, float>; \
+                                   rc = lds_optin(kern, lds); if (rc) return rc; kern<<<g6, WAVE * GGH, lds, s>>>(A, qf, kf, vf, df, lse); }
+#define TAGAN_V6B_G(TTT, DDT) if (GH == 8) TAGAN_V6B(TTT, DDT, 8) else if (GH == 4) TAGAN_V6B(TTT, DDT, 4) else TAGAN_V6B(TTT, DDT, 2)
+#define TAGAN_V6B_D(TTT) if (head_dim == 16) { TAGAN_V6B_G(TTT, 1) } else { TAGAN_V6B_G(TTT, 2) }
+        if (TT == 1) { TAGAN_V6B_D(1) } else { TAGAN_V6B_D(2) }
+#undef TAGAN_V6B_D
+#undef TAGAN_V6B_G
+#undef TAGAN_V6B
+        TAGAN_CHECK_LAUNCH("temporal_attn_bwd_v6");
+        if (dbias_table) {
+            const int n = heads * (2 * T - 1);
+            launch_colsum(A.part, (int)G6, n, dbias_table, nullptr, n, s);
+            TAGAN_CHECK_LAUNCH("temporal_attn_bwd_sum");
+        }
+        if (dsum_qkv) {
+            const int n = 3 * heads * head_dim;
+            launch_colsum(A.qkv_part, (int)G6, n, dsum_qkv, nullptr, n, s);
+            TAGAN_CHECK_LAUNCH("temporal_attn_bwd_qkv_sum");
+        }
+        return TAGAN_OK;
+    }
     if (al4 && v5_ok(T, head_dim)) {
         // grid = G5 partial rows x heads; each workgroup keeps one head (v4_wave_map)
         const int TT = v5_tiles(T);
