@@ -1590,8 +1590,16 @@ __global__ void __launch_bounds__(WAVE * GH, (TT == 2 && DT == 2) ? 2 : TAGAN_V6
     const int hgc = A.heads / GH, hg = blockIdx.x % hgc, h = hg * GH + w;
     const int64_t rg = blockIdx.x / hgc, G = gridDim.x / hgc;
     float* X = sm + TP * SP + w * TP * LD;   // this wave's [TP][LD] transpose tile (dS, then P')
-    float bst[TT][TT][4];
-    v4_static_bias<TT>(A, h, c0, g0, bst);
+    // static score part: registers at TT = 1; at TT = 2 the head's bias-table row lives in the unused padding
+    // columns TP..TP+7 of this wave's X tile (row t/8, column TP + t%8; 2T-1 <= 63 entries), which keeps the
+    // kernel inside 168 VGPRs (3 waves/SIMD) -- with 54 KB of LDS per 4-wave workgroup, 3 fit per CU
+    constexpr bool BREG = TT == 1;
+    float bst[BREG ? TT : 1][BREG ? TT : 1][4];
+    if constexpr (BREG) {
+        v4_static_bias<TT>(A, h, c0, g0, bst);
+    } else {
+        for (int t = lane; t < NB; t += WAVE) X[(t >> 3) * LD + TP + (t & 7)] = A.bias_table ? A.bias_table[h * NB + t] : 0.f;
+    }
     const float msc = A.p_drop > 0.f ? A.inv_keep : 1.f;
     f4v gsum[TT][TT];
 #pragma unroll
@@ -1682,7 +1690,14 @@ __global__ void __launch_bounds__(WAVE * GH, (TT == 2 && DT == 2) ? 2 : TAGAN_V6
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int j = jt * 16 + 4 * g + e;
-                    const float sc = v4_score(A, bst[jt][it][e], r, h, i, j, s[jt][it][e]);
+                    float b0;
+                    if constexpr (BREG) {
+                        b0 = bst[jt][it][e];
+                    } else {
+                        const int tb = i - j + T - 1;
+                        b0 = (i < T && j < T && !(A.causal && j > i)) ? X[(tb >> 3) * LD + TP + (tb & 7)] : -INFINITY;
+                    }
+                    const float sc = v4_score(A, b0, r, h, i, j, s[jt][it][e]);
                     const float p = (sc == -INFINITY) ? 0.f : __expf(sc - lse_i[it]);
                     const float m = drop_scale(A, drk, i, j);
                     keep |= (m != 0.f ? 1u : 0u) << ((jt * TT + it) * 4 + e);
