@@ -327,12 +327,76 @@ def proj_ln_bwd(da, w, x2, mean, rstd, gamma, dres):
                               ptr(dgb[0]), ptr(dgb[1]), ptr(ws), wsb, stream_of(da)), "tagan_proj_ln_bwd")
     return dx, dgb[0], dgb[1]
 
+# TAGAN_WGRAD_ASYNC=1: the block's weight-gradient GEMMs (dW_out, dW_qkv and the QKV bias column) run on a side
+# stream, overlapping the rest of the backward (the next layer's HBM-bound edge / LayerNorm kernels); nothing in
+# the backward reads them, so they are handed to the parameters by an end-of-backward callback after the main
+# stream has joined the side stream (HIP-graph capturable: fork / join through stream waits).  Measured at C2
+# (profiles/r2_wgrad_async_ab.txt): 8.56-8.61 ms against 8.19-8.22 ms synchronous -- the hipBLASLt GEMMs and the
+# edge / LayerNorm kernels slow each other down more than they overlap, so the default stays synchronous.
+WGRAD_ASYNC = os.environ.get("TAGAN_WGRAD_ASYNC", "0") == "1"
+_SIDE = {}
+
+
+def _side_stream(dev):
+    st = _SIDE.get(dev.index)
+    if st is None:
+        st = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
+    return st
+
+
+class WGradSink:
+    """Parameters of one attention block whose weight gradients may arrive asynchronously (TAGAN_WGRAD_ASYNC)."""
+
+    def __init__(self, q_lin, k_lin, v_lin, out_lin):
+        self.qkv = (q_lin, k_lin, v_lin)
+        self.out = out_lin
+
+
+def _give(p, g):
+    if p.grad is None:
+        p.grad = g
+    else:
+        p.grad.add_(g)
+
+
+class _AsyncWGrad:
+    """Side-stream weight gradients of one backward call, joined and assigned at the end of the backward."""
+
+    def __init__(self, sink, dev):
+        self.sink, self.main, self.side = sink, torch.cuda.current_stream(dev), _side_stream(dev)
+        self.keep, self.dw_o, self.dw_qkv, self.db_qkv = [], None, None, None
+        torch.autograd.Variable._execution_engine.queue_callback(self.finish)
+
+    def run(self, fn, *inputs):
+        self.side.wait_stream(self.main)   # the inputs are complete on the main stream
+        self.keep.extend(inputs)           # alive until the main stream has joined the side stream
+        with torch.cuda.stream(self.side):
+            return fn(*inputs)
+
+    def finish(self):
+        self.main.wait_stream(self.side)
+        with torch.cuda.stream(self.main):
+            H = self.sink.out.weight.shape[1]
+            if self.dw_o is not None:
+                _give(self.sink.out.weight, self.dw_o)
+            for i, lin in enumerate(self.sink.qkv):
+                if self.dw_qkv is not None:
+                    _give(lin.weight, self.dw_qkv[i * H:(i + 1) * H])
+                if self.db_qkv is not None:
+                    _give(lin.bias, self.db_qkv[i * H:(i + 1) * H])
+        if not torch.cuda.is_current_stream_capturing():
+            for t in (self.dw_o, self.dw_qkv, self.db_qkv):
+                if t is not None:
+                    t.record_stream(self.main)   # allocated on the side stream, read on the main one
+        self.keep.clear()
+
+
 class AttnBlockFn(torch.autograd.Function):
     """y = LN2(dropout(out_proj(core(QKV(LN1(x))))) + x) with LayerNorm on both sides (use_layer_norm=True)."""
 
     @staticmethod
     def forward(ctx, x, p1, p2, ln1_w, ln1_b, w_qkv, b_qkv, w_o, b_o, ln2_w, ln2_b, core, eps1: float,
-                eps2: float, p_out: float, seed_out: int, lns_w=None, lns_b=None, eps_s: float = 1e-5):
+                eps2: float, p_out: float, seed_out: int, lns_w=None, lns_b=None, eps_s: float = 1e-5, sink=None):
         require_hip(x)
         H = x.shape[-1]
         x2 = x.reshape(-1, H).contiguous()
@@ -368,6 +432,7 @@ class AttnBlockFn(torch.autograd.Function):
             ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
             ctx.inter = (h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
             ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, proj)
+            ctx.sink = sink
             return y.view(x.shape)
         if OUT_BIAS_LN:   # out-projection bias added in the closing LayerNorm (no GEMM epilogue)
             o, b_o_ln = _mm(cg, w_o.t(), bf), b_o
@@ -382,6 +447,7 @@ class AttnBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
         ctx.inter = (h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
         ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, False)
+        ctx.sink = sink
         return y.view(x.shape)
 
     @staticmethod
@@ -391,17 +457,36 @@ class AttnBlockFn(torch.autograd.Function):
         core, p_out, seed_out, shape, bf, act, proj = ctx.cfg
         ng = ctx.needs_input_grad
         dy2 = dy.reshape(-1, shape[-1]).contiguous()
+        # weight gradients on the side stream: only for the default fp32 QKV_AUG form (bias from the ones column)
+        aw = (_AsyncWGrad(ctx.sink, dy.device) if (WGRAD_ASYNC and ctx.sink is not None and dy.is_cuda and not bf
+                                                    and not proj and h_aug is not None and WGRAD_BIAS_AUG
+                                                    and ng[5] and ng[6] and ng[7]) else None)
         dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True,
                                          da_dtype=torch.bfloat16 if bf else torch.float32)
         dgs = dbs = None
         if skip is not None:       # skip branch: LN_s backward with the residual gradient added in-kernel
             dres, _, dgs, dbs, _ = ln_bwd(x2, skip[0], skip[1], lns_w, dy2, dres, 0.0, 0, True, False, False)
         dc = proj_mm(do, w_o.contiguous(), True) if (proj and "dc" in PROJ_SET) else _mm(do, w_o, bf, out_bf16=act)
-        dw_o = _wgrad(do, cg, bf) if ng[7] else None
+        if aw is not None:
+            aw.dw_o = aw.run(lambda a, b: _wgrad(a, b, bf), do, cg)
+            dw_o = None
+        else:
+            dw_o = _wgrad(do, cg, bf) if ng[7] else None
         dqkv, dp1, dp2, db_core = core.bwd(qkv, c, saved, dc, ng[1], ng[2], want_bias_sum=bool(ng[6]))
         del dc, do
         H = shape[-1]
-        if db_core is None and ng[5] and ng[6] and h_aug is not None and WGRAD_BIAS_AUG:
+        if aw is not None:
+            if db_core is None:
+                def qkv_aug(a, b):
+                    dw = _wgrad(a, b, bf, WGRAD_ROWS_QKV)
+                    return dw[:, :H].contiguous(), dw[:, H].contiguous()
+                aw.dw_qkv, aw.db_qkv = aw.run(qkv_aug, dqkv, h_aug)
+                db_qkv = None
+            else:
+                aw.dw_qkv = aw.run(lambda a, b: _wgrad(a, b, bf, WGRAD_ROWS_QKV), dqkv, h)
+                db_qkv = db_core
+            dw_qkv = None
+        elif db_core is None and ng[5] and ng[6] and h_aug is not None and WGRAD_BIAS_AUG:
             # dqkvᵀ·[h | 1 0 0 0]: column H of the product is the column sum of dqkv (the bias gradient)
             # -- 4 more GEMM columns instead of a 491 MB column-sum pass at C2
             dw_aug = _wgrad(dqkv, h_aug, bf, WGRAD_ROWS_QKV)
@@ -415,17 +500,17 @@ class AttnBlockFn(torch.autograd.Function):
             dx, dg1, db1 = proj_ln_bwd(dqkv, w_qkv, x2, mean1, rstd1, ln1_w, dres)
             ctx.inter = None
             return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
-                    None, None, None, None, None, dgs, dbs, None)
+                    None, None, None, None, None, dgs, dbs, None, None)
         if bf:
             dqkv = _b(dqkv)
         dh = _mm(dqkv, w_qkv, bf)
-        if dw_qkv is None and ng[5]:
+        if dw_qkv is None and ng[5] and aw is None:
             dw_qkv = _wgrad(dqkv, h, bf, WGRAD_ROWS_QKV)
         del dqkv
         dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
         ctx.inter = None
         return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
-                None, None, None, None, None, dgs, dbs, None)
+                None, None, None, None, None, dgs, dbs, None, None)
 
 
 def attention_block(x, core, p1: Optional[torch.Tensor], p2: Optional[torch.Tensor], ln1, q_lin, k_lin, v_lin,
@@ -434,12 +519,14 @@ def attention_block(x, core, p1: Optional[torch.Tensor], p2: Optional[torch.Tens
     (TAGAN's first geometric layer, model.py:258-262), fused into the closing LayerNorm."""
     w_qkv = torch.cat([q_lin.weight, k_lin.weight, v_lin.weight], 0)
     b_qkv = torch.cat([q_lin.bias, k_lin.bias, v_lin.bias], 0)
+    sink = WGradSink(q_lin, k_lin, v_lin, out_lin) if WGRAD_ASYNC else None
     if skip_ln is not None:
         return AttnBlockFn.apply(x, p1, p2, ln1.weight, ln1.bias, w_qkv, b_qkv, out_lin.weight, out_lin.bias,
                                  ln2.weight, ln2.bias, core, ln1.eps, ln2.eps, float(p_out), seed_out,
-                                 skip_ln.weight, skip_ln.bias, skip_ln.eps)
+                                 skip_ln.weight, skip_ln.bias, skip_ln.eps, sink)
     return AttnBlockFn.apply(x, p1, p2, ln1.weight, ln1.bias, w_qkv, b_qkv, out_lin.weight, out_lin.bias,
-                             ln2.weight, ln2.bias, core, ln1.eps, ln2.eps, float(p_out), seed_out)
+                             ln2.weight, ln2.bias, core, ln1.eps, ln2.eps, float(p_out), seed_out,
+                             None, None, 1e-5, sink)
 
 
 def fusable(x: torch.Tensor, use_layer_norm: bool) -> bool:
