@@ -134,9 +134,19 @@ def window_aggregate(x: torch.Tensor, w: int, aggregation: str) -> torch.Tensor:
     """TemporalSkipConnection's windowed aggregation (mean over the in-range steps / max / sum) of x [T, N, H]."""
     if w <= 0:
         return x
-    if x.shape[-1] % 4 != 0 or x.dtype != torch.float32:
-        raise ValueError(f"window aggregation kernel takes fp32 with H % 4 == 0, got {x.dtype} H={x.shape[-1]}")
-    return WindowFn.apply(x, int(w), _AGG_MODE.get(aggregation, 2))
+    if x.shape[-1] % 4 == 0 and x.dtype == torch.float32:
+        return WindowFn.apply(x, int(w), _AGG_MODE.get(aggregation, 2))
+    # widths the kernel's float4 lanes do not take: the same windows as device pooling along T
+    T, N, Hd = x.shape
+    seq = x.permute(1, 2, 0).reshape(N * Hd, 1, T)
+    k = 2 * w + 1
+    if aggregation == "mean":
+        agg = torch.nn.functional.avg_pool1d(seq, k, 1, w, count_include_pad=False)
+    elif aggregation == "max":
+        agg = torch.nn.functional.max_pool1d(seq, k, 1, w)
+    else:
+        agg = torch.nn.functional.avg_pool1d(seq, k, 1, w, count_include_pad=True) * k
+    return agg.reshape(N, Hd, T).permute(2, 0, 1)
 
 
 class TemporalGRUCell(nn.Module):

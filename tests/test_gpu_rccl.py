@@ -72,3 +72,64 @@ def test_rccl_world1_shard_and_buckets():
                 assert p.grad is None, k
     finally:
         dist.destroy_process_group()
+
+
+def test_rccl_world1_graph_split_step():
+    """bench.py's N > 1 launch form at world size 1: forward + backward captured as one HIP graph, the RCCL
+    gradient all-reduce (static bucket, forced) run eagerly between the two replays, clip + Adam captured as the
+    second graph -- the same loss trajectory and weights as the eager step (dropout off)."""
+    import tempfile
+    import tagan_amd  # noqa: F401
+    from tagan_amd import TAGAN, synthetic
+    from tagan_amd.distributed import GradBucket
+    from tagan_amd.graph_step import GraphedStep
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    store = os.path.join(tempfile.mkdtemp(prefix="tagan_rccl_g_"), "store")
+    dist.init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1)
+    try:
+        cfg = synthetic.config_for("c2", dropout=0.0)
+        seq = synthetic.make_sequence("c2", dev, seed=7, snapshots=6, nodes=400, edges=3000)
+        labels = torch.tensor([1.0], device=dev)
+
+        def setup():
+            torch.manual_seed(3)
+            m = TAGAN(cfg).to(dev).train()
+            o = torch.optim.Adam(m.parameters(), lr=1e-3, capturable=True)
+            return m, o, GradBucket(m.parameters())
+
+        m1, o1, b1 = setup()
+        eager = []
+        for _ in range(6):
+            o1.zero_grad(set_to_none=True)
+            out = m1(seq, labels=labels)
+            out["loss"].backward()
+            b1.allreduce_mean(force=True)
+            torch.nn.utils.clip_grad_norm_(m1.parameters(), 1.0)
+            o1.step()
+            eager.append(float(out["loss"]))
+
+        m2, o2, b2 = setup()
+
+        def fb():
+            out = m2(seq, labels=labels)
+            out["loss"].backward()
+            return out["loss"]
+
+        def post():
+            torch.nn.utils.clip_grad_norm_(m2.parameters(), 1.0)
+            o2.step()
+
+        g = GraphedStep(m2, fb, optimizer=o2, warmup=3, between=lambda: b2.allreduce_mean(force=True, static=True),
+                        post=post)
+        try:
+            graphed = [float(g()) for _ in range(3)]
+        finally:
+            g.close()
+        torch.cuda.synchronize()
+        for a, b in zip(eager[3:], graphed):
+            assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (eager, graphed)
+        for (k, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+            torch.testing.assert_close(p2, p1, atol=1e-5, rtol=1e-4, msg=k)
+    finally:
+        dist.destroy_process_group()

@@ -26,7 +26,8 @@ def _ref(x, w, agg):
 
 
 @pytest.mark.parametrize("agg", ["mean", "max", "sum"])
-@pytest.mark.parametrize("T,N,H,w", [(16, 300, 64, 3), (5, 17, 12, 8), (1, 9, 4, 2), (40, 1000, 128, 1)])
+@pytest.mark.parametrize("T,N,H,w", [(16, 300, 64, 3), (5, 17, 12, 8), (1, 9, 4, 2), (40, 1000, 128, 1),
+                                     (7, 33, 10, 2)])    # H % 4 != 0: the device pooling form
 def test_window_vs_reference_loop(dev, agg, T, N, H, w):
     from tagan_amd.layers.temporal_propagation import window_aggregate
     g = torch.Generator().manual_seed(T * 7 + w)
