@@ -11,7 +11,9 @@
 //   h_t = LN_out(u)                                     (LayerNorm eps as passed; use_layer_norm only)
 // A workgroup owns R = 8·(256/hc) rows for all T steps: thread j <-> hidden unit j of its row group, the row
 // states live in LDS between steps, row statistics are shuffle (+ LDS for hc > 64) reductions, the
-// recurrent products are VALU dot products against W rows (fwd) / columns (bwd) streamed from L1/L2.
+// recurrent products are VALU dot products with the weights streamed from L1/L2 as coalesced runs: the forward
+// takes them k-major (Wᵀ: at fixed k the threads j read consecutive words), the backward in nn.Linear layout
+// (its transposed product reads columns, consecutive words again); row states are float4 LDS broadcasts.
 // Saved for the backward: hn, r⊙hn, r, z, h~, u [T, N, hc] and the two LayerNorms' (mean, rstd) [T, N].
 // Backward walks t = T-1..0 with dL/dh_t carried in LDS and writes dgx [T, N, 3hc] (the gate pre-activation
 // gradients; the caller turns them into the W_h gradients with one GEMM each against the saved hn / r⊙hn)
@@ -29,8 +31,8 @@ struct GruArgs {
     int64_t N;
     int T, hc;
     const float* gx;                  // [T, N, 3hc]
-    const float* Wrz;                 // [2hc, hc]  (W_r | W_z, the h-side columns)
-    const float* Wc;                  // [hc, hc]
+    const float* Wrz;                 // fwd: [hc, 2hc] k-major (W_r | W_z)ᵀ; bwd: [2hc, hc] (nn.Linear layout)
+    const float* Wc;                  // fwd: [hc, hc] k-major W_cᵀ; bwd: [hc, hc]
     const float* gh; const float* bh; float eps_h;     // LN_h (null: no LayerNorm)
     const float* go; const float* bo; float eps_o;     // LN_out (null: no LayerNorm)
     const float* tscale;              // [T, N] exp(-clamp(Δt)) factors or null
@@ -132,17 +134,21 @@ __global__ void __launch_bounds__(GB) k_gru_fwd(GruArgs A) {
             az[i] = gp[HC + j];
         }
         if (t > 0) {
-            const float* wr = A.Wrz + (int64_t)j * HC;
-            const float* wz = A.Wrz + (int64_t)(HC + j) * HC;
+            // k-major weights: at fixed k the HC threads read one contiguous run (coalesced), the row states come
+            // from LDS as float4 broadcasts
 #pragma unroll 2
             for (int k = 0; k < HC; k += 4) {
-                const float4 a = *reinterpret_cast<const float4*>(wr + k);
-                const float4 b = *reinterpret_cast<const float4*>(wz + k);
+                float a[4], b[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    a[q] = A.Wrz[(int64_t)(k + q) * 2 * HC + j];
+                    b[q] = A.Wrz[(int64_t)(k + q) * 2 * HC + HC + j];
+                }
 #pragma unroll
                 for (int i = 0; i < RPG; ++i) {
                     const float4 h = *reinterpret_cast<const float4*>(hs + (g * RPG + i) * HC + k);
-                    ar[i] += (a.x * h.x + a.y * h.y) + (a.z * h.z + a.w * h.w);
-                    az[i] += (b.x * h.x + b.y * h.y) + (b.z * h.z + b.w * h.w);
+                    ar[i] += (a[0] * h.x + a[1] * h.y) + (a[2] * h.z + a[3] * h.w);
+                    az[i] += (b[0] * h.x + b[1] * h.y) + (b[2] * h.z + b[3] * h.w);
                 }
             }
         }
@@ -161,14 +167,15 @@ __global__ void __launch_bounds__(GB) k_gru_fwd(GruArgs A) {
             ac[i] = A.gx[((int64_t)t * N + rc) * 3 * HC + 2 * HC + j];
         }
         if (t > 0) {
-            const float* wc = A.Wc + (int64_t)j * HC;
 #pragma unroll 2
             for (int k = 0; k < HC; k += 4) {
-                const float4 a = *reinterpret_cast<const float4*>(wc + k);
+                float a[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] = A.Wc[(int64_t)(k + q) * HC + j];
 #pragma unroll
                 for (int i = 0; i < RPG; ++i) {
                     const float4 h = *reinterpret_cast<const float4*>(rh + (g * RPG + i) * HC + k);
-                    ac[i] += (a.x * h.x + a.y * h.y) + (a.z * h.z + a.w * h.w);
+                    ac[i] += (a[0] * h.x + a[1] * h.y) + (a[2] * h.z + a[3] * h.w);
                 }
             }
         }
@@ -296,11 +303,16 @@ __global__ void __launch_bounds__(GB) k_gru_bwd(GruArgs A) {
             float drh[RPB];
 #pragma unroll
             for (int i = 0; i < RPB; ++i) drh[i] = 0.f;
-#pragma unroll 4
-        for (int jj = 0; jj < HC; ++jj) {
-                const float w = A.Wc[(int64_t)jj * HC + j];
+#pragma unroll 2
+            for (int jj = 0; jj < HC; jj += 4) {
+                float w[4];
 #pragma unroll
-                for (int i = 0; i < RPB; ++i) drh[i] += w * da[(g * RPB + i) * HC + jj];
+                for (int q = 0; q < 4; ++q) w[q] = A.Wc[(int64_t)(jj + q) * HC + j];
+#pragma unroll
+                for (int i = 0; i < RPB; ++i) {
+                    const float4 d = *reinterpret_cast<const float4*>(da + (g * RPB + i) * HC + jj);
+                    drh[i] += (w[0] * d.x + w[1] * d.y) + (w[2] * d.z + w[3] * d.w);
+                }
             }
 #pragma unroll
             for (int i = 0; i < RPB; ++i) {
@@ -333,13 +345,21 @@ __global__ void __launch_bounds__(GB) k_gru_bwd(GruArgs A) {
         }
         __syncthreads();
         // dhn[k = j] += Σ_jj W_r[jj][j] dar[jj] + W_z[jj][j] daz[jj]
-#pragma unroll 4
-        for (int jj = 0; jj < HC; ++jj) {
-            const float wr = A.Wrz[(int64_t)jj * HC + j];
-            const float wz = A.Wrz[(int64_t)(HC + jj) * HC + j];
+#pragma unroll 2
+        for (int jj = 0; jj < HC; jj += 4) {
+            float wr[4], wz[4];
 #pragma unroll
-            for (int i = 0; i < RPB; ++i)
-                dhn[i] += wr * da[(g * RPB + i) * HC + jj] + wz * db[(g * RPB + i) * HC + jj];
+            for (int q = 0; q < 4; ++q) {
+                wr[q] = A.Wrz[(int64_t)(jj + q) * HC + j];
+                wz[q] = A.Wrz[(int64_t)(HC + jj + q) * HC + j];
+            }
+#pragma unroll
+            for (int i = 0; i < RPB; ++i) {
+                const float4 d1 = *reinterpret_cast<const float4*>(da + (g * RPB + i) * HC + jj);
+                const float4 d2 = *reinterpret_cast<const float4*>(db + (g * RPB + i) * HC + jj);
+                dhn[i] += (wr[0] * d1.x + wr[1] * d1.y) + (wr[2] * d1.z + wr[3] * d1.w) +
+                          (wz[0] * d2.x + wz[1] * d2.y) + (wz[2] * d2.z + wz[3] * d2.w);
+            }
         }
         // hn = LN_h(h_{t-1}) · scale  ->  carry = dL/dh_{t-1}
         float gp2[RPB], xh2[RPB], e1[RPB], e2[RPB], rsh[RPB];

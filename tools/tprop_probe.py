@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--bidirectional", type=int, default=0)
+    ap.add_argument("--only", default="", help="gru_kernel | python_steps: time one mode (profiling)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     N, _E, T, H = synthetic.CONFIGS[a.config][:4]
@@ -35,6 +36,8 @@ def main():
     dy = torch.randn(T, N, H, device=dev, generator=g)
     res = {"config": a.config, "rows": N, "T": T, "H": H, "bidirectional": bool(a.bidirectional)}
     for name, kern in (("gru_kernel", True), ("python_steps", False)):
+        if a.only and name != a.only:
+            continue
         tp.USE_GRU_KERNEL = kern
         for _ in range(2):
             mod.zero_grad(set_to_none=True)
