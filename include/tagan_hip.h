@@ -343,9 +343,8 @@ int tagan_head_bwd(int32_t B, int32_t T, int32_t H, int32_t C, const float* x0, 
  * GRU recurrence of TemporalEvolutionLayer over T (csrc/gru.hip; TemporalPropagation's intended compute,
  * temporal_propagation.py:402-558 inside :648-755), one launch per direction over all T steps.
  * gx [T, N, 3hc] = the x-side of the reset | update | candidate gates (LN_x(x)·W_xᵀ + b, one GEMM by the
- * caller); Wrz = the h-side columns of W_reset | W_update, Wc = the h-side columns of W_candidate: the FORWARD
- * takes them k-major (Wrz [hc, 2hc] = (W_r | W_z)ᵀ, Wc [hc, hc] = W_cᵀ: coalesced reads at fixed k), the
- * BACKWARD in nn.Linear layout (Wrz [2hc, hc], Wc [hc, hc]).  Per step: hn = LN_h(h_{t-1})·tscale[t] (h_{-1} = 0, no LayerNorm),
+ * caller); Wrz [2hc, hc] = the h-side columns of W_reset | W_update; Wc [hc, hc] = the h-side columns of
+ * W_candidate (nn.Linear layout).  Per step: hn = LN_h(h_{t-1})·tscale[t] (h_{-1} = 0, no LayerNorm),
  * r, z = σ(gx + W·hn), h~ = tanh(gx_c + Wc·(r⊙hn)), u = dropout((1-z)⊙hn + z⊙h~) (stream row·T + t,
  * counter unit), states[t] = LN_out(u).  LayerNorm pointers NULL = use_layer_norm False; tscale [T, N]
  * (row t = exp(-clamp(Δt, 0, 10)) of step t) or NULL.  saved: tagan_gru_saved_floats(N, T, hc) floats.

@@ -11,9 +11,8 @@
 //   h_t = LN_out(u)                                     (LayerNorm eps as passed; use_layer_norm only)
 // A workgroup owns R = 8·(256/hc) rows for all T steps: thread j <-> hidden unit j of its row group, the row
 // states live in LDS between steps, row statistics are shuffle (+ LDS for hc > 64) reductions, the
-// recurrent products are VALU dot products with the weights streamed from L1/L2 as coalesced runs: the forward
-// takes them k-major (Wᵀ: at fixed k the threads j read consecutive words), the backward in nn.Linear layout
-// (its transposed product reads columns, consecutive words again); row states are float4 LDS broadcasts.
+// recurrent products are VALU dot products against W rows (fwd) / columns (bwd) streamed from L1/L2, the row
+// states float4 LDS broadcasts.  For hc in {64, 128, 256} the forward is k_gru_fwd_mfma below instead.
 // Saved for the backward: hn, r⊙hn, r, z, h~, u [T, N, hc] and the two LayerNorms' (mean, rstd) [T, N].
 // Backward walks t = T-1..0 with dL/dh_t carried in LDS and writes dgx [T, N, 3hc] (the gate pre-activation
 // gradients; the caller turns them into the W_h gradients with one GEMM each against the saved hn / r⊙hn)
@@ -31,8 +30,8 @@ struct GruArgs {
     int64_t N;
     int T, hc;
     const float* gx;                  // [T, N, 3hc]
-    const float* Wrz;                 // fwd: [hc, 2hc] k-major (W_r | W_z)ᵀ; bwd: [2hc, hc] (nn.Linear layout)
-    const float* Wc;                  // fwd: [hc, hc] k-major W_cᵀ; bwd: [hc, hc]
+    const float* Wrz;                 // [2hc, hc]  (W_r | W_z, the h-side columns; nn.Linear layout)
+    const float* Wc;                  // [hc, hc]
     const float* gh; const float* bh; float eps_h;     // LN_h (null: no LayerNorm)
     const float* go; const float* bo; float eps_o;     // LN_out (null: no LayerNorm)
     const float* tscale;              // [T, N] exp(-clamp(Δt)) factors or null
@@ -134,21 +133,17 @@ __global__ void __launch_bounds__(GB) k_gru_fwd(GruArgs A) {
             az[i] = gp[HC + j];
         }
         if (t > 0) {
-            // k-major weights: at fixed k the HC threads read one contiguous run (coalesced), the row states come
-            // from LDS as float4 broadcasts
+            const float* wr = A.Wrz + (int64_t)j * HC;
+            const float* wz = A.Wrz + (int64_t)(HC + j) * HC;
 #pragma unroll 2
             for (int k = 0; k < HC; k += 4) {
-                float a[4], b[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    a[q] = A.Wrz[(int64_t)(k + q) * 2 * HC + j];
-                    b[q] = A.Wrz[(int64_t)(k + q) * 2 * HC + HC + j];
-                }
+                const float4 a = *reinterpret_cast<const float4*>(wr + k);
+                const float4 b = *reinterpret_cast<const float4*>(wz + k);
 #pragma unroll
                 for (int i = 0; i < RPG; ++i) {
                     const float4 h = *reinterpret_cast<const float4*>(hs + (g * RPG + i) * HC + k);
-                    ar[i] += (a[0] * h.x + a[1] * h.y) + (a[2] * h.z + a[3] * h.w);
-                    az[i] += (b[0] * h.x + b[1] * h.y) + (b[2] * h.z + b[3] * h.w);
+                    ar[i] += (a.x * h.x + a.y * h.y) + (a.z * h.z + a.w * h.w);
+                    az[i] += (b.x * h.x + b.y * h.y) + (b.z * h.z + b.w * h.w);
                 }
             }
         }
@@ -167,15 +162,14 @@ __global__ void __launch_bounds__(GB) k_gru_fwd(GruArgs A) {
             ac[i] = A.gx[((int64_t)t * N + rc) * 3 * HC + 2 * HC + j];
         }
         if (t > 0) {
+            const float* wc = A.Wc + (int64_t)j * HC;
 #pragma unroll 2
             for (int k = 0; k < HC; k += 4) {
-                float a[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) a[q] = A.Wc[(int64_t)(k + q) * HC + j];
+                const float4 a = *reinterpret_cast<const float4*>(wc + k);
 #pragma unroll
                 for (int i = 0; i < RPG; ++i) {
                     const float4 h = *reinterpret_cast<const float4*>(rh + (g * RPG + i) * HC + k);
-                    ac[i] += (a[0] * h.x + a[1] * h.y) + (a[2] * h.z + a[3] * h.w);
+                    ac[i] += (a.x * h.x + a.y * h.y) + (a.z * h.z + a.w * h.w);
                 }
             }
         }
@@ -408,6 +402,262 @@ __global__ void __launch_bounds__(GB) k_gru_bwd(GruArgs A) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------
+// Forward on the matrix cores (hc in {64, 128, 256}).  The VALU form above is LDS-bound: every FMA needs an
+// h operand broadcast from LDS.  Here a workgroup (4 waves) owns MR = 32 node rows for all T steps and each
+// step's recurrent products are small GEMMs on v_mfma_f32_16x16x4_f32 (exact fp32 products): [32 x hc] hn
+// (A operand, LDS, float4 = four k) times W_rzᵀ / W_cᵀ (B operand: nn.Linear rows straight from L2, float4).
+// Wave w owns hc/32 column tiles of the r|z product and hc/64 of the candidate product, for both 16-row
+// tiles; the accumulators go to an LDS pre-activation tile and the gate math runs with one thread per
+// (row, column) element, so gx loads and the saved-tensor stores are row-contiguous runs.
+// Per step: LN_h (wave w: rows 8w..8w+7) | r|z MFMA -> pre | r, z, r⊙hn in place | candidate MFMA -> pre |
+// h~, u = (1-z)·hn + z·h~ (+dropout) in place | LN_out rows -> h_t; a barrier between phases.  The saved
+// tensors and statistics are those of k_gru_fwd, so the backward is shared.
+// ---------------------------------------------------------------------------------------------------------
+typedef float f4m __attribute__((ext_vector_type(4)));
+constexpr int MR = 32;   // max rows per workgroup (MT = 1 or 2 16-row MFMA tiles; TAGAN_GRU_MR=16 picks one)
+
+__device__ __forceinline__ f4m mfma16(float a, float b, f4m c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// LDS pitches (floats): 4m with m = 2 (mod 4) -> conflict-free float4 A-operand reads of lanes (c, g)
+template <int HC> constexpr int gm_ph() { return HC + 8; }        // hs [MR][HC]
+template <int HC> constexpr int gm_pp() { return 2 * HC + 8; }    // pre [MR][2HC]
+
+// acc tiles of column tiles [nt0, nt0 + NQ) (both row tiles) -> pre[m][nt·16 + c]
+template <int HC, int NQ, int MT>
+__device__ __forceinline__ void gm_park(float* pre, const f4m (&acc)[MT][NQ], int nt0, int c, int g) {
+    constexpr int PP = gm_pp<HC>();
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pre[(mt * 16 + 4 * g + e) * PP + (nt0 + q) * 16 + c] = acc[mt][q][e];
+}
+
+// acc[mt][q] = A[32 x HC] (LDS, pitch PA) · W[rows (nt0 + q)·16 .. +15][0..HC)ᵀ
+template <int HC, int NQ, int PA, int MT>
+__device__ __forceinline__ void gm_product(const float* Als, const float* __restrict__ W, int nt0, int c, int g,
+                                           f4m (&acc)[MT][NQ]) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[mt][q] = f4m{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int k0 = 0; k0 < HC; k0 += 16) {
+        f4m a[MT], b[NQ];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) a[mt] = *(const f4m*)(Als + (mt * 16 + c) * PA + k0 + 4 * g);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) b[q] = *(const f4m*)(W + (int64_t)((nt0 + q) * 16 + c) * HC + k0 + 4 * g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) acc[mt][q] = mfma16(a[mt][e], b[q][e], acc[mt][q]);
+    }
+}
+
+template <int HC, int MT>
+__global__ void __launch_bounds__(256) k_gru_fwd_mfma(GruArgs A) {
+    constexpr int RW = MT * 4;   // rows per wave in the row-wise phases
+    TAGAN_LIVE_SEED(A);
+    constexpr int PH = gm_ph<HC>(), PP = gm_pp<HC>(), NT = HC / 16, RZT = NT / 2, CT = NT / 4, PL = HC / 64;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* hs = sm;              // [MR][PH] h_{t-1}, then hn
+    float* pre = hs + MR * PH;   // [MR][PP] gate pre-activations -> r⊙hn | z -> candidate pre-act | z -> u | z
+    const int tid0 = threadIdx.x, w = tid0 >> 6;
+    const int N = (int)A.N, T = A.T;
+    const int row0 = blockIdx.x * (MT * 16);
+    for (int t = 0; t < T; ++t) {
+        // The thread index is re-derived per step behind an empty asm: otherwise every per-element row / column
+        // / offset of the element loops is hoisted out of the step loop into live registers (4x the VGPRs).
+        int tid = tid0;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63, c = lane & 15, g = lane >> 4;
+        // per-step bases; row offsets stay 32-bit (the host guarantees N·3hc < 2^31)
+        const float* gxt = A.gx + (int64_t)t * N * 3 * HC;
+        const int64_t so = (int64_t)t * N * HC;
+        float* sst = A.s_stat + (int64_t)t * N * 4;
+        // uniform per-step bases + 32-bit element offsets (saddr + voffset addressing)
+        float* const s_hn = A.s_hn + so;
+        float* const s_r = A.s_r + so;
+        float* const s_rh = A.s_rh + so;
+        float* const s_z = A.s_z + so;
+        float* const s_ht = A.s_ht + so;
+        float* const s_u = A.s_u + so;
+        float* const s_st = A.states + so;
+        // ---- hn = LN_h(h_{t-1}) · tscale (wave w: rows 8w .. 8w+7; lane: features lane + 64q)
+#pragma unroll 1
+        for (int rr = 0; rr < RW; ++rr) {
+            const int m = w * RW + rr, row = row0 + m;
+            float v[PL];
+            if (t == 0) {
+#pragma unroll
+                for (int q = 0; q < PL; ++q) v[q] = 0.f;
+            } else {
+                float s1 = 0.f;
+#pragma unroll
+                for (int q = 0; q < PL; ++q) { v[q] = hs[m * PH + lane + 64 * q]; s1 += v[q]; }
+                float mean = 0.f, rs = 1.f;
+                if (A.gh) {
+                    mean = wave_sum(s1) / (float)HC;
+                    float s2 = 0.f;
+#pragma unroll
+                    for (int q = 0; q < PL; ++q) s2 += (v[q] - mean) * (v[q] - mean);
+                    rs = 1.f / sqrtf(wave_sum(s2) / (float)HC + A.eps_h);
+#pragma unroll
+                    for (int q = 0; q < PL; ++q) {
+                        const int jj = lane + 64 * q;
+                        v[q] = (v[q] - mean) * rs * A.gh[jj] + A.bh[jj];
+                    }
+                }
+                const float sc = A.tscale ? A.tscale[(int64_t)t * N + (row < N ? row : N - 1)] : 1.f;
+#pragma unroll
+                for (int q = 0; q < PL; ++q) v[q] *= sc;
+                if (lane == 0 && row < N) {
+                    sst[row * 4 + 0] = mean;
+                    sst[row * 4 + 1] = rs;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < PL; ++q) {
+                hs[m * PH + lane + 64 * q] = v[q];
+                if (row < N) s_hn[row * HC + lane + 64 * q] = v[q];
+            }
+        }
+        __syncthreads();
+        // ---- r | z pre-activations (zero at t = 0: h_{-1} = 0)
+        {
+            f4m acc[MT][RZT];
+            if (t > 0) {
+                gm_product<HC, RZT, PH, MT>(hs, A.Wrz, w * RZT, c, g, acc);
+            } else {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int q = 0; q < RZT; ++q) acc[mt][q] = f4m{0.f, 0.f, 0.f, 0.f};
+            }
+            gm_park<HC, RZT, MT>(pre, acc, w * RZT, c, g);
+        }
+        __syncthreads();
+        // ---- r = σ(·), z = σ(·); pre[:, :HC] <- r ⊙ hn, pre[:, HC:] <- z
+#pragma unroll 4
+        for (int i = tid; i < MT * 16 * 2 * HC; i += 256) {
+            const int m = i / (2 * HC), n = i % (2 * HC), row = row0 + m;
+            const bool ok = row < N;
+            const float x = pre[m * PP + n] + gxt[(ok ? row : N - 1) * 3 * HC + n];
+            const float sg = 1.f / (1.f + expf(-x));
+            if (n < HC) {
+                const float v = sg * hs[m * PH + n];
+                pre[m * PP + n] = v;
+                if (ok) { s_r[row * HC + n] = sg; s_rh[row * HC + n] = v; }
+            } else {
+                pre[m * PP + n] = sg;
+                if (ok) s_z[row * HC + n - HC] = sg;
+            }
+        }
+        __syncthreads();
+        // ---- candidate pre-activation -> pre[:, :HC] (after every wave has read r⊙hn)
+        {
+            f4m acc[MT][CT];
+            if (t > 0) {
+                gm_product<HC, CT, PP, MT>(pre, A.Wc, w * CT, c, g, acc);
+            } else {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int q = 0; q < CT; ++q) acc[mt][q] = f4m{0.f, 0.f, 0.f, 0.f};
+            }
+            __syncthreads();
+            gm_park<HC, CT, MT>(pre, acc, w * CT, c, g);
+        }
+        __syncthreads();
+        // ---- h~ = tanh(·), u = dropout((1 - z)·hn + z·h~) -> pre[:, :HC]
+#pragma unroll 4
+        for (int i = tid; i < MT * 16 * HC; i += 256) {
+            const int m = i / HC, n = i % HC, row = row0 + m;
+            const bool ok = row < N;
+            const float ht = tanhf(pre[m * PP + n] + gxt[(ok ? row : N - 1) * 3 * HC + 2 * HC + n]);
+            const float z = pre[m * PP + HC + n];
+            float u = (1.f - z) * hs[m * PH + n] + z * ht;
+            if (A.p_drop > 0.f) {
+                const uint32_t key = drop_key(A.seed, (uint64_t)row * (uint64_t)T + (uint64_t)t);
+                u = drop_u(key, (uint32_t)n) >= A.p_drop ? u * A.inv_keep : 0.f;
+            }
+            pre[m * PP + n] = u;
+            if (ok) {
+                s_ht[row * HC + n] = ht;
+                s_u[row * HC + n] = u;
+            }
+        }
+        __syncthreads();
+        // ---- h_t = LN_out(u) (rows 8w .. 8w+7)
+#pragma unroll 1
+        for (int rr = 0; rr < RW; ++rr) {
+            const int m = w * RW + rr, row = row0 + m;
+            float v[PL];
+            float s1 = 0.f;
+#pragma unroll
+            for (int q = 0; q < PL; ++q) { v[q] = pre[m * PP + lane + 64 * q]; s1 += v[q]; }
+            float mean = 0.f, rs = 1.f;
+            if (A.go) {
+                mean = wave_sum(s1) / (float)HC;
+                float s2 = 0.f;
+#pragma unroll
+                for (int q = 0; q < PL; ++q) s2 += (v[q] - mean) * (v[q] - mean);
+                rs = 1.f / sqrtf(wave_sum(s2) / (float)HC + A.eps_o);
+#pragma unroll
+                for (int q = 0; q < PL; ++q) {
+                    const int jj = lane + 64 * q;
+                    v[q] = (v[q] - mean) * rs * A.go[jj] + A.bo[jj];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < PL; ++q) {
+                hs[m * PH + lane + 64 * q] = v[q];
+                if (row < N) s_st[row * HC + lane + 64 * q] = v[q];
+            }
+            if (lane == 0 && row < N) {
+                sst[row * 4 + 2] = mean;
+                sst[row * 4 + 3] = rs;
+            }
+        }
+        __syncthreads();   // h_t rows complete before the next step's products
+    }
+}
+
+size_t gru_mfma_lds(int hc) { return (size_t)MR * ((hc + 8) + (2 * hc + 8)) * sizeof(float); }
+
+int gru_mfma_optin(int hc) {
+    static bool done[3] = {false, false, false};
+    const int idx = hc == 64 ? 0 : hc == 128 ? 1 : 2;
+    const size_t lds = gru_mfma_lds(hc);
+    if (done[idx] || lds <= 64 * 1024) return TAGAN_OK;
+    const void* k1 = hc == 64 ? reinterpret_cast<const void*>(&k_gru_fwd_mfma<64, 1>)
+                   : hc == 128 ? reinterpret_cast<const void*>(&k_gru_fwd_mfma<128, 1>)
+                               : reinterpret_cast<const void*>(&k_gru_fwd_mfma<256, 1>);
+    const void* k2 = hc == 64 ? reinterpret_cast<const void*>(&k_gru_fwd_mfma<64, 2>)
+                   : hc == 128 ? reinterpret_cast<const void*>(&k_gru_fwd_mfma<128, 2>)
+                               : reinterpret_cast<const void*>(&k_gru_fwd_mfma<256, 2>);
+    hipError_t e = hipFuncSetAttribute(k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e == hipSuccess) e = hipFuncSetAttribute(k2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    TAGAN_REQUIRE(e == hipSuccess, TAGAN_ERR_LAUNCH, "gru_fwd_mfma: LDS opt-in");
+    done[idx] = true;
+    return TAGAN_OK;
+}
+
+// TAGAN_GRU_MFMA=0 keeps the VALU forward (A/B, parity of the two forms)
+bool gru_mfma_ok(int hc, int64_t N) {
+    const char* e = getenv("TAGAN_GRU_MFMA");
+    if (e && e[0] == '0') return false;
+    return (hc == 64 || hc == 128 || hc == 256) && N * 3 * hc < ((int64_t)1 << 31);   // 32-bit row offsets
+}
+
 size_t gru_lds(int hc) { return (size_t)(2 * 8 * GB + (GB / 64) * RPG) * sizeof(float); }   // 2·R·hc = 2·8·256
 
 template <bool FWD>
@@ -455,6 +705,21 @@ int tagan_gru_fwd(int64_t N, int32_t T, int32_t hc, const float* gx, const float
     A.s_hn = saved; A.s_rh = saved + S; A.s_r = saved + 2 * S; A.s_z = saved + 3 * S; A.s_ht = saved + 4 * S;
     A.s_u = saved + 5 * S; A.s_stat = saved + 6 * S;
     hipStream_t s = as_stream(stream);
+    if (gru_mfma_ok(hc, N)) {
+        if (int rc = gru_mfma_optin(hc)) return rc;
+        // 16 rows per workgroup while that still leaves < 2 workgroups per CU at 32 (more of them in flight:
+        // C2's 10k rows 3.58 -> 3.00 ms intended forward), 32 above (halves the weight reads from L2)
+        const char* em = getenv("TAGAN_GRU_MR");
+        const int mr = em ? (atoi(em) == 16 ? 16 : 32) : (N <= 32 * 512 ? 16 : 32);
+        const unsigned nb = (unsigned)((N + mr - 1) / mr);
+        const size_t lds = gru_mfma_lds(hc);
+#define TAGAN_GRUM(H) { if (mr == 16) k_gru_fwd_mfma<H, 1><<<nb, 256, lds, s>>>(A); \
+                        else k_gru_fwd_mfma<H, 2><<<nb, 256, lds, s>>>(A); }
+        if (hc == 64) TAGAN_GRUM(64) else if (hc == 128) TAGAN_GRUM(128) else TAGAN_GRUM(256)
+#undef TAGAN_GRUM
+        TAGAN_CHECK_LAUNCH("gru_fwd_mfma");
+        return TAGAN_OK;
+    }
     TAGAN_REQUIRE(launch_gru<true>(A, s, gru_blocks(N, hc)) == TAGAN_OK, TAGAN_ERR_UNSUPPORTED, "gru_fwd: hc");
     TAGAN_CHECK_LAUNCH("gru_fwd");
     return TAGAN_OK;

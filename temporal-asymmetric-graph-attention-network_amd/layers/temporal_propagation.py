@@ -57,8 +57,7 @@ class GRUSeqFn(torch.autograd.Function):
         states = torch.empty(T, N, hc, device=dev)
         saved = torch.empty(int(L.tagan_gru_saved_floats(N, T, hc)), device=dev)
         prm = [None if t is None else t.detach().contiguous() for t in (w_rz, w_c, lnh_w, lnh_b, lno_w, lno_b)]
-        wt = [prm[0].t().contiguous(), prm[1].t().contiguous()]   # the forward reads the weights k-major
-        check(L.tagan_gru_fwd(N, T, hc, ptr(gx), ptr(wt[0]), ptr(wt[1]), ptr(prm[2]), ptr(prm[3]), float(eps_h),
+        check(L.tagan_gru_fwd(N, T, hc, ptr(gx), ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(prm[3]), float(eps_h),
                               ptr(prm[4]), ptr(prm[5]), float(eps_o), ptr(tscale), float(p), seed, ptr(states),
                               ptr(saved), stream_of(gx)), "tagan_gru_fwd")
         ctx.save_for_backward(states, saved, tscale, *prm)
