@@ -438,6 +438,17 @@ __device__ __forceinline__ void gm_park(float* pre, const f4m (&acc)[MT][NQ], in
             for (int e = 0; e < 4; ++e) pre[(mt * 16 + 4 * g + e) * PP + (nt0 + q) * 16 + c] = acc[mt][q][e];
 }
 
+// acc tiles -> T[m][nt·16 + c] for an LDS tile of pitch PT
+template <int HC, int NQ, int MT, int PT>
+__device__ __forceinline__ void gm_park_p(float* tile, const f4m (&acc)[MT][NQ], int nt0, int c, int g) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) tile[(mt * 16 + 4 * g + e) * PT + (nt0 + q) * 16 + c] = acc[mt][q][e];
+}
+
 // acc[mt][q] = A[32 x HC] (LDS, pitch PA) · W[rows (nt0 + q)·16 .. +15][0..HC)ᵀ
 template <int HC, int NQ, int PA, int MT>
 __device__ __forceinline__ void gm_product(const float* Als, const float* __restrict__ W, int nt0, int c, int g,
@@ -631,6 +642,223 @@ __global__ void __launch_bounds__(256) k_gru_fwd_mfma(GruArgs A) {
     }
 }
 
+// Backward on the matrix cores (same workgroup geometry as k_gru_fwd_mfma): per step, walking t = T-1 .. 0,
+//   P1 rows (wave w: its RW rows, lane = features): LN_out backward, dropout, gate derivatives -> dac, daz, dhn0
+//   P2 d(r⊙hn) = dac · W_c          (MFMA; B operand = W_c rows k, four scalar reads per k-quad, coalesced in c)
+//   P3 rows: dar = (d(r⊙hn) ⊙ hn)·r(1-r), dhn0 += d(r⊙hn) ⊙ r
+//   P4 dhn_rec = [dar | daz] · W_rz  (MFMA, K = 2hc)
+//   P5 rows: LN_h backward of dhn0 + dhn_rec (times the time factor) -> dL/dh_{t-1}, kept in the dhn tile
+// with a barrier after P1 .. P4.  dgx and the LayerNorm parameter partials as in k_gru_bwd (shared host code).
+template <int HC, int NQ, int PA, int MT, int K>
+__device__ __forceinline__ void gm_product_t(const float* Als, const float* __restrict__ W, int nt0, int c, int g,
+                                             f4m (&acc)[MT][NQ]) {
+    // acc[mt][q] = A[16·MT x K] (LDS, pitch PA) · W[0..K)[(nt0 + q)·16 .. +15]   (W row-major [K][HC])
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[mt][q] = f4m{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int k0 = 0; k0 < K; k0 += 16) {
+        f4m a[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) a[mt] = *(const f4m*)(Als + (mt * 16 + c) * PA + k0 + 4 * g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float b[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) b[q] = W[(int64_t)(k0 + 4 * g + e) * HC + (nt0 + q) * 16 + c];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) acc[mt][q] = mfma16(a[mt][e], b[q], acc[mt][q]);
+        }
+    }
+}
+
+template <int HC> constexpr int gb_p1() { return HC + 8; }       // dac, d(r⊙hn) / dhn_rec park, dhn tiles
+template <int HC> constexpr int gb_p2() { return 2 * HC + 8; }   // [dar | daz]
+
+template <int HC, int MT>
+__global__ void __launch_bounds__(256) k_gru_bwd_mfma(GruArgs A) {
+    TAGAN_LIVE_SEED(A);
+    constexpr int P1 = gb_p1<HC>(), P2 = gb_p2<HC>(), NT = HC / 16, CT = NT / 4, PL = HC / 64, RW = MT * 4;
+    constexpr int RT = MT * 16;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* ta = sm;               // [RT][P1] dac
+    float* tz = ta + RT * P1;     // [RT][P2] dar | daz
+    float* td = tz + RT * P2;     // [RT][P1] d(r⊙hn), then dhn_rec
+    float* th = td + RT * P1;     // [RT][P1] dhn partial; between steps dL/dh_t (the carry)
+    const int tid0 = threadIdx.x, w = tid0 >> 6;
+    const int N = (int)A.N, T = A.T;
+    const int row0 = blockIdx.x * RT;
+    float pgh[PL], pbh[PL], pgo[PL], pbo[PL];
+#pragma unroll
+    for (int q = 0; q < PL; ++q) pgh[q] = pbh[q] = pgo[q] = pbo[q] = 0.f;
+    {   // carry = 0
+        for (int i = tid0; i < RT * P1; i += 256) th[i] = 0.f;
+    }
+    __syncthreads();
+    for (int t = T - 1; t >= 0; --t) {
+        int tid = tid0;
+        asm volatile("" : "+v"(tid));   // see k_gru_fwd_mfma
+        const int lane = tid & 63, c = lane & 15, g = lane >> 4;
+        const int64_t so = (int64_t)t * N * HC;
+        const float* sst = A.s_stat + (int64_t)t * N * 4;
+        float* dgt = A.dgx + (int64_t)t * N * 3 * HC;
+        // ---- P1
+#pragma unroll 1
+        for (int rr = 0; rr < RW; ++rr) {
+            const int m = w * RW + rr, row = row0 + m;
+            const bool ok = row < N;
+            const int rc = ok ? row : N - 1;
+            float gh[PL], xh[PL], gq[PL];
+            float c1 = 0.f, c2 = 0.f, rso = 1.f;
+            const float mo = A.go ? sst[rc * 4 + 2] : 0.f;
+            if (A.go) rso = sst[rc * 4 + 3];
+#pragma unroll
+            for (int q = 0; q < PL; ++q) {
+                const int j = lane + 64 * q;
+                gh[q] = (ok ? A.dstates[so + rc * HC + j] : 0.f) + th[m * P1 + j];
+                if (A.go) {
+                    xh[q] = (A.s_u[so + rc * HC + j] - mo) * rso;
+                    if (ok) { pgo[q] += gh[q] * xh[q]; pbo[q] += gh[q]; }
+                    gq[q] = gh[q] * A.go[j];
+                    c1 += gq[q] * xh[q];
+                    c2 += gq[q];
+                } else {
+                    gq[q] = gh[q];
+                }
+            }
+            if (A.go) {
+                c1 = wave_sum(c1);
+                c2 = wave_sum(c2);
+            }
+#pragma unroll
+            for (int q = 0; q < PL; ++q) {
+                const int j = lane + 64 * q;
+                float du = A.go ? rso * (gq[q] - xh[q] * c1 / (float)HC - c2 / (float)HC) : gq[q];
+                if (A.p_drop > 0.f) {
+                    const uint32_t key = drop_key(A.seed, (uint64_t)row * (uint64_t)T + (uint64_t)t);
+                    du = drop_u(key, (uint32_t)j) >= A.p_drop ? du * A.inv_keep : 0.f;
+                }
+                const int o = rc * HC + j;
+                const float hn = A.s_hn[so + o], z = A.s_z[so + o], ht = A.s_ht[so + o];
+                const float dz = du * (ht - hn), dht = du * z;
+                float dac = dht * (1.f - ht * ht), daz = dz * z * (1.f - z);
+                if (!ok) { dac = 0.f; daz = 0.f; }
+                ta[m * P1 + j] = dac;
+                tz[m * P2 + HC + j] = daz;
+                th[m * P1 + j] = du * (1.f - z);
+                if (ok) {
+                    dgt[row * 3 * HC + HC + j] = daz;
+                    dgt[row * 3 * HC + 2 * HC + j] = dac;
+                }
+            }
+        }
+        if (t == 0) {   // r multiplies hn = 0: no gradient reaches ar, and nothing flows to h_{-1}
+#pragma unroll 1
+            for (int rr = 0; rr < RW; ++rr) {
+                const int row = row0 + w * RW + rr;
+                if (row < N)
+#pragma unroll
+                    for (int q = 0; q < PL; ++q) dgt[row * 3 * HC + lane + 64 * q] = 0.f;
+            }
+            break;
+        }
+        __syncthreads();
+        // ---- P2: d(r⊙hn) = dac · W_c -> td
+        {
+            f4m acc[MT][CT];
+            gm_product_t<HC, CT, P1, MT, HC>(ta, A.Wc, w * CT, c, g, acc);
+            gm_park_p<HC, CT, MT, P1>(td, acc, w * CT, c, g);
+        }
+        __syncthreads();
+        // ---- P3
+#pragma unroll 1
+        for (int rr = 0; rr < RW; ++rr) {
+            const int m = w * RW + rr, row = row0 + m;
+            const bool ok = row < N;
+            const int rc = ok ? row : N - 1;
+#pragma unroll
+            for (int q = 0; q < PL; ++q) {
+                const int j = lane + 64 * q;
+                const float drh = td[m * P1 + j];
+                const float hn = A.s_hn[so + rc * HC + j], r = A.s_r[so + rc * HC + j];
+                th[m * P1 + j] += drh * r;
+                const float dar = ok ? drh * hn * r * (1.f - r) : 0.f;
+                tz[m * P2 + j] = dar;
+                if (ok) dgt[row * 3 * HC + j] = dar;
+            }
+        }
+        __syncthreads();
+        // ---- P4: dhn_rec = [dar | daz] · W_rz -> td
+        {
+            f4m acc[MT][CT];
+            gm_product_t<HC, CT, P2, MT, 2 * HC>(tz, A.Wrz, w * CT, c, g, acc);
+            gm_park_p<HC, CT, MT, P1>(td, acc, w * CT, c, g);
+        }
+        __syncthreads();
+        // ---- P5: LN_h backward -> carry (in th)
+        const float* stp = A.states + (int64_t)(t - 1) * N * HC;
+#pragma unroll 1
+        for (int rr = 0; rr < RW; ++rr) {
+            const int m = w * RW + rr, row = row0 + m;
+            const bool ok = row < N;
+            const int rc = ok ? row : N - 1;
+            const float sc = A.tscale ? A.tscale[(int64_t)t * N + rc] : 1.f;
+            float g2[PL], xh2[PL], gp2[PL];
+            float e1 = 0.f, e2 = 0.f, rsh = 1.f;
+            const float mh = A.gh ? sst[rc * 4 + 0] : 0.f;
+            if (A.gh) rsh = sst[rc * 4 + 1];
+#pragma unroll
+            for (int q = 0; q < PL; ++q) {
+                const int j = lane + 64 * q;
+                g2[q] = ok ? (th[m * P1 + j] + td[m * P1 + j]) * sc : 0.f;
+                if (A.gh) {
+                    xh2[q] = (stp[rc * HC + j] - mh) * rsh;
+                    pgh[q] += g2[q] * xh2[q];
+                    pbh[q] += g2[q];
+                    gp2[q] = g2[q] * A.gh[j];
+                    e1 += gp2[q] * xh2[q];
+                    e2 += gp2[q];
+                } else {
+                    gp2[q] = g2[q];
+                }
+            }
+            if (A.gh) {
+                e1 = wave_sum(e1);
+                e2 = wave_sum(e2);
+            }
+#pragma unroll
+            for (int q = 0; q < PL; ++q) {
+                const int j = lane + 64 * q;
+                th[m * P1 + j] = A.gh ? rsh * (gp2[q] - xh2[q] * e1 / (float)HC - e2 / (float)HC) : gp2[q];
+            }
+        }
+        // the next step's P1 reads only this wave's rows of th; its MFMAs wait for the barrier after it
+    }
+    if (A.part) {   // LayerNorm parameter partials: the four waves in order
+        __syncthreads();
+        float* pp = sm;   // [4 waves][4][HC]
+#pragma unroll
+        for (int q = 0; q < PL; ++q) {
+            const int j = (tid0 & 63) + 64 * q;
+            pp[(w * 4 + 0) * HC + j] = pgh[q];
+            pp[(w * 4 + 1) * HC + j] = pbh[q];
+            pp[(w * 4 + 2) * HC + j] = pgo[q];
+            pp[(w * 4 + 3) * HC + j] = pbo[q];
+        }
+        __syncthreads();
+        for (int x = tid0; x < 4 * HC; x += 256) {
+            float sum = 0.f;
+            for (int ww = 0; ww < 4; ++ww) sum += pp[ww * 4 * HC + x];
+            A.part[(int64_t)blockIdx.x * 4 * HC + x] = sum;
+        }
+    }
+}
+
+size_t gru_bwd_mfma_lds(int hc, int mt) { return (size_t)mt * 16 * (3 * (hc + 8) + (2 * hc + 8)) * sizeof(float); }
+
 size_t gru_mfma_lds(int hc) { return (size_t)MR * ((hc + 8) + (2 * hc + 8)) * sizeof(float); }
 
 int gru_mfma_optin(int hc) {
@@ -651,7 +879,17 @@ int gru_mfma_optin(int hc) {
     return TAGAN_OK;
 }
 
-// TAGAN_GRU_MFMA=0 keeps the VALU forward (A/B, parity of the two forms)
+// Rows per workgroup of the matrix-core kernels: 16 while that still leaves < 2 workgroups per CU at 32 (more
+// of them in flight: C2's 10k rows 3.58 -> 3.00 ms intended forward), 32 above (halves the weight reads from
+// L2).  TAGAN_GRU_MR=16|32 overrides.
+int gru_mfma_rows(int64_t N, bool bwd = false) {
+    const char* em = getenv("TAGAN_GRU_MR");
+    if (em) return atoi(em) == 16 ? 16 : 32;
+    // the backward measured faster at 16 at every size (C4: 211 vs 264 ms, profiles/r2_gru_mfma_ab.txt)
+    return (bwd || N <= 32 * 512) ? 16 : 32;
+}
+
+// TAGAN_GRU_MFMA=0 keeps the VALU kernels (A/B, parity of the two forms)
 bool gru_mfma_ok(int hc, int64_t N) {
     const char* e = getenv("TAGAN_GRU_MFMA");
     if (e && e[0] == '0') return false;
@@ -707,10 +945,7 @@ int tagan_gru_fwd(int64_t N, int32_t T, int32_t hc, const float* gx, const float
     hipStream_t s = as_stream(stream);
     if (gru_mfma_ok(hc, N)) {
         if (int rc = gru_mfma_optin(hc)) return rc;
-        // 16 rows per workgroup while that still leaves < 2 workgroups per CU at 32 (more of them in flight:
-        // C2's 10k rows 3.58 -> 3.00 ms intended forward), 32 above (halves the weight reads from L2)
-        const char* em = getenv("TAGAN_GRU_MR");
-        const int mr = em ? (atoi(em) == 16 ? 16 : 32) : (N <= 32 * 512 ? 16 : 32);
+        const int mr = gru_mfma_rows(N);
         const unsigned nb = (unsigned)((N + mr - 1) / mr);
         const size_t lds = gru_mfma_lds(hc);
 #define TAGAN_GRUM(H) { if (mr == 16) k_gru_fwd_mfma<H, 1><<<nb, 256, lds, s>>>(A); \
@@ -753,9 +988,29 @@ int tagan_gru_bwd(int64_t N, int32_t T, int32_t hc, const float* Wrz, const floa
     A.s_stat = sv + 6 * S;
     A.dstates = dstates; A.dgx = dgx; A.part = want ? (float*)workspace : nullptr;
     hipStream_t s = as_stream(stream);
-    const unsigned nblk = gru_blocks(N, hc, RPB);
-    TAGAN_REQUIRE(launch_gru<false>(A, s, nblk) == TAGAN_OK, TAGAN_ERR_UNSUPPORTED, "gru_bwd: hc");
-    TAGAN_CHECK_LAUNCH("gru_bwd");
+    unsigned nblk;
+    if (gru_mfma_ok(hc, N)) {
+        int mr = gru_mfma_rows(N, true);
+        if (gru_bwd_mfma_lds(hc, mr / 16) > 160 * 1024) mr = 16;
+        nblk = (unsigned)((N + mr - 1) / mr);   // <= gru_blocks(N, hc, RPB): the workspace rows
+        const size_t lds = gru_bwd_mfma_lds(hc, mr / 16);
+#define TAGAN_GRUB(H, M) { auto kern = k_gru_bwd_mfma<H, M>; \
+        if (lds > 64 * 1024) { hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+                               TAGAN_REQUIRE(e == hipSuccess, TAGAN_ERR_LAUNCH, "gru_bwd_mfma: LDS opt-in"); } \
+        kern<<<nblk, 256, lds, s>>>(A); }
+        if (mr == 16) {
+            if (hc == 64) TAGAN_GRUB(64, 1) else if (hc == 128) TAGAN_GRUB(128, 1) else TAGAN_GRUB(256, 1)
+        } else {
+            if (hc == 64) TAGAN_GRUB(64, 2) else if (hc == 128) TAGAN_GRUB(128, 2) else TAGAN_GRUB(256, 2)
+        }
+#undef TAGAN_GRUB
+        TAGAN_CHECK_LAUNCH("gru_bwd_mfma");
+    } else {
+        nblk = gru_blocks(N, hc, RPB);
+        TAGAN_REQUIRE(launch_gru<false>(A, s, nblk) == TAGAN_OK, TAGAN_ERR_UNSUPPORTED, "gru_bwd: hc");
+        TAGAN_CHECK_LAUNCH("gru_bwd");
+    }
     if (want) {
         launch_colsum(A.part, (int)nblk, 2 * hc, dln_h_w, dln_h_b, hc, s, 1.f, 4 * hc);
         launch_colsum(A.part + 2 * hc, (int)nblk, 2 * hc, dln_o_w, dln_o_b, hc, s, 1.f, 4 * hc);
