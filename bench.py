@@ -480,15 +480,14 @@ def main():
     launch_trial = None
     gstep = None
     if use_graph:
+        # eager trial first, then ONE capture that is kept when it wins (no capture / destroy / re-capture)
+        te = trial(eager_step) if launch == "auto" else None
         gstep = graphed(model, opt, cfg, fwd, world, None if args.shard else bucket)
         if launch == "auto":
             tg = trial(gstep)
-            gstep.close()
-            te = trial(eager_step)
             launch_trial = {"graph_ms": round(tg * 1e3, 3), "eager_ms": round(te * 1e3, 3)}
-            if tg < te:
-                gstep = graphed(model, opt, cfg, fwd, world, None if args.shard else bucket)
-            else:
+            if tg >= te:
+                gstep.close()
                 gstep = None
     if gstep is not None:
         step = gstep
@@ -515,6 +514,7 @@ def main():
         return el
 
     elapsed = timed(args.steps, args.warmup)
+
     seqs_per_step = 1 if args.shard else world
     value = seqs_per_step * T * args.steps / elapsed
     rec = {
@@ -550,12 +550,13 @@ def main():
         # the same step with bf16 activations between kernels (BASELINE's C2 dtype), fp32 math inside
         # every kernel; held to the fp32 mode by tests/test_gpu_bf16.py (loss 2e-2, gradients 8e-2)
         model.precision = "bf16"
+        te = trial(eager_step) if (use_graph and launch == "auto") else None
         gstep = graphed(model, opt, cfg, fwd, world, None if args.shard else bucket) if use_graph else None
         if gstep is not None and launch == "auto":
             tg = trial(gstep)
-            gstep.close()
-            te = trial(eager_step)
-            gstep = graphed(model, opt, cfg, fwd, world, None if args.shard else bucket) if tg < te else None
+            if tg >= te:
+                gstep.close()
+                gstep = None
             alt_launch = {"graph_ms": round(tg * 1e3, 3), "eager_ms": round(te * 1e3, 3)}
         else:
             alt_launch = None
