@@ -57,7 +57,9 @@ class GraphedStep:
         if optimizer is not None:
             optimizer.zero_grad(set_to_none=True)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # captured on the warm-up stream: autograd nodes that outlive a warm-up step (a loss the caller kept,
+        # AccumulateGrad nodes) then belong to the capture stream, so the backward adds no cross-stream join
+        with torch.cuda.graph(self.graph, stream=side):
             s = torch.cuda.current_stream(dev)
             check(lib().tagan_seed_counter_step(ptr(self.counter), ctypes.c_void_p(s.cuda_stream)),
                   "tagan_seed_counter_step")
@@ -65,7 +67,7 @@ class GraphedStep:
         self.post_graph = None
         if post is not None:
             self.post_graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.post_graph, pool=self.graph.pool()):
+            with torch.cuda.graph(self.post_graph, pool=self.graph.pool(), stream=side):
                 post()
 
     def __call__(self) -> torch.Tensor:

@@ -200,7 +200,10 @@ class TAGAN(nn.Module):
                                dropout_seed)
             if fused is not None:
                 logits, predictions, loss = fused
-                self.last_predictions = predictions
+                # detached (the reference keeps the autograd history): a stored graph would keep the previous
+                # step's AccumulateGrad nodes -- and the stream they were created on -- alive into the next
+                # backward (a cross-stream join inside a captured HIP graph step)
+                self.last_predictions = predictions.detach()
                 if self.config.output_dim == 1:
                     self.last_binary_predictions = (predictions > 0.65).float()
                 return {"logits": logits, "predictions": predictions, "loss": loss}
@@ -219,11 +222,11 @@ class TAGAN(nn.Module):
                 loss = self.loss_fn(logits, labels)
         if self.config.output_dim == 1:
             predictions = torch.sigmoid(logits)
-            self.last_predictions = predictions
+            self.last_predictions = predictions.detach()
             self.last_binary_predictions = (predictions > 0.65).float()
         else:
             predictions = F.softmax(logits, dim=1)
-            self.last_predictions = predictions
+            self.last_predictions = predictions.detach()
         return {"logits": logits, "predictions": predictions, "loss": loss}
 
     def infer(self, graph_sequence, return_probs: bool = True) -> Dict[str, Any]:
