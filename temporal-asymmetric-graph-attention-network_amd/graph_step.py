@@ -84,3 +84,4 @@ class GraphedStep:
         if self.prev_validate is not None:
             self.model.validate_edges = self.prev_validate
         self.graph = self.post_graph = None
+        self.loss = None   # releases the captured step's autograd graph (its AccumulateGrad nodes)
