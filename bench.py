@@ -24,6 +24,7 @@ reference's own dense N×N mask + per-(head, node) loop, cross-checked against t
 profiles/r2_cpu_crosscheck.json), next to a GPU C1 step measured here.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -179,6 +180,67 @@ def roofline_c4(reps=10):
     del k, graph
     torch.cuda.empty_cache()
     return rec
+
+
+def temporal_kernels(config, reps=10):
+    """The temporal attention kernels alone (forward + backward, HIP events) on a config's [T, N, 3H] time-major
+    projection with the folded bias table, its gradient and dropout 0.1 -- the kernel VERDICT r01 named furthest
+    below the roofline.  Algorithmic bytes: forward Q, K, V in + O out; backward Q, K, V, dO in + dQ, dK, dV out
+    (O is not read: delta comes from P·dP); + the LSE rows."""
+    from tagan_amd import _lib, synthetic
+    dev = torch.device("cuda", torch.cuda.current_device())
+    N, _E, T, H, heads = synthetic.CONFIGS[config][:5]
+    d = H // heads
+    g = torch.Generator(device=dev).manual_seed(3)
+    qkv = torch.randn(T, N, 3 * H, device=dev, generator=g)
+    out = torch.empty(T, N, H, device=dev)
+    dout = torch.randn(T, N, H, device=dev, generator=g)
+    dqkv = torch.empty_like(qkv)
+    lse = torch.empty(N, heads, T, device=dev)
+    table = torch.randn(heads, 2 * T - 1, device=dev, generator=g) * 0.1
+    dtable = torch.empty_like(table)
+    L = _lib.lib()
+    wsb = L.tagan_temporal_attn_bwd_workspace(N, T, heads, d)
+    ws = torch.empty(max(int(wsb), 1), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(st.cuda_stream)
+    b, db, es = qkv.data_ptr(), dqkv.data_ptr(), 4
+    sr, stt = 3 * H, N * 3 * H
+
+    def fwd():
+        _lib.check(L.tagan_temporal_attn_fwd(0, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, stt,
+                                             _lib.ptr(table), None, 0, None, 0, 0, 0, 0.1, 99,
+                                             _lib.ptr(out), H, N * H, _lib.ptr(lse), None, sp), "fwd")
+
+    def bwd():
+        _lib.check(L.tagan_temporal_attn_bwd(0, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, stt,
+                                             _lib.ptr(table), None, 0, None, 0, 0, 0, 0.1, 99,
+                                             _lib.ptr(out), H, N * H, _lib.ptr(lse), _lib.ptr(dout), H, N * H,
+                                             db, db + H * es, db + 2 * H * es, sr, stt, _lib.ptr(dtable), None, None,
+                                             _lib.ptr(ws), wsb, sp), "bwd")
+    for _ in range(2):
+        fwd()
+        bwd()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    tf = tb = 0.0
+    for _ in range(reps):
+        ev[0].record(st)
+        fwd()
+        ev[1].record(st)
+        bwd()
+        ev[2].record(st)
+        ev[2].synchronize()
+        tf += ev[0].elapsed_time(ev[1])
+        tb += ev[1].elapsed_time(ev[2])
+    tf, tb = tf / reps / 1e3, tb / reps / 1e3
+    unit = N * T * H * 4
+    bf, bb = 4 * unit + N * heads * T * 4, 7 * unit + N * heads * T * 4
+    del qkv, out, dout, dqkv, lse, ws
+    torch.cuda.empty_cache()
+    return {"config": config, "rows": N, "T": T, "heads": heads, "head_dim": d,
+            "ms_fwd": round(tf * 1e3, 4), "ms_bwd": round(tb * 1e3, 4),
+            "gbs_fwd": round(bf / tf / 1e9, 1), "gbs_bwd": round(bb / tb / 1e9, 1),
+            "frac_fwd": round(bf / tf / 1e9 / HBM_PEAK_GBS, 4), "frac_bwd": round(bb / tb / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def roofline_cache_assisted(seq, cfg, reps=20):
@@ -575,6 +637,9 @@ def main():
         roof = roofline_c4(args.roofline_reps)
         roof["cache_assisted"] = dict(roofline_cache_assisted(seq, cfg), config=args.config)
         rec["roofline"] = roof
+        # the temporal kernels: C4 (v6 head-group slabs) and C2 (v6 forward, v4 backward: 64-B per-head slices,
+        # at the bandwidth that access pattern allows)
+        rec["temporal_kernels"] = [temporal_kernels("c4"), temporal_kernels("c2")]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         c1 = None if args.no_c1 else gpu_c1_line(dev, args.precision, graph=launch != "eager")
         rec["cpu_baseline"] = cpu_baseline(cfg, args.config, init_state, args.cpu_sample_snapshots, gpu_c1=c1,
