@@ -22,6 +22,9 @@
 // then summed in block order by a second kernel.
 #include "common.cuh"
 
+#include <mutex>
+#include <unordered_set>
+
 namespace tagan {
 namespace {
 
@@ -2280,9 +2283,16 @@ bool v6_bwd_ok(int T, int d) {
 template <typename K>
 int lds_optin(K* kern, size_t bytes) {
     if (bytes <= 64 * 1024) return TAGAN_OK;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)bytes);
+    // once per kernel, to the full 160 KB (later launches of any size skip the runtime call)
+    static std::mutex mu;
+    static std::unordered_set<const void*> done;
+    const void* key = reinterpret_cast<const void*>(kern);
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count(key)) return TAGAN_OK;
+    TAGAN_REQUIRE(bytes <= 160 * 1024, TAGAN_ERR_UNSUPPORTED, "temporal_attn: %zu B of LDS", bytes);
+    hipError_t e = hipFuncSetAttribute(key, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     TAGAN_REQUIRE(e == hipSuccess, TAGAN_ERR_LAUNCH, "temporal_attn: LDS opt-in %zu B: %s", bytes, hipGetErrorString(e));
+    done.insert(key);
     return TAGAN_OK;
 }
 
