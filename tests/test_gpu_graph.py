@@ -91,3 +91,39 @@ def test_counter_unregistered_restores_eager_seeds(dev):
     g.close()
     assert int(g.counter.item()) >= 2
     assert torch.equal(fwd(), before)
+
+
+def test_graph_intended_propagation_matches_eager(dev):
+    """TAGAN with the intended TemporalPropagation (matrix-core GRU kernels, skip-window kernel) captured as one
+    graph: replays 4-6 follow the eager trajectory (dropout off)."""
+    from tagan_amd import TAGAN, synthetic
+    from tagan_amd.graph_step import GraphedStep
+    cfg = synthetic.config_for("c2", dropout=0.0)
+    seq = synthetic.make_sequence("c2", dev, seed=7, snapshots=6, nodes=400, edges=3000)
+    labels = torch.tensor([1.0], device=dev)
+
+    def setup():
+        torch.manual_seed(3)
+        m = TAGAN(cfg, temporal_propagation="intended").to(dev).train()
+        o = torch.optim.Adam(m.parameters(), lr=1e-3, capturable=True)
+
+        def step():
+            out = m(seq, labels=labels)
+            out["loss"].backward()
+            o.step()
+            return out["loss"]
+        return m, o, step
+    m1, o1, s1 = setup()
+    eager = []
+    for _ in range(6):
+        o1.zero_grad(set_to_none=True)
+        eager.append(float(s1()))
+    m2, o2, s2 = setup()
+    g = GraphedStep(m2, s2, optimizer=o2, warmup=3)
+    try:
+        graphed = [float(g()) for _ in range(3)]
+    finally:
+        g.close()
+    torch.cuda.synchronize()
+    for a, b in zip(eager[3:], graphed):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (eager, graphed)

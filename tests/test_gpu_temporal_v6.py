@@ -38,6 +38,7 @@ def _run(dev, qkv, T, R, time_major, heads, mask, p, seed, bt, bd, dctx, monkeyp
     (32, 64, 2, True, 0.2, True, True, False, torch.float32, 37),       # d = 32, mask + causal + dropout
     (32, 128, 8, True, 0.1, False, False, False, torch.float32, 5),     # rows < 8
     (16, 128, 8, True, 0.1, False, False, False, torch.float32, 2061),  # > 1024 rows: several rows per workgroup
+    (24, 96, 6, True, 0.1, False, False, False, torch.float32, 41),     # 6 heads: GH = 2 whatever is asked
 ])
 def test_v6_matches_v4(dev, monkeypatch, gh, T, H, heads, time_major, p, causal, masked, dense, dtype, R):
     from tagan_amd.kernels import TemporalMask
