@@ -158,7 +158,14 @@ typedef struct tagan_graph {
     const int32_t* col_counts;
     const int32_t* row_chunk_order;  /* [chunk_cap] processing order (tagan_chunk_order); NULL = identity */
     const int32_t* col_chunk_order;
+    int64_t nnz_cap;            /* capacity of col / csc_row / csc_eid (>= nnz) */
+    const int32_t* csr_cpos;    /* [nnz] CSC position of each CSR entry (tagan_csr_csc_pos), or NULL.  With
+                                   nnz_cap > 0 and csr_cpos the backward runs column-first (see
+                                   tagan_geo_attn_bwd); otherwise row-first */
 } tagan_graph;
+
+/* csr_cpos[csc_eid[p]] = p for p < *nnz: the inverse of csc_eid (the CSC position of each CSR entry). */
+int tagan_csr_csc_pos(const int32_t* csc_eid, const int64_t* nnz, int64_t nnz_cap, int32_t* csr_cpos, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Geometric (edge-softmax) attention.  Replaces geometric_attention.py:332-516
@@ -178,11 +185,18 @@ int tagan_geo_attn_fwd(int dtype, int metric, const tagan_graph* g, int32_t head
                        void* out, float* lse, float* edge_alpha,
                        void* workspace, size_t workspace_bytes, void* stream);
 
-/* Backward of tagan_geo_attn_fwd: row pass over CSR (dq, delta = rowsum(dO∘O))
- * then column pass over CSC (dk, dv).  Atomic-free and deterministic.
+/* Backward of tagan_geo_attn_fwd.  Atomic-free and deterministic.  With g->nnz_cap > 0 and g->csr_cpos
+ * (fast-path shapes) on graphs whose K|V rows exceed the caches (n_nodes·H·8 > 512 MB): node pass (delta = rowsum(dO∘O) per head) -> column pass over CSC (dk, dv; dS per edge
+ * into the workspace in CSC order) -> row pass over CSR (dq from dS[csr_cpos[e]], gathering K only).  Otherwise
+ * (or with TAGAN_GEO_BWD_ORDER=row): row pass over CSR (dq, delta) then column pass over CSC (dk, dv).  Both
+ * orders give the same bits.
  * dq/dk/dv: [n_nodes, H] with row stride ld_dqkv (may alias one [n,3H] buffer).
  * dmetric_param: [heads] (gaussian/rbf learnable parameter) or NULL. */
 size_t tagan_geo_attn_bwd_workspace(const tagan_graph* g, int32_t heads, int32_t head_dim);
+/* Process-wide backward order: 0 row-first, 1 column-first (where the graph allows it), 2 by graph size (the
+ * default; env TAGAN_GEO_BWD_ORDER=row|col sets 0|1 at load).  Returns the previous mode, or TAGAN_ERR_ARG.
+ * Change it only between a workspace query and the matching call's completion on no stream. */
+int tagan_geo_set_bwd_order(int32_t mode);
 int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t heads, int32_t head_dim,
                        const void* q, const void* k, const void* v, int64_t ld_qkv,
                        const float* metric_param, float p_drop, uint64_t seed,

@@ -51,6 +51,8 @@ _SIGNATURES = {
     "tagan_part_capacity": (_i64, [_i64, _i32]),
     "tagan_graph_chunks_workspace": (_sz, [_i64]),
     "tagan_graph_chunks": (_c.c_int, [_p, _i64, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
+    "tagan_geo_set_bwd_order": (_c.c_int, [_i32]),
+    "tagan_csr_csc_pos": (_c.c_int, [_p, _p, _i64, _p, _p]),
     "tagan_chunk_order": (_c.c_int, [_p, _i64, _p, _p, _p, _i32, _i32, _p, _p]),
     "tagan_geo_attn_fwd_workspace": (_sz, [_p, _i32, _i32]),
     "tagan_geo_attn_fwd": (_c.c_int, [_c.c_int, _c.c_int, _p, _i32, _i32, _p, _p, _p, _i64, _p, _f32,
@@ -116,7 +118,8 @@ class TaganGraph(ctypes.Structure):
                 ("row_chunk_ptr", _p), ("row_chunk_seg", _p), ("row_chunk_beg", _p), ("row_chunk_part", _p),
                 ("row_multi", _p), ("row_counts", _p),
                 ("col_chunk_ptr", _p), ("col_chunk_seg", _p), ("col_chunk_beg", _p), ("col_chunk_part", _p),
-                ("col_multi", _p), ("col_counts", _p), ("row_chunk_order", _p), ("col_chunk_order", _p)]
+                ("col_multi", _p), ("col_counts", _p), ("row_chunk_order", _p), ("col_chunk_order", _p),
+                ("nnz_cap", _i64), ("csr_cpos", _p)]
 
 
 _lib = None

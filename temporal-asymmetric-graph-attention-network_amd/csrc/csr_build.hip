@@ -132,6 +132,14 @@ __global__ void __launch_bounds__(BLK) k_scatter_csc(const uint32_t* __restrict_
     }
 }
 
+// inverse of csc_eid: the CSC position of each CSR entry (the column-first edge backward reads dS through it)
+__global__ void __launch_bounds__(BLK) k_csc_pos(const int32_t* __restrict__ csc_eid, const int64_t* __restrict__ nnz_p,
+                                                 int32_t* __restrict__ cpos) {
+    const int64_t nnz = *nnz_p;
+    for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * BLK)
+        cpos[csc_eid[p]] = (int32_t)p;
+}
+
 int key_bits(int64_t N) {
     int b = 1;
     while (b < 32 && ((int64_t)1 << b) <= N) ++b;   // values 0..N inclusive (sentinel = N)
@@ -269,6 +277,14 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     k_scatter_csc<<<grid_for(M), BLK, 0, s>>>(ckeys_b, cvals_b, srcq, nnz_out, n_nodes, csc_ptr, csc_row,
                                               csc_eid);
     TAGAN_CHECK_LAUNCH("csr_build.scatter_csc");
+    return TAGAN_OK;
+}
+
+int tagan_csr_csc_pos(const int32_t* csc_eid, const int64_t* nnz, int64_t nnz_cap, int32_t* csr_cpos, void* stream) {
+    using namespace tagan;
+    TAGAN_REQUIRE(csc_eid && nnz && csr_cpos && nnz_cap > 0, TAGAN_ERR_ARG, "csr_csc_pos: bad argument");
+    k_csc_pos<<<grid_for(nnz_cap), BLK, 0, as_stream(stream)>>>(csc_eid, nnz, csr_cpos);
+    TAGAN_CHECK_LAUNCH("csr_csc_pos");
     return TAGAN_OK;
 }
 

@@ -21,8 +21,8 @@
 //   row pass (CSR):    delta_i = Σ_f dO_i·O_i per head, dq_i = Σ_j ds_ij ∂s/∂q_i
 //   column pass (CSC): dk_j = Σ_i ds_ij ∂s/∂k_j,  dv_j = Σ_i α'_ij dO_i
 // with ds_ij = α_ij (dα'_ij·v_j·mask/(1-p) − delta_i), α recomputed from LSE.
-// The row pass writes {lse_i, delta_i} per (node, head) as one packed 8-B record, so the column
-// pass's per-edge gather of both touches one line instead of two (C4: -2 GB of fetch per backward).
+// {lse_i, delta_i} per (node, head) are one packed 8-B record, so the column pass's per-edge gather of both
+// touches one line instead of two (C4: -2 GB of fetch per backward).  Column-first order: see below.
 #include "common.cuh"
 
 namespace tagan {
@@ -196,6 +196,7 @@ struct GeoArgs {
     float* dv;
     int64_t ldd;
     float* delta;
+    float* ds_edge;     // [nnz_cap, heads] dS per edge in CSC order (column-first backward) or null
     float* prm_partial;
     float* part_m;      // [part_cap, heads]
     float* part_l;      // [part_cap, heads]
@@ -591,6 +592,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
                 pw = keep ? p * A.inv_keep : 0.f;
             }
             const float ds = p * (dp - D[u]);
+            if (A.ds_edge && (L.sl % lph) == 0) A.ds_edge[(int64_t)(e0 + jj + u) * A.heads + h] = ds;   // CSC order
             const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
 #pragma unroll
             for (int c = 0; c < FPL; ++c) {
@@ -610,6 +612,117 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
     } else {
         stf<float>(A.part_v2, (int64_t)part * 2 * A.H + f0, dk);
         stf<float>(A.part_v2, (int64_t)part * 2 * A.H + A.H + f0, dv);
+    }
+}
+
+// ------------------------------------------------------------------ backward, column-first order
+// With a per-edge dS buffer the backward runs: node pass (delta_i) -> column pass (dk, dv, and dS_ij stored
+// per CSR edge) -> row pass (dq from the stored dS).  The row pass then gathers only K_j (not K_j and V_j) and
+// reads no O / dO / LSE: 1.5 KB instead of 2 KB of gathers per edge at H = 128 fp32.  dS and delta are the
+// same bits the row-first order computes (same lane layout, same reductions), so dq, dk, dv do not change.
+
+// delta_i = Σ_f dO_i·O_i per head, written with lse_i as the packed {lse, delta} record; rows as "chunks".
+template <int LPR, int FPL, typename S>
+__global__ void __launch_bounds__(BLK) k_geo_bwd_delta(GeoArgs A) {
+    TAGAN_LIVE_SEED(A);
+    Lanes<LPR> L;
+    const bool valid = L.chunk < A.N;
+    if (!__any(valid)) return;
+    const int64_t row = valid ? L.chunk : 0;
+    const int lph = A.d / FPL;
+    const int f0 = L.sl * FPL;
+    const int h = f0 / A.d;
+    float ov[FPL], dov[FPL];
+    ldf<S>(A.o, row * A.H + f0, ov);
+    ldf<S>(A.dout, row * A.H + f0, dov);
+    const float D = grp_sum(dotf(dov, ov), lph);
+    if (valid && (L.sl % lph) == 0)
+        *(float2*)(A.delta + (row * A.heads + h) * 2) = make_float2(A.lse_in[row * A.heads + h], D);
+}
+
+// Row pass from the stored dS: dq_i = Σ_j dS_ij ∂s/∂q_i, gathering K_j only; dS is read through the CSC
+// position of each CSR entry (the column pass writes it sequentially in CSC order, not scattered).
+template <int METRIC, int LPR, int FPL, typename S>
+__global__ void __launch_bounds__(BLK) k_geo_bwd_row_ds(GeoArgs A) {
+    TAGAN_LIVE_SEED(A);
+    constexpr int UN = Unroll<FPL>::v;
+    __shared__ float red[BLK];
+    Lanes<LPR> L;
+    const int nchunks = A.g.row_counts[0];
+    const bool valid = L.chunk < nchunks;
+    if (valid && A.g.row_chunk_order) L.chunk = A.g.row_chunk_order[L.chunk];   // length-sorted order
+    int row = 0, e0 = 0, cnt = 0;
+    if (valid) {
+        row = A.g.row_chunk_seg[L.chunk];
+        e0 = A.g.row_chunk_beg[L.chunk];
+        cnt = min(A.g.chunk, A.g.rowptr[row + 1] - e0);
+    }
+    const int lph = A.d / FPL;
+    const int f0 = L.sl * FPL;
+    const int h = f0 / A.d;
+    float prm_acc = 0.f;
+    if (__any(valid)) {
+        float qv[FPL];
+        ldf<S>(A.q, (int64_t)row * A.ld + f0, qv);
+        float qq = 0.f;
+        if constexpr (MetricTraits<METRIC>::fam == FAM_COS) qq = grp_sum(dotf(qv, qv), lph);
+        const float prm = A.mparam ? A.mparam[h] : 1.f;
+        float dq[FPL];
+#pragma unroll
+        for (int c = 0; c < FPL; ++c) dq[c] = 0.f;
+        int mycol = 0, mypos = 0;
+        for (int jj = 0; __any(jj < cnt); jj += UN) {
+            if ((jj % LPR) == 0) {
+                const bool in = jj + L.sl < cnt;
+                mycol = in ? A.g.col[e0 + jj + L.sl] : 0;
+                mypos = in ? A.g.csr_cpos[e0 + jj + L.sl] : 0;
+            }
+            float kv[UN][FPL], dsv[UN];
+#pragma unroll
+            for (int u = 0; u < UN; ++u) {
+                const int src = L.base + ((jj + u) % LPR);
+                const int j = __shfl(mycol, src, WAVE);
+                const int cp = __shfl(mypos, src, WAVE);
+                ldf<S>(A.k, (int64_t)j * A.ld + f0, kv[u]);
+                dsv[u] = (jj + u < cnt) ? A.ds_edge[(int64_t)cp * A.heads + h] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < UN; ++u) {
+                const bool live = jj + u < cnt;
+                float a, b;
+                pair_partial<METRIC, FPL>(qv, kv[u], a, b);
+                a = grp_sum(a, lph);
+                if constexpr (MetricTraits<METRIC>::fam == FAM_COS) b = grp_sum(b, lph);
+                if (!live) continue;
+                const float s = finalize<METRIC>(a, b, qq, A.inv_sqrt_d, prm);
+                const float ds = dsv[u];
+                const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
+#pragma unroll
+                for (int c = 0; c < FPL; ++c) {
+                    const float qc = qv[c], kc = kv[u][c];
+                    float t = fmaf(g.cq_q, qc, g.cq_k * kc);
+                    if constexpr (MetricTraits<METRIC>::fam == FAM_ABS) t = g.sg * sgnf(qc - kc);
+                    dq[c] += ds * t;
+                }
+                prm_acc = fmaf(ds, g.dprm, prm_acc);
+            }
+        }
+        if (valid) {
+            const int part = A.g.row_chunk_part[L.chunk];
+            if (part < 0) stf<S>(A.dq, (int64_t)row * A.ldd + f0, dq);
+            else stf<float>(A.part_v, (int64_t)part * A.H + f0, dq);
+        }
+    }
+    if (A.prm_partial) {
+        red[threadIdx.x] = (valid && (L.sl % lph) == 0) ? prm_acc : 0.f;
+        __syncthreads();
+        if (threadIdx.x < A.heads) {
+            float sacc = 0.f;
+            const int off = threadIdx.x * lph;              // lane of head threadIdx.x inside a group
+            for (int w = 0; w < BLK / WAVE; ++w)
+                for (int sg = 0; sg < Lanes<LPR>::RPW; ++sg) sacc += red[w * WAVE + sg * LPR + off];
+            A.prm_partial[(int64_t)blockIdx.x * A.heads + threadIdx.x] = sacc;
+        }
     }
 }
 
@@ -810,7 +923,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_generic(GeoArgs A) {
 #define TAGAN_GEO_FPL_BWD 4
 #endif
 
-enum Pass { P_FWD, P_BWD_ROW, P_BWD_COL, P_ALPHA };
+enum Pass { P_FWD, P_BWD_ROW, P_BWD_COL, P_ALPHA, P_BWD_DELTA, P_BWD_ROW_DS };
 
 int pick_lpr(int H, int d) {   // nonzero = fast path
     if (d % 4 != 0) return 0;
@@ -837,7 +950,11 @@ void launch_fast_s(Pass pass, const GeoArgs& A, hipStream_t s) {
     const dim3 g((unsigned)chunk_blocks(A, LPR));
     if (pass == P_FWD) k_geo_fwd_chunk<METRIC, LPR, FPL, S><<<g, BLK, 0, s>>>(A);
     else if (pass == P_BWD_ROW) k_geo_bwd_row_chunk<METRIC, LPR, FPL, S><<<g, BLK, 0, s>>>(A);
-    else k_geo_bwd_col_chunk<METRIC, LPR, FPL, S><<<g, BLK, 0, s>>>(A);
+    else if (pass == P_BWD_ROW_DS) k_geo_bwd_row_ds<METRIC, LPR, FPL, S><<<g, BLK, 0, s>>>(A);
+    else if (pass == P_BWD_DELTA) {
+        const int64_t waves = (A.N + (WAVE / LPR) - 1) / (WAVE / LPR);
+        k_geo_bwd_delta<LPR, FPL, S><<<(unsigned)((waves + (BLK / WAVE) - 1) / (BLK / WAVE)), BLK, 0, s>>>(A);
+    } else k_geo_bwd_col_chunk<METRIC, LPR, FPL, S><<<g, BLK, 0, s>>>(A);
 }
 
 template <int METRIC, int LPR, int FPL>
@@ -946,8 +1063,26 @@ size_t fwd_ws(const tagan_graph* g, int heads, int d) {
 }
 
 struct BwdWs {
-    size_t delta, prm, pv, pv2, total;
+    size_t delta, prm, pv, pv2, ds, total;
+    bool col_first;
 };
+
+// Backward order.  Column-first (node pass -> column pass storing dS -> row pass from dS) saves the row pass's V_j
+// gathers at the price of a node pass over O and dO and a dS round trip; it pays where the gathers miss the caches:
+// C4 backward 8.8 -> 7.7 ms, while at C2 (its K|V rows mostly served by L2 / Infinity Cache) it measured 0.04 ms per
+// layer slower (profiles/r2_geo_bwd_order_ab.txt).  Default: column-first when the graph's K|V rows at fp32
+// (N·H·8 bytes) exceed 512 MB, twice the 256-MB Infinity Cache.  TAGAN_GEO_BWD_ORDER=row|col forces an order
+// (A/B; read at load time) and tagan_geo_set_bwd_order() sets it.  The choice depends on the graph and H only,
+// so the workspace query agrees with the call.
+int g_bwd_order = [] {
+    const char* e = getenv("TAGAN_GEO_BWD_ORDER");
+    return (e && strcmp(e, "row") == 0) ? 0 : (e && strcmp(e, "col") == 0) ? 1 : 2;
+}();
+
+bool col_first_wanted(int64_t N, int H) {
+    const int mode = __atomic_load_n(&g_bwd_order, __ATOMIC_RELAXED);
+    return mode == 2 ? (double)N * H * 8.0 > 512.0 * 1024 * 1024 : mode == 1;
+}
 
 BwdWs bwd_ws(const tagan_graph* g, int heads, int d) {
     BwdWs w{};
@@ -965,6 +1100,8 @@ BwdWs bwd_ws(const tagan_graph* g, int heads, int d) {
     w.prm = take((size_t)nprm * heads * 4);
     w.pv = take(lpr ? (size_t)g->part_cap * H * 4 : 0);
     w.pv2 = take(lpr ? (size_t)g->part_cap * 2 * H * 4 : 0);
+    w.col_first = lpr && g->nnz_cap > 0 && g->csr_cpos && col_first_wanted(g->n_nodes, H);
+    w.ds = take(w.col_first ? (size_t)g->nnz_cap * heads * 4 : 0);
     w.total = off;
     return w;
 }
@@ -1019,6 +1156,11 @@ int tagan_geo_attn_fwd(int dtype, int metric, const tagan_graph* g, int32_t head
     return TAGAN_OK;
 }
 
+int tagan_geo_set_bwd_order(int32_t mode) {
+    TAGAN_REQUIRE(mode >= 0 && mode <= 2, TAGAN_ERR_ARG, "geo_set_bwd_order: mode %d", mode);
+    return __atomic_exchange_n(&tagan::g_bwd_order, mode, __ATOMIC_RELAXED);
+}
+
 size_t tagan_geo_attn_bwd_workspace(const tagan_graph* g, int32_t heads, int32_t head_dim) {
     if (!g || g->n_nodes <= 0 || heads <= 0 || head_dim <= 0) return 0;
     return tagan::bwd_ws(g, heads, head_dim).total;
@@ -1062,30 +1204,47 @@ int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t head
     A.part_v = (float*)(ws + w.pv);
     A.part_v2 = (float*)(ws + w.pv2);
     hipStream_t s = as_stream(stream);
-    rc = launch(metric, P_BWD_ROW, lpr, A, s);
-    if (rc) return rc;
-    TAGAN_CHECK_LAUNCH("geo_attn_bwd_row");
     const unsigned gm = (unsigned)((g->part_cap + (BLK / WAVE) - 1) / (BLK / WAVE));
-    if (lpr) {
-        if (A.bf16)
-            k_geo_sum_parts<bf16s><<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr,
-                                                      g->row_chunk_part, A.part_v, H, A.dq, A.dq, A.ldd, H);
-        else
-            k_geo_sum_parts<float><<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr,
-                                                      g->row_chunk_part, A.part_v, H, A.dq, A.dq, A.ldd, H);
-        TAGAN_CHECK_LAUNCH("geo_attn_bwd_row_merge");
-    }
-    rc = launch(metric, P_BWD_COL, lpr, A, s);
-    if (rc) return rc;
-    TAGAN_CHECK_LAUNCH("geo_attn_bwd_col");
-    if (lpr) {
+    auto sum_cols = [&]() {
         if (A.bf16)
             k_geo_sum_parts<bf16s><<<gm, BLK, 0, s>>>(g->col_counts, g->col_multi, g->col_chunk_ptr,
                                                       g->col_chunk_part, A.part_v2, 2 * H, A.dk, A.dv, A.ldd, H);
         else
             k_geo_sum_parts<float><<<gm, BLK, 0, s>>>(g->col_counts, g->col_multi, g->col_chunk_ptr,
                                                       g->col_chunk_part, A.part_v2, 2 * H, A.dk, A.dv, A.ldd, H);
-        TAGAN_CHECK_LAUNCH("geo_attn_bwd_col_merge");
+        return hipGetLastError();
+    };
+    auto sum_rows = [&]() {
+        if (A.bf16)
+            k_geo_sum_parts<bf16s><<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr,
+                                                      g->row_chunk_part, A.part_v, H, A.dq, A.dq, A.ldd, H);
+        else
+            k_geo_sum_parts<float><<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr,
+                                                      g->row_chunk_part, A.part_v, H, A.dq, A.dq, A.ldd, H);
+        return hipGetLastError();
+    };
+    if (w.col_first) {
+        A.ds_edge = (float*)(ws + w.ds);
+        rc = launch(metric, P_BWD_DELTA, lpr, A, s);
+        if (rc) return rc;
+        TAGAN_CHECK_LAUNCH("geo_attn_bwd_delta");
+        rc = launch(metric, P_BWD_COL, lpr, A, s);
+        if (rc) return rc;
+        TAGAN_CHECK_LAUNCH("geo_attn_bwd_col");
+        TAGAN_CHECK_HIP(sum_cols(), "geo_attn_bwd_col_merge");
+        rc = launch(metric, P_BWD_ROW_DS, lpr, A, s);
+        if (rc) return rc;
+        TAGAN_CHECK_LAUNCH("geo_attn_bwd_row_ds");
+        TAGAN_CHECK_HIP(sum_rows(), "geo_attn_bwd_row_merge");
+    } else {   // row pass (dq, delta) -> column pass (dk, dv)
+        rc = launch(metric, P_BWD_ROW, lpr, A, s);
+        if (rc) return rc;
+        TAGAN_CHECK_LAUNCH("geo_attn_bwd_row");
+        if (lpr) TAGAN_CHECK_HIP(sum_rows(), "geo_attn_bwd_row_merge");
+        rc = launch(metric, P_BWD_COL, lpr, A, s);
+        if (rc) return rc;
+        TAGAN_CHECK_LAUNCH("geo_attn_bwd_col");
+        if (lpr) TAGAN_CHECK_HIP(sum_cols(), "geo_attn_bwd_col_merge");
     }
     if (dmetric_param) {
         if (want_prm) {

@@ -68,6 +68,8 @@ class SnapshotGraph:
     chunk: int = CHUNK
     chunk_cap: int = 0
     part_cap: int = 0
+    nnz_cap: int = 0               # capacity of col / csc arrays (sizes the backward's per-edge dS buffer)
+    csr_cpos: Optional[torch.Tensor] = None   # CSC position of each CSR entry (column-first edge backward)
     _struct: object = None
     pending_err: object = None     # (pinned int32 flag, event) of a deferred index validation
 
@@ -91,7 +93,8 @@ class SnapshotGraph:
             self._struct = _lib.TaganGraph(self.num_nodes, p(self.rowptr), p(self.col), p(self.csc_ptr),
                                            p(self.csc_row), p(self.csc_eid), self.chunk, self.chunk_cap,
                                            self.part_cap, *[p(t) for t in r], *[p(t) for t in c],
-                                           *[None if t is None else p(t) for t in (self.row_order, self.col_order)])
+                                           *[None if t is None else p(t) for t in (self.row_order, self.col_order)],
+                                           self.nnz_cap, None if self.csr_cpos is None else p(self.csr_cpos))
         return ctypes.byref(self._struct)
 
 
@@ -122,6 +125,10 @@ def _finish(g: SnapshotGraph, nnz_cap: int, chunk: int = CHUNK) -> SnapshotGraph
     g.row_chunks, g.chunk_cap, g.part_cap, g.row_order = _chunk_lists(g.rowptr, g.num_nodes, nnz_cap, chunk)
     g.col_chunks, _, _, g.col_order = _chunk_lists(g.csc_ptr, g.num_nodes, nnz_cap, chunk)
     g.chunk = chunk
+    g.nnz_cap = nnz_cap
+    g.csr_cpos = torch.empty(nnz_cap, dtype=torch.int32, device=g.csc_eid.device)
+    check(lib().tagan_csr_csc_pos(ptr(g.csc_eid), ptr(g.nnz), nnz_cap, ptr(g.csr_cpos), stream_of(g.csc_eid)),
+          "tagan_csr_csc_pos")
     return g
 
 

@@ -369,3 +369,41 @@ def test_chunk_order_is_a_length_sorted_permutation_and_results_do_not_depend_on
         res.append((out.detach(), x.grad))
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("metric", ["euclidean", "cosine_similarity", "manhattan", "gaussian_kernel"])
+@pytest.mark.parametrize("chunk", [4, 64])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_geo_backward_orders_are_bitwise_identical(dev, metric, chunk, dtype):
+    """Column-first backward (node pass -> CSC pass storing dS per edge -> CSR pass from dS, gathering K only)
+    against the row-first order (graph without nnz_cap): same delta, same dS bits, so dq, dk, dv and the metric
+    parameter gradient are bitwise identical, with dropout, hub rows split over many chunks, and bf16 storage."""
+    from tagan_amd import _lib
+    from tagan_amd.fused import GeoCore
+    from tagan_amd.kernels import build_graph
+    counts = [300, 257]
+    eis = [_hub_graph(n, 21 + i) for i, n in enumerate(counts)]
+    N, H, heads = sum(counts), 128, 8
+    g = torch.Generator().manual_seed(4)
+    qkv = (torch.randn(N, 3 * H, generator=g) * 0.5).to(dev, dtype)
+    gout = torch.randn(N, H, generator=g).to(dev, dtype)
+    param = torch.linspace(0.7, 1.3, heads).to(dev) if metric == "gaussian_kernel" else None
+    graph = build_graph([e.to(dev) for e in eis], counts, chunk=chunk)
+    assert graph.nnz_cap > 0
+    core = GeoCore(graph, _lib.METRIC_IDS[metric], heads, 0.1, 1234)
+    L = _lib.lib()
+    res = []
+    for mode in (1, 0):                                # column-first, then row-first
+        prev = L.tagan_geo_set_bwd_order(mode)
+        try:
+            out, saved = core.fwd(qkv, param, None)
+            dqkv, dprm, _ = core.bwd(qkv, out, saved, gout, param is not None, False)
+            torch.cuda.synchronize()
+        finally:
+            L.tagan_geo_set_bwd_order(prev)
+        res.append((out, dqkv, dprm))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.isfinite(res[0][1].float()).all()
+    assert torch.equal(res[0][1], res[1][1])
+    if param is not None:
+        assert torch.equal(res[0][2], res[1][2])

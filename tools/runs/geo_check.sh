@@ -13,6 +13,9 @@ tail -2 $OUT/gpu_tests.log
 timeout -k 10 200 python bench.py --roofline-only --roofline-reps 10 > $OUT/roof.json 2> $OUT/roof.err \
     || { tail -20 $OUT/roof.err; exit 1; }
 cat $OUT/roof.json
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-roofline --no-c1 > $OUT/bench.json 2> $OUT/bench.err \
+    || { tail -20 $OUT/bench.err; exit 1; }
+python -c "import json; d=json.load(open('$OUT/bench.json')); print('C2', d['ms_per_step'], 'ms; bf16', d['alt_precision']['ms_per_step'], 'ms', d['breakdown'])"
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_c4 -o run -- \
     python bench.py --roofline-only --roofline-reps 10 > $OUT/stats_c4.log 2>&1 || { tail -20 $OUT/stats_c4.log; exit 1; }
