@@ -140,6 +140,15 @@ __global__ void __launch_bounds__(BLK) k_csc_pos(const int32_t* __restrict__ csc
         cpos[csc_eid[p]] = (int32_t)p;
 }
 
+// CSC sort (32-bit dst keys over key_bits(N) bits, int32 values): 10-bit digits instead of rocPRIM's default 8 --
+// two onesweep passes instead of three at N < 2^20.  3.2M pairs / 19 bits (C2): 129 -> 105 us; the CSR key sort
+// stays on the default (11-bit digits measured slower there: 142 vs 180 us; tools/probes/sort_probe.hip).
+using CscSortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 32>, rocprim::kernel_config<1024, 12>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+
 int key_bits(int64_t N) {
     int b = 1;
     while (b < 32 && ((int64_t)1 << b) <= N) ++b;   // values 0..N inclusive (sentinel = N)
@@ -169,8 +178,8 @@ CsrWs plan(int64_t E, int64_t N) {
     (void)rocprim::radix_sort_keys(nullptr, t1, (uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)M, 0, 64);
     (void)rocprim::radix_sort_keys(nullptr, t1b, (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)M, 0, 32);
     t1 = std::max(t1, t1b);
-    (void)rocprim::radix_sort_pairs(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
-                              (int32_t*)nullptr, (size_t)M, 0, bits);
+    (void)rocprim::radix_sort_pairs<CscSortCfg>(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
+                                                (int32_t*)nullptr, (size_t)M, 0, bits);
     (void)rocprim::exclusive_scan(nullptr, t3, (int32_t*)nullptr, (int32_t*)nullptr, 0, (size_t)M,
                             rocprim::plus<int32_t>());
     w.temp_bytes = std::max(t1, std::max(t2, t3));
@@ -271,8 +280,8 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     k_fill_tail<<<grid_for(M), BLK, 0, s>>>(ckeys_a, cvals_a, nnz_out, M, n_nodes);
     TAGAN_CHECK_LAUNCH("csr_build.fill_tail");
     tb = w.temp_bytes;
-    TAGAN_CHECK_HIP(rocprim::radix_sort_pairs(temp, tb, ckeys_a, ckeys_b, cvals_a, cvals_b, (size_t)M, 0,
-                                              bits, s),
+    TAGAN_CHECK_HIP(rocprim::radix_sort_pairs<CscSortCfg>(temp, tb, ckeys_a, ckeys_b, cvals_a, cvals_b, (size_t)M, 0,
+                                                          bits, s),
                     "csr_build radix_sort_pairs");
     k_scatter_csc<<<grid_for(M), BLK, 0, s>>>(ckeys_b, cvals_b, srcq, nnz_out, n_nodes, csc_ptr, csc_row,
                                               csc_eid);
