@@ -463,6 +463,20 @@ size_t tagan_colsum_workspace(int64_t M, int32_t N);
 int tagan_colsum(int dtype, int64_t M, int32_t N, const void* x, int64_t ld, float* out, void* workspace,
                  size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Projection-parameter packing.  Replaces the per-step torch.cat of q_linear / k_linear / v_linear
+ * (geometric_attention.py:263-266, temporal_attention.py:356-359 -- the reference calls the three Linears
+ * separately; the fused block multiplies by their concatenation).
+ * pack:   w[r, c] (row stride ld_w) = [Wq; Wk; Wv][r, c] for c < H; with bias_col: w[r, H] = [bq; bk; bv][r] and
+ *         w[r, H+1 .. ld_w-1] = 0 (the augmented QKV GEMM operand); b (optional) = [bq; bk; bv].
+ * unpack: dwq | dwk | dwv [H, H] = row blocks of dw (row stride ld_dw), dbq | dbk | dbv [H] = db[r * db_stride];
+ *         any output (or dw / db) may be NULL.
+ * ------------------------------------------------------------------------- */
+int tagan_qkv_pack(int64_t H, const float* wq, const float* wk, const float* wv, const float* bq, const float* bk,
+                   const float* bv, float* w, int64_t ld_w, int32_t bias_col, float* b, void* stream);
+int tagan_qkv_unpack(int64_t H, const float* dw, int64_t ld_dw, const float* db, int64_t db_stride, float* dwq,
+                     float* dwk, float* dwv, float* dbq, float* dbk, float* dbv, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -52,6 +52,8 @@ _SIGNATURES = {
     "tagan_graph_chunks_workspace": (_sz, [_i64]),
     "tagan_graph_chunks": (_c.c_int, [_p, _i64, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
     "tagan_geo_set_bwd_order": (_c.c_int, [_i32]),
+    "tagan_qkv_pack": (_c.c_int, [_i64, _p, _p, _p, _p, _p, _p, _p, _i64, _i32, _p, _p]),
+    "tagan_qkv_unpack": (_c.c_int, [_i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, _p]),
     "tagan_csr_csc_pos": (_c.c_int, [_p, _p, _i64, _p, _p]),
     "tagan_chunk_order": (_c.c_int, [_p, _i64, _p, _p, _p, _i32, _i32, _p, _p]),
     "tagan_geo_attn_fwd_workspace": (_sz, [_p, _i32, _i32]),

@@ -247,6 +247,8 @@ def _wgrad(dy, x, bf, rows: int = 2048):
 
 
 # ----------------------------------------------------------------------------- the fused block
+# TAGAN_QKV_PACK=0: torch.cat of the q/k/v parameters per block instead of PackQKVFn's one-launch pack (A/B)
+QKV_PACK = os.environ.get("TAGAN_QKV_PACK", "1") != "0"
 # TAGAN_QKV_AUG=0: QKV GEMM with the hipBLASLt bias epilogue instead of the bias-as-weight-column form (A/B)
 QKV_AUG = os.environ.get("TAGAN_QKV_AUG", "1") != "0"
 # TAGAN_OUT_BIAS_LN=0: out-projection bias in the GEMM epilogue instead of the closing LayerNorm (A/B)
@@ -396,7 +398,8 @@ class AttnBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, p1, p2, ln1_w, ln1_b, w_qkv, b_qkv, w_o, b_o, ln2_w, ln2_b, core, eps1: float,
-                eps2: float, p_out: float, seed_out: int, lns_w=None, lns_b=None, eps_s: float = 1e-5, sink=None):
+                eps2: float, p_out: float, seed_out: int, lns_w=None, lns_b=None, eps_s: float = 1e-5, sink=None,
+                w_aug_packed=None):
         require_hip(x)
         H = x.shape[-1]
         x2 = x.reshape(-1, H).contiguous()
@@ -414,7 +417,9 @@ class AttnBlockFn(torch.autograd.Function):
             # hipBLASLt (tools/runs/qkv_aug.sh); with bf16 operands the epilogue form is the faster one
             h_aug = torch.empty(x2.shape[0], H + 4, device=x2.device)
             _, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False, y=h_aug)
-            w_aug = torch.cat([w_qkv, b_qkv[:, None], w_qkv.new_zeros(w_qkv.shape[0], 3)], 1)
+            w_aug = w_aug_packed   # [W | b | 0 0 0] from PackQKVFn, else concatenated here
+            if w_aug is None:
+                w_aug = torch.cat([w_qkv, b_qkv[:, None], w_qkv.new_zeros(w_qkv.shape[0], 3)], 1)
             qkv = h_aug @ w_aug.t()
             h = h_aug[:, :H]
         else:
@@ -433,6 +438,7 @@ class AttnBlockFn(torch.autograd.Function):
             ctx.inter = (h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
             ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, proj)
             ctx.sink = sink
+            ctx.packed_aug = False
             return y.view(x.shape)
         if OUT_BIAS_LN:   # out-projection bias added in the closing LayerNorm (no GEMM epilogue)
             o, b_o_ln = _mm(cg, w_o.t(), bf), b_o
@@ -448,6 +454,7 @@ class AttnBlockFn(torch.autograd.Function):
         ctx.inter = (h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
         ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, False)
         ctx.sink = sink
+        ctx.packed_aug = h_aug is not None and w_aug_packed is not None
         return y.view(x.shape)
 
     @staticmethod
@@ -490,7 +497,9 @@ class AttnBlockFn(torch.autograd.Function):
             # dqkvᵀ·[h | 1 0 0 0]: column H of the product is the column sum of dqkv (the bias gradient)
             # -- 4 more GEMM columns instead of a 491 MB column-sum pass at C2
             dw_aug = _wgrad(dqkv, h_aug, bf, WGRAD_ROWS_QKV)
-            dw_qkv, db_qkv = dw_aug[:, :H].contiguous(), dw_aug[:, H].contiguous()
+            dw_qkv, db_qkv = dw_aug[:, :H], dw_aug[:, H]          # views: PackQKVFn unpacks them in one launch
+            if not ctx.packed_aug:
+                dw_qkv, db_qkv = dw_qkv.contiguous(), db_qkv.contiguous()
         else:
             db_qkv = (db_core if db_core is not None else colsum(dqkv)) if ng[6] else None
             dw_qkv = None
@@ -500,7 +509,7 @@ class AttnBlockFn(torch.autograd.Function):
             dx, dg1, db1 = proj_ln_bwd(dqkv, w_qkv, x2, mean1, rstd1, ln1_w, dres)
             ctx.inter = None
             return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
-                    None, None, None, None, None, dgs, dbs, None, None)
+                    None, None, None, None, None, dgs, dbs, None, None, None)
         if bf:
             dqkv = _b(dqkv)
         dh = _mm(dqkv, w_qkv, bf)
@@ -510,23 +519,68 @@ class AttnBlockFn(torch.autograd.Function):
         dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
         ctx.inter = None
         return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
-                None, None, None, None, None, dgs, dbs, None, None)
+                None, None, None, None, None, dgs, dbs, None, None, None)
+
+
+class PackQKVFn(torch.autograd.Function):
+    """[W_q; W_k; W_v] and [b_q; b_k; b_v] in one launch (csrc/params.hip), the parameter gradients unpacked in one
+    launch (they arrive as views of the block's augmented weight gradient).  ``aug``: the same launch also writes
+    [W | b | 0 0 0] ([3H, H + 4], the fp32 augmented QKV GEMM operand), returned as a third, non-differentiable
+    output; W and b stay contiguous so every GEMM keeps the shapes (and leading dimensions) of the tuned table."""
+
+    @staticmethod
+    def forward(ctx, wq, wk, wv, bq, bk, bv, aug: bool):
+        H = wq.shape[1]
+        dev = wq.device
+        args = [ptr(t.contiguous()) for t in (wq, wk, wv, bq, bk, bv)]
+        w = torch.empty(3 * H, H, device=dev)
+        b = torch.empty(3 * H, device=dev)
+        st = stream_of(wq)
+        check(lib().tagan_qkv_pack(H, *args, ptr(w), H, 0, ptr(b), st), "tagan_qkv_pack")
+        w_aug = None
+        if aug:
+            w_aug = torch.empty(3 * H, H + 4, device=dev)
+            check(lib().tagan_qkv_pack(H, *args, ptr(w_aug), H + 4, 1, None, st), "tagan_qkv_pack")
+            ctx.mark_non_differentiable(w_aug)
+        ctx.H = H
+        return w, b, w_aug
+
+    @staticmethod
+    def backward(ctx, dw, db, _unused):
+        H = ctx.H
+        ng = ctx.needs_input_grad
+        ref = dw if dw is not None else db
+        outs = [torch.empty(H, H, device=ref.device) if (ng[i] and dw is not None) else None for i in range(3)] + \
+               [torch.empty(H, device=ref.device) if (ng[3 + i] and db is not None) else None for i in range(3)]
+        if dw is not None and dw.stride(1) != 1:
+            dw = dw.contiguous()
+        check(lib().tagan_qkv_unpack(H, ptr(dw), dw.stride(0) if dw is not None else H, ptr(db),
+                                     db.stride(0) if db is not None else 1, *[ptr(t) for t in outs],
+                                     stream_of(ref)), "tagan_qkv_unpack")
+        return (*outs, None)
 
 
 def attention_block(x, core, p1: Optional[torch.Tensor], p2: Optional[torch.Tensor], ln1, q_lin, k_lin, v_lin,
                     out_lin, ln2, p_out: float, seed_out: int, skip_ln=None):
     """``skip_ln``: a LayerNorm whose output of the block input is added to the block output
     (TAGAN's first geometric layer, model.py:258-262), fused into the closing LayerNorm."""
-    w_qkv = torch.cat([q_lin.weight, k_lin.weight, v_lin.weight], 0)
-    b_qkv = torch.cat([q_lin.bias, k_lin.bias, v_lin.bias], 0)
+    H = q_lin.weight.shape[1]
+    w_aug = None
+    if QKV_PACK and x.is_cuda and q_lin.weight.dtype == torch.float32 and not WGRAD_ASYNC:
+        aug = QKV_AUG and _PREC == "fp32" and not (_proj_ok(H, False) and "qkv" in PROJ_SET)
+        w_qkv, b_qkv, w_aug = PackQKVFn.apply(q_lin.weight, k_lin.weight, v_lin.weight, q_lin.bias, k_lin.bias,
+                                              v_lin.bias, aug)
+    else:
+        w_qkv = torch.cat([q_lin.weight, k_lin.weight, v_lin.weight], 0)
+        b_qkv = torch.cat([q_lin.bias, k_lin.bias, v_lin.bias], 0)
     sink = WGradSink(q_lin, k_lin, v_lin, out_lin) if WGRAD_ASYNC else None
     if skip_ln is not None:
         return AttnBlockFn.apply(x, p1, p2, ln1.weight, ln1.bias, w_qkv, b_qkv, out_lin.weight, out_lin.bias,
                                  ln2.weight, ln2.bias, core, ln1.eps, ln2.eps, float(p_out), seed_out,
-                                 skip_ln.weight, skip_ln.bias, skip_ln.eps, sink)
+                                 skip_ln.weight, skip_ln.bias, skip_ln.eps, sink, w_aug)
     return AttnBlockFn.apply(x, p1, p2, ln1.weight, ln1.bias, w_qkv, b_qkv, out_lin.weight, out_lin.bias,
                              ln2.weight, ln2.bias, core, ln1.eps, ln2.eps, float(p_out), seed_out,
-                             None, None, 1e-5, sink)
+                             None, None, 1e-5, sink, w_aug)
 
 
 def fusable(x: torch.Tensor, use_layer_norm: bool) -> bool:
