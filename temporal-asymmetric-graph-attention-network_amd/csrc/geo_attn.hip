@@ -371,40 +371,94 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
     }
 }
 
-// Merge the partial softmax states of multi-chunk rows, in chunk order.  One wave per row,
-// lane owns 4 features (H <= 256).
+// Merge of multi-chunk segments (hub rows / columns).  A wave per segment, persistent over segments (the grid is
+// bounded: the partial capacity is a worst case, most of it unused).  A lane owns 4 features; the wave's
+// 64 / (width / 4) lane groups ("phases") take interleaved chunks, and each lane keeps MG independent partial states
+// over its chunks, so MG·phases partial loads are in flight instead of one dependent chain per chunk (a C2 hub row
+// spans ~100 chunks).  The states combine in a fixed order (accumulators, then phases by xor-shuffle): the result
+// is deterministic (bitwise reproducible), in another summation order than a chunk-serial loop.
+constexpr int MG = 4;
+struct SoftState {
+    float m, l;
+    float4 a;
+};
+
+__device__ __forceinline__ SoftState soft_merge(const SoftState& x, const SoftState& y) {
+    const float mn = fmaxf(x.m, y.m);
+    const float cx = (x.m == -INFINITY) ? 0.f : __expf(x.m - mn);
+    const float cy = (y.m == -INFINITY) ? 0.f : __expf(y.m - mn);
+    SoftState r;
+    r.m = mn;
+    r.l = x.l * cx + y.l * cy;
+    r.a = make_float4(x.a.x * cx + y.a.x * cy, x.a.y * cx + y.a.y * cy, x.a.z * cx + y.a.z * cy,
+                      x.a.w * cx + y.a.w * cy);
+    return r;
+}
+
+__device__ __forceinline__ SoftState soft_shfl_xor(const SoftState& x, int mask) {
+    SoftState r;
+    r.m = __shfl_xor(x.m, mask, WAVE);
+    r.l = __shfl_xor(x.l, mask, WAVE);
+    r.a = make_float4(__shfl_xor(x.a.x, mask, WAVE), __shfl_xor(x.a.y, mask, WAVE), __shfl_xor(x.a.z, mask, WAVE),
+                      __shfl_xor(x.a.w, mask, WAVE));
+    return r;
+}
+
+__device__ __forceinline__ float4 f4add(const float4& x, const float4& y) {
+    return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+}
+
+__device__ __forceinline__ float4 f4shfl_xor(const float4& x, int mask) {
+    return make_float4(__shfl_xor(x.x, mask, WAVE), __shfl_xor(x.y, mask, WAVE), __shfl_xor(x.z, mask, WAVE),
+                       __shfl_xor(x.w, mask, WAVE));
+}
+
+unsigned merge_grid(int64_t part_cap) {
+    const int64_t b = (part_cap + (BLK / WAVE) - 1) / (BLK / WAVE);
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(b, 1024));
+}
+
+// Merge the partial softmax states {m, l, acc} of multi-chunk rows (H <= 256).
 template <typename S>
 __global__ void __launch_bounds__(BLK) k_geo_fwd_merge(GeoArgs A) {
     TAGAN_LIVE_SEED(A);
     using IO = Io<S>;
-    const int64_t k = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6);
-    if (k >= A.g.row_counts[1]) return;
     const int lane = threadIdx.x & (WAVE - 1);
-    const int f0 = lane * 4;
-    if (f0 >= A.H) return;
+    const int lanes = A.H / 4;                              // lanes per phase (<= 64)
+    const int nph = WAVE / lanes;                           // phases
+    const int ph = lane / lanes;
+    const int f0 = (lane % lanes) * 4;
     const int h = f0 / A.d;
-    const int row = A.g.row_multi[k];
-    const int c0 = A.g.row_chunk_ptr[row], c1 = A.g.row_chunk_ptr[row + 1];
-    float M = -INFINITY, Lsum = 0.f;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int c = c0; c < c1; ++c) {
-        const int part = A.g.row_chunk_part[c];
-        const float m = A.part_m[(int64_t)part * A.heads + h];
-        const float l = A.part_l[(int64_t)part * A.heads + h];
-        const float4 a = ld4(A.part_v + (int64_t)part * A.H + f0);
-        const float mn = fmaxf(M, m);
-        const float ca = (M == -INFINITY) ? 0.f : __expf(M - mn);
-        const float cb = (m == -INFINITY) ? 0.f : __expf(m - mn);
-        Lsum = Lsum * ca + l * cb;
-        acc.x = acc.x * ca + a.x * cb;
-        acc.y = acc.y * ca + a.y * cb;
-        acc.z = acc.z * ca + a.z * cb;
-        acc.w = acc.w * ca + a.w * cb;
-        M = mn;
+    const int64_t nmulti = A.g.row_counts[1];
+    const int64_t stride = (int64_t)gridDim.x * (BLK / WAVE);
+    for (int64_t k = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6); k < nmulti; k += stride) {
+        const int row = A.g.row_multi[k];
+        const int c0 = A.g.row_chunk_ptr[row], c1 = A.g.row_chunk_ptr[row + 1];
+        SoftState st[MG];
+#pragma unroll
+        for (int u = 0; u < MG; ++u) st[u] = SoftState{-INFINITY, 0.f, make_float4(0.f, 0.f, 0.f, 0.f)};
+        for (int c = c0 + ph; c < c1; c += nph * MG) {
+#pragma unroll
+            for (int u = 0; u < MG; ++u) {
+                const int cc = c + u * nph;
+                if (cc < c1) {
+                    const int part = A.g.row_chunk_part[cc];
+                    SoftState y;
+                    y.m = A.part_m[(int64_t)part * A.heads + h];
+                    y.l = A.part_l[(int64_t)part * A.heads + h];
+                    y.a = ld4(A.part_v + (int64_t)part * A.H + f0);
+                    st[u] = soft_merge(st[u], y);
+                }
+            }
+        }
+        SoftState r = soft_merge(soft_merge(st[0], st[1]), soft_merge(st[2], st[3]));
+        for (int m = lanes; m < WAVE; m <<= 1) r = soft_merge(r, soft_shfl_xor(r, m));   // phases, fixed order
+        if (ph == 0) {
+            const float inv = (r.l > 0.f) ? 1.f / r.l : NAN;
+            IO::st(A.out, (int64_t)row * A.H + f0, make_float4(r.a.x * inv, r.a.y * inv, r.a.z * inv, r.a.w * inv));
+            if ((f0 / 4) % A.lph == 0) A.lse[(int64_t)row * A.heads + h] = r.m + __logf(r.l);
+        }
     }
-    const float inv = (Lsum > 0.f) ? 1.f / Lsum : NAN;
-    IO::st(A.out, (int64_t)row * A.H + f0, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
-    if ((lane % A.lph) == 0) A.lse[(int64_t)row * A.heads + h] = M + __logf(Lsum);
 }
 
 // ------------------------------------------------------------------ backward, row pass (CSR chunks)
@@ -497,7 +551,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
     }
 }
 
-// Sum partial rows (bwd row: dq; bwd col: dk|dv) of multi-chunk segments in chunk order.
+// Sum partial rows (bwd row: dq; bwd col: dk|dv) of multi-chunk segments; same lane / phase / MG-accumulator
+// scheme and bounded persistent grid as k_geo_fwd_merge, fixed combination order.
 template <typename S>
 __global__ void __launch_bounds__(BLK) k_geo_sum_parts(const int32_t* __restrict__ counts,
                                                        const int32_t* __restrict__ multi,
@@ -506,19 +561,34 @@ __global__ void __launch_bounds__(BLK) k_geo_sum_parts(const int32_t* __restrict
                                                        const float* __restrict__ part, int width,
                                                        void* __restrict__ dst0, void* __restrict__ dst1,
                                                        int64_t ldd, int H) {
-    const int64_t k = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6);
-    if (k >= counts[1]) return;
     const int lane = threadIdx.x & (WAVE - 1);
-    const int seg = multi[k];
-    const int c0 = chunk_ptr[seg], c1 = chunk_ptr[seg + 1];
-    for (int f0 = lane * 4; f0 < width; f0 += WAVE * 4) {
-        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int c = c0; c < c1; ++c) {
-            const float4 a = ld4(part + (int64_t)chunk_part[c] * width + f0);
-            s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    const int lanes = min(width / 4, WAVE);                 // lanes per phase
+    const int nph = WAVE / lanes;
+    const int ph = lane / lanes;
+    const int64_t nmulti = counts[1];
+    const int64_t stride = (int64_t)gridDim.x * (BLK / WAVE);
+    for (int64_t k = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6); k < nmulti; k += stride) {
+        const int seg = multi[k];
+        const int c0 = chunk_ptr[seg], c1 = chunk_ptr[seg + 1];
+        for (int fb = 0; fb < width; fb += lanes * 4) {
+            const int f0 = fb + (lane % lanes) * 4;
+            float4 acc[MG];
+#pragma unroll
+            for (int u = 0; u < MG; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int c = c0 + ph; c < c1; c += nph * MG) {
+#pragma unroll
+                for (int u = 0; u < MG; ++u) {
+                    const int cc = c + u * nph;
+                    if (cc < c1) acc[u] = f4add(acc[u], ld4(part + (int64_t)chunk_part[cc] * width + f0));
+                }
+            }
+            float4 sum = f4add(f4add(acc[0], acc[1]), f4add(acc[2], acc[3]));
+            for (int m = lanes; m < WAVE; m <<= 1) sum = f4add(sum, f4shfl_xor(sum, m));
+            if (ph == 0) {
+                if (f0 < H) Io<S>::st(dst0, (int64_t)seg * ldd + f0, sum);
+                else Io<S>::st(dst1, (int64_t)seg * ldd + (f0 - H), sum);
+            }
         }
-        if (f0 < H) Io<S>::st(dst0, (int64_t)seg * ldd + f0, s);
-        else Io<S>::st(dst1, (int64_t)seg * ldd + (f0 - H), s);
     }
 }
 
@@ -1143,7 +1213,7 @@ int tagan_geo_attn_fwd(int dtype, int metric, const tagan_graph* g, int32_t head
     if (rc) return rc;
     TAGAN_CHECK_LAUNCH("geo_attn_fwd");
     if (lpr) {
-        const unsigned gm = (unsigned)((g->part_cap + (BLK / WAVE) - 1) / (BLK / WAVE));
+        const unsigned gm = merge_grid(g->part_cap);
         if (A.bf16) k_geo_fwd_merge<bf16s><<<gm, BLK, 0, s>>>(A);
         else k_geo_fwd_merge<float><<<gm, BLK, 0, s>>>(A);
         TAGAN_CHECK_LAUNCH("geo_attn_fwd_merge");
@@ -1204,7 +1274,7 @@ int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t head
     A.part_v = (float*)(ws + w.pv);
     A.part_v2 = (float*)(ws + w.pv2);
     hipStream_t s = as_stream(stream);
-    const unsigned gm = (unsigned)((g->part_cap + (BLK / WAVE) - 1) / (BLK / WAVE));
+    const unsigned gm = merge_grid(g->part_cap);
     auto sum_cols = [&]() {
         if (A.bf16)
             k_geo_sum_parts<bf16s><<<gm, BLK, 0, s>>>(g->col_counts, g->col_multi, g->col_chunk_ptr,
