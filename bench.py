@@ -19,9 +19,11 @@ stream; achieved = SURVEY §8(d)'s algorithmic bytes ÷ time, peak = 8.0 TB/s; t
 of the same launches (profiles/pmc_c4.json).  The same kernels on the bench's own C2 graph are reported
 beside it as ``cache_assisted`` (C2's gathers are served partly by L2 / Infinity Cache).
 cpu_baseline: the CPU oracle (oracle/, restatements of the reference algorithm) on bounded samples,
-rank 0, N=1 only: sparse CSR at C2 (the headline ratio), and at C1 both sparse and dense_faithful (the
-reference's own dense N×N mask + per-(head, node) loop, cross-checked against the literal reference in
-profiles/r2_cpu_crosscheck.json), next to a GPU C1 step measured here.
+rank 0, N=1 only: sparse CSR at C2 (the headline ratio); dense_faithful (the reference's own dense N×N mask +
+per-(head, node) loop) at C2 extrapolated from a measured N = 250/500/1000 sweep (labelled as such;
+tools/cpu_ref_crosscheck.py --sweep sets the same sweep beside the literal reference); and at C1 both sparse and
+dense_faithful (cross-checked against the literal reference in profiles/r2_cpu_crosscheck.json), next to a GPU
+C1 step measured here.
 """
 import argparse
 import ctypes
@@ -326,6 +328,35 @@ def _oracle_rate(P, c, seq, lab, mode, min_seconds, max_reps=1000):
             return done / dt, done, dt
 
 
+DF_SWEEP_N = (250, 500, 1000)
+
+
+def dense_faithful_sweep(P, c, name, lab, nodes=DF_SWEEP_N, snapshots=1, reps=2):
+    """The reference's own algorithm (oracle ``dense_faithful``: dense N×N mask, per-(head, node) distance loop,
+    geometric_attention.py:386-401) on ``name``-shaped sequences at small N (E = 10 N, ``snapshots`` snapshots,
+    fwd+bwd, best of ``reps``: single runs of this loop-heavy path see occasional 2-3x host stalls), and the power
+    law t = a·N^p fitted to the per-snapshot times (the loop's backward is ≈N³, so a whole C2 snapshot, ≈3 h, is
+    out of reach).  Returns ([(N, seconds per snapshot)], p, a)."""
+    import math
+    import oracle
+    from tagan_amd import synthetic
+    pts = []
+    for n in nodes:
+        seq = synthetic.make_sequence(name, "cpu", seed=7, snapshots=snapshots, nodes=n, edges=10 * n)
+        best = float("inf")
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            oracle.tagan_forward(P, c, seq, lab, mode="dense_faithful")["loss"].backward()
+            best = min(best, time.perf_counter() - t0)
+        pts.append((n, best / snapshots))
+    xs = [math.log(n) for n, _ in pts]
+    ys = [math.log(t) for _, t in pts]
+    mx, my = sum(xs) / len(xs), sum(ys) / len(ys)
+    p = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sum((x - mx) ** 2 for x in xs)
+    a = math.exp(my - p * mx)
+    return pts, p, a
+
+
 def cpu_baseline(cfg, name, model_state, n_snap, gpu_c1=None, gpu_value=None, min_seconds=8.0):
     """CPU oracle on bounded samples of the workloads, fwd+bwd (no optimizer), fp32, on the host's cores:
 
@@ -353,6 +384,20 @@ def cpu_baseline(cfg, name, model_state, n_snap, gpu_c1=None, gpu_value=None, mi
            "host": host}
     if gpu_value:
         rec["gpu_over_cpu"] = round(gpu_value / rate, 1)
+    # the headline config against the reference's own algorithm: measured at small N, extrapolated to the config's N
+    pts, p, a = dense_faithful_sweep(P, c, name, lab)
+    n_full = synthetic.CONFIGS[name][0]
+    df_ext = 1.0 / (a * n_full ** p)
+    rec["dense_faithful"] = {
+        "value": float("%.3g" % df_ext), "unit": "graph-snapshots/s", "kind": "port", "extrapolated": True,
+        "sample": "oracle dense_faithful (the reference's dense N×N per-(head, node) loop), fwd+bwd, %s shape with "
+                  "N = %s, E = 10 N, one snapshot each (best of 2), %d threads; t = a·N^p fitted (p = %.2f) and extrapolated to "
+                  "N = %d: an upper bound on the CPU rate (the loop's ≈N³ backward takes over above N ≈ 1000, BASELINE.md, "
+                  "so the true exponent at C2 is larger)" % (name, "/".join(str(n) for n, _ in pts), threads, p, n_full),
+        "sweep_s_per_snapshot": {str(n): round(t, 3) for n, t in pts},
+        "fit_exponent": round(p, 3)}
+    if gpu_value:
+        rec["gpu_over_dense_faithful"] = float("%.3g" % (gpu_value / df_ext))
     # C1: the reference's own configuration (example.py), the only one the literal reference runs in full
     c1cfg = synthetic.config_for("c1")
     torch.manual_seed(0)

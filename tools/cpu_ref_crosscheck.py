@@ -9,6 +9,12 @@ on the C1 workload (example.py:35-48 shapes, N = 500, T = 10, train mode, dropou
 the same threads, the oracle in ``dense_faithful`` and ``sparse`` mode on the same inputs and weights.
 
     python tools/cpu_ref_crosscheck.py [--threads 8] [--reps 3] [--out profiles/r2_cpu_crosscheck.json]
+    python tools/cpu_ref_crosscheck.py --sweep [--out profiles/r2_cpu_crosscheck_c2sweep.json]
+
+``--sweep``: the C2 shape (H = 128, 8 heads, F = 27, euclidean, dropout 0.1) at N = 250 / 500 / 1000 with E = 10 N
+and 1 snapshot (best of 2), literal reference against ``dense_faithful`` (bench.py's sweep, same inputs and weights), both
+power laws fitted and extrapolated to C2's N = 10,000: the check behind the bench's extrapolated C2
+``cpu_baseline.dense_faithful``.
 
 Never runs on the GPU box (the reference does not travel); the result is committed under profiles/.
 """
@@ -44,12 +50,86 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
+def _fit(pts):
+    import math
+    xs = [math.log(n) for n, _ in pts]
+    ys = [math.log(t) for _, t in pts]
+    mx, my = sum(xs) / len(xs), sum(ys) / len(ys)
+    p = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sum((x - mx) ** 2 for x in xs)
+    return p, math.exp(my - p * mx)
+
+
+def sweep(args):
+    import torch
+    torch.set_num_threads(args.threads)
+    sys.path.insert(0, ROOT)
+    import oracle
+    from tagan_amd import synthetic
+    sys.path.insert(0, REF)
+    cwd = os.getcwd()
+    os.chdir(tempfile.mkdtemp(prefix="tagan_xcheck_"))
+    nodes, snaps = (250, 500, 1000), 1
+    try:
+        with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+            from src.tagan.model import TAGAN as RefTAGAN
+            from src.tagan.utils.config import TAGANConfig as RefConfig
+        N2, E2, T2, H, heads, F, De, _ = synthetic.CONFIGS["c2"]
+        kw = dict(hidden_dim=H, num_heads=heads, node_feature_dim=F, edge_feature_dim=De, use_edge_features=True,
+                  output_dim=1, loss_type="bce", dropout=0.1, device="cpu")
+        torch.manual_seed(0)
+        model = _quiet(RefTAGAN, _quiet(RefConfig, **kw)).train()
+        P = {k: v.detach().clone().requires_grad_(v.is_floating_point()) for k, v in model.state_dict().items()}
+        labels = torch.tensor([1.0])
+        small = synthetic.make_sequence("c2", "cpu", seed=1, snapshots=1, nodes=100, edges=1000)
+        _quiet(lambda: model(small, labels=labels)["loss"].backward())          # warm-up
+        oracle.tagan_forward(P, dict(kw), small, labels, mode="dense_faithful")["loss"].backward()
+        lit, dfa = [], []
+        for n in nodes:
+            seq = synthetic.make_sequence("c2", "cpu", seed=7, snapshots=snaps, nodes=n, edges=10 * n)
+            tl = td = float("inf")
+            for _ in range(2):                     # best of 2, interleaved (as bench.py's sweep)
+                t0 = time.perf_counter()
+                _quiet(lambda: model(seq, labels=labels)["loss"].backward())
+                tl = min(tl, time.perf_counter() - t0)
+                t0 = time.perf_counter()
+                oracle.tagan_forward(P, dict(kw), seq, labels, mode="dense_faithful")["loss"].backward()
+                td = min(td, time.perf_counter() - t0)
+            lit.append((n, tl / snaps))
+            dfa.append((n, td / snaps))
+            print(n, lit[-1][1], dfa[-1][1], flush=True)
+    finally:
+        os.chdir(cwd)
+    pl, al = _fit(lit)
+    pd, ad = _fit(dfa)
+    ext_l, ext_d = 1.0 / (al * N2 ** pl), 1.0 / (ad * N2 ** pd)
+    rec = {"workload": "C2 shape (H=128, 8 heads, F=27, euclidean, train, dropout 0.1), N = 250/500/1000, E = 10 N, "
+                       "1 snapshot (best of 2), TAGAN.forward + loss.backward(); seconds per snapshot",
+           "host": {"cpu_model": _cpu_model(), "nproc": os.cpu_count(), "threads": args.threads},
+           "torch": torch.__version__,
+           "reference_literal": {str(n): round(t, 3) for n, t in lit},
+           "oracle_dense_faithful": {str(n): round(t, 3) for n, t in dfa},
+           "fit_exponent": {"reference_literal": round(pl, 3), "oracle_dense_faithful": round(pd, 3)},
+           "extrapolated_c2_snapshots_per_s": {"reference_literal": float("%.3g" % ext_l),
+                                               "oracle_dense_faithful": float("%.3g" % ext_d)},
+           "dense_faithful_over_literal_per_N": {str(n): round(tl / td, 3) for (n, tl), (_, td) in zip(lit, dfa)},
+           "dense_faithful_over_literal_at_c2": round(ext_d / ext_l, 3)}
+    out = args.out or os.path.join(ROOT, "profiles", "r2_cpu_crosscheck_c2sweep.json")
+    with open(out, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=os.cpu_count())
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r2_cpu_crosscheck.json"))
+    ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--out", default=None)
     args = ap.parse_args()
+    if args.sweep:
+        return sweep(args)
+    if args.out is None:
+        args.out = os.path.join(ROOT, "profiles", "r2_cpu_crosscheck.json")
     import torch
     torch.set_num_threads(args.threads)
     sys.path.insert(0, ROOT)

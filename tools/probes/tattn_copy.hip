@@ -12,7 +12,8 @@
 template <int TT, int MODE>
 __global__ void __launch_bounds__(64) k_copy(long rows, int T, int heads, int d, long s_row, long s_t,
                                              const float* qkv, const float* dout, float* o1, float* o2, float* o3,
-                                             int xcd) {
+                                             int xcd, long do_row = -1, long do_t = -1) {
+    if (do_row < 0) { do_row = heads * d; do_t = rows * heads * d; }
     const int lane = threadIdx.x, c = lane & 15, g = lane >> 4;
     const int b = blockIdx.x, nb = gridDim.x;
     int h; long rg;
@@ -30,14 +31,14 @@ __global__ void __launch_bounds__(64) k_copy(long rows, int T, int heads, int d,
                 q[t] = *(const float4*)(qkv + off);
                 k[t] = *(const float4*)(qkv + off + H);
                 v[t] = *(const float4*)(qkv + off + 2 * H);
-                if (MODE) dd[t] = *(const float4*)(dout + r * H + (long)i * rows * H + h * d + 4 * g);
+                if (MODE) dd[t] = *(const float4*)(dout + r * do_row + (long)i * do_t + h * d + 4 * g);
             }
         }
 #pragma unroll
         for (int t = 0; t < TT; ++t) {
             const int i = t * 16 + c;
             if (i >= T) continue;
-            const long oo = r * H + (long)i * rows * H + h * d + 4 * g;
+            const long oo = r * do_row + (long)i * do_t + h * d + 4 * g;
             float4 a = make_float4(q[t].x + k[t].x + v[t].x, q[t].y + k[t].y + v[t].y, q[t].z + k[t].z + v[t].z,
                                    q[t].w + k[t].w + v[t].w);
             if (!MODE) { *(float4*)(o1 + oo) = a; continue; }
@@ -190,6 +191,28 @@ int main(int argc, char** argv) {
                 const double bytes = mode == 0 ? 4 * unit : 7 * unit;
                 printf("PAIR N=%ld T=%d groups=%d %s: %.1f us  %.0f GB/s\n", N, T, G, mode ? "bwd(4r+3w)" : "fwd(3r+1w)",
                        ms * 1e3, bytes / ms / 1e6);
+            }
+        }
+    }
+    // node-major layouts: [N, T, 3H] projection (s_row = T*3H, s_t = 3H); dO / O time-major (nm=1) or node-major (nm=2)
+    for (int nm = 1; nm <= 2; ++nm) {
+        for (int G : {1024, 4096}) {
+            for (int mode = 0; mode < 2; ++mode) {
+                const int grid = (int)std::min<long>(N, G) / 8 * 8 * heads;
+                const long dr = nm == 2 ? (long)T * H : H, dt = nm == 2 ? H : N * H;
+                auto go = [&] {
+                    if (mode == 0) k_copy<2, 0><<<grid, 64>>>(N, T, heads, d, (long)T * 3 * H, 3 * H, qkv, dout, o, o, o, 1, dr, dt);
+                    else k_copy<2, 1><<<grid, 64>>>(N, T, heads, d, (long)T * 3 * H, 3 * H, qkv, dout, dq, dq, dq, 1, dr, dt);
+                };
+                for (int i = 0; i < 3; ++i) go();
+                CK(hipEventRecord(e0));
+                const int reps = 20;
+                for (int i = 0; i < reps; ++i) go();
+                CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ms /= reps;
+                const double bytes = mode == 0 ? 4 * unit : 7 * unit;
+                printf("NODEMAJOR%s N=%ld T=%d groups=%d %s: %.1f us  %.0f GB/s\n", nm == 2 ? "-all" : "-qkv", N, T, G,
+                       mode ? "bwd(4r+3w)" : "fwd(3r+1w)", ms * 1e3, bytes / ms / 1e6);
             }
         }
     }
