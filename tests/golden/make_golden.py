@@ -110,6 +110,33 @@ def make_sequence(n_list, F, De, seed, edges_per_node=2, zipf=False):
     return seq
 
 
+def make_edge_case_sequence(F, De, seed):
+    """Edge cases of the adjacency semantics (graph_attention.py:96-105: adj[src, dst] = 1 over the edge list, then
+    + eye(N)): a one-node snapshot and a twelve-node one without edges (self-loops only), duplicate edges, explicit
+    self-loops and negative indices (torch indexing wraps them), a star hub (every node <-> node 0), a complete
+    graph, and a plain random snapshot; ragged N throughout."""
+    g = torch.Generator().manual_seed(seed)
+    seq = []
+
+    def snap(N, ei):
+        x = torch.randn(N, F, generator=g)
+        ea = torch.randn(ei.shape[1], De, generator=g)
+        return (x, ei, ea, torch.randperm(N, generator=g).tolist())
+
+    seq.append(snap(1, torch.zeros(2, 0, dtype=torch.int64)))
+    seq.append(snap(12, torch.zeros(2, 0, dtype=torch.int64)))
+    base = torch.randint(0, 40, (2, 60), generator=g)
+    loops = torch.arange(0, 40, 4).repeat(2, 1)
+    neg = torch.randint(-40, 0, (2, 10), generator=g)
+    seq.append(snap(40, torch.cat([base, base[:, :20], loops, neg], 1)))
+    j = torch.arange(1, 64)
+    seq.append(snap(64, torch.cat([torch.stack([torch.zeros_like(j), j]), torch.stack([j, torch.zeros_like(j)])], 1)))
+    a = torch.arange(24)
+    seq.append(snap(24, torch.stack([a.repeat_interleave(24), a.repeat(24)])))
+    seq.append(snap(37, torch.randint(0, 37, (2, 74), generator=g)))
+    return seq
+
+
 def seq_tensors(seq):
     t = {}
     for i, (x, ei, ea, ids) in enumerate(seq):
@@ -122,7 +149,7 @@ def seq_tensors(seq):
 
 
 # --------------------------------------------------------------------------- e2e
-def e2e_case(R, case, cfg_kw, n_list, seed, labels, with_attn=False, store_intermediate=True):
+def e2e_case(R, case, cfg_kw, n_list, seed, labels, with_attn=False, store_intermediate=True, seq_fn=None):
     cfg_kw = dict(cfg_kw)
     cfg_kw.setdefault("device", "cpu")
     cfg_kw.setdefault("dropout", 0.0)
@@ -132,7 +159,8 @@ def e2e_case(R, case, cfg_kw, n_list, seed, labels, with_attn=False, store_inter
     model.train()
     F = cfg.node_feature_dim
     De = cfg.edge_feature_dim
-    seq = make_sequence(n_list, F, De if De > 0 else 8, seed + 1)
+    seq = (seq_fn or (lambda: make_sequence(n_list, F, De if De > 0 else 8, seed + 1)))()
+    n_list = [x.shape[0] for x, _, _, _ in seq]
     seq = [(x.clone().requires_grad_(True), ei, ea, ids) for (x, ei, ea, ids) in seq]
 
     geo_out, temporal_out, gf = [], [], []
@@ -453,6 +481,10 @@ def main(prefixes):
     cases.append(("e2e_attnw", lambda: e2e_case(R, "e2e_attnw", base, [16, 19, 17, 15, 18], 109, lab1,
                                                 with_attn=True)))
     cases.append(("e2e_nolabels", lambda: e2e_case_nolabel(R)))
+    edge_seq = (lambda: make_edge_case_sequence(16, 8, 111))
+    cases.append(("e2e_edgecases", lambda: e2e_case(R, "e2e_edgecases", base, None, 110, lab1, seq_fn=edge_seq)))
+    cases.append(("e2e_edgecases_sdp", lambda: e2e_case(R, "e2e_edgecases_sdp", dict(base, learnable_distance=True),
+                                                        None, 112, lab1, seq_fn=edge_seq)))
     # ingestion: dict snapshots with global ids, variable N, edge_attr absent / present
     soc = dict(base, node_feature_dim=27, edge_feature_dim=2)
     cases.append(("ingest_dict_social", lambda: ingest_dict_case(R, "ingest_dict_social", soc, 6, 60, 150, 120,
