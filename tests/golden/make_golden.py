@@ -481,6 +481,8 @@ def main(prefixes):
     cases.append(("e2e_attnw", lambda: e2e_case(R, "e2e_attnw", base, [16, 19, 17, 15, 18], 109, lab1,
                                                 with_attn=True)))
     cases.append(("e2e_nolabels", lambda: e2e_case_nolabel(R)))
+    cases.append(("e2e_T1", lambda: e2e_case(R, "e2e_T1", base, [25], 113, lab1)))
+    cases.append(("e2e_T2", lambda: e2e_case(R, "e2e_T2", base, [19, 23], 114, torch.tensor([0.0]))))
     edge_seq = (lambda: make_edge_case_sequence(16, 8, 111))
     cases.append(("e2e_edgecases", lambda: e2e_case(R, "e2e_edgecases", base, None, 110, lab1, seq_fn=edge_seq)))
     cases.append(("e2e_edgecases_sdp", lambda: e2e_case(R, "e2e_edgecases_sdp", dict(base, learnable_distance=True),
