@@ -511,16 +511,24 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    # rehearsal knobs (never set by the driver): TAGAN_BENCH_BACKEND=gloo + TAGAN_BENCH_DEVICE=0 run the N-rank data-
+    # parallel flow with every rank on one GPU (RCCL refuses two ranks per device), e.g. on a one-GPU box
+    backend = os.environ.get("TAGAN_BENCH_BACKEND", "nccl")
+    if os.environ.get("TAGAN_BENCH_DEVICE"):
+        local = int(os.environ["TAGAN_BENCH_DEVICE"])
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     import tagan_amd
     from tagan_amd import TAGAN, synthetic
-    from tagan_amd.distributed import GradBucket, broadcast_parameters
+    from tagan_amd.distributed import GradBucket, all_reduce_, broadcast_parameters
     from tagan_amd.gemm_tuning import use_tuned_gemms
     if args.roofline_only:
         print(json.dumps({"roofline": roofline_c4(args.roofline_reps)}), flush=True)
@@ -581,7 +589,7 @@ def main():
         torch.cuda.synchronize()
         t = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
         if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)   # every rank takes the same decision
+            all_reduce_(t, dist.ReduceOp.MAX)   # every rank takes the same decision
         return float(t.item()) / n
 
     launch_trial = None
@@ -615,7 +623,7 @@ def main():
         el = time.perf_counter() - t0
         if world > 1:
             t = torch.tensor([el], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            all_reduce_(t, dist.ReduceOp.MAX)
             el = float(t.item())
         assert torch.isfinite(loss).item(), "non-finite loss"
         return el
@@ -637,8 +645,8 @@ def main():
                                % (args.config, N, E, T, H, heads, cfg.dropout),
                    "sequences_per_step": seqs_per_step, "snapshots_per_sequence": T,
                    "parallelism": ("snapshot-shard%d" % world) if args.shard else ("dp%d" % world)},
-        "backend": "nccl (RCCL over xGMI)" if world > 1 else "none (single rank)",
-        "n_ranks_rccl": world if world > 1 else 0,
+        "backend": ("nccl (RCCL over xGMI)" if backend == "nccl" else backend) if world > 1 else "none (single rank)",
+        "n_ranks_rccl": world if (world > 1 and backend == "nccl") else 0,
         "parallelism": ("snapshot-shard%d" % world) if args.shard else ("dp%d" % world),
     }
     rec["config"]["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)

@@ -15,6 +15,31 @@ import torch
 import torch.distributed as dist
 
 
+def _staged(t: torch.Tensor, group) -> bool:
+    # gloo moves device tensors through the host (CPU tests; several ranks sharing one GPU): its own device-tensor
+    # path is not used on ROCm (a rehearsal with it faulted the GPU) -- RCCL ("nccl") takes device tensors directly
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> None:
+    """In-place all-reduce of ``t`` on any backend (host-staged for gloo with a device tensor)."""
+    if _staged(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+
+
+def broadcast_(t: torch.Tensor, src: int = 0, group=None) -> None:
+    if _staged(t, group):
+        h = t.cpu()
+        dist.broadcast(h, src=src, group=group)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src=src, group=group)
+
+
 class GradBucket:
     """ONE flat all-reduce of every trainable parameter's gradient plus a has-grad flag per parameter.
 
@@ -48,7 +73,7 @@ class GradBucket:
             if self.flat is None or self.flat.device != live[0].device or self.flat.numel() < n:
                 self.flat = torch.empty(max(n, self.n + len(self.params)), dtype=torch.float32, device=live[0].device)
             torch.cat([p.grad.reshape(-1) for p in live], out=self.flat[:n])
-            dist.all_reduce(self.flat[:n], op=dist.ReduceOp.SUM, group=group)
+            all_reduce_(self.flat[:n], dist.ReduceOp.SUM, group)
             self.flat[:n].div_(dist.get_world_size(group))
             off = 0
             for p in live:
@@ -70,7 +95,7 @@ class GradBucket:
                 self.flat[off:off + m].zero_()
             off += m
         flags.copy_(torch.tensor([p.grad is not None for p in self.params], dtype=torch.float32), non_blocking=True)
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+        all_reduce_(self.flat, dist.ReduceOp.SUM, group)
         self.flat[:self.n].div_(dist.get_world_size(group))
         has = (flags > 0).tolist()
         off = 0
@@ -90,4 +115,4 @@ def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None) -> N
     if not dist.is_available() or not dist.is_initialized():
         return
     for t in list(module.parameters()) + list(module.buffers()):
-        dist.broadcast(t.data, src=src, group=group)
+        broadcast_(t.data, src, group)
