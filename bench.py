@@ -537,7 +537,12 @@ def main():
     os.environ["TAGAN_BENCH_CONFIG"] = args.config
     cfg = synthetic.config_for(args.config)
     N, E, T, H, heads = synthetic.CONFIGS[args.config][:5]
-    launch = "eager" if (args.no_graph or args.shard) else args.launch
+    # N > 1 launches eagerly: the split capture (fwd+bwd graph, eager all-reduce, clip+Adam graph in the same memory
+    # pool) faulted in its first replay inside the CSR key sort at C2 size (two ranks on one GPU, gloo; the small
+    # split-graph test, tests/test_gpu_rccl.py, never reaches rocPRIM's onesweep path) -- until that is understood the
+    # multi-GPU step is the eager one (≈ 3 % slower at C2).  TAGAN_SPLIT_GRAPH=1 re-enables it for investigation.
+    split_ok = os.environ.get("TAGAN_SPLIT_GRAPH") == "1"
+    launch = "eager" if (args.no_graph or args.shard or (world > 1 and not split_ok)) else args.launch
     use_graph = launch != "eager"   # capturable optimizer whenever a graph may be captured
     torch.manual_seed(0)
     model = TAGAN(cfg, precision=args.precision).to(dev).train()
