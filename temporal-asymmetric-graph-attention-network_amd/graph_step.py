@@ -34,7 +34,8 @@ class GraphedStep:
     ``step_fn``'s graph, runs ``between()`` eagerly and replays ``post``'s graph."""
 
     def __init__(self, model: torch.nn.Module, step_fn: Callable[[], torch.Tensor], optimizer=None, warmup: int = 3,
-                 between: Optional[Callable[[], None]] = None, post: Optional[Callable[[], None]] = None):
+                 between: Optional[Callable[[], None]] = None, post: Optional[Callable[[], None]] = None,
+                 share_pool: bool = True):
         dev = next(model.parameters()).device
         self.model, self.dev, self.between = model, dev, between
         self.prev_validate = getattr(model, "validate_edges", None)
@@ -67,7 +68,7 @@ class GraphedStep:
         self.post_graph = None
         if post is not None:
             self.post_graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.post_graph, pool=self.graph.pool(), stream=side):
+            with torch.cuda.graph(self.post_graph, pool=self.graph.pool() if share_pool else None, stream=side):
                 post()
 
     def __call__(self) -> torch.Tensor:
