@@ -77,7 +77,9 @@ def test_rccl_world1_shard_and_buckets():
 def test_rccl_world1_graph_split_step():
     """bench.py's N > 1 launch form at world size 1: forward + backward captured as one HIP graph, the RCCL
     gradient all-reduce (static bucket, forced) run eagerly between the two replays, clip + Adam captured as the
-    second graph -- the same loss trajectory and weights as the eager step (dropout off)."""
+    second graph -- the same loss trajectory and weights as the eager step (dropout off).  At this size the CSR
+    build does not reach rocPRIM's onesweep path; at C2 size the same split form faults in its second replay
+    (tools/split_graph_probe.py --pg nccl), which is why bench.py launches N > 1 steps eagerly."""
     import tempfile
     import tagan_amd  # noqa: F401
     from tagan_amd import TAGAN, synthetic
