@@ -68,6 +68,9 @@ def parse():
                     help="graph: replay the step as a HIP graph (graph_step.py); eager: launch every kernel from "
                          "Python; auto (default): time a short trial of both and keep the faster (--shard: eager)")
     ap.add_argument("--no-graph", action="store_true", help="same as --launch eager")
+    ap.add_argument("--sub-records", default="auto",
+                    help="BASELINE multi-GPU workloads measured beside the headline: auto (c3_dp at N = 2, 4; "
+                         "c5_shard at N = 8), none, or a comma list of c3_dp, c5_shard")
     ap.add_argument("--shard", action="store_true",
                     help="one sequence sharded by snapshot over all ranks (strong scaling; C5 mode) instead of "
                          "one sequence per rank (data parallel, weak scaling)")
@@ -168,10 +171,14 @@ def roofline_c4(reps=10):
     bf, bb = geo_bytes(k.E, k.N, H)
     achieved = (bf + bb) / (tf + tb) / 1e9
     traffic = _pmc_traffic("c4")
-    rec = {"kernel": "tagan_geo_attn fwd (k_geo_fwd_chunk + merge) + bwd (k_geo_bwd_row_chunk + k_geo_bwd_col_chunk "
-                     "+ 2 k_geo_sum_parts): edge-softmax + aggregate of one layer, one C4 snapshot",
+    rec = {"kernel": "tagan_geo_attn fwd (k_geo_fwd_chunk + k_geo_fwd_merge) + bwd in the column-first order this "
+                     "graph takes (k_geo_bwd_delta + k_geo_bwd_col_chunk + k_geo_bwd_row_ds + 2 k_geo_sum_parts): "
+                     "edge-softmax + aggregate of one layer, one C4 snapshot",
            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+           "traffic_source": ("profiles/pmc_c4.json: rocprofv3 --pmc FETCH_SIZE x 2 + WRITE_SIZE of these launches, "
+                              "collected by the builder (tools/pmc_summary.py), not measured in this run")
+           if traffic else None,
            "algorithmic_bytes": int(bf + bb), "bytes_fwd": int(bf), "bytes_bwd": int(bb),
            "edges": k.E, "nodes": k.N, "H": H, "heads": heads, "dtype": "fp32",
            "ms_fwd": round(tf * 1e3, 4), "ms_bwd": round(tb * 1e3, 4), "reps": reps,
@@ -433,28 +440,20 @@ def make_step(model, opt, cfg, fwd, bwd):
     return step
 
 
-def graphed(model, opt, cfg, fwd, world=1, bucket=None, warmup=3):
-    """The bench step as a replayable HIP graph (graph_step.GraphedStep): forward, backward, clip, Adam in one
-    graph at N = 1; at N > 1 the RCCL gradient all-reduce runs eagerly between two captured segments."""
+def graphed(model, opt, cfg, fwd, exchange=None, warmup=3):
+    """The bench step as ONE replayable HIP graph (graph_step.GraphedStep): forward, backward, the gradient
+    exchange (N > 1: ``exchange()`` = the static RCCL bucket all-reduce, captured into the same graph), clip, Adam."""
     from tagan_amd.graph_step import GraphedStep
 
-    def fb():
+    def whole():
         out = fwd()
         out["loss"].backward()
-        return out["loss"]
-
-    def post():
+        if exchange is not None:
+            exchange()
         torch.nn.utils.clip_grad_norm_(model.parameters(), cfg.gradient_clip_val)
         opt.step()
-
-    if world == 1:
-        def whole():
-            loss = fb()
-            post()
-            return loss
-        return GraphedStep(model, whole, optimizer=opt, warmup=warmup)
-    return GraphedStep(model, fb, optimizer=opt, warmup=warmup, between=lambda: bucket.allreduce_mean(static=True),
-                       post=post)
+        return out["loss"]
+    return GraphedStep(model, whole, optimizer=opt, warmup=warmup)
 
 
 def gpu_c1_line(dev, precision, steps=20, warmup=5, graph=True):
@@ -485,6 +484,130 @@ def gpu_c1_line(dev, precision, steps=20, warmup=5, graph=True):
         g.close()
     return {"value": round(T * steps / el, 3), "unit": "graph-snapshots/s", "ms_per_step": round(el / steps * 1e3, 3),
             "steps": steps, "dtype": precision, "launch": "hip-graph" if graph else "eager"}
+
+
+EXCHANGE_PHASES = ("grad_allreduce", "all_to_all", "pool_allreduce")
+
+
+def sub_record(workload, step, world, group=None, steps=5, warmup=3, snapshots_per_step=1, extra=None):
+    """One measured multi-GPU sub-record of the bench line (DESIGN.md §4 'sub-records'): ``warmup`` untimed calls
+    of ``step``, then ``steps`` timed ones between two barriers + device syncs on ``group`` (a gloo group of host
+    tensors), wall time = the MAX over ranks; the collectives inside the step are timed per phase by
+    ``distributed.ExchangeTimer`` (HIP events around each call on the current stream; wall clock for host
+    tensors) and reported per step, each phase its MAX over ranks.  Runs on CPU too (gloo tests)."""
+    from tagan_amd import distributed as D
+    sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    timer = D.ExchangeTimer()
+    D.TIMER = timer
+    try:
+        for _ in range(warmup):
+            step()
+        sync()
+        if world > 1:
+            dist.barrier(group=group)
+        timer.reset()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        sync()
+        if world > 1:
+            dist.barrier(group=group)
+        el = time.perf_counter() - t0
+        tot = timer.totals()
+    finally:
+        D.TIMER = None
+    vals = torch.tensor([el] + [tot.get(k, 0.0) for k in EXCHANGE_PHASES], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(vals, dist.ReduceOp.MAX, group=group)
+    el = float(vals[0])
+    rec = {"workload": workload, "value": round(snapshots_per_step * steps / el, 3), "unit": "graph-snapshots/s",
+           "ms_per_step": round(el / steps * 1e3, 3), "steps": steps, "warmup": warmup, "n_ranks": world,
+           "exchange_ms_per_step": {k: round(float(v) / steps, 4) for k, v in zip(EXCHANGE_PHASES, vals[1:].tolist())
+                                    if tot.get(k) is not None or float(v) > 0}}
+    if extra:
+        rec.update(extra)
+    return rec
+
+
+def sub_records_for(spec, world):
+    """``--sub-records``: "auto" = c3_dp at N in {2, 4} (BASELINE configs[2]: "snapshot-batch DP over 2 then 4
+    GPUs"), c5_shard at N = 8 (configs[4]: "8x snapshot-sharded ... scaling-curve config"); "none"; or a comma
+    list of c3_dp / c5_shard (any N, e.g. a one-GPU rehearsal of the code path)."""
+    spec = (spec or "auto").strip().lower()
+    if spec == "none":
+        return []
+    if spec == "auto":
+        return ["c3_dp"] if world in (2, 4) else (["c5_shard"] if world == 8 else [])
+    out = [x.strip() for x in spec.split(",") if x.strip()]
+    bad = [x for x in out if x not in ("c3_dp", "c5_shard")]
+    if bad:
+        raise SystemExit("bench.py: unknown sub-record(s) %s" % bad)
+    return out
+
+
+def c3_dp_record(dev, rank, world, ctl, backend, steps=5, warmup=3):
+    """BASELINE configs[2] at N ranks: 100k nodes / 2M edges per snapshot, 64 snapshots, hidden 256, 8 heads, fp32,
+    one sequence per rank (snapshot-batch data parallel), the flagged gradient bucket over RCCL; eager launches
+    (a 0.6-s step: launch overhead is noise, and a captured graph would double the 195-GB working set)."""
+    from tagan_amd import TAGAN, synthetic
+    from tagan_amd.distributed import GradBucket, broadcast_parameters
+    cfg = synthetic.config_for("c3")
+    torch.manual_seed(0)
+    model = TAGAN(cfg).to(dev).train()
+    broadcast_parameters(model)
+    opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay, fused=True)
+    seq = synthetic.make_sequence("c3", dev, seed=2000 + rank)
+    labels = torch.tensor([1.0 if rank % 2 == 0 else 0.0], device=dev)
+    bucket = GradBucket(model.parameters())
+
+    def bwd(out):
+        out["loss"].backward()
+        bucket.allreduce_mean()
+    step = make_step(model, opt, cfg, lambda: model(seq, labels=labels), bwd)
+    N, E, T, H, heads = synthetic.CONFIGS["c3"][:5]
+    rec = sub_record("c3 (BASELINE configs[2]): %d nodes, %d edges/snapshot, %d snapshots, hidden %d, %d heads, fp32, "
+                     "one sequence per rank" % (N, E, T, H, heads), step, world, ctl, steps, warmup, T * world,
+                     {"parallelism": "dp%d" % world, "scaling": "weak", "launch": "eager", "dtype": "fp32",
+                      "n_ranks_rccl": world if backend == "nccl" else 0,
+                      "grad_bucket_mb": round(4 * (bucket.n + len(bucket.params)) / 1e6, 3)})
+    rec["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
+    return rec
+
+
+def c5_shard_record(dev, rank, world, ctl, backend, steps=5, warmup=3):
+    """BASELINE configs[4] over N ranks: ONE sequence of 128 snapshots (100k nodes / 2M edges each, hidden 256,
+    16 heads, fp32) sharded by snapshot (sharded.py): the geometric stage on each rank's 128/N snapshots, one
+    all-to-all to node rows, the temporal stage on the rank's rows, one pooling all-reduce, one flagged gradient
+    all-reduce; eager launches."""
+    from tagan_amd import TAGAN, synthetic
+    from tagan_amd.distributed import broadcast_parameters
+    from tagan_amd.sharded import ShardGradSync, SnapshotShardedTAGAN, blocks
+    cfg = synthetic.config_for("c5")
+    N, E, T, H, heads = synthetic.CONFIGS["c5"][:5]
+    torch.manual_seed(0)
+    model = TAGAN(cfg).to(dev).train()
+    broadcast_parameters(model)
+    opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay, fused=True)
+    t0, t1 = blocks(T, world)[rank]
+    full = synthetic.make_sequence("c5", dev, seed=5000)   # the same sequence on every rank; keep this rank's block
+    seq = full[t0:t1]
+    del full
+    counts_all = [N] * T
+    sharded = SnapshotShardedTAGAN.for_model(model)
+    sync = ShardGradSync(list(model.named_parameters()))
+    labels = torch.tensor([1.0], device=dev)
+
+    def bwd(out):
+        out["loss"].backward()
+        sync.sync()
+    step = make_step(model, opt, cfg, lambda: sharded(seq, counts_all, labels), bwd)
+    rec = sub_record("c5 (BASELINE configs[4]): one sequence of %d snapshots (%d nodes, %d edges each), hidden %d, "
+                     "%d heads, fp32, sharded by snapshot over %d ranks" % (T, N, E, H, heads, world),
+                     step, world, ctl, steps, warmup, T,
+                     {"parallelism": "snapshot-shard%d" % world, "scaling": "strong", "launch": "eager",
+                      "dtype": "fp32", "n_ranks_rccl": world if backend == "nccl" else 0})
+    rec["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
+    return rec
 
 
 def _relaunch(n):
@@ -537,12 +660,13 @@ def main():
     os.environ["TAGAN_BENCH_CONFIG"] = args.config
     cfg = synthetic.config_for(args.config)
     N, E, T, H, heads = synthetic.CONFIGS[args.config][:5]
-    # N > 1 launches eagerly: the split capture (fwd+bwd graph, eager all-reduce, clip+Adam graph in the same memory
-    # pool) faulted in its first replay inside the CSR key sort at C2 size (two ranks on one GPU, gloo; the small
-    # split-graph test, tests/test_gpu_rccl.py, never reaches rocPRIM's onesweep path) -- until that is understood the
-    # multi-GPU step is the eager one (≈ 3 % slower at C2).  TAGAN_SPLIT_GRAPH=1 re-enables it for investigation.
-    split_ok = os.environ.get("TAGAN_SPLIT_GRAPH") == "1"
-    launch = "eager" if (args.no_graph or args.shard or (world > 1 and not split_ok)) else args.launch
+    # control plane (N > 1): timing maxima and the barriers around the timed region go over a gloo group of host
+    # tensors, so no eager device work sits between two replays of the step graph
+    ctl = dist.new_group(backend="gloo") if world > 1 else None
+    # every form of the step is captured whole (the RCCL all-reduce inside the graph); only a gloo data plane
+    # (the one-GPU rehearsal knob) cannot be captured and launches eagerly
+    capturable = world == 1 or backend == "nccl"
+    launch = "eager" if (args.no_graph or not capturable) else args.launch
     use_graph = launch != "eager"   # capturable optimizer whenever a graph may be captured
     torch.manual_seed(0)
     model = TAGAN(cfg, precision=args.precision).to(dev).train()
@@ -569,6 +693,9 @@ def main():
         def bwd(out):
             out["loss"].backward()
             sync.sync()
+
+        def exchange():
+            sync.sync(static=True)
     else:
         bucket = GradBucket(model.parameters())
         seq = synthetic.make_sequence(args.config, dev, seed=1000 + rank)
@@ -579,10 +706,20 @@ def main():
 
         def bwd(out):
             out["loss"].backward()
-            bucket.allreduce_mean(static=use_graph)
+            bucket.allreduce_mean()
+
+        def exchange():
+            bucket.allreduce_mean(static=True)
 
     step = make_step(model, opt, cfg, fwd, bwd)
     eager_step = step
+
+    def host_max(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, dist.ReduceOp.MAX, group=ctl)
+        return float(t.item())
 
     def trial(fn, n=5):
         for _ in range(2):
@@ -592,17 +729,14 @@ def main():
         for _ in range(n):
             fn()
         torch.cuda.synchronize()
-        t = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-        if world > 1:
-            all_reduce_(t, dist.ReduceOp.MAX)   # every rank takes the same decision
-        return float(t.item()) / n
+        return host_max(time.perf_counter() - t0) / n   # every rank takes the same decision
 
     launch_trial = None
     gstep = None
     if use_graph:
         # eager trial first, then ONE capture that is kept when it wins (no capture / destroy / re-capture)
         te = trial(eager_step) if launch == "auto" else None
-        gstep = graphed(model, opt, cfg, fwd, world, None if args.shard else bucket)
+        gstep = graphed(model, opt, cfg, fwd, exchange if world > 1 else None)
         if launch == "auto":
             tg = trial(gstep)
             launch_trial = {"graph_ms": round(tg * 1e3, 3), "eager_ms": round(te * 1e3, 3)}
@@ -618,18 +752,14 @@ def main():
             step()
         torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=ctl)
         t0 = time.perf_counter()
         for _ in range(steps):
             loss = step()
         torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], device=dev, dtype=torch.float64)
-            all_reduce_(t, dist.ReduceOp.MAX)
-            el = float(t.item())
+            dist.barrier(group=ctl)
+        el = host_max(time.perf_counter() - t0)
         assert torch.isfinite(loss).item(), "non-finite loss"
         return el
 
@@ -657,9 +787,9 @@ def main():
     rec["config"]["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
     rec["config"]["gemms"] = ("hipBLASLt/rocBLAS solutions from the TunableOp table %s" % os.path.basename(gemm_table)
                               if gemm_table else "library-default heuristic")
-    rec["launch"] = ("hip-graph (one replay per step)" if world == 1 else
-                     "hip-graph (fwd+bwd and clip+Adam replays, RCCL all-reduce between)") if gstep is not None \
-        else "eager"
+    rec["launch"] = (("hip-graph (one replay per step)" if world == 1 else
+                      "hip-graph (one replay per step; the RCCL gradient all-reduce captured inside it)")
+                     if gstep is not None else "eager")
     if launch_trial:
         rec["launch_trial"] = dict(launch_trial, note="5-step trial of both launch modes; the faster one is timed")
     if gstep is not None:
@@ -671,7 +801,7 @@ def main():
         # every kernel; held to the fp32 mode by tests/test_gpu_bf16.py (loss 2e-2, gradients 8e-2)
         model.precision = "bf16"
         te = trial(eager_step) if (use_graph and launch == "auto") else None
-        gstep = graphed(model, opt, cfg, fwd, world, None if args.shard else bucket) if use_graph else None
+        gstep = graphed(model, opt, cfg, fwd, exchange if world > 1 else None) if use_graph else None
         if gstep is not None and launch == "auto":
             tg = trial(gstep)
             if tg >= te:
@@ -691,6 +821,17 @@ def main():
                                 "ms_per_step": round(alt / args.steps * 1e3, 3),
                                 "launch": "hip-graph" if gstep is not None else "eager", "launch_trial": alt_launch,
                                 "dtype": "bf16 (activations; fp32 math and accumulation)"}
+    subs = sub_records_for(args.sub_records, world)
+    if subs:
+        # BASELINE's multi-GPU workloads beside the C2 headline (DESIGN.md §4 'sub-records'): every rank takes part
+        if gstep is not None:
+            gstep.close()
+        del step, gstep
+        torch.cuda.empty_cache()
+        for name in subs:
+            fn = {"c3_dp": c3_dp_record, "c5_shard": c5_shard_record}[name]
+            rec[name] = fn(dev, rank, world, ctl, backend)
+            torch.cuda.empty_cache()
     if rank == 0 and not args.no_roofline:
         roof = roofline_c4(args.roofline_reps)
         roof["cache_assisted"] = dict(roofline_cache_assisted(seq, cfg), config=args.config)

@@ -97,6 +97,16 @@ __device__ __forceinline__ void xw_t(const float* __restrict__ W, const float* x
     }
 }
 
+// nn.CrossEntropyLoss's default ignore_index (model.py:439-441 uses the default constructor): rows labelled -100
+// contribute nothing and the mean divides by the rows that remain
+constexpr int CE_IGNORE = -100;
+
+__device__ __forceinline__ int ce_count(const HeadArgs& A) {
+    int n = 0;
+    for (int b = 0; b < A.B; ++b) n += (int)A.labels[b] != CE_IGNORE;
+    return n;
+}
+
 __global__ void __launch_bounds__(HB) k_head_fwd(HeadArgs A) {
     TAGAN_LIVE_SEED(A);
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -200,9 +210,9 @@ __global__ void __launch_bounds__(HB) k_head_fwd(HeadArgs A) {
                     lsum += fmaxf(z, 0.f) - z * y + log1pf(expf(-fabsf(z)));
                 }
             }
-            if (A.loss_kind == 2) {   // an out-of-range class index poisons the loss (torch would raise)
-                const int y = (int)A.labels[b];
-                lsum += (y >= 0 && y < C) ? (m + logf(den)) - L.vl[y] : NAN;
+            if (A.loss_kind == 2) {   // nn.CrossEntropyLoss(): ignore_index -100 rows drop out of the mean; any
+                const int y = (int)A.labels[b];   // other out-of-range class poisons the loss (torch would raise)
+                if (y != CE_IGNORE) lsum += (y >= 0 && y < C) ? (m + logf(den)) - L.vl[y] : NAN;
             }
         }
         // saved: z | a | pooled | u | mean, rstd | h2
@@ -216,8 +226,8 @@ __global__ void __launch_bounds__(HB) k_head_fwd(HeadArgs A) {
         if (tid == 0) { sv[T * H + T + 2 * H] = mean; sv[T * H + T + 2 * H + 1] = rstd; }
         __syncthreads();
     }
-    if (tid == 0 && A.loss_kind && A.loss)
-        A.loss[0] = A.loss_kind == 1 ? lsum / (float)(A.B * C) : lsum / (float)A.B;
+    if (tid == 0 && A.loss_kind && A.loss)   // CE over no counted row: 0/0 = NaN, as torch's mean reduction
+        A.loss[0] = A.loss_kind == 1 ? lsum / (float)(A.B * C) : lsum / (float)ce_count(A);
 }
 
 __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
@@ -247,8 +257,8 @@ __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
                     const float z = A.logits[b * C + c];
                     g += gL * (1.f / (1.f + expf(-z)) - A.labels[b * C + c]) / (float)(A.B * C);
                 }
-                if (A.loss_kind == 2 && A.g_loss)
-                    g += gL * (p - (c == (int)A.labels[b] ? 1.f : 0.f)) / (float)A.B;
+                if (A.loss_kind == 2 && A.g_loss && (int)A.labels[b] != CE_IGNORE)
+                    g += gL * (p - (c == (int)A.labels[b] ? 1.f : 0.f)) / (float)ce_count(A);
                 L.vl[c] = g;
             }
         }

@@ -9,26 +9,84 @@ so one collective beats per-tensor calls); parameters whose grad is None on
 every rank (edge_embedding, temporal_propagation.*, time_encoding — dead in the
 shipped forward) are skipped identically on all ranks.
 """
-from typing import Iterable, List
+import time
+from contextlib import contextmanager
+from typing import Dict, Iterable, List, Optional
 
 import torch
 import torch.distributed as dist
 
 
 def _staged(t: torch.Tensor, group) -> bool:
-    # gloo moves device tensors through the host (CPU tests; several ranks sharing one GPU): its own device-tensor
-    # path is not used on ROCm (a rehearsal with it faulted the GPU) -- RCCL ("nccl") takes device tensors directly
+    # gloo moves device tensors through the host (CPU tests; several ranks sharing one GPU).  PyTorch's gloo backend
+    # has no ROCm device-tensor path of its own (ProcessGroupGloo's device collectives are the CUDA-stream ones), so
+    # device tensors are always staged here; RCCL ("nccl") takes device tensors directly.
     return t.is_cuda and dist.get_backend(group) == "gloo"
 
 
-def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> None:
-    """In-place all-reduce of ``t`` on any backend (host-staged for gloo with a device tensor)."""
-    if _staged(t, group):
-        h = t.cpu()
-        dist.all_reduce(h, op=op, group=group)
-        t.copy_(h)
+class ExchangeTimer:
+    """Per-phase time of the collectives inside a step (``bench.py`` sub-records: gradient all-reduce, all-to-all,
+    pooling all-reduce).  Device tensors: HIP events recorded on the current stream around the call, so the time is
+    what the collective costs the step (the current stream waits for RCCL's); host tensors: wall clock.
+    Events are resolved after the caller's synchronisation (``totals``)."""
+
+    def __init__(self):
+        self.marks: Dict[str, list] = {}
+        self.host: Dict[str, float] = {}
+        self.calls: Dict[str, int] = {}
+
+    @contextmanager
+    def phase(self, name: str, t: Optional[torch.Tensor] = None):
+        self.calls[name] = self.calls.get(name, 0) + 1
+        if t is not None and t.is_cuda and not torch.cuda.is_current_stream_capturing():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            yield
+            b.record()
+            self.marks.setdefault(name, []).append((a, b))
+        else:
+            t0 = time.perf_counter()
+            yield
+            self.host[name] = self.host.get(name, 0.0) + (time.perf_counter() - t0) * 1e3
+
+    def totals(self) -> Dict[str, float]:
+        """Milliseconds per phase since the last ``reset`` (device events synchronised here)."""
+        out = dict(self.host)
+        for name, evs in self.marks.items():
+            ms = 0.0
+            for a, b in evs:
+                b.synchronize()
+                ms += a.elapsed_time(b)
+            out[name] = out.get(name, 0.0) + ms
+        return out
+
+    def reset(self) -> None:
+        self.marks.clear()
+        self.host.clear()
+        self.calls.clear()
+
+
+TIMER: Optional[ExchangeTimer] = None   # set by bench.py around its sub-record steps
+
+
+@contextmanager
+def _phase(name: str, t: torch.Tensor):
+    if TIMER is None:
+        yield
     else:
-        dist.all_reduce(t, op=op, group=group)
+        with TIMER.phase(name, t):
+            yield
+
+
+def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None, phase: str = "all_reduce") -> None:
+    """In-place all-reduce of ``t`` on any backend (host-staged for gloo with a device tensor)."""
+    with _phase(phase, t):
+        if _staged(t, group):
+            h = t.cpu()
+            dist.all_reduce(h, op=op, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op, group=group)
 
 
 def broadcast_(t: torch.Tensor, src: int = 0, group=None) -> None:
@@ -73,7 +131,7 @@ class GradBucket:
             if self.flat is None or self.flat.device != live[0].device or self.flat.numel() < n:
                 self.flat = torch.empty(max(n, self.n + len(self.params)), dtype=torch.float32, device=live[0].device)
             torch.cat([p.grad.reshape(-1) for p in live], out=self.flat[:n])
-            all_reduce_(self.flat[:n], dist.ReduceOp.SUM, group)
+            all_reduce_(self.flat[:n], dist.ReduceOp.SUM, group, phase="grad_allreduce")
             self.flat[:n].div_(dist.get_world_size(group))
             off = 0
             for p in live:
@@ -95,7 +153,7 @@ class GradBucket:
                 self.flat[off:off + m].zero_()
             off += m
         flags.copy_(torch.tensor([p.grad is not None for p in self.params], dtype=torch.float32), non_blocking=True)
-        all_reduce_(self.flat, dist.ReduceOp.SUM, group)
+        all_reduce_(self.flat, dist.ReduceOp.SUM, group, phase="grad_allreduce")
         self.flat[:self.n].div_(dist.get_world_size(group))
         has = (flags > 0).tolist()
         off = 0

@@ -532,7 +532,8 @@ class PackQKVFn(torch.autograd.Function):
     def forward(ctx, wq, wk, wv, bq, bk, bv, aug: bool):
         H = wq.shape[1]
         dev = wq.device
-        args = [ptr(t.contiguous()) for t in (wq, wk, wv, bq, bk, bv)]
+        src = [t.contiguous() for t in (wq, wk, wv, bq, bk, bv)]   # alive until the launches below are issued
+        args = [ptr(t) for t in src]
         w = torch.empty(3 * H, H, device=dev)
         b = torch.empty(3 * H, device=dev)
         st = stream_of(wq)

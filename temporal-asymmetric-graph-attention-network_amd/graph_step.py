@@ -3,8 +3,8 @@
 The reference trainer's step (trainer.py:295-311: forward, loss, backward, clip_grad_norm_, optimizer step)
 issues ~300 launches per C2 sequence from Python: at C2 bf16 and at C1 the host, not the GPU, sets the pace
 (DESIGN.md §4).  ``GraphedStep`` captures the step once with ``torch.cuda.graph`` and replays it: the CSR
-build, both attention stacks, the fused head + loss, their backward passes, the gradient all-reduce (N > 1,
-RCCL captures into the graph), clipping and Adam all run from one ``hipGraphLaunch``.
+build, both attention stacks, the fused head + loss, their backward passes, the gradient all-reduce (N > 1:
+the RCCL collective is captured into the same graph), clipping and Adam all run from one ``hipGraphLaunch``.
 
 What capture needs from the hot path, and how it gets it:
 * fresh dropout masks per replay — the seeds drawn at capture time are constants in the graph, so the step
@@ -15,10 +15,15 @@ What capture needs from the hot path, and how it gets it:
   gradient bucket runs in its static form (``GradBucket.allreduce_mean(static=True)``);
 * static inputs — the replay re-runs the step on the same input tensors (the bench's resident sequence);
   a caller feeding new data copies it into those tensors before ``__call__``;
+* device tables the graph reads by address stay alive — the snapshot offset tables cached by
+  ``kernels._ptr_table`` are pinned when they are looked up during a capture;
 * a capturable optimizer (``torch.optim.Adam(..., capturable=True)``).
+
+There is deliberately no split form (an eager segment between two captured ones): DESIGN.md §6 records how
+that form faulted and why the collective lives inside the one graph instead.
 """
 import ctypes
-from typing import Callable, Optional
+from typing import Callable
 
 import torch
 
@@ -27,17 +32,15 @@ from ._lib import check, lib, ptr
 
 class GraphedStep:
     """``step_fn()`` (no ``zero_grad`` inside: gradients are written, not accumulated, by the captured backward)
-    captured after ``warmup`` eager calls on a side stream; ``__call__`` replays it and returns the static loss.
-
-    ``between`` / ``post``: an optional eager call (e.g. the RCCL gradient all-reduce of a multi-GPU step, kept out
-    of the graph) and a second captured segment after it (clipping + optimizer): ``__call__`` then replays
-    ``step_fn``'s graph, runs ``between()`` eagerly and replays ``post``'s graph."""
+    captured after ``warmup`` eager calls on a side stream; ``__call__`` replays it and returns the static loss."""
 
     def __init__(self, model: torch.nn.Module, step_fn: Callable[[], torch.Tensor], optimizer=None, warmup: int = 3,
-                 between: Optional[Callable[[], None]] = None, post: Optional[Callable[[], None]] = None,
-                 share_pool: bool = True):
+                 **unsupported):
+        if unsupported:
+            raise TypeError("GraphedStep captures the whole step as one graph; unsupported arguments: %s"
+                            % sorted(unsupported))
         dev = next(model.parameters()).device
-        self.model, self.dev, self.between = model, dev, between
+        self.model, self.dev = model, dev
         self.prev_validate = getattr(model, "validate_edges", None)
         if self.prev_validate is not None:
             model.validate_edges = False
@@ -50,10 +53,6 @@ class GraphedStep:
                 if optimizer is not None:
                     optimizer.zero_grad(set_to_none=True)
                 step_fn()
-                if between is not None:
-                    between()
-                if post is not None:
-                    post()
         torch.cuda.current_stream(dev).wait_stream(side)
         if optimizer is not None:
             optimizer.zero_grad(set_to_none=True)
@@ -65,18 +64,9 @@ class GraphedStep:
             check(lib().tagan_seed_counter_step(ptr(self.counter), ctypes.c_void_p(s.cuda_stream)),
                   "tagan_seed_counter_step")
             self.loss = step_fn()
-        self.post_graph = None
-        if post is not None:
-            self.post_graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.post_graph, pool=self.graph.pool() if share_pool else None, stream=side):
-                post()
 
     def __call__(self) -> torch.Tensor:
         self.graph.replay()
-        if self.between is not None:
-            self.between()
-        if self.post_graph is not None:
-            self.post_graph.replay()
         return self.loss
 
     def close(self) -> None:
@@ -84,5 +74,5 @@ class GraphedStep:
         lib().tagan_set_seed_counter(None)
         if self.prev_validate is not None:
             self.model.validate_edges = self.prev_validate
-        self.graph = self.post_graph = None
+        self.graph = None
         self.loss = None   # releases the captured step's autograd graph (its AccumulateGrad nodes)

@@ -13,7 +13,12 @@ device one snapshot at a time and builds a dense [N_t, N_t] mask per snapshot an
 * edges          -> edge_index [2, ΣE_t] int64 (still local ids), snapshot t at columns
                     [edge_ptr[t], edge_ptr[t+1]) — exactly what ``kernels.build_graph_cat`` (the device
                     COO -> CSR/CSC builder, tagan_csr_build) consumes, with no per-snapshot concatenation;
-* node ids       -> node_ids [ΣN_t] int64 (global ids, any values);
+* node ids       -> node_ids [ΣN_t] int64 (global ids, any values).  Ids that are not integers (the reference
+                    accepts any sortable, hashable id, e.g. string user ids: model.py:186-204) are coded on the
+                    host by their rank in ``sorted(set(all ids))`` -- the reference's own ordering -- and the
+                    original values are kept in ``id_values`` (code i <-> id_values[i]).  The reference never
+                    checks that a snapshot has one id per row; neither does this (``ids_row_aligned`` says whether
+                    every snapshot does);
 * edge_attr      -> kept only when every snapshot has one (the reference's edge embedding output is
                     dead, model.py:236-239, so it never reaches a kernel);
 * timestep       -> a host list (the time stamps of time-aware callers).
@@ -40,10 +45,27 @@ def unpack(snapshot):
     raise ValueError(f"Unsupported snapshot type: {type(snapshot)}")
 
 
-def _ids_tensor(ids) -> torch.Tensor:
+def _ids_tensor(ids) -> Optional[torch.Tensor]:
+    """int64 tensor of the ids, or None when they are not integers (strings, tuples, ...)."""
     if isinstance(ids, torch.Tensor):
+        if ids.is_floating_point() or ids.is_complex():
+            return None
         return ids.reshape(-1).to(torch.int64)
-    return torch.as_tensor(list(ids), dtype=torch.int64)
+    ids = list(ids)
+    if not all(isinstance(i, int) or (hasattr(i, "__index__") and not isinstance(i, (str, bytes))) for i in ids):
+        return None
+    try:
+        return torch.as_tensor([int(i) for i in ids], dtype=torch.int64)
+    except (TypeError, ValueError, OverflowError):
+        return None
+
+
+def _coded_ids(raw_ids):
+    """Non-integer ids of every snapshot -> int64 codes = rank in sorted(set(all ids)) (model.py:184-201's
+    all_node_ids ordering), and that sorted list."""
+    values = sorted(set(i for ids in raw_ids for i in ids))
+    code = {v: k for k, v in enumerate(values)}
+    return [torch.as_tensor([code[i] for i in ids], dtype=torch.int64) for ids in raw_ids], values
 
 
 @dataclass
@@ -55,6 +77,8 @@ class SnapshotBatch:
     node_ids: torch.Tensor               # [ΣN_t] int64, global ids
     edge_attr: Optional[torch.Tensor] = None
     timesteps: Optional[List[Any]] = None
+    id_values: Optional[List[Any]] = None   # non-integer ids: code i stands for id_values[i]
+    ids_row_aligned: bool = True
     _index: Optional[tuple] = field(default=None, repr=False)
 
     @property
@@ -79,14 +103,16 @@ class SnapshotBatch:
         eis = [p[1] for p in parts]
         eas = [p[2] for p in parts]
         ids = [_ids_tensor(p[3]) for p in parts]
+        id_values = None
+        if any(i is None for i in ids):
+            ids, id_values = _coded_ids([list(p[3]) for p in parts])
         F = int(xs[0].shape[1])
-        for t, (x, ei, i) in enumerate(zip(xs, eis, ids)):
+        for t, (x, ei) in enumerate(zip(xs, eis)):
             if x.dim() != 2 or int(x.shape[1]) != F:
                 raise ValueError("snapshot %d: x must be [N_t, %d], got %s" % (t, F, tuple(x.shape)))
             if ei.dim() != 2 or int(ei.shape[0]) != 2:
                 raise ValueError("snapshot %d: edge_index must be [2, E_t], got %s" % (t, tuple(ei.shape)))
-            if int(i.numel()) != int(x.shape[0]):
-                raise ValueError("snapshot %d: %d node ids for %d rows of x" % (t, int(i.numel()), int(x.shape[0])))
+        aligned = all(int(i.numel()) == int(x.shape[0]) for i, x in zip(ids, xs))
         counts = [int(x.shape[0]) for x in xs]
         e_ptr = [0]
         for ei in eis:
@@ -102,7 +128,7 @@ class SnapshotBatch:
             N, E = sum(counts), e_ptr[-1]
             hx = torch.empty(N, F, dtype=torch.float32, pin_memory=pin)
             hei = torch.empty(2, E, dtype=torch.int64, pin_memory=pin)
-            hid = torch.empty(N, dtype=torch.int64, pin_memory=pin)
+            hid = torch.empty(sum(int(i.numel()) for i in ids), dtype=torch.int64, pin_memory=pin)
             torch.cat([x.to(torch.float32) for x in xs], 0, out=hx)
             torch.cat([ei.to(torch.int64) for ei in eis], 1, out=hei)
             torch.cat(ids, 0, out=hid)
@@ -116,16 +142,19 @@ class SnapshotBatch:
             ei = torch.cat([t.to(dev, torch.int64) for t in eis], 1)
             nid = torch.cat([t.to(dev) for t in ids], 0)
             ea = torch.cat([t.to(dev, torch.float32) for t in eas], 0) if with_ea else None
-        return cls(x, ei, counts, e_ptr, nid, ea, tss)
+        return cls(x, ei, counts, e_ptr, nid, ea, tss, id_values, aligned)
 
     def to(self, device) -> "SnapshotBatch":
         mv = lambda t: None if t is None else t.to(device, non_blocking=True)  # noqa: E731
         return SnapshotBatch(mv(self.x), mv(self.edge_index), list(self.node_counts), list(self.edge_ptr),
-                             mv(self.node_ids), mv(self.edge_attr), self.timesteps)
+                             mv(self.node_ids), mv(self.edge_attr), self.timesteps, self.id_values,
+                             self.ids_row_aligned)
 
     def global_index(self):
         """(all_node_ids [U] sorted unique global ids, row_index [ΣN_t]: position of each row's id in it) —
-        the reference's sorted id list and node_id_to_idx (model.py:184-201), on the device."""
+        the reference's sorted id list and node_id_to_idx (model.py:184-201), on the device.  Non-integer ids:
+        all_node_ids holds their codes (``id_values[code]`` is the id).  row_index follows the concatenated ids,
+        so it indexes rows only when ``ids_row_aligned``."""
         if self._index is None:
             uniq, inv = torch.unique(self.node_ids, sorted=True, return_inverse=True)
             self._index = (uniq, inv)
@@ -136,7 +165,12 @@ class SnapshotBatch:
         n0, n1 = self.node_ptr[t], self.node_ptr[t + 1]
         e0, e1 = self.edge_ptr[t], self.edge_ptr[t + 1]
         ea = self.edge_attr[e0:e1] if self.edge_attr is not None else None
-        return self.x[n0:n1], self.edge_index[:, e0:e1], ea, self.node_ids[n0:n1].tolist()
+        if not self.ids_row_aligned:
+            raise ValueError("snapshot(): node ids are not one per row in this batch")
+        ids = self.node_ids[n0:n1].tolist()
+        if self.id_values is not None:
+            ids = [self.id_values[i] for i in ids]
+        return self.x[n0:n1], self.edge_index[:, e0:e1], ea, ids
 
     def to_list(self) -> List[tuple]:
         return [self.snapshot(t) for t in range(self.num_snapshots)]

@@ -133,20 +133,35 @@ def _finish(g: SnapshotGraph, nnz_cap: int, chunk: int = CHUNK) -> SnapshotGraph
 
 
 _PTR_TABLES = OrderedDict()
+_PTR_PINNED = {}     # tables a captured HIP graph reads by address: never evicted
 
 
 def _ptr_table(dev, values):
     """Device copy of the snapshot edge/node offset table, cached per (device, offsets): a repeated shape (every
-    training step of a sequence, a captured HIP graph) issues no host-to-device copy."""
+    training step of a sequence, a captured HIP graph) issues no host-to-device copy.
+
+    A table looked up while the current stream is capturing is pinned for the life of the process: the graph bakes
+    its address into ``tagan_csr_build``, and an LRU eviction (more than 256 other shapes seen between two replays)
+    would otherwise free memory the next replay reads.  A table first needed inside a capture is refused (the H2D
+    copy from a host temporary would be replayed from a freed host buffer): warm the step up eagerly first."""
     key = (str(dev), tuple(values))
+    t = _PTR_PINNED.get(key)
+    if t is not None:
+        return t
+    capturing = torch.device(dev).type == "cuda" and torch.cuda.is_current_stream_capturing()
     t = _PTR_TABLES.get(key)
     if t is None:
+        if capturing:
+            raise RuntimeError("snapshot offset table first needed inside a HIP-graph capture: run the step "
+                               "eagerly once before capturing it")
         t = torch.tensor(values, dtype=torch.int64).to(dev)
         _PTR_TABLES[key] = t
         if len(_PTR_TABLES) > 256:
             _PTR_TABLES.popitem(last=False)
     else:
         _PTR_TABLES.move_to_end(key)
+    if capturing:
+        _PTR_PINNED[key] = _PTR_TABLES.pop(key)
     return t
 
 

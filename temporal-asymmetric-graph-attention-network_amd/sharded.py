@@ -25,6 +25,8 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from .distributed import _phase
+
 
 def blocks(n: int, parts: int) -> List[Tuple[int, int]]:
     """Contiguous near-equal split of range(n) into ``parts`` blocks (first blocks one longer)."""
@@ -52,25 +54,27 @@ def _all_to_all(sends: List[torch.Tensor], recv_shapes: List[Tuple[int, ...]], g
     """Variable-size all-to-all as ONE all_to_all_single over flat buffers (RCCL over xGMI)."""
     x = torch.cat([s.reshape(-1) for s in sends])
     dev = x.device
-    staged = _host_staged(x, group)
-    if staged:
-        x = x.cpu()
-    out_sizes = [int(torch.Size(sh).numel()) for sh in recv_shapes]
-    y = x.new_empty(sum(out_sizes))
-    dist.all_to_all_single(y, x, output_split_sizes=out_sizes, input_split_sizes=[s.numel() for s in sends],
-                           group=group)
-    if staged:
-        y = y.to(dev)
+    with _phase("all_to_all", x):
+        staged = _host_staged(x, group)
+        if staged:
+            x = x.cpu()
+        out_sizes = [int(torch.Size(sh).numel()) for sh in recv_shapes]
+        y = x.new_empty(sum(out_sizes))
+        dist.all_to_all_single(y, x, output_split_sizes=out_sizes, input_split_sizes=[s.numel() for s in sends],
+                               group=group)
+        if staged:
+            y = y.to(dev)
     return [c.view(sh) for c, sh in zip(y.split(out_sizes), recv_shapes)]
 
 
-def _all_reduce_sum(t: torch.Tensor, group) -> None:
-    if _host_staged(t, group):
-        h = t.cpu()
-        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
-        t.copy_(h)
-    else:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+def _all_reduce_sum(t: torch.Tensor, group, phase: str = "pool_allreduce") -> None:
+    with _phase(phase, t):
+        if _host_staged(t, group):
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
 
 
 class _SnapshotsToRows(torch.autograd.Function):
@@ -123,7 +127,22 @@ def pool_partial(out_rows: torch.Tensor, n0: int, n_max: int) -> torch.Tensor:
     flat = out_rows.transpose(0, 1).reshape(n_r * T, H)
     f0, f1 = n0 * T, (n0 + n_r) * T
     lengths = [max(0, min((t + 1) * n_max, f1) - max(t * n_max, f0)) for t in range(T)]
-    return torch.segment_reduce(flat, "sum", lengths=torch.tensor(lengths, device=flat.device), axis=0)
+    return torch.segment_reduce(flat, "sum", lengths=_lengths_table(lengths, flat.device), axis=0)
+
+
+_LENGTHS = {}
+
+
+def _lengths_table(lengths, dev):
+    """Device copy of the pooling segment lengths, made once per (lengths, device): no host-to-device copy inside
+    the step (a captured HIP graph would otherwise re-read a freed host buffer at every replay)."""
+    key = (tuple(lengths), str(dev))
+    t = _LENGTHS.get(key)
+    if t is None:
+        if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("pool_partial: segment-length table first needed inside a capture (warm up eagerly)")
+        t = _LENGTHS[key] = torch.tensor(lengths, device=dev)
+    return t
 
 
 class SnapshotShardedTAGAN:
@@ -179,6 +198,10 @@ class SnapshotShardedTAGAN:
         out_rows = self.temporal(xt_rows) if n1 > n0 else xt_rows
         pooled = _SumAcrossRanks.apply(pool_partial(out_rows, n0, n_max), self.group) / n_max
         self.step += 1
+        if getattr(self, "head_takes_seed", False):
+            # the fused head kernel takes its dropout seed directly (the same on every rank; under a captured
+            # HIP graph the device seed counter is mixed in at run time): no torch generator involved
+            return self.head(pooled, labels, (self.head_seed * 0x9E3779B1 + self.step) & 0x3FFFFFFFFFFFFFFF)
         # same head-dropout mask on every rank: the head draws from a generator seeded from a per-step
         # counter shared by all ranks, inside fork_rng so the caller's generators are left as they were
         devices = [pooled.device] if pooled.is_cuda else []
@@ -187,8 +210,6 @@ class SnapshotShardedTAGAN:
                 torch.cuda.manual_seed(self.head_seed + self.step)
             else:
                 torch.manual_seed(self.head_seed + self.step)
-            if getattr(self, "head_takes_seed", False):
-                return self.head(pooled, labels, (self.head_seed * 0x9E3779B1 + self.step) & 0x3FFFFFFFFFFFFFFF)
             return self.head(pooled, labels)
 
     __call__ = forward
@@ -207,11 +228,35 @@ class ShardGradSync:
         self.items = [(n, p) for n, p in named_params if p.requires_grad]
         self.replicated = [any(n.startswith(x) for x in replicated_prefixes) for n, _ in self.items]
         self.group = group
+        self.flat = None
 
-    def sync(self, force: bool = False):
-        """``force``: run the collective even at world size 1 (exercises the RCCL path on one GPU)."""
+    def sync(self, force: bool = False, static: bool = False):
+        """``force``: run the collective even at world size 1 (exercises the RCCL path on one GPU).
+        ``static``: the capturable form (HIP graph step): no has-grad flags and no host read-back -- the grads
+        present locally are packed, summed, the replicated ones scaled by 1/P, and written back; every rank must
+        hold the same set of grads (the flagged eager form run during warm-up establishes that)."""
         P, _ = _world(self.group)
         if P == 1 and not (force and dist.is_available() and dist.is_initialized()):
+            return
+        if static:
+            live = [(k, p) for k, (_, p) in enumerate(self.items) if p.grad is not None]
+            if not live:
+                return
+            n = sum(p.numel() for _, p in live)
+            if self.flat is None or self.flat.numel() < n or self.flat.device != live[0][1].device:
+                self.flat = torch.empty(n, dtype=live[0][1].dtype, device=live[0][1].device)
+            flat = self.flat[:n]
+            torch.cat([p.grad.reshape(-1) for _, p in live], out=flat)
+            _all_reduce_sum(flat, self.group, phase="grad_allreduce")
+            off = 0
+            for k, p in live:
+                m = p.numel()
+                g = flat[off:off + m].view_as(p)
+                if self.replicated[k]:
+                    p.grad.copy_(g).div_(P)
+                else:
+                    p.grad.copy_(g)
+                off += m
             return
         ref = self.items[0][1]
         n = sum(p.numel() for _, p in self.items)
@@ -223,7 +268,7 @@ class ShardGradSync:
                 flat[off:off + m].copy_(p.grad.reshape(-1))
                 flat[n + k] = 1.0
             off += m
-        _all_reduce_sum(flat, self.group)
+        _all_reduce_sum(flat, self.group, phase="grad_allreduce")
         has = (flat[n:] > 0).tolist()
         off = 0
         for k, (_, p) in enumerate(self.items):

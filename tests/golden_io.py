@@ -79,10 +79,45 @@ def normwise_rel(got, want):
     return float((got - want).norm()) / max(float(want.norm()), 1e-300)
 
 
-def assert_close(name, got, want, atol, rtol=0.0):
+# Normwise bound on every gradient check: ||got - want|| <= GRAD_NORM_RTOL * ||want||.  The elementwise
+# atol + rtol*|want| bound alone is vacuous for a gradient whose entries are all below atol (a tiny-norm bias);
+# observed normwise errors of real gradients are 4e-7 (median) to 9.2e-5 (max, the C2 attention-pool bias,
+# norm 1e-5) against the fp64 oracle and the reference fixtures (profiles/r2h_parity_errors.json), so 1e-3 holds
+# every correct kernel and fails any wrong one (a real bug shows as an O(1) normwise error).
+GRAD_NORM_RTOL = 1e-3
+
+# Gradients that are analytically zero, so no normwise bound can hold (both sides are rounding noise) -- declared
+# here with the reason; for them the check is that the reference's own value is zero to within atol (so a
+# non-zero case, e.g. the euclidean metric's k bias, still gets the normwise bound) and that ours is too.
+#   *k_linear.bias (temporal attention; geometric attention with a dot-product score): a bias b on every key
+#       adds q_i.b to the whole score row i -- softmax is shift-invariant, so d loss / d b = 0;
+#   *time_q_proj.bias, *time_encoding.basis_proj.bias (the time-aware temporal branch): both add the same
+#       constant to every score of a row through the linear time_q_proj, the same shift invariance.
+ANALYTIC_ZERO = ("k_linear.bias", "time_q_proj.bias", "time_encoding.basis_proj.bias")
+
+
+def is_grad_check(name):
+    return name.startswith("grad") or name in ("dqkv", "dparam", "dx")
+
+
+def declared_zero(name):
+    return is_grad_check(name) and name.endswith(ANALYTIC_ZERO)
+
+
+def assert_close(name, got, want, atol, rtol=0.0, norm_rtol=None):
+    """Elementwise |got - want| <= atol + rtol*|want|; for gradient checks (``is_grad_check``) also the normwise
+    bound ``norm_rtol`` (default GRAD_NORM_RTOL), except for the declared analytically-zero tensors."""
     got = got.detach().to("cpu", torch.float64)
     want = want.detach().to("cpu", torch.float64)
     assert got.shape == want.shape, "%s: shape %s vs %s" % (name, tuple(got.shape), tuple(want.shape))
+    if norm_rtol is None and is_grad_check(name):
+        if declared_zero(name) and float(want.abs().max() if want.numel() else 0.0) <= atol:
+            zmax = float(got.abs().max()) if got.numel() else 0.0
+            ERRORS.setdefault(os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0], {})[name] = \
+                [zmax, 0.0, 0.0, atol, rtol, "declared analytically zero"]
+            assert zmax <= atol, "%s: declared analytically zero, but max |got| = %.3e > %.1e" % (name, zmax, atol)
+            return
+        norm_rtol = GRAD_NORM_RTOL
     both_nan = torch.isnan(got) & torch.isnan(want)
     diff = torch.where(both_nan, torch.zeros_like(got), (got - want).abs())
     _record(name, diff, want, atol, rtol)
@@ -93,3 +128,11 @@ def assert_close(name, got, want, atol, rtol=0.0):
         raise AssertionError("%s: max |diff| %.3e (atol %.1e rtol %.1e); first bad flat[%d] got %r want %r"
                              % (name, float(diff[~both_nan].max()), atol, rtol, i,
                                 float(got.flatten()[i]), float(want.flatten()[i])))
+    if norm_rtol is not None:
+        fin = torch.isfinite(want) & torch.isfinite(got)
+        dn = float((got[fin] - want[fin]).norm())
+        wn = float(want[fin].norm())
+        # a reference gradient that is zero to within atol as a whole: no relative bound exists, hold the norm of
+        # the difference to atol instead
+        assert dn <= (norm_rtol * wn if wn > atol else atol), ("%s: normwise error %.3e > %.1e x ||want|| (||want|| = %.3e)"
+                                      % (name, dn / max(wn, 1e-300), norm_rtol, wn))

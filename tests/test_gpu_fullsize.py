@@ -105,33 +105,120 @@ def _segments(rp, rows):
 
 
 # ----------------------------------------------------------------------------- C2 whole model
-@pytest.mark.timeout(900)
-def test_c2_full_model_vs_oracle(dev):
+_C2_REF = {}
+
+
+def _c2_oracle(model, seq, labels, cfg):
+    """The fp64 oracle on the C2 workload (logits, loss, every parameter and input gradient), computed once per
+    session: the fp32 and the bf16 tests share it (same seeds, same weights)."""
+    if "ref" not in _C2_REF:
+        P = _p64(model)
+        seq64 = [(x.detach().cpu().double().requires_grad_(True), ei.cpu(), None, ids) for x, ei, _, ids in seq]
+        ref = oracle.tagan_forward(P, cfg.to_dict(), seq64, labels.cpu().double())
+        ref["loss"].backward()
+        _C2_REF["ref"] = ({"logits": ref["logits"].detach(), "loss": ref["loss"].detach()},
+                          {k: (None if v.grad is None else v.grad.detach()) for k, v in P.items()},
+                          [x64.grad.detach() for x64, _, _, _ in seq64])
+    return _C2_REF["ref"]
+
+
+def _c2_run(dev, precision):
     from tagan_amd import TAGAN, synthetic
     cfg = synthetic.config_for("c2", dropout=0.0)
     torch.manual_seed(0)
-    model = TAGAN(cfg).to(dev).train()
+    model = TAGAN(cfg, precision=precision).to(dev).train()
     seq = synthetic.make_sequence("c2", dev, seed=1000)
     seq = [(x.clone().requires_grad_(True), ei, ea, ids) for x, ei, ea, ids in seq]
     labels = torch.tensor([1.0], device=dev)
     out = model(seq, labels=labels)
     out["loss"].backward()
-    P = _p64(model)
-    seq64 = [(x.detach().cpu().double().requires_grad_(True), ei.cpu(), None, ids) for x, ei, _, ids in seq]
-    ref = oracle.tagan_forward(P, cfg.to_dict(), seq64, labels.cpu().double())
+    return cfg, model, seq, labels, out
+
+
+@pytest.mark.timeout(900)
+def test_c2_full_model_vs_oracle(dev):
+    cfg, model, seq, labels, out = _c2_run(dev, "fp32")
+    ref, pgrad, xgrad = _c2_oracle(model, seq, labels, cfg)
     G.assert_close("logits", out["logits"], ref["logits"], OUT_ATOL, OUT_RTOL)
     G.assert_close("loss", out["loss"].reshape(1), ref["loss"].reshape(1), OUT_ATOL, OUT_RTOL)
-    ref["loss"].backward()
     n_checked = 0
     for name, p in model.named_parameters():
-        if P[name].grad is not None:
-            _close_grad("grad " + name, p.grad, P[name].grad)
+        if pgrad[name] is not None:
+            _close_grad("grad " + name, p.grad, pgrad[name])
             n_checked += 1
         else:
             assert p.grad is None or float(p.grad.abs().max()) == 0.0, name
     assert n_checked >= 30
-    for t, ((x, _, _, _), (x64, _, _, _)) in enumerate(zip(seq, seq64)):
-        _close_grad("grad x.%d" % t, x.grad, x64.grad)
+    for t, ((x, _, _, _), g64) in enumerate(zip(seq, xgrad)):
+        _close_grad("grad x.%d" % t, x.grad, g64)
+
+
+# bf16 mode (BASELINE's C2 dtype; fused.py "bf16": activations stored in bf16 between kernels, fp32 math and
+# accumulation inside every kernel, bf16 GEMM operands) against the same fp64 oracle.  Tolerance per tensor t,
+# derived from the bf16 roundings on t's dependency path (DESIGN.md §5):
+#     bound_t = KAPPA * U_RMS * sqrt(n_t)
+#   U_RMS = 2^-8 / sqrt(3): RMS relative error of one round-to-nearest store to bf16 (8 significant bits, error
+#           uniform within half an ulp);
+#   n_t   = the bf16 stores whose errors reach t: every attention block stores h = LN1(x), Q|K|V and the
+#           attention output and rounds its two weight operands (5 per block, 3 blocks = 15 before the logits);
+#           its backward stores d(out-proj output), d(context) and dQ|dK|dV and re-uses the two rounded weights
+#           (5 more per block the gradient flows back through): head 15, temporal block 20, geometric layer 1 25,
+#           geometric layer 0 / skip LayerNorm / node embedding / d(node features) 30;
+#   KAPPA = 4: the amplification of independent relative perturbations through LayerNorm, softmax and the
+#           BCE head (their Jacobians are O(1) in norm; 4 leaves 2x margin over the largest measured ratio).
+# Written exceptions: the analytically zero gradients (golden_io.ANALYTIC_ZERO: noise on both sides, checked to be
+# zero) and the ill-conditioned attention-pool bias (COND_GRADS: its fp32 oracle already carries a 1.7e-4
+# normwise error, i.e. a ~2900x amplification of fp32 rounding -- at bf16 precision that tensor has no correct
+# digits in ANY bf16 implementation; it is held to the element-wise bound only).
+U_RMS = 2.0 ** -8 / 3 ** 0.5
+KAPPA = 4.0
+
+
+def _bf16_stores(name):
+    if name.startswith(("classification_head.", "loss_fn.")):
+        return 15
+    if name.startswith("temporal_attention."):
+        return 20
+    if name.startswith("geometric_attention_layers.1."):
+        return 25
+    return 30      # geometric layer 0, skip LayerNorm, node embedding, d(node features)
+
+
+@pytest.mark.timeout(900)
+def test_c2_bf16_vs_oracle(dev):
+    cfg, model, seq, labels, out = _c2_run(dev, "bf16")
+    # the oracle runs on the fp32 master weights (the same initialisation as the fp32 test)
+    ref, pgrad, xgrad = _c2_oracle(model, seq, labels, cfg)
+    bound_out = KAPPA * U_RMS * 15 ** 0.5
+    for key, got, want in (("logits", out["logits"], ref["logits"]),
+                           ("loss", out["loss"].reshape(1), ref["loss"].reshape(1))):
+        nr = G.normwise_rel(got, want)
+        G.ERRORS.setdefault("test_c2_bf16_vs_oracle", {})[key] = [nr, bound_out]
+        assert nr <= bound_out, "%s: bf16 normwise %.3e > %.3e" % (key, nr, bound_out)
+    n_checked = 0
+    worst = (0.0, None)
+    for name, p in model.named_parameters():
+        if pgrad[name] is None:
+            continue
+        n_checked += 1
+        if G.declared_zero("grad " + name) and float(pgrad[name].abs().max()) <= GRAD_ATOL:
+            assert float(p.grad.abs().max()) <= 1e-3, name    # bf16 noise around an exact zero
+            continue
+        if any(name.endswith(k) for k in COND_GRADS):
+            G.assert_close("grad " + name, p.grad, pgrad[name], GRAD_ATOL, GRAD_RTOL, norm_rtol=float("inf"))
+            continue
+        bound = KAPPA * U_RMS * _bf16_stores(name) ** 0.5
+        nr = G.normwise_rel(p.grad, pgrad[name])
+        G.ERRORS.setdefault("test_c2_bf16_vs_oracle", {})["grad " + name] = [nr, bound]
+        worst = max(worst, (nr / bound, name))
+        assert nr <= bound, "grad %s: bf16 normwise %.3e > %.3e" % (name, nr, bound)
+    assert n_checked >= 30
+    bound_x = KAPPA * U_RMS * 30 ** 0.5
+    for t, ((x, _, _, _), g64) in enumerate(zip(seq, xgrad)):
+        nr = G.normwise_rel(x.grad, g64)
+        G.ERRORS.setdefault("test_c2_bf16_vs_oracle", {})["grad x.%d" % t] = [nr, bound_x]
+        assert nr <= bound_x, "grad x.%d: bf16 normwise %.3e > %.3e" % (t, nr, bound_x)
+    print("bf16 C2: worst normwise / bound = %.3f (%s)" % worst)
 
 
 # ----------------------------------------------------------------------------- C3-C5 sampled checks

@@ -127,3 +127,39 @@ def test_graph_intended_propagation_matches_eager(dev):
     torch.cuda.synchronize()
     for a, b in zip(eager[3:], graphed):
         assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (eager, graphed)
+
+
+def test_graph_keeps_offset_table_through_cache_eviction(dev):
+    """The snapshot offset table a captured step reads by address is pinned: flooding the LRU cache with 300 other
+    shapes between replays (kernels._ptr_table evicts beyond 256) neither frees it nor changes the trajectory."""
+    from tagan_amd import kernels
+    from tagan_amd.graph_step import GraphedStep
+    m1, o1, s1 = _setup(dev, 0.0)
+    m2, o2, s2 = _setup(dev, 0.0)
+    eager = []
+    for _ in range(6):
+        o1.zero_grad(set_to_none=True)
+        eager.append(float(s1()))
+    g = GraphedStep(m2, s2, optimizer=o2, warmup=3)
+    try:
+        assert len(kernels._PTR_PINNED) >= 1
+        pinned = dict(kernels._PTR_PINNED)
+        graphed = [float(g())]
+        for i in range(300):                      # evict every unpinned entry, allocating over the freed blocks
+            kernels._ptr_table(dev, [0, i + 1, 2 * i + 7])
+        junk = torch.full((1 << 20,), -1, dtype=torch.int64, device=dev)
+        graphed += [float(g()) for _ in range(2)]
+        del junk
+        assert all(kernels._PTR_PINNED[k] is t for k, t in pinned.items())
+    finally:
+        g.close()
+    torch.cuda.synchronize()
+    for a, b in zip(eager[3:], graphed):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (eager, graphed)
+
+
+def test_graphed_step_has_no_split_form(dev):
+    from tagan_amd.graph_step import GraphedStep
+    m, o, s = _setup(dev, 0.0)
+    with pytest.raises(TypeError):
+        GraphedStep(m, s, optimizer=o, warmup=1, between=lambda: None, post=lambda: None)

@@ -66,6 +66,7 @@ CASES = [  # T, H, C, B, kind, label shape
     (128, 64, 1, 1, "bce", "1d"),
     (32, 256, 1, 2, "bce", "1d"),     # T·H = 8192: the largest head the kernel takes, 4 step groups
     (20, 96, 4, 2, "ce", "1d"),       # H not a power of two: 10 step groups, 64 idle threads
+    (16, 128, 3, 4, "ce_ignore", "1d"),   # nn.CrossEntropyLoss's ignore_index -100 on one row
 ]
 
 
@@ -81,8 +82,10 @@ def test_fused_head(dev, T, H, C, B, kind, lshape, p):
     if kind == "bce":
         labels = (torch.rand(B, generator=g) > 0.5).float() if lshape == "1d" else \
             (torch.rand(B, C, generator=g) > 0.5).float()
-    elif kind == "ce":
+    elif kind in ("ce", "ce_ignore"):
         labels = torch.randint(0, C, (B,), generator=g)
+        if kind == "ce_ignore":
+            labels[1] = -100
     labels = labels.to(dev) if labels is not None else None
     seed = 12345
     out = fused_head(m, pooled, B, labels, C, seed=seed)
@@ -97,7 +100,8 @@ def test_fused_head(dev, T, H, C, B, kind, lshape, p):
                 mask[b, j] = keep if L.tagan_uniform(seed, b, j) >= p else 0.0
     import copy
     x0, P, rl, rp, rloss = _ref(copy.deepcopy(m).cpu(), pooled.detach().cpu(), B,
-                                labels.cpu() if labels is not None else None, kind, mask)
+                                labels.cpu() if labels is not None else None, "ce" if kind == "ce_ignore" else kind,
+                                mask)
     torch.testing.assert_close(logits.double().cpu(), rl.detach(), atol=ATOL, rtol=RTOL)
     torch.testing.assert_close(preds.double().cpu(), rp.detach(), atol=ATOL, rtol=RTOL)
     if kind == "none":

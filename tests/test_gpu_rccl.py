@@ -74,64 +74,83 @@ def test_rccl_world1_shard_and_buckets():
         dist.destroy_process_group()
 
 
-def test_rccl_world1_graph_split_step():
-    """bench.py's N > 1 launch form at world size 1: forward + backward captured as one HIP graph, the RCCL
-    gradient all-reduce (static bucket, forced) run eagerly between the two replays, clip + Adam captured as the
-    second graph -- the same loss trajectory and weights as the eager step (dropout off).  At this size the CSR
-    build does not reach rocPRIM's onesweep path; at C2 size the same split form faults in its second replay
-    (tools/split_graph_probe.py --pg nccl), which is why bench.py launches N > 1 steps eagerly."""
-    import tempfile
-    import tagan_amd  # noqa: F401
+def _graph_vs_eager(dev, seq, steps_eager=6, replays=3, seed=3):
+    """bench.py's N > 1 step at world size 1: forward, backward, the static gradient bucket's RCCL all-reduce
+    (forced), clip and Adam captured as ONE HIP graph -- replayed, against the same step launched eagerly with the
+    flagged bucket (dropout off): the same loss trajectory and weights."""
     from tagan_amd import TAGAN, synthetic
     from tagan_amd.distributed import GradBucket
     from tagan_amd.graph_step import GraphedStep
-    dev = torch.device("cuda:0")
-    torch.cuda.set_device(dev)
-    store = os.path.join(tempfile.mkdtemp(prefix="tagan_rccl_g_"), "store")
-    dist.init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1)
+    cfg = synthetic.config_for("c2", dropout=0.0)
+    labels = torch.tensor([1.0], device=dev)
+
+    def setup():
+        torch.manual_seed(seed)
+        m = TAGAN(cfg).to(dev).train()
+        o = torch.optim.Adam(m.parameters(), lr=1e-3, capturable=True)
+        return m, o, GradBucket(m.parameters())
+
+    m1, o1, b1 = setup()
+    eager = []
+    for _ in range(steps_eager):
+        o1.zero_grad(set_to_none=True)
+        out = m1(seq, labels=labels)
+        out["loss"].backward()
+        b1.allreduce_mean(force=True)
+        torch.nn.utils.clip_grad_norm_(m1.parameters(), 1.0)
+        o1.step()
+        eager.append(float(out["loss"]))
+
+    m2, o2, b2 = setup()
+
+    def whole():
+        out = m2(seq, labels=labels)
+        out["loss"].backward()
+        b2.allreduce_mean(force=True, static=True)
+        torch.nn.utils.clip_grad_norm_(m2.parameters(), 1.0)
+        o2.step()
+        return out["loss"]
+
+    g = GraphedStep(m2, whole, optimizer=o2, warmup=steps_eager - replays)
     try:
-        cfg = synthetic.config_for("c2", dropout=0.0)
+        graphed = [float(g()) for _ in range(replays)]
+    finally:
+        g.close()
+    torch.cuda.synchronize()
+    for a, b in zip(eager[steps_eager - replays:], graphed):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (eager, graphed)
+    for (k, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        torch.testing.assert_close(p2, p1, atol=1e-5, rtol=1e-4, msg=k)
+
+
+def _init_nccl(dev, tag):
+    import tempfile
+    torch.cuda.set_device(dev)
+    store = os.path.join(tempfile.mkdtemp(prefix="tagan_rccl_%s_" % tag), "store")
+    dist.init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1)
+
+
+def test_rccl_world1_graph_step_small():
+    import tagan_amd  # noqa: F401
+    from tagan_amd import synthetic
+    dev = torch.device("cuda:0")
+    _init_nccl(dev, "gs")
+    try:
         seq = synthetic.make_sequence("c2", dev, seed=7, snapshots=6, nodes=400, edges=3000)
-        labels = torch.tensor([1.0], device=dev)
+        _graph_vs_eager(dev, seq)
+    finally:
+        dist.destroy_process_group()
 
-        def setup():
-            torch.manual_seed(3)
-            m = TAGAN(cfg).to(dev).train()
-            o = torch.optim.Adam(m.parameters(), lr=1e-3, capturable=True)
-            return m, o, GradBucket(m.parameters())
 
-        m1, o1, b1 = setup()
-        eager = []
-        for _ in range(6):
-            o1.zero_grad(set_to_none=True)
-            out = m1(seq, labels=labels)
-            out["loss"].backward()
-            b1.allreduce_mean(force=True)
-            torch.nn.utils.clip_grad_norm_(m1.parameters(), 1.0)
-            o1.step()
-            eager.append(float(out["loss"]))
-
-        m2, o2, b2 = setup()
-
-        def fb():
-            out = m2(seq, labels=labels)
-            out["loss"].backward()
-            return out["loss"]
-
-        def post():
-            torch.nn.utils.clip_grad_norm_(m2.parameters(), 1.0)
-            o2.step()
-
-        g = GraphedStep(m2, fb, optimizer=o2, warmup=3, between=lambda: b2.allreduce_mean(force=True, static=True),
-                        post=post)
-        try:
-            graphed = [float(g()) for _ in range(3)]
-        finally:
-            g.close()
-        torch.cuda.synchronize()
-        for a, b in zip(eager[3:], graphed):
-            assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (eager, graphed)
-        for (k, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
-            torch.testing.assert_close(p2, p1, atol=1e-5, rtol=1e-4, msg=k)
+def test_rccl_world1_graph_step_c2():
+    """The same at the full C2 workload (10k nodes, 100k Zipf edges per snapshot, 32 snapshots): the size at which
+    the round-2 split capture (an eager all-reduce between two captured segments) faulted on replay."""
+    import tagan_amd  # noqa: F401
+    from tagan_amd import synthetic
+    dev = torch.device("cuda:0")
+    _init_nccl(dev, "gc2")
+    try:
+        seq = synthetic.make_sequence("c2", dev, seed=1000)
+        _graph_vs_eager(dev, seq, steps_eager=7, replays=4)
     finally:
         dist.destroy_process_group()

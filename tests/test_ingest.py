@@ -69,8 +69,28 @@ def test_snapshot_batch_errors():
         SnapshotBatch.from_sequence([[x, ei, None, [0] * 5]], "cpu")
     with pytest.raises(KeyError):
         SnapshotBatch.from_sequence([{"x": x, "edge_index": ei}], "cpu")   # the reference's snapshot['node_ids']
+    # the reference never checks one id per row (model.py:186-204): accepted, marked, snapshot() refuses
+    b = SnapshotBatch.from_sequence([(x, ei, None, [0, 1])], "cpu")
+    assert not b.ids_row_aligned and b.global_index()[0].tolist() == [0, 1]
     with pytest.raises(ValueError, match="node ids"):
-        SnapshotBatch.from_sequence([(x, ei, None, [0, 1])], "cpu")
+        b.snapshot(0)
+
+
+def test_snapshot_batch_string_ids():
+    """Non-integer global ids (string user ids): coded by rank in sorted(set(ids)), the reference's
+    all_node_ids order (model.py:184-201); snapshot() gives the original ids back."""
+    from tagan_amd.ingest import SnapshotBatch
+    g = torch.Generator().manual_seed(3)
+    ids0, ids1 = ["u17", "u03", "u99"], ["u03", "alice", "u17", "bob"]
+    seq = [(torch.randn(3, 4, generator=g), torch.tensor([[0, 1], [2, 0]]), None, ids0),
+           (torch.randn(4, 4, generator=g), torch.tensor([[0, 3], [1, 2]]), None, ids1)]
+    b = SnapshotBatch.from_sequence(seq, "cpu")
+    all_ids = sorted(set(ids0 + ids1))
+    assert b.id_values == all_ids and b.ids_row_aligned
+    uniq, inv = b.global_index()
+    assert [all_ids[k] for k in uniq.tolist()] == all_ids
+    assert [all_ids[k] for k in inv.tolist()] == ids0 + ids1
+    assert b.snapshot(0)[3] == ids0 and b.snapshot(1)[3] == ids1
 
 
 def test_social_generator_shape():
