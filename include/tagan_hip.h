@@ -86,6 +86,10 @@ int tagan_seed_counter_step(uint64_t* counter, void* stream);
  * (those edges are dropped; the reference raises IndexError).
  * max_graph_nodes = the largest snapshot's node count (<= 0: n_nodes); it sets
  * the width of the local-id field of the sort keys.  n_nodes < 2^31.
+ * csr_cpos (nullable, capacity as col): the CSC position of each CSR entry (the
+ * inverse of csc_eid), written by the same pass.  Kernel launches only (no library
+ * sort, no memset nodes): safe to capture in a HIP graph and to replay with other
+ * work in between.
  * ------------------------------------------------------------------------- */
 size_t tagan_csr_build_workspace(int64_t n_edges, int64_t n_nodes);
 int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges,
@@ -93,7 +97,7 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges,
                     int64_t n_nodes, int64_t max_graph_nodes,
                     int32_t* rowptr, int32_t* col,
                     int32_t* csc_ptr, int32_t* csc_row, int32_t* csc_eid,
-                    int64_t* nnz_out, int32_t* err_out,
+                    int64_t* nnz_out, int32_t* err_out, int32_t* csr_cpos,
                     void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------

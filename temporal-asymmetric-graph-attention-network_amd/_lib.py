@@ -45,7 +45,7 @@ _SIGNATURES = {
     "tagan_colsum": (_c.c_int, [_c.c_int, _i64, _i32, _p, _i64, _p, _p, _sz, _p]),
     "tagan_pool_fwd": (_c.c_int, [_c.c_int, _i32, _i64, _i32, _p, _i64, _i64, _p, _p, _sz, _p]),
     "tagan_pool_bwd": (_c.c_int, [_c.c_int, _i32, _i64, _i32, _p, _p, _i64, _i64, _p]),
-    "tagan_csr_build": (_c.c_int, [_p, _i64, _i64, _p, _p, _i32, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _sz,
+    "tagan_csr_build": (_c.c_int, [_p, _i64, _i64, _p, _p, _i32, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _sz,
                                    _p]),
     "tagan_chunk_capacity": (_i64, [_i64, _i64, _i32]),
     "tagan_part_capacity": (_i64, [_i64, _i32]),

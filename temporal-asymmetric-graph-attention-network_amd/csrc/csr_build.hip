@@ -1,138 +1,701 @@
 // Snapshot CSR/CSC builder: the sparse form of graph_attention.py:96-105
 //   adj = zeros(N,N); adj[edge_index[0], edge_index[1]] = 1; adj += eye(N)
-// for a block-diagonal batch of snapshots.  Integer/byte work: HBM-bound,
-// no MFMA.  Keys global_src * NL + local_dst (NL = the largest snapshot) are
-// radix-sorted with rocPRIM over only the bits of N * NL -- 32-bit keys when that
-// fits (32 bits at C2 instead of a 33-bit key in 64), de-duplicated, scattered into CSR.  The CSC (with CSR edge
-// ids) is a STABLE 32-bit key-value sort of the CSR entries by dst alone: the CSR
-// order is by src, so stability keeps src ascending within each column.
-#include <cstring>
-
-#include <rocprim/rocprim.hpp>
+// for a block-diagonal batch of snapshots.  Integer/byte work: HBM-bound, no MFMA, no library sort.
+//
+// Bucketed counting sort, every bucket finished in LDS:
+//   rows are grouped into BUCKETS of 2^SB consecutive global node ids (SB set so a bucket holds ~2k entries),
+//   buckets into COARSE BINS of 2^SC buckets (SC set so one snapshot spans <= ~256 bins: every partition pass
+//   keeps at most a few hundred write frontiers per block, so its scattered 4-B stores merge into whole lines
+//   in L2 instead of costing a read-modify-write each);
+//   1. count   : one pass over the raw edges, per-block LDS histograms of src AND dst buckets per snapshot
+//                (one atomic per non-empty bin), index validation;
+//   2. scan    : bucket capacities (raw edges + the bucket's self-loops) -> bucket regions;
+//   3. part    : second pass over the raw edges into the coarse bins, 32-bit keys
+//                (bucket-in-bin << SB+LB | row-in-bucket << LB | local dst);
+//   4. refine  : one workgroup per coarse bin moves its keys into the bucket regions (skipped when SC = 0);
+//   5. finish  : one workgroup per bucket loads its keys (+ its rows' self-loops) into LDS, radix-sorts them
+//                (stable LSD, 8-bit digits, wave-ballot ranks, up to 8 keys per thread per round), drops
+//                duplicates, counts entries per row;
+//   6. scan    : unique counts per bucket -> CSR offsets;  place: col, rowptr, and each entry's local src;
+//   7. CSC     : steps 3-5 again over the final CSR entries keyed by dst, carrying the CSR position
+//                (key = column-in-bucket << LB | local src, value = CSR position); the finish sorts the pairs
+//                (src ascending within a column = CSR order) and writes csc_ptr, csc_row, csc_eid and the
+//                CSR -> CSC position map in the same pass.
+// Buckets too large for the small LDS finish (power-law hubs) go on a device-side list that a persistent
+// 1024-thread kernel with 128 KB of LDS works through; beyond that, the same sort runs in global memory.
+// Every result is bitwise deterministic (a bucket is sorted on its full key); the launches are kernel nodes
+// only -- no library sort (rocPRIM's onesweep faulted on HIP-graph replay with eager kernels in between,
+// DESIGN.md §6), no memset nodes, no host synchronisation.
+#include <algorithm>
 
 #include "common.cuh"
+#include "scan.cuh"
 
 namespace tagan {
 namespace {
 
-constexpr int BLK = 256;
+constexpr int BLK = 256;           // generic grid-stride kernels
+constexpr int PNT = 1024;          // partition (count / part) blocks
+constexpr int LDS_BINS = 16384;    // LDS histogram bins per partition block and direction
+constexpr int RNT = 1024;          // refine blocks (one per coarse bin)
+constexpr int FNT = 256;           // small-bucket finish workgroups
+constexpr int FIPT = 8;            // keys per thread per sort round in the small finish
+constexpr int CAP_S = FNT * FIPT;  // keys (CSR) / pairs (CSC) per small finish: one round
+constexpr int BNT = 1024;          // big-bucket finish workgroups
+constexpr int BIG_LDS = 128 * 1024;   // dynamic LDS of the big-bucket kernels (2 key buffers / 2 + 2 pair buffers)
+constexpr int BIG_WG = 128;        // persistent workgroups of the big-bucket kernels
+constexpr int RB = 8;              // radix digit bits
+constexpr int RBINS = 1 << RB;
+constexpr int TARGET = 2048;       // average entries per bucket
+constexpr int SB_MAX = 10;         // at most 1024 rows per bucket
+constexpr int SC_MAX = 8;          // at most 256 buckets per coarse bin
+constexpr int COARSE_PER_SNAPSHOT = 192;
 
 // Graph of edge e: binary search in edge_ptr[0..G] (G small; edge_ptr in L2/scalar cache).
-__device__ __forceinline__ int find_graph(const int64_t* __restrict__ edge_ptr, int G, int64_t e) {
+__device__ __forceinline__ int find_graph(const int64_t* __restrict__ ptr, int G, int64_t e) {
     int lo = 0, hi = G - 1;
     while (lo < hi) {
         int mid = (lo + hi + 1) >> 1;
-        if (edge_ptr[mid] <= e) lo = mid; else hi = mid - 1;
+        if (ptr[mid] <= e) lo = mid; else hi = mid - 1;
     }
     return lo;
 }
 
-// Graph of global node n (n < N): binary search in node_ptr[0..G].
 __device__ __forceinline__ int64_t node_base(const int64_t* __restrict__ node_ptr, int G, int64_t n) {
     return node_ptr[find_graph(node_ptr, G, n)];
 }
 
-// Sort key of the pair (global src s, local dst d): s * NL + d with NL = the largest snapshot's node
-// count, so ascending keys are the CSR order (src-major, dst-minor); the key N * NL marks a dropped
-// (out-of-range) edge.  K = uint32_t whenever N * NL < 2^32 (C1, C2: 320k x 10k = 3.2e9): half the key
-// bytes of the 64-bit form and one radix pass fewer.
-template <typename K>
-__global__ void __launch_bounds__(BLK) k_make_keys(const int64_t* __restrict__ ei, int64_t ld_ei, int64_t E,
-                                                   const int64_t* __restrict__ edge_ptr,
-                                                   const int64_t* __restrict__ node_ptr, int G,
-                                                   int64_t N, int64_t NL, K* __restrict__ keys,
-                                                   int32_t* __restrict__ err) {
-    const K sentinel = (K)N * (K)NL;
-    for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < E + N; p += (int64_t)gridDim.x * BLK) {
-        K key;
-        if (p < E) {
-            const int g = find_graph(edge_ptr, G, p);
-            const int64_t base = node_ptr[g];
-            const int64_t n = node_ptr[g + 1] - base;
-            int64_t s = ei[p], d = ei[ld_ei + p];
-            s += (s < 0) ? n : 0;                 // torch advanced indexing wraps negatives
-            d += (d < 0) ? n : 0;
-            if (s < 0 || s >= n || d < 0 || d >= n) {
-                atomicOr(err, 1);
-                key = sentinel;
-            } else {
-                key = (K)(base + s) * (K)NL + (K)d;
+struct Geo {
+    int64_t N, E, NL;
+    int G, LB, SB, SC;
+    int64_t NB, NCB;     // buckets, coarse bins (the same geometry for CSR rows and CSC columns)
+    int64_t CHn;         // raw edges per count block (>> the buckets one snapshot spans: few flush atomics)
+    int64_t CH, CHc;     // raw edges / CSR entries per partition block
+};
+
+int bits_for(int64_t x) {   // bits to hold values 0..x
+    int b = 0;
+    while (b < 62 && ((int64_t)1 << b) <= x) ++b;
+    return b;
+}
+
+Geo geometry(int64_t E, int64_t N, int G, int64_t NL) {
+    Geo g{};
+    g.N = N; g.E = E; g.G = G; g.NL = NL;
+    g.LB = bits_for(NL - 1);
+    const double per_node = (double)(E + N) / (double)N;
+    int sb = 0;
+    while (sb < SB_MAX && (double)((int64_t)1 << (sb + 1)) * per_node <= TARGET) ++sb;
+    if (sb + g.LB > 31) sb = 31 - g.LB;
+    if (sb < 0) sb = 0;
+    g.SB = sb;
+    g.NB = (N + ((int64_t)1 << sb) - 1) >> sb;
+    const int64_t per_snap = (NL >> sb) + 2;   // buckets one snapshot spans
+    int sc = 0;
+    while (sc < SC_MAX && (per_snap >> sc) > COARSE_PER_SNAPSHOT && sc + 1 + sb + g.LB <= 32) ++sc;
+    g.SC = sc;
+    g.NCB = (g.NB + ((int64_t)1 << sc) - 1) >> sc;
+    int64_t chn = 65536;
+    while (chn < 16 * per_snap && chn < ((int64_t)1 << 20)) chn <<= 1;
+    g.CHn = chn;
+    g.CH = 65536;
+    g.CHc = 65536;
+    return g;
+}
+
+__device__ __forceinline__ int64_t bucket_rows(int64_t b, int sb, int64_t N) {
+    const int64_t r0 = b << sb;
+    return min(N, r0 + ((int64_t)1 << sb)) - r0;
+}
+
+// ---------------------------------------------------------------------------------------------- LDS radix sort
+// Stable LSD radix sort of n 32-bit keys over bits [0, nbits) (+ int32 values), NTH threads, ping-pong between
+// (ka, va) and (kb, vb) -- LDS or global (the big-bucket fallback).  Per pass and per round of NTH*IPT keys
+// (key i = r0 + k*NTH + tid: item slot k, wave w, lane): a lane's rank among the lanes of its wave with the same
+// digit comes from RB ballots; the per-(slot, wave) digit counts are prefixed in (slot, wave) order -> stable.
+// A single-round sort takes the digit offsets from that table; larger ones pre-count the pass's digits.
+// Returns the parity of the buffer holding the result (0 = a, 1 = b).
+// LDS: sh_base, sh_tot: RBINS ints each; sh_wc: IPT * (NTH/64) * RBINS ints; sh_sm: NTH/64 + 1 ints.
+template <int NTH, int IPT, bool VAL>
+__device__ int block_radix_sort(uint32_t* ka, uint32_t* kb, int32_t* va, int32_t* vb, int n, int nbits,
+                                int* sh_base, int* sh_tot, int* sh_wc, int32_t* sh_sm) {
+    constexpr int NW = NTH / WAVE;
+    constexpr int RND = NTH * IPT;
+    constexpr int SLOTS = IPT * NW;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & (WAVE - 1);
+    const uint64_t below = lane ? (~0ull >> (WAVE - lane)) : 0ull;
+    const bool multi = n > RND;
+    int par = 0;
+    for (int sh = 0; sh < nbits; sh += RB) {
+        const int dbits = min(RB, nbits - sh);
+        if (multi) {   // digit offsets of the whole pass
+            for (int i = tid; i < RBINS; i += NTH) sh_tot[i] = 0;
+            __syncthreads();
+            for (int i = tid; i < n; i += NTH) atomicAdd(&sh_tot[(ka[i] >> sh) & (RBINS - 1)], 1);
+            __syncthreads();
+            int32_t tot;
+            int x = 0;
+            if (tid < RBINS) x = sh_tot[tid];
+            const int32_t ex = scan::block_excl<NTH>((int32_t)x, (int32_t)0, scan::Plus(), sh_sm, &tot);
+            if (tid < RBINS) sh_base[tid] = ex;
+            __syncthreads();
+        }
+        for (int r0 = 0; r0 < n; r0 += RND) {
+            for (int i = tid; i < SLOTS * RBINS; i += NTH) sh_wc[i] = 0;
+            __syncthreads();
+            uint32_t key[IPT];
+            int32_t val[IPT];
+            int dig[IPT], rank[IPT];
+#pragma unroll
+            for (int k = 0; k < IPT; ++k) {
+                const int i = r0 + k * NTH + tid;
+                const bool ok = i < n;
+                key[k] = ok ? ka[i] : 0u;
+                val[k] = 0;
+                if (VAL && ok) val[k] = va[i];
+                const int d = (int)((key[k] >> sh) & (RBINS - 1));
+                uint64_t peers = __ballot(ok);
+                for (int b = 0; b < dbits; ++b) {
+                    const bool bit = (d >> b) & 1;
+                    const uint64_t m = __ballot(bit);
+                    peers &= bit ? m : ~m;
+                }
+                dig[k] = ok ? d : -1;
+                rank[k] = __popcll(peers & below);
+                if (ok && rank[k] == 0) sh_wc[(k * NW + w) * RBINS + d] = __popcll(peers);
             }
+            __syncthreads();
+            int x = 0;
+            for (int dd = tid; dd < RBINS; dd += NTH) {   // per digit: offsets of the (slot, wave) groups in order
+                int run = 0;
+                for (int s = 0; s < SLOTS; ++s) {
+                    const int c = sh_wc[s * RBINS + dd];
+                    sh_wc[s * RBINS + dd] = run;
+                    run += c;
+                }
+                sh_tot[dd] = run;
+                x = run;
+            }
+            if (!multi) {   // one round: the digit offsets are the scan of this round's totals
+                int32_t tot;
+                const int32_t ex = scan::block_excl<NTH>((int32_t)(tid < RBINS ? x : 0), (int32_t)0, scan::Plus(),
+                                                         sh_sm, &tot);
+                if (tid < RBINS) sh_base[tid] = ex;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < IPT; ++k) {
+                if (dig[k] >= 0) {
+                    const int p = sh_base[dig[k]] + sh_wc[(k * NW + w) * RBINS + dig[k]] + rank[k];
+                    kb[p] = key[k];
+                    if (VAL) vb[p] = val[k];
+                }
+            }
+            __syncthreads();
+            if (multi) {
+                for (int dd = tid; dd < RBINS; dd += NTH) sh_base[dd] += sh_tot[dd];
+                __syncthreads();
+            }
+        }
+        uint32_t* tk = ka; ka = kb; kb = tk;
+        int32_t* tv = va; va = vb; vb = tv;
+        par ^= 1;
+    }
+    return par;
+}
+
+// --------------------------------------------------------------------------------------------- the kernels
+__global__ void __launch_bounds__(BLK) k_init(Geo g, int32_t* __restrict__ cap_src, int32_t* __restrict__ fill_src,
+                                              int32_t* __restrict__ cap_dst, int32_t* __restrict__ fill_dst,
+                                              int32_t* __restrict__ fillc_src, int32_t* __restrict__ fillc_dst,
+                                              int32_t* __restrict__ nbig, int32_t* __restrict__ err) {
+    for (int64_t b = blockIdx.x * (int64_t)BLK + threadIdx.x; b < g.NB; b += (int64_t)gridDim.x * BLK) {
+        const int32_t rows = (int32_t)bucket_rows(b, g.SB, g.N);
+        cap_src[b] = rows;
+        cap_dst[b] = rows;
+        fill_src[b] = 0;
+        fill_dst[b] = 0;
+        if (b < g.NCB) { fillc_src[b] = 0; fillc_dst[b] = 0; }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) { nbig[0] = 0; nbig[1] = 0; *err = 0; }
+}
+
+__device__ __forceinline__ bool valid_edge(int64_t s, int64_t d, int64_t base, int64_t n, int64_t& gs,
+                                           int64_t& dl) {
+    s += (s < 0) ? n : 0;
+    d += (d < 0) ? n : 0;
+    if (s < 0 || s >= n || d < 0 || d >= n) return false;
+    gs = base + s;
+    dl = d;
+    return true;
+}
+
+constexpr int UNR = 4;   // loads in flight per lane in the streaming passes
+
+// bins of shift `sh` spanned by the nodes [v0, v1) of one snapshot
+struct Span {
+    int64_t b0;
+    int nb;
+    bool lds;
+};
+
+__device__ __forceinline__ Span span_of(int64_t v0, int64_t v1, int sh) {
+    Span s;
+    s.b0 = v0 >> sh;
+    const int64_t b1 = v1 > v0 ? ((v1 - 1) >> sh) + 1 : s.b0;
+    s.lds = b1 - s.b0 <= LDS_BINS;
+    s.nb = s.lds ? (int)(b1 - s.b0) : 0;
+    return s;
+}
+
+// 1. bucket histograms of the raw edges (src and dst), index validation; snapshot by snapshot inside the block
+__global__ void __launch_bounds__(PNT) k_count(Geo g, const int64_t* __restrict__ ei, int64_t ld,
+                                               const int64_t* __restrict__ edge_ptr,
+                                               const int64_t* __restrict__ node_ptr, int32_t* __restrict__ cap_src,
+                                               int32_t* __restrict__ cap_dst, int32_t* __restrict__ err) {
+    __shared__ int hs[LDS_BINS], hd[LDS_BINS];
+    __shared__ int bad;
+    const int64_t e0 = blockIdx.x * g.CHn, e1 = min(g.E, e0 + g.CHn);
+    const int g0 = find_graph(edge_ptr, g.G, e0), g1 = find_graph(edge_ptr, g.G, e1 - 1);
+    if (threadIdx.x == 0) bad = 0;
+    bool my_bad = false;
+    for (int gg = g0; gg <= g1; ++gg) {
+        const int64_t base = node_ptr[gg], n = node_ptr[gg + 1] - base;
+        const int64_t a = max(e0, edge_ptr[gg]), z = min(e1, edge_ptr[gg + 1]);
+        const Span sp = span_of(base, base + n, g.SB);
+        for (int i = threadIdx.x; i < sp.nb; i += PNT) { hs[i] = 0; hd[i] = 0; }
+        __syncthreads();
+        for (int64_t e4 = a + threadIdx.x; e4 < z; e4 += UNR * PNT) {   // UNR edges' loads in flight per lane
+            int64_t sv[UNR], dv[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int64_t e = e4 + u * PNT;
+                sv[u] = e < z ? ei[e] : 0;
+                dv[u] = e < z ? ei[ld + e] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                if (e4 + u * PNT >= z) break;
+                int64_t gs, dl;
+                if (!valid_edge(sv[u], dv[u], base, n, gs, dl)) { my_bad = true; continue; }
+                const int64_t bs = gs >> g.SB, bd = (base + dl) >> g.SB;
+                if (sp.lds) { atomicAdd(&hs[bs - sp.b0], 1); atomicAdd(&hd[bd - sp.b0], 1); }
+                else { atomicAdd(&cap_src[bs], 1); atomicAdd(&cap_dst[bd], 1); }
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < sp.nb; i += PNT) {
+            if (hs[i]) atomicAdd(&cap_src[sp.b0 + i], hs[i]);
+            if (hd[i]) atomicAdd(&cap_dst[sp.b0 + i], hd[i]);
+        }
+        __syncthreads();
+    }
+    if (my_bad) bad = 1;
+    __syncthreads();
+    if (threadIdx.x == 0 && bad) atomicOr(err, 1);
+}
+
+// 3. raw edges -> coarse src bins (SC > 0: staging layout) or straight into the buckets (SC = 0)
+__global__ void __launch_bounds__(PNT) k_part_edges(Geo g, const int64_t* __restrict__ ei, int64_t ld,
+                                                    const int64_t* __restrict__ edge_ptr,
+                                                    const int64_t* __restrict__ node_ptr,
+                                                    const int32_t* __restrict__ bstart, int32_t* __restrict__ fill,
+                                                    uint32_t* __restrict__ out) {
+    __shared__ int h[LDS_BINS];
+    const int64_t e0 = blockIdx.x * g.CH, e1 = min(g.E, e0 + g.CH);
+    const int g0 = find_graph(edge_ptr, g.G, e0), g1 = find_graph(edge_ptr, g.G, e1 - 1);
+    const int shc = g.SB + g.SC;                       // node id -> coarse bin
+    const uint32_t rmask = (1u << g.SB) - 1u, fmask = (1u << g.SC) - 1u;
+    for (int gg = g0; gg <= g1; ++gg) {
+        const int64_t base = node_ptr[gg], n = node_ptr[gg + 1] - base;
+        const int64_t a = max(e0, edge_ptr[gg]), z = min(e1, edge_ptr[gg + 1]);
+        const Span sp = span_of(base, base + n, shc);
+        if (sp.lds) {
+            for (int i = threadIdx.x; i < sp.nb; i += PNT) h[i] = 0;
+            __syncthreads();
+            for (int64_t e4 = a + threadIdx.x; e4 < z; e4 += UNR * PNT) {
+                int64_t sv[UNR], dv[UNR];
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    const int64_t e = e4 + u * PNT;
+                    sv[u] = e < z ? ei[e] : 0;
+                    dv[u] = e < z ? ei[ld + e] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    int64_t gs, dl;
+                    if (e4 + u * PNT < z && valid_edge(sv[u], dv[u], base, n, gs, dl))
+                        atomicAdd(&h[(gs >> shc) - sp.b0], 1);
+                }
+            }
+            __syncthreads();
+            for (int i = threadIdx.x; i < sp.nb; i += PNT) {   // one reservation per non-empty bin
+                const int c = h[i];
+                const int64_t bin = sp.b0 + i;
+                if (c) h[i] = bstart[bin << g.SC] + atomicAdd(&fill[bin], c);
+            }
+            __syncthreads();
+        }
+        for (int64_t e4 = a + threadIdx.x; e4 < z; e4 += UNR * PNT) {
+            int64_t sv[UNR], dv[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int64_t e = e4 + u * PNT;
+                sv[u] = e < z ? ei[e] : 0;
+                dv[u] = e < z ? ei[ld + e] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                if (e4 + u * PNT >= z) break;
+                int64_t gs, dl;
+                if (!valid_edge(sv[u], dv[u], base, n, gs, dl)) continue;
+                const int64_t bin = gs >> shc;
+                const int pos = sp.lds ? atomicAdd(&h[bin - sp.b0], 1)
+                                       : bstart[bin << g.SC] + atomicAdd(&fill[bin], 1);
+                out[pos] = ((((uint32_t)(gs >> g.SB) & fmask) << g.SB | ((uint32_t)gs & rmask)) << g.LB) |
+                           (uint32_t)dl;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// 4. one workgroup per coarse bin: its staged keys (bucket-in-bin in the bits above SB + LB) -> bucket regions
+template <bool VAL>
+__global__ void __launch_bounds__(RNT) k_refine(Geo g, const int32_t* __restrict__ bstart,
+                                                const int32_t* __restrict__ fillc, const uint32_t* __restrict__ skey,
+                                                const int32_t* __restrict__ sval, int32_t* __restrict__ fill,
+                                                uint32_t* __restrict__ key, int32_t* __restrict__ val) {
+    __shared__ int h[1 << SC_MAX];
+    const int64_t c = blockIdx.x;
+    const int64_t f0 = c << g.SC;
+    const int nf = (int)(min(g.NB, f0 + ((int64_t)1 << g.SC)) - f0);
+    const int32_t s0 = bstart[f0], cnt = fillc[c];
+    const int kb = g.SB + g.LB;
+    const uint32_t kmask = (uint32_t)(((uint64_t)1 << kb) - 1);
+    for (int i = threadIdx.x; i < nf; i += RNT) h[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < cnt; i += RNT) atomicAdd(&h[skey[s0 + i] >> kb], 1);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nf; i += RNT) {
+        fill[f0 + i] = h[i];
+        h[i] = bstart[f0 + i];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < cnt; i += RNT) {
+        const uint32_t k = skey[s0 + i];
+        const int p = atomicAdd(&h[k >> kb], 1);
+        key[p] = k & kmask;
+        if (VAL) val[p] = sval[s0 + i];
+    }
+}
+
+// 5. CSR bucket finish: sort + dedupe + per-row counts.  Writes the unique keys back over the bucket's region,
+// the in-bucket row prefix into rowptr and the bucket's unique count.  R holds the m sorted keys on return of the
+// sort; the compaction runs IPT consecutive keys per thread (one block scan for up to NTH * IPT keys per round).
+template <int NTH, int IPT>
+__device__ void csr_finish(const Geo& g, int64_t b, uint32_t* A, uint32_t* B, int m, int c, int32_t off,
+                           const int64_t* __restrict__ node_ptr, uint32_t* __restrict__ keys,
+                           int32_t* __restrict__ rowptr, int32_t* __restrict__ ucnt, int* sh_base, int* sh_tot,
+                           int* sh_wc, int* sh_rc, int32_t* sh_sm) {
+    const int tid = threadIdx.x;
+    const int64_t r0 = b << g.SB;
+    const int nv = (int)bucket_rows(b, g.SB, g.N);
+    for (int j = tid; j < nv; j += NTH) {     // the bucket's self-loops ("+ eye")
+        const int64_t v = r0 + j;
+        A[c + j] = ((uint32_t)j << g.LB) | (uint32_t)(v - node_base(node_ptr, g.G, v));
+        sh_rc[j] = 0;
+    }
+    __syncthreads();
+    const uint32_t* R = block_radix_sort<NTH, IPT, false>(A, B, nullptr, nullptr, m, g.SB + g.LB, sh_base, sh_tot,
+                                                          sh_wc, sh_sm) ? B : A;
+    int32_t run = 0;
+    for (int t0 = 0; t0 < m; t0 += NTH * IPT) {
+        const int i0 = t0 + tid * IPT;
+        uint32_t k[IPT];
+        int u = 0;
+        uint32_t first = 0;     // bit q: key i0 + q is the first of its run (kept)
+#pragma unroll
+        for (int q = 0; q < IPT; ++q) {
+            const int i = i0 + q;
+            k[q] = i < m ? R[i] : 0u;
+            if (i < m && (i == 0 || R[i - 1] != k[q])) { first |= 1u << q; ++u; }
+        }
+        int32_t tot;
+        int32_t pos = run + scan::block_excl<NTH>((int32_t)u, (int32_t)0, scan::Plus(), sh_sm, &tot);
+#pragma unroll
+        for (int q = 0; q < IPT; ++q) {
+            if ((first >> q) & 1u) {
+                keys[off + pos++] = k[q];
+                atomicAdd(&sh_rc[k[q] >> g.LB], 1);
+            }
+        }
+        run += tot;
+        __syncthreads();
+    }
+    // in-bucket row prefix (rows <= 1024: a few per thread, one block scan)
+    constexpr int RPT = (1 << SB_MAX) / NTH > 0 ? (1 << SB_MAX) / NTH : 1;
+    int v[RPT], t = 0;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int j = tid * RPT + q;
+        v[q] = j < nv ? sh_rc[j] : 0;
+        t += v[q];
+    }
+    int32_t tot;
+    int32_t pre = scan::block_excl<NTH>((int32_t)t, (int32_t)0, scan::Plus(), sh_sm, &tot);
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int j = tid * RPT + q;
+        if (j < nv) rowptr[r0 + j] = pre;
+        pre += v[q];
+    }
+    if (tid == 0) ucnt[b] = run;
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(FNT) k_csr_finish(Geo g, const int32_t* __restrict__ bstart,
+                                                    const int32_t* __restrict__ fill_src,
+                                                    const int64_t* __restrict__ node_ptr, uint32_t* __restrict__ keys,
+                                                    int32_t* __restrict__ rowptr, int32_t* __restrict__ ucnt,
+                                                    int32_t* __restrict__ big, int32_t* __restrict__ nbig) {
+    __shared__ uint32_t A[CAP_S], Bk[CAP_S];
+    __shared__ int base[RBINS], tot[RBINS], wc[FIPT * (FNT / WAVE) * RBINS], rc[1 << SB_MAX];
+    __shared__ int32_t sm[FNT / WAVE + 1];
+    const int64_t b = blockIdx.x;
+    const int c = fill_src[b];
+    const int m = c + (int)bucket_rows(b, g.SB, g.N);
+    if (m > CAP_S) {
+        if (threadIdx.x == 0) big[atomicAdd(nbig, 1)] = (int32_t)b;
+        return;
+    }
+    const int32_t off = bstart[b];
+    for (int i = threadIdx.x; i < c; i += FNT) A[i] = keys[off + i];
+    csr_finish<FNT, FIPT>(g, b, A, Bk, m, c, off, node_ptr, keys, rowptr, ucnt, base, tot, wc, rc, sm);
+}
+
+__global__ void __launch_bounds__(BNT) k_csr_finish_big(Geo g, const int32_t* __restrict__ bstart,
+                                                        const int32_t* __restrict__ fill_src,
+                                                        const int64_t* __restrict__ node_ptr,
+                                                        uint32_t* __restrict__ keys, uint32_t* __restrict__ scratch,
+                                                        int32_t* __restrict__ rowptr, int32_t* __restrict__ ucnt,
+                                                        const int32_t* __restrict__ big,
+                                                        const int32_t* __restrict__ nbig) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    __shared__ int base[RBINS], tot[RBINS], wc[(BNT / WAVE) * RBINS], rc[1 << SB_MAX];
+    __shared__ int32_t sm[BNT / WAVE + 1];
+    constexpr int CAP = BIG_LDS / 8;
+    const int nb = *nbig;
+    for (int q = blockIdx.x; q < nb; q += gridDim.x) {
+        const int64_t b = big[q];
+        const int c = fill_src[b];
+        const int m = c + (int)bucket_rows(b, g.SB, g.N);
+        const int32_t off = bstart[b];
+        if (m <= CAP) {
+            uint32_t* A = dyn;
+            uint32_t* Bk = dyn + CAP;
+            for (int i = threadIdx.x; i < c; i += BNT) A[i] = keys[off + i];
+            csr_finish<BNT, 1>(g, b, A, Bk, m, c, off, node_ptr, keys, rowptr, ucnt, base, tot, wc, rc, sm);
+        } else {   // in global memory: the bucket's own region (room for its self-loops) and the scratch twin
+            csr_finish<BNT, 1>(g, b, keys + off, scratch + off, m, c, off, node_ptr, keys, rowptr, ucnt, base, tot, wc,
+                               rc, sm);
+        }
+    }
+}
+
+// 6. place: CSR col, rowptr (+ the bucket's offset), each entry's local src (for the CSC pass), nnz
+__global__ void __launch_bounds__(FNT) k_csr_place(Geo g, const int32_t* __restrict__ bstart,
+                                                   const int32_t* __restrict__ uoff,
+                                                   const int64_t* __restrict__ node_ptr,
+                                                   const uint32_t* __restrict__ keys, int32_t* __restrict__ rowptr,
+                                                   int32_t* __restrict__ col, int32_t* __restrict__ sloc,
+                                                   int64_t* __restrict__ nnz_out) {
+    __shared__ int32_t rb[1 << SB_MAX];
+    const int64_t b = blockIdx.x;
+    const int64_t r0 = b << g.SB;
+    const int nv = (int)bucket_rows(b, g.SB, g.N);
+    const int32_t off = bstart[b], u = uoff[b], cnt = uoff[b + 1] - u;
+    for (int j = threadIdx.x; j < nv; j += FNT) {
+        rb[j] = (int32_t)node_base(node_ptr, g.G, r0 + j);
+        rowptr[r0 + j] += u;
+    }
+    __syncthreads();
+    const uint32_t lmask = (uint32_t)(((uint64_t)1 << g.LB) - 1);
+    for (int i = threadIdx.x; i < cnt; i += FNT) {
+        const uint32_t k = keys[off + i];
+        const int j = (int)(k >> g.LB);
+        col[u + i] = rb[j] + (int32_t)(k & lmask);
+        sloc[u + i] = (int32_t)(r0 + j) - rb[j];
+    }
+    if (b == g.NB - 1 && threadIdx.x == 0) {
+        rowptr[g.N] = uoff[g.NB];
+        *nnz_out = uoff[g.NB];
+    }
+}
+
+// 7a. CSR entries -> (bucket-in-bin << SB+LB | column-in-bucket << LB | local src, CSR position), coarse dst bins
+// (SC = 0: straight into the dst buckets); snapshot by snapshot inside the block
+__global__ void __launch_bounds__(PNT) k_part_csr(Geo g, const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col, const int32_t* __restrict__ sloc,
+                                                  const int64_t* __restrict__ node_ptr,
+                                                  const int64_t* __restrict__ nnz_p,
+                                                  const int32_t* __restrict__ cstart, int32_t* __restrict__ fill,
+                                                  uint32_t* __restrict__ okey, int32_t* __restrict__ oval) {
+    __shared__ int h[LDS_BINS];
+    __shared__ int gr[2];
+    const int64_t nnz = *nnz_p;
+    const int64_t e0 = blockIdx.x * g.CHc, e1 = min(nnz, e0 + g.CHc);
+    if (e0 >= e1) return;
+    if (threadIdx.x < 2) {   // snapshots of the first / last entry's row (binary search of rowptr)
+        const int64_t e = threadIdx.x == 0 ? e0 : e1 - 1;
+        int64_t lo = 0, hi = g.N - 1;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) >> 1;
+            if (rowptr[mid] <= e) lo = mid; else hi = mid - 1;
+        }
+        gr[threadIdx.x] = find_graph(node_ptr, g.G, lo);
+    }
+    __syncthreads();
+    const int shc = g.SB + g.SC;
+    const uint32_t cmask = (1u << g.SB) - 1u, fmask = (1u << g.SC) - 1u;
+    const int g0 = gr[0], g1 = gr[1];
+    for (int gg = g0; gg <= g1; ++gg) {
+        const int64_t v0 = node_ptr[gg], v1 = node_ptr[gg + 1];
+        const int64_t a = max(e0, (int64_t)rowptr[v0]), z = min(e1, (int64_t)rowptr[v1]);
+        const Span sp = span_of(v0, v1, shc);
+        if (sp.lds) {
+            for (int i = threadIdx.x; i < sp.nb; i += PNT) h[i] = 0;
+            __syncthreads();
+            for (int64_t e = a + threadIdx.x; e < z; e += PNT) atomicAdd(&h[(col[e] >> shc) - sp.b0], 1);
+            __syncthreads();
+            for (int i = threadIdx.x; i < sp.nb; i += PNT) {
+                const int c = h[i];
+                const int64_t bin = sp.b0 + i;
+                if (c) h[i] = cstart[bin << g.SC] + atomicAdd(&fill[bin], c);
+            }
+            __syncthreads();
+        }
+        for (int64_t e = a + threadIdx.x; e < z; e += PNT) {
+            const int32_t d = col[e];
+            const int64_t bin = d >> shc;
+            const int pos = sp.lds ? atomicAdd(&h[bin - sp.b0], 1) : cstart[bin << g.SC] + atomicAdd(&fill[bin], 1);
+            okey[pos] = ((((uint32_t)(d >> g.SB) & fmask) << g.SB | ((uint32_t)d & cmask)) << g.LB) |
+                        (uint32_t)sloc[e];
+            oval[pos] = (int32_t)e;
+        }
+        __syncthreads();
+    }
+}
+
+// 7b. CSC bucket finish: sort (key, CSR position) pairs, write csc_row / csc_eid / csc_ptr and the CSR -> CSC map
+template <int NTH, int IPT>
+__device__ void csc_finish(const Geo& g, int64_t b, uint32_t* K, uint32_t* K2, int32_t* V, int32_t* V2, int m,
+                           int32_t o, const int64_t* __restrict__ node_ptr, int32_t* __restrict__ csc_ptr,
+                           int32_t* __restrict__ csc_row, int32_t* __restrict__ csc_eid, int32_t* __restrict__ cpos,
+                           int* sh_base, int* sh_tot, int* sh_wc, int* sh_cc, int32_t* sh_sm) {
+    const int tid = threadIdx.x;
+    const int64_t c0 = b << g.SB;
+    const int nv = (int)bucket_rows(b, g.SB, g.N);
+    for (int j = tid; j < nv; j += NTH) {
+        sh_cc[j] = 0;
+        sh_cc[(1 << SB_MAX) + j] = (int)node_base(node_ptr, g.G, c0 + j);
+    }
+    __syncthreads();
+    const int par = block_radix_sort<NTH, IPT, true>(K, K2, V, V2, m, g.SB + g.LB, sh_base, sh_tot, sh_wc, sh_sm);
+    const uint32_t* RK = par ? K2 : K;
+    const int32_t* RV = par ? V2 : V;
+    const uint32_t lmask = (uint32_t)(((uint64_t)1 << g.LB) - 1);
+    for (int i = tid; i < m; i += NTH) {
+        const uint32_t k = RK[i];
+        const int j = (int)(k >> g.LB);
+        const int32_t e = RV[i];
+        csc_row[o + i] = sh_cc[(1 << SB_MAX) + j] + (int32_t)(k & lmask);
+        csc_eid[o + i] = e;
+        if (cpos) cpos[e] = o + i;
+        atomicAdd(&sh_cc[j], 1);
+    }
+    __syncthreads();
+    constexpr int RPT = (1 << SB_MAX) / NTH > 0 ? (1 << SB_MAX) / NTH : 1;
+    int v[RPT], t = 0;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int j = tid * RPT + q;
+        v[q] = j < nv ? sh_cc[j] : 0;
+        t += v[q];
+    }
+    int32_t tot;
+    int32_t pre = o + scan::block_excl<NTH>((int32_t)t, (int32_t)0, scan::Plus(), sh_sm, &tot);
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int j = tid * RPT + q;
+        if (j < nv) csc_ptr[c0 + j] = pre;
+        pre += v[q];
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(FNT) k_csc_finish(Geo g, const int32_t* __restrict__ cstart,
+                                                    const int32_t* __restrict__ fill_dst,
+                                                    const int32_t* __restrict__ coff,
+                                                    const int64_t* __restrict__ node_ptr,
+                                                    const uint32_t* __restrict__ ckey,
+                                                    const int32_t* __restrict__ cval, int32_t* __restrict__ csc_ptr,
+                                                    int32_t* __restrict__ csc_row, int32_t* __restrict__ csc_eid,
+                                                    int32_t* __restrict__ cpos, int32_t* __restrict__ big,
+                                                    int32_t* __restrict__ nbig) {
+    __shared__ uint32_t K[CAP_S], K2[CAP_S];
+    __shared__ int32_t V[CAP_S], V2[CAP_S];
+    __shared__ int base[RBINS], tot[RBINS], wc[FIPT * (FNT / WAVE) * RBINS], cc[2 << SB_MAX];
+    __shared__ int32_t sm[FNT / WAVE + 1];
+    const int64_t b = blockIdx.x;
+    const int m = fill_dst[b];
+    if (m > CAP_S) {
+        if (threadIdx.x == 0) big[atomicAdd(nbig + 1, 1)] = (int32_t)b;
+        return;
+    }
+    const int32_t ro = cstart[b];
+    for (int i = threadIdx.x; i < m; i += FNT) { K[i] = ckey[ro + i]; V[i] = cval[ro + i]; }
+    csc_finish<FNT, FIPT>(g, b, K, K2, V, V2, m, coff[b], node_ptr, csc_ptr, csc_row, csc_eid, cpos, base, tot, wc,
+                          cc, sm);
+    if (b == g.NB - 1 && threadIdx.x == 0) csc_ptr[g.N] = coff[g.NB];
+}
+
+__global__ void __launch_bounds__(BNT) k_csc_finish_big(Geo g, const int32_t* __restrict__ cstart,
+                                                        const int32_t* __restrict__ fill_dst,
+                                                        const int32_t* __restrict__ coff,
+                                                        const int64_t* __restrict__ node_ptr,
+                                                        uint32_t* __restrict__ ckey, int32_t* __restrict__ cval,
+                                                        uint32_t* __restrict__ sk, int32_t* __restrict__ sv,
+                                                        int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_row,
+                                                        int32_t* __restrict__ csc_eid, int32_t* __restrict__ cpos,
+                                                        const int32_t* __restrict__ big,
+                                                        const int32_t* __restrict__ nbig) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    __shared__ int base[RBINS], tot[RBINS], wc[(BNT / WAVE) * RBINS], cc[2 << SB_MAX];
+    __shared__ int32_t sm[BNT / WAVE + 1];
+    constexpr int CAP = BIG_LDS / 16;
+    const int nb = nbig[1];
+    for (int q = blockIdx.x; q < nb; q += gridDim.x) {
+        const int64_t b = big[q];
+        const int m = fill_dst[b];
+        const int32_t ro = cstart[b];
+        if (m <= CAP) {
+            uint32_t* K = dyn;
+            uint32_t* K2 = dyn + CAP;
+            int32_t* V = (int32_t*)(dyn + 2 * CAP);
+            int32_t* V2 = (int32_t*)(dyn + 3 * CAP);
+            for (int i = threadIdx.x; i < m; i += BNT) { K[i] = ckey[ro + i]; V[i] = cval[ro + i]; }
+            csc_finish<BNT, 1>(g, b, K, K2, V, V2, m, coff[b], node_ptr, csc_ptr, csc_row, csc_eid, cpos, base, tot,
+                               wc, cc, sm);
         } else {
-            const int64_t i = p - E;                // self-loop of global node i (the "+ eye")
-            key = (K)i * (K)NL + (K)(i - node_base(node_ptr, G, i));
+            csc_finish<BNT, 1>(g, b, ckey + ro, sk + ro, cval + ro, sv + ro, m, coff[b], node_ptr, csc_ptr, csc_row,
+                               csc_eid, cpos, base, tot, wc, cc, sm);
         }
-        keys[p] = key;
+        if (b == g.NB - 1 && threadIdx.x == 0) csc_ptr[g.N] = coff[g.NB];
     }
 }
 
-template <typename K>
-__global__ void __launch_bounds__(BLK) k_unique_flags(const K* __restrict__ keys, int64_t M, int64_t N, int64_t NL,
-                                                      int32_t* __restrict__ flags) {
-    const K sentinel = (K)N * (K)NL;
-    for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
-        const K k = keys[p];
-        flags[p] = (k < sentinel && (p == 0 || keys[p - 1] != k)) ? 1 : 0;
-    }
-}
-
-// Scatter unique keys into CSR; emit CSC keys (global dst) with value = CSR position and the
-// row of every CSR position (srcq) for the CSC scatter.
-template <typename K>
-__global__ void __launch_bounds__(BLK) k_scatter_csr(const K* __restrict__ keys, const int32_t* __restrict__ flags,
-                                                     const int32_t* __restrict__ pos, int64_t M, int64_t N,
-                                                     int64_t NL, const int64_t* __restrict__ node_ptr, int G,
-                                                     int32_t* __restrict__ rowptr, int32_t* __restrict__ col,
-                                                     uint32_t* __restrict__ ckeys, int32_t* __restrict__ cvals,
-                                                     int32_t* __restrict__ srcq, int64_t* __restrict__ nnz_out) {
-    const K nl = (K)NL;
-    for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
-        if (p == M - 1) {
-            const int64_t nnz = (int64_t)pos[p] + flags[p];
-            *nnz_out = nnz;
-            rowptr[N] = (int32_t)nnz;
-        }
-        if (!flags[p]) continue;
-        const K k = keys[p];
-        const K rk = k / nl;
-        const int64_t r = (int64_t)rk;
-        const int32_t c = (int32_t)(node_base(node_ptr, G, r) + (int64_t)(k - rk * nl));
-        const int32_t q = pos[p];
-        col[q] = c;
-        if (p == 0 || keys[p - 1] / nl != rk) rowptr[r] = q;   // every row has its self-loop
-        ckeys[q] = (uint32_t)c;
-        cvals[q] = q;
-        srcq[q] = (int32_t)r;
-    }
-}
-
-__global__ void __launch_bounds__(BLK) k_fill_tail(uint32_t* __restrict__ ckeys, int32_t* __restrict__ cvals,
-                                                   const int64_t* __restrict__ nnz_p, int64_t M, int64_t N) {
-    const int64_t nnz = *nnz_p;
-    for (int64_t p = nnz + blockIdx.x * (int64_t)BLK + threadIdx.x; p < M; p += (int64_t)gridDim.x * BLK) {
-        ckeys[p] = (uint32_t)N;    // sentinel: sorts after every column
-        cvals[p] = -1;
-    }
-}
-
-__global__ void __launch_bounds__(BLK) k_scatter_csc(const uint32_t* __restrict__ ckeys,
-                                                     const int32_t* __restrict__ cvals,
-                                                     const int32_t* __restrict__ srcq,
-                                                     const int64_t* __restrict__ nnz_p, int64_t N,
-                                                     int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_row,
-                                                     int32_t* __restrict__ csc_eid) {
-    const int64_t nnz = *nnz_p;
-    for (int64_t p = blockIdx.x * (int64_t)BLK + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * BLK) {
-        const uint32_t c = ckeys[p];
-        const int32_t q = cvals[p];
-        csc_row[p] = srcq[q];
-        csc_eid[p] = q;
-        if (p == 0 || ckeys[p - 1] != c) csc_ptr[c] = (int32_t)p;
-        if (p == nnz - 1) csc_ptr[N] = (int32_t)nnz;
-    }
-}
-
-// inverse of csc_eid: the CSC position of each CSR entry (the column-first edge backward reads dS through it)
+// inverse of csc_eid: the CSC position of each CSR entry (graphs not built by tagan_csr_build)
 __global__ void __launch_bounds__(BLK) k_csc_pos(const int32_t* __restrict__ csc_eid, const int64_t* __restrict__ nnz_p,
                                                  int32_t* __restrict__ cpos) {
     const int64_t nnz = *nnz_p;
@@ -140,86 +703,41 @@ __global__ void __launch_bounds__(BLK) k_csc_pos(const int32_t* __restrict__ csc
         cpos[csc_eid[p]] = (int32_t)p;
 }
 
-// CSC sort (32-bit dst keys over key_bits(N) bits, int32 values): 10-bit digits instead of rocPRIM's default 8 --
-// two onesweep passes instead of three at N < 2^20.  3.2M pairs / 19 bits (C2): 129 -> 105 us; the CSR key sort
-// stays on the default (11-bit digits measured slower there: 142 vs 180 us; tools/probes/sort_probe.hip).
-using CscSortCfg = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 32>, rocprim::kernel_config<1024, 12>, 10,
-                                        rocprim::block_radix_rank_algorithm::match>,
-    0>;
-
-int key_bits(int64_t N) {
-    int b = 1;
-    while (b < 32 && ((int64_t)1 << b) <= N) ++b;   // values 0..N inclusive (sentinel = N)
-    return b;
+int grid_for(int64_t n) {
+    int64_t gsz = (n + BLK - 1) / BLK;
+    if (gsz > 256 * 16) gsz = 256 * 16;
+    return (int)(gsz < 1 ? 1 : gsz);
 }
 
 struct CsrWs {
-    size_t keys_a, keys_b, ckeys_b, cvals_b, srcq, flags, pos, temp, total;
-    size_t temp_bytes;
+    size_t cap_src, fill_src, fillc_src, ucnt, cap_dst, fill_dst, fillc_dst, coff, big_src, big_dst, nbig, part,
+        keys, stage, sloc, cval, sval, total;
 };
 
-CsrWs plan(int64_t E, int64_t N) {
-    const int64_t M = E + N;
+CsrWs plan(const Geo& g) {
+    const int64_t M = g.E + g.N;
     CsrWs w{};
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
-    w.keys_a = take(M * 8);
-    w.keys_b = take(M * 8);
-    w.ckeys_b = take(M * 4);
-    w.cvals_b = take(M * 4);
-    w.srcq = take(M * 4);
-    w.flags = take(M * 4);
-    w.pos = take(M * 4);
-    const int bits = key_bits(N);
-    size_t t1 = 0, t2 = 0, t3 = 0;
-    size_t t1b = 0;
-    (void)rocprim::radix_sort_keys(nullptr, t1, (uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)M, 0, 64);
-    (void)rocprim::radix_sort_keys(nullptr, t1b, (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)M, 0, 32);
-    t1 = std::max(t1, t1b);
-    (void)rocprim::radix_sort_pairs<CscSortCfg>(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
-                                                (int32_t*)nullptr, (size_t)M, 0, bits);
-    (void)rocprim::exclusive_scan(nullptr, t3, (int32_t*)nullptr, (int32_t*)nullptr, 0, (size_t)M,
-                            rocprim::plus<int32_t>());
-    w.temp_bytes = std::max(t1, std::max(t2, t3));
-    w.temp = take(w.temp_bytes);
+    w.cap_src = take((g.NB + 1) * 4);
+    w.fill_src = take(g.NB * 4);
+    w.fillc_src = take(g.NCB * 4);
+    w.ucnt = take((g.NB + 1) * 4);
+    w.cap_dst = take((g.NB + 1) * 4);
+    w.fill_dst = take(g.NB * 4);
+    w.fillc_dst = take(g.NCB * 4);
+    w.coff = take((g.NB + 1) * 4);
+    w.big_src = take(g.NB * 4);
+    w.big_dst = take(g.NB * 4);
+    w.nbig = take(2 * 4);
+    w.part = take(scan::parts_len(g.NB) * 4);
+    w.keys = take(M * 4);      // bucket layout: CSR keys, then the CSC keys
+    w.stage = take(M * 4);     // coarse staging keys; the big buckets' global-memory sort twin
+    w.sloc = take(M * 4);
+    w.cval = take(M * 4);      // bucket layout CSC values
+    w.sval = take(M * 4);      // staging values / value twin
     w.total = off;
     return w;
-}
-
-int grid_for(int64_t n) {
-    int64_t g = (n + BLK - 1) / BLK;
-    if (g > 256 * 16) g = 256 * 16;
-    return (int)(g < 1 ? 1 : g);
-}
-
-// Key build, key sort, de-duplication and CSR scatter with K-wide keys; writes the unsorted CSC
-// keys/values (ckeys_a aliases the unsorted key buffer, free once the key sort is done).
-template <typename K>
-int csr_keys(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, const int64_t* edge_ptr,
-             const int64_t* node_ptr, int32_t n_graphs, int64_t n_nodes, int64_t NL, int sort_bits, char* ws,
-             const CsrWs& w, int32_t* rowptr, int32_t* col, uint32_t* ckeys_a, int32_t* cvals_a, int32_t* srcq,
-             int32_t* flags, int32_t* pos, int64_t* nnz_out, int32_t* err_out, hipStream_t s) {
-    const int64_t M = n_edges + n_nodes;
-    K* keys_a = (K*)(ws + w.keys_a);
-    K* keys_b = (K*)(ws + w.keys_b);
-    void* temp = ws + w.temp;
-    k_make_keys<K><<<grid_for(M), BLK, 0, s>>>(edge_index, ld_ei, n_edges, edge_ptr, node_ptr, n_graphs, n_nodes, NL,
-                                               keys_a, err_out);
-    TAGAN_CHECK_LAUNCH("csr_build.make_keys");
-    size_t tb = w.temp_bytes;
-    TAGAN_CHECK_HIP(rocprim::radix_sort_keys(temp, tb, keys_a, keys_b, (size_t)M, 0, sort_bits, s),
-                    "csr_build radix_sort_keys");
-    k_unique_flags<K><<<grid_for(M), BLK, 0, s>>>(keys_b, M, n_nodes, NL, flags);
-    TAGAN_CHECK_LAUNCH("csr_build.unique_flags");
-    tb = w.temp_bytes;
-    TAGAN_CHECK_HIP(rocprim::exclusive_scan(temp, tb, flags, pos, 0, (size_t)M, rocprim::plus<int32_t>(), s),
-                    "csr_build exclusive_scan");
-    k_scatter_csr<K><<<grid_for(M), BLK, 0, s>>>(keys_b, flags, pos, M, n_nodes, NL, node_ptr, n_graphs, rowptr, col,
-                                                 ckeys_a, cvals_a, srcq, nnz_out);
-    TAGAN_CHECK_LAUNCH("csr_build.scatter_csr");
-    return TAGAN_OK;
 }
 
 }  // namespace
@@ -229,14 +747,17 @@ extern "C" {
 
 size_t tagan_csr_build_workspace(int64_t n_edges, int64_t n_nodes) {
     if (n_edges < 0 || n_nodes <= 0) return 0;
-    return tagan::plan(n_edges, n_nodes).total;
+    // sized for both extremes of max_graph_nodes (the local-id width caps the bucket bits: more buckets)
+    using namespace tagan;
+    const Geo a = geometry(n_edges, n_nodes, 1, n_nodes), b = geometry(n_edges, n_nodes, 1, 1);
+    return std::max(plan(a).total, plan(b).total);
 }
 
 int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, const int64_t* edge_ptr,
                     const int64_t* node_ptr, int32_t n_graphs, int64_t n_nodes, int64_t max_graph_nodes,
                     int32_t* rowptr, int32_t* col,
                     int32_t* csc_ptr, int32_t* csc_row, int32_t* csc_eid, int64_t* nnz_out, int32_t* err_out,
-                    void* workspace, size_t workspace_bytes, void* stream) {
+                    int32_t* csr_cpos, void* workspace, size_t workspace_bytes, void* stream) {
     using namespace tagan;
     TAGAN_REQUIRE(n_nodes > 0 && n_nodes < (int64_t)INT32_MAX - 1, TAGAN_ERR_ARG,
                   "tagan_csr_build: n_nodes=%lld out of range", (long long)n_nodes);
@@ -246,46 +767,88 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     TAGAN_REQUIRE(n_graphs >= 1 && edge_ptr && node_ptr, TAGAN_ERR_ARG, "tagan_csr_build: bad graph pointers");
     TAGAN_REQUIRE(rowptr && col && csc_ptr && csc_row && csc_eid && nnz_out && err_out, TAGAN_ERR_ARG,
                   "tagan_csr_build: null output");
-    const CsrWs w = plan(n_edges, n_nodes);
+    TAGAN_REQUIRE(max_graph_nodes <= n_nodes, TAGAN_ERR_ARG, "tagan_csr_build: max_graph_nodes > n_nodes");
+    const int64_t NL = max_graph_nodes > 0 ? max_graph_nodes : n_nodes;
+    const Geo g = geometry(n_edges, n_nodes, n_graphs, NL);
+    const CsrWs w = plan(g);
     TAGAN_REQUIRE(workspace && workspace_bytes >= w.total, TAGAN_ERR_WORKSPACE,
                   "tagan_csr_build: workspace %zu < %zu", workspace_bytes, w.total);
+    static const bool lds_ok = [] {
+        hipError_t e1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_csr_finish_big),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, BIG_LDS);
+        hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_csc_finish_big),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, BIG_LDS);
+        return e1 == hipSuccess && e2 == hipSuccess;
+    }();
+    TAGAN_REQUIRE(lds_ok, TAGAN_ERR_LAUNCH, "tagan_csr_build: cannot enable %d B of dynamic LDS", BIG_LDS);
     hipStream_t s = as_stream(stream);
     char* ws = (char*)workspace;
-    uint32_t* ckeys_b = (uint32_t*)(ws + w.ckeys_b);
-    int32_t* cvals_b = (int32_t*)(ws + w.cvals_b);
-    int32_t* srcq = (int32_t*)(ws + w.srcq);
-    int32_t* flags = (int32_t*)(ws + w.flags);
-    int32_t* pos = (int32_t*)(ws + w.pos);
-    void* temp = ws + w.temp;
-    const int64_t M = n_edges + n_nodes;
-    const int bits = key_bits(n_nodes);
-    TAGAN_REQUIRE(max_graph_nodes <= n_nodes, TAGAN_ERR_ARG, "tagan_csr_build: max_graph_nodes > n_nodes");
-    const int64_t NL = max_graph_nodes > 0 ? max_graph_nodes : n_nodes;   // local ids 0..NL-1
-    const uint64_t sentinel = (uint64_t)n_nodes * (uint64_t)NL;
-    int sort_bits = 0;
-    while (sort_bits < 64 && (sentinel >> sort_bits) != 0) ++sort_bits;   // keys 0..sentinel
+    int32_t* cap_src = (int32_t*)(ws + w.cap_src);
+    int32_t* fill_src = (int32_t*)(ws + w.fill_src);
+    int32_t* fillc_src = (int32_t*)(ws + w.fillc_src);
+    int32_t* ucnt = (int32_t*)(ws + w.ucnt);
+    int32_t* cap_dst = (int32_t*)(ws + w.cap_dst);
+    int32_t* fill_dst = (int32_t*)(ws + w.fill_dst);
+    int32_t* fillc_dst = (int32_t*)(ws + w.fillc_dst);
+    int32_t* coff = (int32_t*)(ws + w.coff);
+    int32_t* big_src = (int32_t*)(ws + w.big_src);
+    int32_t* big_dst = (int32_t*)(ws + w.big_dst);
+    int32_t* nbig = (int32_t*)(ws + w.nbig);
+    int32_t* part = (int32_t*)(ws + w.part);
+    uint32_t* keys = (uint32_t*)(ws + w.keys);
+    uint32_t* stage = (uint32_t*)(ws + w.stage);
+    int32_t* sloc = (int32_t*)(ws + w.sloc);
+    int32_t* cval = (int32_t*)(ws + w.cval);
+    int32_t* sval = (int32_t*)(ws + w.sval);
+    const scan::Plus plus;
+    const bool two_level = g.SC > 0;
 
-    TAGAN_CHECK_HIP(hipMemsetAsync(err_out, 0, sizeof(int32_t), s), "csr_build memset");
-    uint32_t* ckeys_a = (uint32_t*)(ws + w.keys_a);   // unsorted CSC keys (the key buffer is free by then)
-    int32_t* cvals_a = csc_row;   // staging only; overwritten by the final CSC scatter
-    const int rc = sentinel <= 0xFFFFFFFFull
-                       ? csr_keys<uint32_t>(edge_index, ld_ei, n_edges, edge_ptr, node_ptr, n_graphs, n_nodes, NL,
-                                            sort_bits, ws, w, rowptr, col, ckeys_a, cvals_a, srcq, flags, pos,
-                                            nnz_out, err_out, s)
-                       : csr_keys<uint64_t>(edge_index, ld_ei, n_edges, edge_ptr, node_ptr, n_graphs, n_nodes, NL,
-                                            sort_bits, ws, w, rowptr, col, ckeys_a, cvals_a, srcq, flags, pos,
-                                            nnz_out, err_out, s);
-    if (rc) return rc;
-    size_t tb = 0;
-    k_fill_tail<<<grid_for(M), BLK, 0, s>>>(ckeys_a, cvals_a, nnz_out, M, n_nodes);
-    TAGAN_CHECK_LAUNCH("csr_build.fill_tail");
-    tb = w.temp_bytes;
-    TAGAN_CHECK_HIP(rocprim::radix_sort_pairs<CscSortCfg>(temp, tb, ckeys_a, ckeys_b, cvals_a, cvals_b, (size_t)M, 0,
-                                                          bits, s),
-                    "csr_build radix_sort_pairs");
-    k_scatter_csc<<<grid_for(M), BLK, 0, s>>>(ckeys_b, cvals_b, srcq, nnz_out, n_nodes, csc_ptr, csc_row,
-                                              csc_eid);
-    TAGAN_CHECK_LAUNCH("csr_build.scatter_csc");
+    k_init<<<grid_for(g.NB), BLK, 0, s>>>(g, cap_src, fill_src, cap_dst, fill_dst, fillc_src, fillc_dst, nbig, err_out);
+    TAGAN_CHECK_LAUNCH("csr_build.init");
+    const int64_t nblk = (n_edges + g.CH - 1) / g.CH, nblk_n = (n_edges + g.CHn - 1) / g.CHn;
+    if (nblk > 0) {
+        k_count<<<(unsigned)nblk_n, PNT, 0, s>>>(g, edge_index, ld_ei, edge_ptr, node_ptr, cap_src, cap_dst, err_out);
+        TAGAN_CHECK_LAUNCH("csr_build.count");
+    }
+    scan::exclusive(cap_src, cap_src, g.NB, (int32_t)0, plus, part, true, s);     // -> src bucket regions
+    scan::exclusive(cap_dst, cap_dst, g.NB, (int32_t)0, plus, part, true, s);     // -> dst bucket regions
+    TAGAN_CHECK_LAUNCH("csr_build.scan_capacity");
+    if (nblk > 0) {
+        k_part_edges<<<(unsigned)nblk, PNT, 0, s>>>(g, edge_index, ld_ei, edge_ptr, node_ptr, cap_src,
+                                                    two_level ? fillc_src : fill_src, two_level ? stage : keys);
+        TAGAN_CHECK_LAUNCH("csr_build.part_edges");
+        if (two_level) {
+            k_refine<false><<<(unsigned)g.NCB, RNT, 0, s>>>(g, cap_src, fillc_src, stage, nullptr, fill_src, keys,
+                                                            nullptr);
+            TAGAN_CHECK_LAUNCH("csr_build.refine");
+        }
+    }
+    k_csr_finish<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_src, fill_src, node_ptr, keys, rowptr, ucnt, big_src, nbig);
+    TAGAN_CHECK_LAUNCH("csr_build.csr_finish");
+    k_csr_finish_big<<<BIG_WG, BNT, BIG_LDS, s>>>(g, cap_src, fill_src, node_ptr, keys, stage, rowptr, ucnt,
+                                                  big_src, nbig);
+    TAGAN_CHECK_LAUNCH("csr_build.csr_finish_big");
+    scan::exclusive(ucnt, ucnt, g.NB, (int32_t)0, plus, part, true, s);           // -> CSR bucket offsets
+    TAGAN_CHECK_LAUNCH("csr_build.scan_unique");
+    k_csr_place<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_src, ucnt, node_ptr, keys, rowptr, col, sloc, nnz_out);
+    TAGAN_CHECK_LAUNCH("csr_build.csr_place");
+    const int64_t nblk_c = (n_edges + n_nodes + g.CHc - 1) / g.CHc;   // capacity bound; blocks past nnz exit
+    k_part_csr<<<(unsigned)nblk_c, PNT, 0, s>>>(g, rowptr, col, sloc, node_ptr, nnz_out, cap_dst,
+                                                two_level ? fillc_dst : fill_dst, two_level ? stage : keys,
+                                                two_level ? sval : cval);
+    TAGAN_CHECK_LAUNCH("csr_build.part_csr");
+    if (two_level) {
+        k_refine<true><<<(unsigned)g.NCB, RNT, 0, s>>>(g, cap_dst, fillc_dst, stage, sval, fill_dst, keys, cval);
+        TAGAN_CHECK_LAUNCH("csr_build.refine_csc");
+    }
+    scan::exclusive(fill_dst, coff, g.NB, (int32_t)0, plus, part, true, s);       // -> CSC bucket offsets
+    TAGAN_CHECK_LAUNCH("csr_build.scan_csc");
+    k_csc_finish<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, csc_ptr, csc_row,
+                                                csc_eid, csr_cpos, big_dst, nbig);
+    TAGAN_CHECK_LAUNCH("csr_build.csc_finish");
+    k_csc_finish_big<<<BIG_WG, BNT, BIG_LDS, s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, stage, sval,
+                                                  csc_ptr, csc_row, csc_eid, csr_cpos, big_dst, nbig);
+    TAGAN_CHECK_LAUNCH("csr_build.csc_finish_big");
     return TAGAN_OK;
 }
 
@@ -311,6 +874,10 @@ struct Tri {
 struct TriPlus {
     __host__ __device__ Tri operator()(const Tri& x, const Tri& y) const { return Tri{x.a + y.a, x.b + y.b, x.c + y.c}; }
 };
+
+__device__ __forceinline__ Tri shfl_up(const Tri& x, int o) {
+    return Tri{__shfl_up(x.a, o, WAVE), __shfl_up(x.b, o, WAVE), __shfl_up(x.c, o, WAVE)};
+}
 
 __global__ void __launch_bounds__(BLK) k_chunk_count(const int32_t* __restrict__ ptr, int64_t n, int chunk,
                                                      Tri* __restrict__ cnt) {
@@ -423,9 +990,7 @@ int64_t tagan_part_capacity(int64_t nnz_cap, int32_t chunk) {
 size_t tagan_graph_chunks_workspace(int64_t n) {
     using namespace tagan;
     if (n <= 0) return 0;
-    size_t t = 0;
-    (void)rocprim::exclusive_scan(nullptr, t, (Tri*)nullptr, (Tri*)nullptr, Tri{0, 0, 0}, (size_t)n, TriPlus());
-    return 2 * align_up((size_t)n * sizeof(Tri), 256) + align_up(t, 256);
+    return 2 * align_up((size_t)n * sizeof(Tri), 256) + align_up((size_t)scan::parts_len(n) * sizeof(Tri), 256);
 }
 
 int tagan_graph_chunks(const int32_t* seg_ptr, int64_t n, int32_t chunk, int32_t* chunk_ptr, int32_t* chunk_seg,
@@ -442,11 +1007,11 @@ int tagan_graph_chunks(const int32_t* seg_ptr, int64_t n, int32_t chunk, int32_t
     const size_t a = align_up((size_t)n * sizeof(Tri), 256);
     Tri* cnt = (Tri*)ws;
     Tri* off = (Tri*)(ws + a);
-    void* temp = ws + 2 * a;
-    size_t tb = need - 2 * a;
+    Tri* part = (Tri*)(ws + 2 * a);
     k_chunk_count<<<grid_for(n), BLK, 0, s>>>(seg_ptr, n, chunk, cnt);
     TAGAN_CHECK_LAUNCH("graph_chunks.count");
-    TAGAN_CHECK_HIP(rocprim::exclusive_scan(temp, tb, cnt, off, Tri{0, 0, 0}, (size_t)n, TriPlus(), s), "scan");
+    scan::exclusive(cnt, off, n, Tri{0, 0, 0}, TriPlus(), part, false, s);
+    TAGAN_CHECK_LAUNCH("graph_chunks.scan");
     k_chunk_fill<<<grid_for(n), BLK, 0, s>>>(seg_ptr, n, chunk, cnt, off, chunk_ptr, chunk_seg, chunk_beg,
                                              chunk_part, multi_seg, counts);
     TAGAN_CHECK_LAUNCH("graph_chunks.fill");

@@ -126,9 +126,10 @@ def _finish(g: SnapshotGraph, nnz_cap: int, chunk: int = CHUNK) -> SnapshotGraph
     g.col_chunks, _, _, g.col_order = _chunk_lists(g.csc_ptr, g.num_nodes, nnz_cap, chunk)
     g.chunk = chunk
     g.nnz_cap = nnz_cap
-    g.csr_cpos = torch.empty(nnz_cap, dtype=torch.int32, device=g.csc_eid.device)
-    check(lib().tagan_csr_csc_pos(ptr(g.csc_eid), ptr(g.nnz), nnz_cap, ptr(g.csr_cpos), stream_of(g.csc_eid)),
-          "tagan_csr_csc_pos")
+    if g.csr_cpos is None:   # tagan_csr_build writes it itself; other builders get the inverse of csc_eid here
+        g.csr_cpos = torch.empty(nnz_cap, dtype=torch.int32, device=g.csc_eid.device)
+        check(lib().tagan_csr_csc_pos(ptr(g.csc_eid), ptr(g.nnz), nnz_cap, ptr(g.csr_cpos), stream_of(g.csc_eid)),
+              "tagan_csr_csc_pos")
     return g
 
 
@@ -202,10 +203,11 @@ def build_graph_cat(ei: torch.Tensor, e_ptr: Sequence[int], node_counts: Sequenc
     meta = _ptr_table(dev, list(e_ptr) + n_ptr)
     edge_ptr, node_ptr = meta[:G + 1], meta[G + 1:]
     cap = E + N
-    buf = torch.empty(2 * (N + 1) + 3 * cap, dtype=torch.int32, device=dev)
+    buf = torch.empty(2 * (N + 1) + 4 * cap, dtype=torch.int32, device=dev)
     rowptr, csc_ptr = buf[:N + 1], buf[N + 1:2 * (N + 1)]
     o = 2 * (N + 1)
     col, csc_row, csc_eid = buf[o:o + cap], buf[o + cap:o + 2 * cap], buf[o + 2 * cap:o + 3 * cap]
+    cpos = buf[o + 3 * cap:o + 4 * cap]
     scal = torch.empty(2, dtype=torch.int64, device=dev)
     nnz = scal[0:1]
     err = scal[1:2].view(torch.int32)[:1]
@@ -214,9 +216,10 @@ def build_graph_cat(ei: torch.Tensor, e_ptr: Sequence[int], node_counts: Sequenc
     ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=dev)
     check(L.tagan_csr_build(ptr(ei), E, E, ptr(edge_ptr), ptr(node_ptr), G, N,
                             max(n_ptr[i + 1] - n_ptr[i] for i in range(G)), ptr(rowptr), ptr(col),
-                            ptr(csc_ptr), ptr(csc_row), ptr(csc_eid), ptr(nnz), ptr(err), ptr(ws), ws_bytes,
-                            stream_of(ei)), "tagan_csr_build")
+                            ptr(csc_ptr), ptr(csc_row), ptr(csc_eid), ptr(nnz), ptr(err), ptr(cpos), ptr(ws),
+                            ws_bytes, stream_of(ei)), "tagan_csr_build")
     g = SnapshotGraph(N, rowptr, col, csc_ptr, csc_row, csc_eid, nnz, list(node_counts))
+    g.csr_cpos = cpos
     if validate == "deferred":
         host = torch.empty(1, dtype=torch.int32, pin_memory=True)
         host.copy_(err, non_blocking=True)

@@ -53,6 +53,10 @@ def _check_csr(dev, counts, eis):
     assert torch.equal(want_col[eid], ccol)
     same = ccol[1:] == ccol[:-1]
     assert torch.all(crow.diff()[same] > 0)
+    # the CSR -> CSC position map written by the same build: the inverse of csc_eid
+    cpos = graph.csr_cpos[:nnz].cpu().long()
+    assert torch.equal(cpos[eid], torch.arange(nnz))
+    return graph
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
@@ -74,6 +78,27 @@ def test_csr_build_wide_keys(dev):
     eis = [torch.randint(-n, n, (2, 4 * n), generator=g) for n in counts]
     assert sum(counts) * max(counts) >= 2 ** 32
     _check_csr(dev, counts, eis)
+
+
+def test_csr_build_hub_buckets(dev):
+    """Power-law hubs overflow the small LDS bucket finish: a row with ~40k raw out-edges (duplicates included:
+    beyond the 16k-key LDS of the big-bucket kernel -> its global-memory sort) and columns with ~5k and ~12k
+    distinct in-neighbours (the big kernel's LDS path and, past 8k pairs, its global path), next to ordinary
+    buckets in the same launch; then the same graph again (the device-side big-bucket lists are reset)."""
+    g = torch.Generator().manual_seed(11)
+    n0, n1 = 20_000, 3_000
+    hub_out = torch.stack([torch.full((40_000,), 5), torch.randint(0, n0, (40_000,), generator=g)])
+    hub_in = torch.stack([torch.randperm(n0, generator=g)[:12_000], torch.full((12_000,), 7)])
+    mid_in = torch.stack([torch.randint(0, n0, (6_000,), generator=g), torch.full((6_000,), 9000)])
+    rest = torch.randint(0, n0, (2, 60_000), generator=g)
+    ei0 = torch.cat([hub_out, hub_in, mid_in, rest], 1)
+    ei0 = ei0[:, torch.randperm(ei0.shape[1], generator=g)]
+    ei1 = torch.randint(0, n1, (2, 9_000), generator=g)
+    g1 = _check_csr(dev, [n0, n1], [ei0, ei1])
+    g2 = _check_csr(dev, [n0, n1], [ei0, ei1])
+    for a, b in ((g1.rowptr, g2.rowptr), (g1.col, g2.col), (g1.csc_row, g2.csc_row), (g1.csc_eid, g2.csc_eid)):
+        n = g1.nnz_host()
+        assert torch.equal(a[:n], b[:n])        # bitwise deterministic
 
 
 def test_csr_build_rejects_out_of_range(dev):
