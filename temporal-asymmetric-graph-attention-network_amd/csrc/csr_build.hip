@@ -36,18 +36,19 @@ namespace {
 
 constexpr int BLK = 256;           // generic grid-stride kernels
 constexpr int PNT = 1024;          // partition (count / part) blocks
-constexpr int LDS_BINS = 16384;    // LDS histogram bins per partition block and direction
+constexpr int LDS_BINS = 16384;    // LDS histogram bins per count block and direction
+constexpr int PART_BINS = 2048;    // LDS bins of the partition passes (more: global atomics)
 constexpr int RNT = 1024;          // refine blocks (one per coarse bin)
-constexpr int FNT = 256;           // small-bucket finish workgroups
-constexpr int FIPT = 8;            // keys per thread per sort round in the small finish
-constexpr int CAP_S = FNT * FIPT;  // keys (CSR) / pairs (CSC) per small finish: one round
-constexpr int BNT = 1024;          // big-bucket finish workgroups
-constexpr int BIG_LDS = 128 * 1024;   // dynamic LDS of the big-bucket kernels (2 key buffers / 2 + 2 pair buffers)
-constexpr int BIG_WG = 128;        // persistent workgroups of the big-bucket kernels
+constexpr int FNT = 256;           // small-bucket finish workgroups (4 waves)
+constexpr int CAP_S = 2560;        // keys per small CSR finish (LDS; 4 workgroups per CU)
+constexpr int CAP_C = 2048;        // (key, CSR position) pairs per small CSC finish
+constexpr int BNT = 512;           // big-bucket finish workgroups (8 waves)
+constexpr int BIG_LDS = 140 * 1024;   // dynamic LDS of the big-bucket kernels (2 key buffers / 2 + 2 pair buffers)
+constexpr int BIG_WG = 256;        // persistent workgroups of the big-bucket kernels (one per CU)
 constexpr int RB = 8;              // radix digit bits
 constexpr int RBINS = 1 << RB;
 constexpr int TARGET = 2048;       // average entries per bucket
-constexpr int SB_MAX = 10;         // at most 1024 rows per bucket
+constexpr int SB_MAX = 8;          // at most 256 rows per bucket
 constexpr int SC_MAX = 8;          // at most 256 buckets per coarse bin
 constexpr int COARSE_PER_SNAPSHOT = 192;
 
@@ -95,11 +96,14 @@ Geo geometry(int64_t E, int64_t N, int G, int64_t NL) {
     while (sc < SC_MAX && (per_snap >> sc) > COARSE_PER_SNAPSHOT && sc + 1 + sb + g.LB <= 32) ++sc;
     g.SC = sc;
     g.NCB = (g.NB + ((int64_t)1 << sc) - 1) >> sc;
-    int64_t chn = 65536;
+    // partition blocks: 64k edges each at scale, smaller (down to 4k) so a small batch still fills the 256 CUs
+    int64_t ch = 4096;
+    while (ch < 65536 && ch * 1024 < E + N) ch <<= 1;
+    int64_t chn = ch;
     while (chn < 16 * per_snap && chn < ((int64_t)1 << 20)) chn <<= 1;
     g.CHn = chn;
-    g.CH = 65536;
-    g.CHc = 65536;
+    g.CH = ch;
+    g.CHc = ch;
     return g;
 }
 
@@ -232,6 +236,69 @@ __device__ __forceinline__ bool valid_edge(int64_t s, int64_t d, int64_t base, i
 
 constexpr int UNR = 4;   // loads in flight per lane in the streaming passes
 
+// LDS-staged tile partition.  Each tile of NTH * IPT items (bins bin[k] in [0, NB), -1: no item) is counted per bin
+// with one LDS atomic per item, the per-bin counts are scanned, the items are placed in LDS grouped by bin together
+// with their global position (sh_base[bin] + slot; sh_base advances by the tile's counts), and the tile is written
+// out from LDS in that order: consecutive lanes store consecutive addresses of one bin's run, so a wave touches a few
+// cache lines instead of one per lane.  The order inside a bin is unspecified -- every consumer sorts its bucket on
+// the full key.  The loader fetches item i's raw values one tile ahead (issued before this tile's scan and write-out,
+// so the loads overlap them) and decodes them into (bin, key, value).
+// LDS: tcnt, tstart, gpos: NB ints each (tcnt zero on entry and exit); stk / stv / stp: NTH * IPT each; sm: NTH/64+1.
+template <int NTH, int IPT, int NB, bool VAL, typename Loader>
+__device__ void tile_partition(int64_t a, int64_t z, const Loader& ld, int* sh_base, int* tcnt, int* tstart, int* gpos,
+                               uint32_t* stk, int32_t* stv, int* stp, int32_t* sm, uint32_t* __restrict__ out_k,
+                               int32_t* __restrict__ out_v) {
+    using Raw = typename Loader::Raw;
+    constexpr int TILE = NTH * IPT;
+    const int tid = threadIdx.x;
+    Raw cur[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) cur[k] = ld.fetch(a + k * NTH + tid, z);
+    for (int64_t t0 = a; t0 < z; t0 += TILE) {
+        int bin[IPT], slot[IPT];
+        uint32_t key[IPT];
+        int32_t val[IPT];
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            ld.decode(cur[k], t0 + k * NTH + tid, z, bin[k], key[k], val[k]);
+            slot[k] = bin[k] >= 0 ? atomicAdd(&tcnt[bin[k]], 1) : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) cur[k] = ld.fetch(t0 + TILE + k * NTH + tid, z);   // next tile, in flight
+        __syncthreads();
+        const int c = tid < NB ? tcnt[tid] : 0;
+        int32_t tot;
+        const int32_t ex = scan::block_excl<NTH>((int32_t)c, (int32_t)0, scan::Plus(), sm, &tot);
+        if (tid < NB) {
+            tstart[tid] = ex;
+            gpos[tid] = sh_base[tid];
+            sh_base[tid] += c;
+            tcnt[tid] = 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            if (bin[k] >= 0) {
+                const int l = tstart[bin[k]] + slot[k];
+                stk[l] = key[k];
+                if (VAL) stv[l] = val[k];
+                stp[l] = gpos[bin[k]] + slot[k];
+            }
+        }
+        __syncthreads();
+        for (int t = tid; t < tot; t += NTH) {
+            const int p = stp[t];
+            out_k[p] = stk[t];
+            if (VAL) out_v[p] = stv[t];
+        }
+        __syncthreads();
+    }
+}
+
+constexpr int PNB = 256;   // bins of the staged partition passes (coarse bins per snapshot, buckets per coarse bin)
+constexpr int PIPT = 4;    // items per thread per tile in the partition passes
+constexpr int PTILE = PNT * PIPT;
+
 // bins of shift `sh` spanned by the nodes [v0, v1) of one snapshot
 struct Span {
     int64_t b0;
@@ -239,14 +306,78 @@ struct Span {
     bool lds;
 };
 
-__device__ __forceinline__ Span span_of(int64_t v0, int64_t v1, int sh) {
+__device__ __forceinline__ Span span_of(int64_t v0, int64_t v1, int sh, int maxbins = LDS_BINS) {
     Span s;
     s.b0 = v0 >> sh;
     const int64_t b1 = v1 > v0 ? ((v1 - 1) >> sh) + 1 : s.b0;
-    s.lds = b1 - s.b0 <= LDS_BINS;
+    s.lds = b1 - s.b0 <= maxbins;
     s.nb = s.lds ? (int)(b1 - s.b0) : 0;
     return s;
 }
+
+// raw edge e -> (coarse src bin, key = (bucket-in-bin << SB | row-in-bucket) << LB | local dst)
+struct EdgeLoader {
+    struct Raw { int64_t s, d; };
+    const int64_t* ei;
+    int64_t ld, base, n, b0;
+    int shc, SB, LB;
+    uint32_t rmask, fmask;
+    __device__ Raw fetch(int64_t e, int64_t z) const {
+        Raw r{-1, -1};
+        if (e < z) { r.s = ei[e]; r.d = ei[ld + e]; }
+        return r;
+    }
+    __device__ void decode(const Raw& r, int64_t e, int64_t z, int& bin, uint32_t& key, int32_t& val) const {
+        int64_t gs, dl;
+        bin = -1;
+        key = 0u;
+        val = 0;
+        if (e < z && valid_edge(r.s, r.d, base, n, gs, dl)) {
+            bin = (int)((gs >> shc) - b0);
+            key = ((((uint32_t)(gs >> SB) & fmask) << SB | ((uint32_t)gs & rmask)) << LB) | (uint32_t)dl;
+        }
+    }
+};
+
+// CSR entry e -> (coarse dst bin, key = (bucket-in-bin << SB | column-in-bucket) << LB | local src, value = e)
+struct CsrEntryLoader {
+    struct Raw { int32_t d, sl; };
+    const int32_t* col;
+    const int32_t* sloc;
+    int64_t b0;
+    int shc, SB, LB;
+    uint32_t cmask, fmask;
+    __device__ Raw fetch(int64_t e, int64_t z) const {
+        Raw r{0, 0};
+        if (e < z) { r.d = col[e]; r.sl = sloc[e]; }
+        return r;
+    }
+    __device__ void decode(const Raw& r, int64_t e, int64_t z, int& bin, uint32_t& key, int32_t& val) const {
+        bin = e < z ? (int)((r.d >> shc) - b0) : -1;
+        key = ((((uint32_t)(r.d >> SB) & fmask) << SB | ((uint32_t)r.d & cmask)) << LB) | (uint32_t)r.sl;
+        val = (int32_t)e;
+    }
+};
+
+// staged key (value) i of a coarse bin -> (bucket-in-bin, key without those bits, value)
+template <bool VAL>
+struct StageLoader {
+    struct Raw { uint32_t k; int32_t v; };
+    const uint32_t* skey;
+    const int32_t* sval;
+    int kb;
+    uint32_t kmask;
+    __device__ Raw fetch(int64_t i, int64_t z) const {
+        Raw r{0u, 0};
+        if (i < z) { r.k = skey[i]; if (VAL) r.v = sval[i]; }
+        return r;
+    }
+    __device__ void decode(const Raw& r, int64_t i, int64_t z, int& bin, uint32_t& key, int32_t& val) const {
+        bin = i < z ? (int)(r.k >> kb) : -1;
+        key = r.k & kmask;
+        val = r.v;
+    }
+};
 
 // 1. bucket histograms of the raw edges (src and dst), index validation; snapshot by snapshot inside the block
 __global__ void __launch_bounds__(PNT) k_count(Geo g, const int64_t* __restrict__ ei, int64_t ld,
@@ -296,12 +427,17 @@ __global__ void __launch_bounds__(PNT) k_count(Geo g, const int64_t* __restrict_
 }
 
 // 3. raw edges -> coarse src bins (SC > 0: staging layout) or straight into the buckets (SC = 0)
-__global__ void __launch_bounds__(PNT) k_part_edges(Geo g, const int64_t* __restrict__ ei, int64_t ld,
+__global__ void __launch_bounds__(PNT) k_part_edges(Geo g, const int64_t* __restrict__ ei, int64_t ld_,
                                                     const int64_t* __restrict__ edge_ptr,
                                                     const int64_t* __restrict__ node_ptr,
                                                     const int32_t* __restrict__ bstart, int32_t* __restrict__ fill,
                                                     uint32_t* __restrict__ out) {
-    __shared__ int h[LDS_BINS];
+    __shared__ int h[PART_BINS];
+    __shared__ int tcnt[PNB], tstart[PNB], gpos[PNB];
+    __shared__ uint32_t stk[PTILE];
+    __shared__ int stp[PTILE];
+    __shared__ int32_t sm[PNT / WAVE + 1];
+    for (int i = threadIdx.x; i < PNB; i += PNT) tcnt[i] = 0;
     const int64_t e0 = blockIdx.x * g.CH, e1 = min(g.E, e0 + g.CH);
     const int g0 = find_graph(edge_ptr, g.G, e0), g1 = find_graph(edge_ptr, g.G, e1 - 1);
     const int shc = g.SB + g.SC;                       // node id -> coarse bin
@@ -309,7 +445,7 @@ __global__ void __launch_bounds__(PNT) k_part_edges(Geo g, const int64_t* __rest
     for (int gg = g0; gg <= g1; ++gg) {
         const int64_t base = node_ptr[gg], n = node_ptr[gg + 1] - base;
         const int64_t a = max(e0, edge_ptr[gg]), z = min(e1, edge_ptr[gg + 1]);
-        const Span sp = span_of(base, base + n, shc);
+        const Span sp = span_of(base, base + n, shc, PART_BINS);
         if (sp.lds) {
             for (int i = threadIdx.x; i < sp.nb; i += PNT) h[i] = 0;
             __syncthreads();
@@ -319,7 +455,7 @@ __global__ void __launch_bounds__(PNT) k_part_edges(Geo g, const int64_t* __rest
                 for (int u = 0; u < UNR; ++u) {
                     const int64_t e = e4 + u * PNT;
                     sv[u] = e < z ? ei[e] : 0;
-                    dv[u] = e < z ? ei[ld + e] : 0;
+                    dv[u] = e < z ? ei[ld_ + e] : 0;
                 }
 #pragma unroll
                 for (int u = 0; u < UNR; ++u) {
@@ -336,24 +472,29 @@ __global__ void __launch_bounds__(PNT) k_part_edges(Geo g, const int64_t* __rest
             }
             __syncthreads();
         }
-        for (int64_t e4 = a + threadIdx.x; e4 < z; e4 += UNR * PNT) {
-            int64_t sv[UNR], dv[UNR];
+        if (sp.lds && sp.nb <= PNB) {   // LDS-staged scatter
+            const EdgeLoader ld{ei, ld_, base, n, sp.b0, shc, g.SB, g.LB, rmask, fmask};
+            tile_partition<PNT, PIPT, PNB, false>(a, z, ld, h, tcnt, tstart, gpos, stk, nullptr, stp, sm, out, nullptr);
+        } else {
+            for (int64_t e4 = a + threadIdx.x; e4 < z; e4 += UNR * PNT) {
+                int64_t sv[UNR], dv[UNR];
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                const int64_t e = e4 + u * PNT;
-                sv[u] = e < z ? ei[e] : 0;
-                dv[u] = e < z ? ei[ld + e] : 0;
-            }
+                for (int u = 0; u < UNR; ++u) {
+                    const int64_t e = e4 + u * PNT;
+                    sv[u] = e < z ? ei[e] : 0;
+                    dv[u] = e < z ? ei[ld_ + e] : 0;
+                }
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                if (e4 + u * PNT >= z) break;
-                int64_t gs, dl;
-                if (!valid_edge(sv[u], dv[u], base, n, gs, dl)) continue;
-                const int64_t bin = gs >> shc;
-                const int pos = sp.lds ? atomicAdd(&h[bin - sp.b0], 1)
-                                       : bstart[bin << g.SC] + atomicAdd(&fill[bin], 1);
-                out[pos] = ((((uint32_t)(gs >> g.SB) & fmask) << g.SB | ((uint32_t)gs & rmask)) << g.LB) |
-                           (uint32_t)dl;
+                for (int u = 0; u < UNR; ++u) {
+                    if (e4 + u * PNT >= z) break;
+                    int64_t gs, dl;
+                    if (!valid_edge(sv[u], dv[u], base, n, gs, dl)) continue;
+                    const int64_t bin = gs >> shc;
+                    const int pos = sp.lds ? atomicAdd(&h[bin - sp.b0], 1)
+                                           : bstart[bin << g.SC] + atomicAdd(&fill[bin], 1);
+                    out[pos] = ((((uint32_t)(gs >> g.SB) & fmask) << g.SB | ((uint32_t)gs & rmask)) << g.LB) |
+                               (uint32_t)dl;
+                }
             }
         }
         __syncthreads();
@@ -361,97 +502,342 @@ __global__ void __launch_bounds__(PNT) k_part_edges(Geo g, const int64_t* __rest
 }
 
 // 4. one workgroup per coarse bin: its staged keys (bucket-in-bin in the bits above SB + LB) -> bucket regions
+// (LDS-staged tiles from each bucket's region start); fill[] = the keys each bucket received
 template <bool VAL>
 __global__ void __launch_bounds__(RNT) k_refine(Geo g, const int32_t* __restrict__ bstart,
                                                 const int32_t* __restrict__ fillc, const uint32_t* __restrict__ skey,
                                                 const int32_t* __restrict__ sval, int32_t* __restrict__ fill,
                                                 uint32_t* __restrict__ key, int32_t* __restrict__ val) {
-    __shared__ int h[1 << SC_MAX];
+    constexpr int TILE = RNT * PIPT;
+    __shared__ int base[PNB], tcnt[PNB], tstart[PNB], gpos[PNB];
+    __shared__ uint32_t stk[TILE];
+    __shared__ int32_t stv[VAL ? TILE : 1];
+    __shared__ int stp[TILE];
+    __shared__ int32_t sm[RNT / WAVE + 1];
     const int64_t c = blockIdx.x;
     const int64_t f0 = c << g.SC;
     const int nf = (int)(min(g.NB, f0 + ((int64_t)1 << g.SC)) - f0);
     const int32_t s0 = bstart[f0], cnt = fillc[c];
     const int kb = g.SB + g.LB;
     const uint32_t kmask = (uint32_t)(((uint64_t)1 << kb) - 1);
-    for (int i = threadIdx.x; i < nf; i += RNT) h[i] = 0;
-    __syncthreads();
-    for (int i = threadIdx.x; i < cnt; i += RNT) atomicAdd(&h[skey[s0 + i] >> kb], 1);
-    __syncthreads();
-    for (int i = threadIdx.x; i < nf; i += RNT) {
-        fill[f0 + i] = h[i];
-        h[i] = bstart[f0 + i];
+    for (int i = threadIdx.x; i < PNB; i += RNT) {
+        base[i] = i < nf ? bstart[f0 + i] : 0;
+        tcnt[i] = 0;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < cnt; i += RNT) {
-        const uint32_t k = skey[s0 + i];
-        const int p = atomicAdd(&h[k >> kb], 1);
-        key[p] = k & kmask;
-        if (VAL) val[p] = sval[s0 + i];
+    const StageLoader<VAL> ld{skey + s0, sval ? sval + s0 : nullptr, kb, kmask};
+    tile_partition<RNT, PIPT, PNB, VAL>(0, cnt, ld, base, tcnt, tstart, gpos, stk, stv, stp, sm, key, val);
+    for (int i = threadIdx.x; i < nf; i += RNT) fill[f0 + i] = base[i] - bstart[f0 + i];
+}
+
+// 5. bucket finish.  The bucket's keys (row-in-bucket << LB | low) are counting-sorted by row in LDS (one LDS
+// atomic per key: the order inside a row is free, the row sort below is on the full key), then every row is sorted
+// on its own.  A row of <= 64 entries is RANK-sorted: each entry counts the entries of its row that precede it in
+// (key, index) order -- a few independent LDS reads per entry, no shuffle network, no dependent chains.  A longer row
+// (a power-law hub) goes through a per-wave LDS bitmap over the local ids when LB <= BM_LB -- set the bits, prefix
+// the words' popcounts, and each entry's rank is the number of distinct ids below it: sorted AND deduplicated in
+// O(entries + 2^LB / 32), the payload carried along.  A bucket with a long row and a wider local-id
+// range takes the stable LSD radix sort of the whole bucket instead.  CSR rows are deduplicated on emission (the
+// adjacency is a set: an entry is kept when it differs from its sorted predecessor); CSC columns carry each entry's
+// CSR position.
+constexpr int BM_LB = 14;                      // bitmap path for local ids < 2^14 (C1, C2)
+constexpr int BMW = (1 << BM_LB) / 32;         // bitmap words per wave
+constexpr int SHORT_ROW = WAVE;                // rank-sorted rows: at most this many entries
+
+// LDS (or global) scratch of one bucket finish (rows = 2^SB_MAX at most)
+struct SegLds {
+    int* rc;        // entries per row (2^SB_MAX)
+    int* ro;        // row start in the row-sorted buffer
+    uint32_t* bm;   // NW * BMW bitmap words (null: no bitmap path); may alias rank
+    uint16_t* pw;   // NW * BMW per-word prefixes of the bitmaps
+    int* rank;      // [m] slot of each key within its row (LDS, or global scratch in the big kernels)
+    int* wc;        // the LSD fallback's count table: NTH/64 * RBINS ints (may alias rank)
+    int* flag;      // fallback request
+};
+
+// hub rows of a big bucket, one at a time with the whole block: bitmap over the local ids, block scan of the words'
+// popcounts, rank = distinct ids below (the per-wave form below, spread over NTH threads)
+template <int NTH, bool VAL, bool DEDUP>
+__device__ void hub_rows_block(const Geo& g, int nrows, uint32_t* K, const uint32_t* K2, int32_t* V, const int32_t* V2,
+                               SegLds L, int32_t* sh_sm) {
+    const int tid = threadIdx.x;
+    const uint32_t lmask = (uint32_t)(((uint64_t)1 << g.LB) - 1);
+    const int nw = (int)((lmask >> 5) + 1);
+    uint32_t* bm = L.bm;
+    uint16_t* pw = L.pw;
+    for (int j = 0; j < nrows; ++j) {
+        const int n = L.rc[j];
+        if (n <= SHORT_ROW) continue;
+        const int base = L.ro[j];
+        for (int i = tid; i < nw; i += NTH) bm[i] = 0u;
+        __syncthreads();
+        for (int i = tid; i < n; i += NTH) {
+            const uint32_t lo = K2[base + i] & lmask;
+            atomicOr(&bm[lo >> 5], 1u << (lo & 31));
+        }
+        __syncthreads();
+        const int per = (nw + NTH - 1) / NTH, w0 = tid * per, w1 = min(nw, w0 + per);
+        int cnt = 0;
+        for (int q = w0; q < w1; ++q) cnt += __popc(bm[q]);
+        int32_t tot;
+        int run = scan::block_excl<NTH>((int32_t)cnt, (int32_t)0, scan::Plus(), sh_sm, &tot);
+        for (int q = w0; q < w1; ++q) {
+            pw[q] = (uint16_t)run;
+            run += __popc(bm[q]);
+        }
+        __syncthreads();
+        for (int i = tid; i < n; i += NTH) {
+            const uint32_t k = K2[base + i], lo = k & lmask;
+            const int r = pw[lo >> 5] + __popc(bm[lo >> 5] & ((1u << (lo & 31)) - 1u));
+            K[base + r] = k;
+            if (VAL) V[base + r] = V2[base + i];
+        }
+        if (DEDUP && tot < n) {
+            __syncthreads();
+            const uint32_t last = K[base + tot - 1];
+            for (int i = tot + tid; i < n; i += NTH) K[base + i] = last;
+        }
+        __syncthreads();
     }
 }
 
-// 5. CSR bucket finish: sort + dedupe + per-row counts.  Writes the unique keys back over the bucket's region,
-// the in-bucket row prefix into rowptr and the bucket's unique count.  R holds the m sorted keys on return of the
-// sort; the compaction runs IPT consecutive keys per thread (one block scan for up to NTH * IPT keys per round).
-template <int NTH, int IPT>
-__device__ void csr_finish(const Geo& g, int64_t b, uint32_t* A, uint32_t* B, int m, int c, int32_t off,
-                           const int64_t* __restrict__ node_ptr, uint32_t* __restrict__ keys,
-                           int32_t* __restrict__ rowptr, int32_t* __restrict__ ucnt, int* sh_base, int* sh_tot,
-                           int* sh_wc, int* sh_rc, int32_t* sh_sm) {
-    const int tid = threadIdx.x;
-    const int64_t r0 = b << g.SB;
-    const int nv = (int)bucket_rows(b, g.SB, g.N);
-    for (int j = tid; j < nv; j += NTH) {     // the bucket's self-loops ("+ eye")
-        const int64_t v = r0 + j;
-        A[c + j] = ((uint32_t)j << g.LB) | (uint32_t)(v - node_base(node_ptr, g.G, v));
-        sh_rc[j] = 0;
+// Sorts the bucket K[0..m) (V) by its full key into row order, in place: rows at L.ro[j] with L.rc[j] entries,
+// K2 (V2) the row-grouped staging copy.  DEDUP (CSR): duplicate keys are left next to their first copy (a hub row
+// produced by the bitmap repeats its largest key over the tail), dropped on emission.  Returns false -- K and V
+// untouched -- when the bucket needs the LSD fallback (a long row and LB > BM_LB, or no bitmap space).
+template <int NTH, bool VAL, bool DEDUP>
+__device__ bool seg_sort(const Geo& g, int nrows, uint32_t* K, uint32_t* K2, int32_t* V, int32_t* V2, int m,
+                         SegLds L, int32_t* sh_sm) {
+    constexpr int NW = NTH / WAVE;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & (WAVE - 1);
+    const uint32_t lmask = (uint32_t)(((uint64_t)1 << g.LB) - 1);
+    const bool bitmap_ok = L.bm != nullptr && g.LB <= BM_LB;
+    for (int j = tid; j < (1 << SB_MAX); j += NTH) L.rc[j] = 0;
+    if (tid == 0) *L.flag = 0;
+    __syncthreads();
+    for (int i = tid; i < m; i += NTH) L.rank[i] = atomicAdd(&L.rc[K[i] >> g.LB], 1);
+    __syncthreads();
+    {   // row starts: one block scan over the (<= 256) rows; a long row without the bitmap path -> fallback
+        const int x = tid < nrows ? L.rc[tid] : 0;
+        int32_t tot;
+        const int32_t ex = scan::block_excl<NTH>((int32_t)x, (int32_t)0, scan::Plus(), sh_sm, &tot);
+        if (tid < nrows) L.ro[tid] = ex;
+        if (x > SHORT_ROW && !bitmap_ok) *L.flag = 1;
     }
     __syncthreads();
-    const uint32_t* R = block_radix_sort<NTH, IPT, false>(A, B, nullptr, nullptr, m, g.SB + g.LB, sh_base, sh_tot,
-                                                          sh_wc, sh_sm) ? B : A;
-    int32_t run = 0;
-    for (int t0 = 0; t0 < m; t0 += NTH * IPT) {
-        const int i0 = t0 + tid * IPT;
-        uint32_t k[IPT];
-        int u = 0;
-        uint32_t first = 0;     // bit q: key i0 + q is the first of its run (kept)
+    if (*L.flag) return false;
+    for (int i = tid; i < m; i += NTH) {
+        const uint32_t k = K[i];
+        const int p = L.ro[k >> g.LB] + L.rank[i];
+        K2[p] = k;
+        if (VAL) V2[p] = V[i];
+    }
+    __syncthreads();
+    for (int i = tid; i < m; i += NTH) {   // short rows: rank of (key, index) within the row
+        const uint32_t x = K2[i];
+        const int j = (int)(x >> g.LB), n = L.rc[j];
+        if (n > SHORT_ROW) continue;
+        const int s = L.ro[j];
+        const uint64_t me = ((uint64_t)x << 32) | (uint32_t)i;
+        int p = 0;
+        for (int t = s; t < s + n; ++t) p += (((uint64_t)K2[t] << 32) | (uint32_t)t) < me ? 1 : 0;
+        K[s + p] = x;
+        if (VAL) V[s + p] = V2[i];
+    }
+    if constexpr (NTH >= BNT) {   // big buckets: the whole block ranks one hub row at a time
+        hub_rows_block<NTH, VAL, DEDUP>(g, nrows, K, K2, V, V2, L, sh_sm);
+        __syncthreads();
+        return true;
+    }
+    for (int j = w; j < nrows; j += NW) {   // hub rows: one wave each, ranked through a bitmap over the local ids
+        const int n = L.rc[j], base = L.ro[j];
+        if (n <= SHORT_ROW) continue;
+        uint32_t* bm = L.bm + w * BMW;
+        uint16_t* pw = L.pw + w * BMW;
+        const int nw = (int)((lmask >> 5) + 1);
+        for (int i = lane; i < nw; i += WAVE) bm[i] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        for (int i = lane; i < n; i += WAVE) {
+            const uint32_t lo = K2[base + i] & lmask;
+            atomicOr(&bm[lo >> 5], 1u << (lo & 31));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        const int per = (nw + WAVE - 1) / WAVE, w0 = lane * per, w1 = min(nw, w0 + per);
+        int cnt = 0;
+        for (int q = w0; q < w1; ++q) cnt += __popc(bm[q]);
+        const int inc = scan::wave_incl((int32_t)cnt, scan::Plus());
+        const int tot = __shfl(inc, WAVE - 1, WAVE);
+        int run = inc - cnt;
+        for (int q = w0; q < w1; ++q) {   // distinct ids below each word
+            pw[q] = (uint16_t)run;
+            run += __popc(bm[q]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        for (int i = lane; i < n; i += WAVE) {   // rank = distinct ids below; duplicates share (and rewrite) a slot
+            const uint32_t k = K2[base + i], lo = k & lmask;
+            const int r = pw[lo >> 5] + __popc(bm[lo >> 5] & ((1u << (lo & 31)) - 1u));
+            K[base + r] = k;
+            if (VAL) V[base + r] = V2[base + i];
+        }
+        if (DEDUP && tot < n) {   // the duplicates' slots repeat the row's largest key
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t last = K[base + tot - 1];
+            for (int i = tot + lane; i < n; i += WAVE) K[base + i] = last;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    return true;
+}
+
+// CSR: the sorted bucket S[0..m) -> its unique keys (compacted through C, then out coalesced), the in-bucket row
+// prefix into rowptr (a row starts where the row bits change: every row holds at least its self-loop), unique count
+template <int NTH>
+__device__ void csr_emit(const Geo& g, int64_t b, const uint32_t* S, uint32_t* C, int m, int32_t* sh_sm, int32_t off,
+                         uint32_t* __restrict__ keys, int32_t* __restrict__ rowptr, int32_t* __restrict__ ucnt) {
+    constexpr int EI = 8;
+    const int tid = threadIdx.x;
+    int32_t carry = 0;
+    for (int t0 = 0; t0 < m; t0 += NTH * EI) {
+        const int q0 = t0 + tid * EI;
+        uint32_t v[EI];
+        uint32_t prev = q0 > 0 && q0 < m ? S[q0 - 1] : 0u;
+        int c = 0;
+        unsigned keep = 0, first = 0;
 #pragma unroll
-        for (int q = 0; q < IPT; ++q) {
-            const int i = i0 + q;
-            k[q] = i < m ? R[i] : 0u;
-            if (i < m && (i == 0 || R[i - 1] != k[q])) { first |= 1u << q; ++u; }
+        for (int k = 0; k < EI; ++k) {
+            const int q = q0 + k;
+            v[k] = q < m ? S[q] : 0u;
+            if (q < m) {
+                const bool kp = q == 0 || v[k] != prev;
+                keep |= (unsigned)kp << k;
+                first |= (unsigned)(q == 0 || (v[k] >> g.LB) != (prev >> g.LB)) << k;
+                c += kp ? 1 : 0;
+            }
+            prev = v[k];
         }
         int32_t tot;
-        int32_t pos = run + scan::block_excl<NTH>((int32_t)u, (int32_t)0, scan::Plus(), sh_sm, &tot);
+        int32_t p = carry + scan::block_excl<NTH>((int32_t)c, (int32_t)0, scan::Plus(), sh_sm, &tot);
 #pragma unroll
-        for (int q = 0; q < IPT; ++q) {
-            if ((first >> q) & 1u) {
-                keys[off + pos++] = k[q];
-                atomicAdd(&sh_rc[k[q] >> g.LB], 1);
+        for (int k = 0; k < EI; ++k) {
+            if ((keep >> k) & 1) {
+                if ((first >> k) & 1) rowptr[(b << g.SB) + (v[k] >> g.LB)] = p;
+                C[p++] = v[k];
             }
+        }
+        carry += tot;
+    }
+    __syncthreads();
+    for (int i = tid; i < carry; i += NTH) keys[off + i] = C[i];
+    if (tid == 0) ucnt[b] = carry;
+    __syncthreads();
+}
+
+// CSC: csc_row / csc_eid / csc_ptr of the bucket's columns and the CSR -> CSC position map
+template <int NTH>
+__device__ void csc_emit(const Geo& g, int64_t b, int nrows, const uint32_t* S, const int32_t* SV, int m, SegLds L,
+                         const int32_t* colbase, int32_t o, int32_t* __restrict__ csc_ptr,
+                         int32_t* __restrict__ csc_row, int32_t* __restrict__ csc_eid, int32_t* __restrict__ cpos) {
+    const int tid = threadIdx.x;
+    const uint32_t lmask = (uint32_t)(((uint64_t)1 << g.LB) - 1);
+    if (tid < nrows) csc_ptr[(b << g.SB) + tid] = o + L.ro[tid];
+    for (int q = tid; q < m; q += NTH) {
+        const uint32_t k = S[q];
+        const int32_t e = SV[q];
+        csc_row[o + q] = colbase[k >> g.LB] + (int32_t)(k & lmask);
+        csc_eid[o + q] = e;
+        if (cpos) cpos[e] = o + q;
+    }
+}
+
+// the LSD fallback of a CSR bucket (K holds its m raw keys + self-loops): sort, dedupe, emit
+template <int NTH>
+__device__ void csr_lsd(const Geo& g, int64_t b, int nrows, uint32_t* A, uint32_t* B, int m, int32_t off,
+                        uint32_t* __restrict__ keys, int32_t* __restrict__ rowptr, int32_t* __restrict__ ucnt,
+                        int* sh_base, int* sh_tot, int* sh_wc, int* sh_rc, int32_t* sh_sm) {
+    const int tid = threadIdx.x;
+    for (int j = tid; j < nrows; j += NTH) sh_rc[j] = 0;
+    __syncthreads();
+    const uint32_t* R = block_radix_sort<NTH, 1, false>(A, B, nullptr, nullptr, m, g.SB + g.LB, sh_base, sh_tot,
+                                                        sh_wc, sh_sm) ? B : A;
+    int32_t run = 0;
+    for (int t0 = 0; t0 < m; t0 += NTH) {
+        const int i = t0 + tid;
+        const uint32_t k = i < m ? R[i] : 0u;
+        const bool first = i < m && (i == 0 || R[i - 1] != k);
+        int32_t tot;
+        const int32_t pos = run + scan::block_excl<NTH>((int32_t)(first ? 1 : 0), (int32_t)0, scan::Plus(), sh_sm, &tot);
+        if (first) {
+            keys[off + pos] = k;
+            atomicAdd(&sh_rc[k >> g.LB], 1);
         }
         run += tot;
         __syncthreads();
     }
-    // in-bucket row prefix (rows <= 1024: a few per thread, one block scan)
-    constexpr int RPT = (1 << SB_MAX) / NTH > 0 ? (1 << SB_MAX) / NTH : 1;
-    int v[RPT], t = 0;
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        const int j = tid * RPT + q;
-        v[q] = j < nv ? sh_rc[j] : 0;
-        t += v[q];
-    }
+    const int x = tid < nrows ? sh_rc[tid] : 0;
     int32_t tot;
-    int32_t pre = scan::block_excl<NTH>((int32_t)t, (int32_t)0, scan::Plus(), sh_sm, &tot);
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        const int j = tid * RPT + q;
-        if (j < nv) rowptr[r0 + j] = pre;
-        pre += v[q];
-    }
+    const int32_t ex = scan::block_excl<NTH>((int32_t)x, (int32_t)0, scan::Plus(), sh_sm, &tot);
+    if (tid < nrows) rowptr[(b << g.SB) + tid] = ex;
     if (tid == 0) ucnt[b] = run;
     __syncthreads();
+}
+
+// the LSD fallback of a CSC bucket (K, V its pairs): sort by (column, local src), emit
+template <int NTH>
+__device__ void csc_lsd(const Geo& g, int64_t b, int nrows, uint32_t* K, uint32_t* K2, int32_t* V, int32_t* V2, int m,
+                        int32_t o, const int32_t* colbase, int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_row,
+                        int32_t* __restrict__ csc_eid, int32_t* __restrict__ cpos, int* sh_base, int* sh_tot,
+                        int* sh_wc, int* sh_rc, int32_t* sh_sm) {
+    const int tid = threadIdx.x;
+    for (int j = tid; j < nrows; j += NTH) sh_rc[j] = 0;
+    __syncthreads();
+    const int par = block_radix_sort<NTH, 1, true>(K, K2, V, V2, m, g.SB + g.LB, sh_base, sh_tot, sh_wc, sh_sm);
+    const uint32_t* RK = par ? K2 : K;
+    const int32_t* RV = par ? V2 : V;
+    const uint32_t lmask = (uint32_t)(((uint64_t)1 << g.LB) - 1);
+    for (int i = tid; i < m; i += NTH) {
+        const uint32_t k = RK[i];
+        const int j = (int)(k >> g.LB);
+        const int32_t e = RV[i];
+        csc_row[o + i] = colbase[j] + (int32_t)(k & lmask);
+        csc_eid[o + i] = e;
+        if (cpos) cpos[e] = o + i;
+        atomicAdd(&sh_rc[j], 1);
+    }
+    __syncthreads();
+    const int x = tid < nrows ? sh_rc[tid] : 0;
+    int32_t tot;
+    const int32_t ex = scan::block_excl<NTH>((int32_t)x, (int32_t)0, scan::Plus(), sh_sm, &tot);
+    if (tid < nrows) csc_ptr[(b << g.SB) + tid] = o + ex;
+    __syncthreads();
+}
+
+// one CSR bucket: load its raw keys (+ self-loops) into A, sort in place (B staging), emit (or the LSD fallback)
+template <int NTH>
+__device__ void csr_bucket(const Geo& g, int64_t b, uint32_t* A, uint32_t* B, bool global_bufs, int c, int32_t off,
+                           const int64_t* __restrict__ node_ptr, uint32_t* __restrict__ keys,
+                           int32_t* __restrict__ rowptr, int32_t* __restrict__ ucnt, SegLds L, int* sh_base,
+                           int* sh_tot, int32_t* sh_sm) {
+    const int tid = threadIdx.x;
+    const int64_t r0 = b << g.SB;
+    const int nv = (int)bucket_rows(b, g.SB, g.N);
+    if (!global_bufs)
+        for (int i = tid; i < c; i += NTH) A[i] = keys[off + i];
+    for (int j = tid; j < nv; j += NTH) {     // the bucket's self-loops ("+ eye")
+        const int64_t v = r0 + j;
+        A[c + j] = ((uint32_t)j << g.LB) | (uint32_t)(v - node_base(node_ptr, g.G, v));
+    }
+    __syncthreads();
+    const int m = c + nv;
+    if (seg_sort<NTH, false, true>(g, nv, A, B, nullptr, nullptr, m, L, sh_sm))
+        csr_emit<NTH>(g, b, A, B, m, sh_sm, off, keys, rowptr, ucnt);
+    else
+        csr_lsd<NTH>(g, b, nv, A, B, m, off, keys, rowptr, ucnt, sh_base, sh_tot, L.wc, L.rc, sh_sm);
 }
 
 __global__ void __launch_bounds__(FNT) k_csr_finish(Geo g, const int32_t* __restrict__ bstart,
@@ -459,30 +845,37 @@ __global__ void __launch_bounds__(FNT) k_csr_finish(Geo g, const int32_t* __rest
                                                     const int64_t* __restrict__ node_ptr, uint32_t* __restrict__ keys,
                                                     int32_t* __restrict__ rowptr, int32_t* __restrict__ ucnt,
                                                     int32_t* __restrict__ big, int32_t* __restrict__ nbig) {
+    constexpr int RK = CAP_S > (FNT / WAVE) * BMW * 3 / 2 ? CAP_S : (FNT / WAVE) * BMW * 3 / 2;
+    static_assert(RK >= (FNT / WAVE) * RBINS, "the LSD count table aliases the rank array");
     __shared__ uint32_t A[CAP_S], Bk[CAP_S];
-    __shared__ int base[RBINS], tot[RBINS], wc[FIPT * (FNT / WAVE) * RBINS], rc[1 << SB_MAX];
+    __shared__ int rc[1 << SB_MAX], ro[1 << SB_MAX], flag;
+    __shared__ int rk[RK];   // row slots, then the per-wave bitmaps / the LSD count table
+    __shared__ int base[RBINS], tot[RBINS];
     __shared__ int32_t sm[FNT / WAVE + 1];
     const int64_t b = blockIdx.x;
     const int c = fill_src[b];
-    const int m = c + (int)bucket_rows(b, g.SB, g.N);
-    if (m > CAP_S) {
+    if (c + (int)bucket_rows(b, g.SB, g.N) > CAP_S) {
         if (threadIdx.x == 0) big[atomicAdd(nbig, 1)] = (int32_t)b;
         return;
     }
-    const int32_t off = bstart[b];
-    for (int i = threadIdx.x; i < c; i += FNT) A[i] = keys[off + i];
-    csr_finish<FNT, FIPT>(g, b, A, Bk, m, c, off, node_ptr, keys, rowptr, ucnt, base, tot, wc, rc, sm);
+    const SegLds L{rc, ro, (uint32_t*)rk, (uint16_t*)(rk + (FNT / WAVE) * BMW), rk, rk, &flag};
+    csr_bucket<FNT>(g, b, A, Bk, false, c, bstart[b], node_ptr, keys, rowptr, ucnt, L, base, tot, sm);
 }
 
 __global__ void __launch_bounds__(BNT) k_csr_finish_big(Geo g, const int32_t* __restrict__ bstart,
                                                         const int32_t* __restrict__ fill_src,
                                                         const int64_t* __restrict__ node_ptr,
                                                         uint32_t* __restrict__ keys, uint32_t* __restrict__ scratch,
+                                                        int32_t* __restrict__ rank_g,
                                                         int32_t* __restrict__ rowptr, int32_t* __restrict__ ucnt,
                                                         const int32_t* __restrict__ big,
                                                         const int32_t* __restrict__ nbig) {
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
-    __shared__ int base[RBINS], tot[RBINS], wc[(BNT / WAVE) * RBINS], rc[1 << SB_MAX];
+    __shared__ int rc[1 << SB_MAX], ro[1 << SB_MAX], flag;
+    __shared__ uint32_t bm[BMW];   // one bitmap: the block ranks hub rows together
+    __shared__ uint16_t pw[BMW];
+    __shared__ int wc[(BNT / WAVE) * RBINS];
+    __shared__ int base[RBINS], tot[RBINS];
     __shared__ int32_t sm[BNT / WAVE + 1];
     constexpr int CAP = BIG_LDS / 8;
     const int nb = *nbig;
@@ -491,15 +884,103 @@ __global__ void __launch_bounds__(BNT) k_csr_finish_big(Geo g, const int32_t* __
         const int c = fill_src[b];
         const int m = c + (int)bucket_rows(b, g.SB, g.N);
         const int32_t off = bstart[b];
+        const SegLds L{rc, ro, bm, pw, rank_g + off, wc, &flag};
+        if (m <= CAP)
+            csr_bucket<BNT>(g, b, dyn, dyn + CAP, false, c, off, node_ptr, keys, rowptr, ucnt, L, base, tot, sm);
+        else   // in global memory: the bucket's own region (room for its self-loops) and the scratch twin
+            csr_bucket<BNT>(g, b, keys + off, scratch + off, true, c, off, node_ptr, keys, rowptr, ucnt, L, base, tot,
+                            sm);
+    }
+}
+
+// one CSC bucket: its (key, CSR position) pairs in K / V, sorted in place (K2 / V2 staging), emit (or the fallback)
+template <int NTH>
+__device__ void csc_bucket(const Geo& g, int64_t b, uint32_t* K, uint32_t* K2, int32_t* V, int32_t* V2, int m,
+                           int32_t o, const int64_t* __restrict__ node_ptr, int32_t* __restrict__ csc_ptr,
+                           int32_t* __restrict__ csc_row, int32_t* __restrict__ csc_eid, int32_t* __restrict__ cpos,
+                           SegLds L, int* colbase, int* sh_base, int* sh_tot, int32_t* sh_sm) {
+    const int tid = threadIdx.x;
+    const int64_t c0 = b << g.SB;
+    const int nv = (int)bucket_rows(b, g.SB, g.N);
+    for (int j = tid; j < nv; j += NTH) colbase[j] = (int32_t)node_base(node_ptr, g.G, c0 + j);
+    __syncthreads();
+    if (seg_sort<NTH, true, false>(g, nv, K, K2, V, V2, m, L, sh_sm))
+        csc_emit<NTH>(g, b, nv, K, V, m, L, colbase, o, csc_ptr, csc_row, csc_eid, cpos);
+    else
+        csc_lsd<NTH>(g, b, nv, K, K2, V, V2, m, o, colbase, csc_ptr, csc_row, csc_eid, cpos, sh_base, sh_tot, L.wc,
+                     L.rc, sh_sm);
+}
+
+__global__ void __launch_bounds__(FNT) k_csc_finish(Geo g, const int32_t* __restrict__ cstart,
+                                                    const int32_t* __restrict__ fill_dst,
+                                                    const int32_t* __restrict__ coff,
+                                                    const int64_t* __restrict__ node_ptr,
+                                                    const uint32_t* __restrict__ ckey,
+                                                    const int32_t* __restrict__ cval, int32_t* __restrict__ csc_ptr,
+                                                    int32_t* __restrict__ csc_row, int32_t* __restrict__ csc_eid,
+                                                    int32_t* __restrict__ cpos, int32_t* __restrict__ big,
+                                                    int32_t* __restrict__ nbig) {
+    constexpr int RK = CAP_C > (FNT / WAVE) * BMW * 3 / 2 ? CAP_C : (FNT / WAVE) * BMW * 3 / 2;
+    static_assert(RK >= (FNT / WAVE) * RBINS, "the LSD count table aliases the rank array");
+    __shared__ uint32_t K[CAP_C], K2[CAP_C];
+    __shared__ int32_t V[CAP_C], V2[CAP_C];
+    __shared__ int rc[1 << SB_MAX], ro[1 << SB_MAX], cb[1 << SB_MAX], flag;
+    __shared__ int rk[RK];   // row slots, then the per-wave bitmaps / the LSD count table
+    __shared__ int base[RBINS], tot[RBINS];
+    __shared__ int32_t sm[FNT / WAVE + 1];
+    const int64_t b = blockIdx.x;
+    const int m = fill_dst[b];
+    if (m > CAP_C) {
+        if (threadIdx.x == 0) big[atomicAdd(nbig + 1, 1)] = (int32_t)b;
+        return;
+    }
+    const int32_t ro0 = cstart[b];
+    for (int i = threadIdx.x; i < m; i += FNT) { K[i] = ckey[ro0 + i]; V[i] = cval[ro0 + i]; }
+    const SegLds L{rc, ro, (uint32_t*)rk, (uint16_t*)(rk + (FNT / WAVE) * BMW), rk, rk, &flag};
+    csc_bucket<FNT>(g, b, K, K2, V, V2, m, coff[b], node_ptr, csc_ptr, csc_row, csc_eid, cpos, L, cb, base,
+                    tot, sm);
+    if (b == g.NB - 1 && threadIdx.x == 0) csc_ptr[g.N] = coff[g.NB];
+}
+
+__global__ void __launch_bounds__(BNT) k_csc_finish_big(Geo g, const int32_t* __restrict__ cstart,
+                                                        const int32_t* __restrict__ fill_dst,
+                                                        const int32_t* __restrict__ coff,
+                                                        const int64_t* __restrict__ node_ptr,
+                                                        uint32_t* __restrict__ ckey, int32_t* __restrict__ cval,
+                                                        uint32_t* __restrict__ sk, int32_t* __restrict__ sv,
+                                                        int32_t* __restrict__ rank_g,
+                                                        int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_row,
+                                                        int32_t* __restrict__ csc_eid, int32_t* __restrict__ cpos,
+                                                        const int32_t* __restrict__ big,
+                                                        const int32_t* __restrict__ nbig) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    __shared__ int rc[1 << SB_MAX], ro[1 << SB_MAX], cb[1 << SB_MAX], flag;
+    __shared__ uint32_t bm[BMW];   // one bitmap: the block ranks hub rows together
+    __shared__ uint16_t pw[BMW];
+    __shared__ int wc[(BNT / WAVE) * RBINS];
+    __shared__ int base[RBINS], tot[RBINS];
+    __shared__ int32_t sm[BNT / WAVE + 1];
+    constexpr int CAP = BIG_LDS / 16;
+    const int nb = nbig[1];
+    for (int q = blockIdx.x; q < nb; q += gridDim.x) {
+        const int64_t b = big[q];
+        const int m = fill_dst[b];
+        const int32_t ro0 = cstart[b];
+        const SegLds L{rc, ro, bm, pw, rank_g + ro0, wc, &flag};
         if (m <= CAP) {
-            uint32_t* A = dyn;
-            uint32_t* Bk = dyn + CAP;
-            for (int i = threadIdx.x; i < c; i += BNT) A[i] = keys[off + i];
-            csr_finish<BNT, 1>(g, b, A, Bk, m, c, off, node_ptr, keys, rowptr, ucnt, base, tot, wc, rc, sm);
-        } else {   // in global memory: the bucket's own region (room for its self-loops) and the scratch twin
-            csr_finish<BNT, 1>(g, b, keys + off, scratch + off, m, c, off, node_ptr, keys, rowptr, ucnt, base, tot, wc,
-                               rc, sm);
+            uint32_t* K = dyn;
+            uint32_t* K2 = dyn + CAP;
+            int32_t* V = (int32_t*)(dyn + 2 * CAP);
+            int32_t* V2 = (int32_t*)(dyn + 3 * CAP);
+            for (int i = threadIdx.x; i < m; i += BNT) { K[i] = ckey[ro0 + i]; V[i] = cval[ro0 + i]; }
+            csc_bucket<BNT>(g, b, K, K2, V, V2, m, coff[b], node_ptr, csc_ptr, csc_row, csc_eid, cpos, L,
+                            cb, base, tot, sm);
+        } else {
+            csc_bucket<BNT>(g, b, ckey + ro0, sk + ro0, cval + ro0, sv + ro0, m, coff[b], node_ptr, csc_ptr, csc_row,
+                            csc_eid, cpos, L, cb, base, tot, sm);
         }
+        if (b == g.NB - 1 && threadIdx.x == 0) csc_ptr[g.N] = coff[g.NB];
+        __syncthreads();
     }
 }
 
@@ -541,8 +1022,14 @@ __global__ void __launch_bounds__(PNT) k_part_csr(Geo g, const int32_t* __restri
                                                   const int64_t* __restrict__ nnz_p,
                                                   const int32_t* __restrict__ cstart, int32_t* __restrict__ fill,
                                                   uint32_t* __restrict__ okey, int32_t* __restrict__ oval) {
-    __shared__ int h[LDS_BINS];
+    __shared__ int h[PART_BINS];
+    __shared__ int tcnt[PNB], tstart[PNB], gpos[PNB];
+    __shared__ uint32_t stk[PTILE];
+    __shared__ int32_t stv[PTILE];
+    __shared__ int stp[PTILE];
+    __shared__ int32_t sm[PNT / WAVE + 1];
     __shared__ int gr[2];
+    for (int i = threadIdx.x; i < PNB; i += PNT) tcnt[i] = 0;
     const int64_t nnz = *nnz_p;
     const int64_t e0 = blockIdx.x * g.CHc, e1 = min(nnz, e0 + g.CHc);
     if (e0 >= e1) return;
@@ -562,11 +1049,18 @@ __global__ void __launch_bounds__(PNT) k_part_csr(Geo g, const int32_t* __restri
     for (int gg = g0; gg <= g1; ++gg) {
         const int64_t v0 = node_ptr[gg], v1 = node_ptr[gg + 1];
         const int64_t a = max(e0, (int64_t)rowptr[v0]), z = min(e1, (int64_t)rowptr[v1]);
-        const Span sp = span_of(v0, v1, shc);
+        const Span sp = span_of(v0, v1, shc, PART_BINS);
         if (sp.lds) {
             for (int i = threadIdx.x; i < sp.nb; i += PNT) h[i] = 0;
             __syncthreads();
-            for (int64_t e = a + threadIdx.x; e < z; e += PNT) atomicAdd(&h[(col[e] >> shc) - sp.b0], 1);
+            for (int64_t e4 = a + threadIdx.x; e4 < z; e4 += UNR * PNT) {
+                int32_t d[UNR];
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) d[u] = e4 + u * PNT < z ? col[e4 + u * PNT] : 0;
+#pragma unroll
+                for (int u = 0; u < UNR; ++u)
+                    if (e4 + u * PNT < z) atomicAdd(&h[(d[u] >> shc) - sp.b0], 1);
+            }
             __syncthreads();
             for (int i = threadIdx.x; i < sp.nb; i += PNT) {
                 const int c = h[i];
@@ -575,123 +1069,33 @@ __global__ void __launch_bounds__(PNT) k_part_csr(Geo g, const int32_t* __restri
             }
             __syncthreads();
         }
-        for (int64_t e = a + threadIdx.x; e < z; e += PNT) {
-            const int32_t d = col[e];
-            const int64_t bin = d >> shc;
-            const int pos = sp.lds ? atomicAdd(&h[bin - sp.b0], 1) : cstart[bin << g.SC] + atomicAdd(&fill[bin], 1);
-            okey[pos] = ((((uint32_t)(d >> g.SB) & fmask) << g.SB | ((uint32_t)d & cmask)) << g.LB) |
-                        (uint32_t)sloc[e];
-            oval[pos] = (int32_t)e;
+        if (sp.lds && sp.nb <= PNB) {   // LDS-staged scatter
+            const CsrEntryLoader ld{col, sloc, sp.b0, shc, g.SB, g.LB, cmask, fmask};
+            tile_partition<PNT, PIPT, PNB, true>(a, z, ld, h, tcnt, tstart, gpos, stk, stv, stp, sm, okey, oval);
+        } else {
+            for (int64_t e4 = a + threadIdx.x; e4 < z; e4 += UNR * PNT) {
+                int32_t dd[UNR], sl[UNR];
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    const bool ok = e4 + u * PNT < z;
+                    dd[u] = ok ? col[e4 + u * PNT] : 0;
+                    sl[u] = ok ? sloc[e4 + u * PNT] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    const int64_t e = e4 + u * PNT;
+                    if (e >= z) break;
+                    const int32_t d = dd[u];
+                    const int64_t bin = d >> shc;
+                    const int pos = sp.lds ? atomicAdd(&h[bin - sp.b0], 1)
+                                           : cstart[bin << g.SC] + atomicAdd(&fill[bin], 1);
+                    okey[pos] = ((((uint32_t)(d >> g.SB) & fmask) << g.SB | ((uint32_t)d & cmask)) << g.LB) |
+                                (uint32_t)sl[u];
+                    oval[pos] = (int32_t)e;
+                }
+            }
         }
         __syncthreads();
-    }
-}
-
-// 7b. CSC bucket finish: sort (key, CSR position) pairs, write csc_row / csc_eid / csc_ptr and the CSR -> CSC map
-template <int NTH, int IPT>
-__device__ void csc_finish(const Geo& g, int64_t b, uint32_t* K, uint32_t* K2, int32_t* V, int32_t* V2, int m,
-                           int32_t o, const int64_t* __restrict__ node_ptr, int32_t* __restrict__ csc_ptr,
-                           int32_t* __restrict__ csc_row, int32_t* __restrict__ csc_eid, int32_t* __restrict__ cpos,
-                           int* sh_base, int* sh_tot, int* sh_wc, int* sh_cc, int32_t* sh_sm) {
-    const int tid = threadIdx.x;
-    const int64_t c0 = b << g.SB;
-    const int nv = (int)bucket_rows(b, g.SB, g.N);
-    for (int j = tid; j < nv; j += NTH) {
-        sh_cc[j] = 0;
-        sh_cc[(1 << SB_MAX) + j] = (int)node_base(node_ptr, g.G, c0 + j);
-    }
-    __syncthreads();
-    const int par = block_radix_sort<NTH, IPT, true>(K, K2, V, V2, m, g.SB + g.LB, sh_base, sh_tot, sh_wc, sh_sm);
-    const uint32_t* RK = par ? K2 : K;
-    const int32_t* RV = par ? V2 : V;
-    const uint32_t lmask = (uint32_t)(((uint64_t)1 << g.LB) - 1);
-    for (int i = tid; i < m; i += NTH) {
-        const uint32_t k = RK[i];
-        const int j = (int)(k >> g.LB);
-        const int32_t e = RV[i];
-        csc_row[o + i] = sh_cc[(1 << SB_MAX) + j] + (int32_t)(k & lmask);
-        csc_eid[o + i] = e;
-        if (cpos) cpos[e] = o + i;
-        atomicAdd(&sh_cc[j], 1);
-    }
-    __syncthreads();
-    constexpr int RPT = (1 << SB_MAX) / NTH > 0 ? (1 << SB_MAX) / NTH : 1;
-    int v[RPT], t = 0;
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        const int j = tid * RPT + q;
-        v[q] = j < nv ? sh_cc[j] : 0;
-        t += v[q];
-    }
-    int32_t tot;
-    int32_t pre = o + scan::block_excl<NTH>((int32_t)t, (int32_t)0, scan::Plus(), sh_sm, &tot);
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        const int j = tid * RPT + q;
-        if (j < nv) csc_ptr[c0 + j] = pre;
-        pre += v[q];
-    }
-    __syncthreads();
-}
-
-__global__ void __launch_bounds__(FNT) k_csc_finish(Geo g, const int32_t* __restrict__ cstart,
-                                                    const int32_t* __restrict__ fill_dst,
-                                                    const int32_t* __restrict__ coff,
-                                                    const int64_t* __restrict__ node_ptr,
-                                                    const uint32_t* __restrict__ ckey,
-                                                    const int32_t* __restrict__ cval, int32_t* __restrict__ csc_ptr,
-                                                    int32_t* __restrict__ csc_row, int32_t* __restrict__ csc_eid,
-                                                    int32_t* __restrict__ cpos, int32_t* __restrict__ big,
-                                                    int32_t* __restrict__ nbig) {
-    __shared__ uint32_t K[CAP_S], K2[CAP_S];
-    __shared__ int32_t V[CAP_S], V2[CAP_S];
-    __shared__ int base[RBINS], tot[RBINS], wc[FIPT * (FNT / WAVE) * RBINS], cc[2 << SB_MAX];
-    __shared__ int32_t sm[FNT / WAVE + 1];
-    const int64_t b = blockIdx.x;
-    const int m = fill_dst[b];
-    if (m > CAP_S) {
-        if (threadIdx.x == 0) big[atomicAdd(nbig + 1, 1)] = (int32_t)b;
-        return;
-    }
-    const int32_t ro = cstart[b];
-    for (int i = threadIdx.x; i < m; i += FNT) { K[i] = ckey[ro + i]; V[i] = cval[ro + i]; }
-    csc_finish<FNT, FIPT>(g, b, K, K2, V, V2, m, coff[b], node_ptr, csc_ptr, csc_row, csc_eid, cpos, base, tot, wc,
-                          cc, sm);
-    if (b == g.NB - 1 && threadIdx.x == 0) csc_ptr[g.N] = coff[g.NB];
-}
-
-__global__ void __launch_bounds__(BNT) k_csc_finish_big(Geo g, const int32_t* __restrict__ cstart,
-                                                        const int32_t* __restrict__ fill_dst,
-                                                        const int32_t* __restrict__ coff,
-                                                        const int64_t* __restrict__ node_ptr,
-                                                        uint32_t* __restrict__ ckey, int32_t* __restrict__ cval,
-                                                        uint32_t* __restrict__ sk, int32_t* __restrict__ sv,
-                                                        int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_row,
-                                                        int32_t* __restrict__ csc_eid, int32_t* __restrict__ cpos,
-                                                        const int32_t* __restrict__ big,
-                                                        const int32_t* __restrict__ nbig) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
-    __shared__ int base[RBINS], tot[RBINS], wc[(BNT / WAVE) * RBINS], cc[2 << SB_MAX];
-    __shared__ int32_t sm[BNT / WAVE + 1];
-    constexpr int CAP = BIG_LDS / 16;
-    const int nb = nbig[1];
-    for (int q = blockIdx.x; q < nb; q += gridDim.x) {
-        const int64_t b = big[q];
-        const int m = fill_dst[b];
-        const int32_t ro = cstart[b];
-        if (m <= CAP) {
-            uint32_t* K = dyn;
-            uint32_t* K2 = dyn + CAP;
-            int32_t* V = (int32_t*)(dyn + 2 * CAP);
-            int32_t* V2 = (int32_t*)(dyn + 3 * CAP);
-            for (int i = threadIdx.x; i < m; i += BNT) { K[i] = ckey[ro + i]; V[i] = cval[ro + i]; }
-            csc_finish<BNT, 1>(g, b, K, K2, V, V2, m, coff[b], node_ptr, csc_ptr, csc_row, csc_eid, cpos, base, tot,
-                               wc, cc, sm);
-        } else {
-            csc_finish<BNT, 1>(g, b, ckey + ro, sk + ro, cval + ro, sv + ro, m, coff[b], node_ptr, csc_ptr, csc_row,
-                               csc_eid, cpos, base, tot, wc, cc, sm);
-        }
-        if (b == g.NB - 1 && threadIdx.x == 0) csc_ptr[g.N] = coff[g.NB];
     }
 }
 
@@ -825,7 +1229,7 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     }
     k_csr_finish<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_src, fill_src, node_ptr, keys, rowptr, ucnt, big_src, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.csr_finish");
-    k_csr_finish_big<<<BIG_WG, BNT, BIG_LDS, s>>>(g, cap_src, fill_src, node_ptr, keys, stage, rowptr, ucnt,
+    k_csr_finish_big<<<BIG_WG, BNT, BIG_LDS, s>>>(g, cap_src, fill_src, node_ptr, keys, stage, sloc, rowptr, ucnt,
                                                   big_src, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.csr_finish_big");
     scan::exclusive(ucnt, ucnt, g.NB, (int32_t)0, plus, part, true, s);           // -> CSR bucket offsets
@@ -843,11 +1247,11 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     }
     scan::exclusive(fill_dst, coff, g.NB, (int32_t)0, plus, part, true, s);       // -> CSC bucket offsets
     TAGAN_CHECK_LAUNCH("csr_build.scan_csc");
-    k_csc_finish<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, csc_ptr, csc_row,
-                                                csc_eid, csr_cpos, big_dst, nbig);
+    k_csc_finish<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, csc_ptr,
+                                                csc_row, csc_eid, csr_cpos, big_dst, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.csc_finish");
-    k_csc_finish_big<<<BIG_WG, BNT, BIG_LDS, s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, stage, sval,
-                                                  csc_ptr, csc_row, csc_eid, csr_cpos, big_dst, nbig);
+    k_csc_finish_big<<<BIG_WG, BNT, BIG_LDS, s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, stage,
+                                                  sval, sloc, csc_ptr, csc_row, csc_eid, csr_cpos, big_dst, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.csc_finish_big");
     return TAGAN_OK;
 }

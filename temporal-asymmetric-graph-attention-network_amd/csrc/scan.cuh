@@ -118,9 +118,35 @@ inline int64_t tiles(int64_t n) { return n <= 0 ? 1 : (n + TILE - 1) / TILE; }
 inline int64_t parts_len(int64_t n) { return tiles(n) + 1; }
 
 // out[0..n) = exclusive scan of in (out may alias in); out[n] = total when out_n.  part: parts_len(n) items.
+// one block, one tile (n <= TILE): the whole scan in one launch
+template <typename T, typename Op>
+__global__ void __launch_bounds__(NT) k_scan_one(const T* in, int64_t n, T zero, Op op, T* out, bool out_n) {
+    __shared__ T sm[NT / WAVE + 1];
+    const int64_t base = (int64_t)threadIdx.x * IPT;
+    T v[IPT];
+    T acc = zero;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        v[k] = base + k < n ? in[base + k] : zero;
+        acc = op(acc, v[k]);
+    }
+    T tot;
+    T run = block_excl<NT>(acc, zero, op, sm, &tot);
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        if (base + k < n) out[base + k] = run;
+        run = op(run, v[k]);
+    }
+    if (out_n && threadIdx.x == 0) out[n] = tot;
+}
+
 template <typename T, typename Op>
 inline void exclusive(const T* in, T* out, int64_t n, T zero, Op op, T* part, bool out_n, hipStream_t s) {
     const int64_t nb = tiles(n);
+    if (nb == 1) {
+        k_scan_one<T, Op><<<1, NT, 0, s>>>(in, n, zero, op, out, out_n);
+        return;
+    }
     k_tile_reduce<T, Op><<<(unsigned)nb, NT, 0, s>>>(in, n, zero, op, part);
     k_scan_parts<T, Op><<<1, NT, 0, s>>>(part, nb, zero, op);
     k_tile_scan<T, Op><<<(unsigned)nb, NT, 0, s>>>(in, n, zero, op, part, out, out_n);
