@@ -87,7 +87,8 @@ int tagan_seed_counter_step(uint64_t* counter, void* stream);
  * max_graph_nodes = the largest snapshot's node count (<= 0: n_nodes); it sets
  * the width of the local-id field of the sort keys.  n_nodes < 2^31.
  * csr_cpos (nullable, capacity as col): the CSC position of each CSR entry (the
- * inverse of csc_eid), written by the same pass.  Kernel launches only (no library
+ * inverse of csc_eid), written by the same pass when asked for (a random scatter:
+ * the attention backward does not need it).  Kernel launches only (no library
  * sort, no memset nodes): safe to capture in a HIP graph and to replay with other
  * work in between.
  * ------------------------------------------------------------------------- */
@@ -162,10 +163,8 @@ typedef struct tagan_graph {
     const int32_t* col_counts;
     const int32_t* row_chunk_order;  /* [chunk_cap] processing order (tagan_chunk_order); NULL = identity */
     const int32_t* col_chunk_order;
-    int64_t nnz_cap;            /* capacity of col / csc_row / csc_eid (>= nnz) */
-    const int32_t* csr_cpos;    /* [nnz] CSC position of each CSR entry (tagan_csr_csc_pos), or NULL.  With
-                                   nnz_cap > 0 and csr_cpos the backward runs column-first (see
-                                   tagan_geo_attn_bwd); otherwise row-first */
+    int64_t nnz_cap;            /* capacity of col / csc_row / csc_eid (>= nnz).  With nnz_cap > 0 the backward
+                                   may run column-first (see tagan_geo_attn_bwd); otherwise row-first */
 } tagan_graph;
 
 /* csr_cpos[csc_eid[p]] = p for p < *nnz: the inverse of csc_eid (the CSC position of each CSR entry). */
@@ -189,9 +188,9 @@ int tagan_geo_attn_fwd(int dtype, int metric, const tagan_graph* g, int32_t head
                        void* out, float* lse, float* edge_alpha,
                        void* workspace, size_t workspace_bytes, void* stream);
 
-/* Backward of tagan_geo_attn_fwd.  Atomic-free and deterministic.  With g->nnz_cap > 0 and g->csr_cpos
+/* Backward of tagan_geo_attn_fwd.  Atomic-free and deterministic.  With g->nnz_cap > 0
  * (fast-path shapes) on graphs whose K|V rows exceed the caches (n_nodes·H·8 > 512 MB): node pass (delta = rowsum(dO∘O) per head) -> column pass over CSC (dk, dv; dS per edge
- * into the workspace in CSC order) -> row pass over CSR (dq from dS[csr_cpos[e]], gathering K only).  Otherwise
+ * into the workspace at its CSR position csc_eid) -> row pass over CSR (dq from dS[e], gathering K only).  Otherwise
  * (or with TAGAN_GEO_BWD_ORDER=row): row pass over CSR (dq, delta) then column pass over CSC (dk, dv).  Both
  * orders give the same bits.
  * dq/dk/dv: [n_nodes, H] with row stride ld_dqkv (may alias one [n,3H] buffer).

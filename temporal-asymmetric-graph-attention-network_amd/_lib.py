@@ -121,7 +121,7 @@ class TaganGraph(ctypes.Structure):
                 ("row_multi", _p), ("row_counts", _p),
                 ("col_chunk_ptr", _p), ("col_chunk_seg", _p), ("col_chunk_beg", _p), ("col_chunk_part", _p),
                 ("col_multi", _p), ("col_counts", _p), ("row_chunk_order", _p), ("col_chunk_order", _p),
-                ("nnz_cap", _i64), ("csr_cpos", _p)]
+                ("nnz_cap", _i64)]
 
 
 _lib = None

@@ -40,14 +40,17 @@ constexpr int LDS_BINS = 16384;    // LDS histogram bins per count block and dir
 constexpr int PART_BINS = 2048;    // LDS bins of the partition passes (more: global atomics)
 constexpr int RNT = 1024;          // refine blocks (one per coarse bin)
 constexpr int FNT = 256;           // small-bucket finish workgroups (4 waves)
-constexpr int CAP_S = 2560;        // keys per small CSR finish (LDS; 4 workgroups per CU)
-constexpr int CAP_C = 2048;        // (key, CSR position) pairs per small CSC finish
+#ifndef TAGAN_CSR_TARGET
+#define TAGAN_CSR_TARGET 2048
+#endif
+constexpr int CAP_S = TAGAN_CSR_TARGET * 5 / 4;   // keys per small CSR finish (LDS)
+constexpr int CAP_C = TAGAN_CSR_TARGET;           // (key, CSR position) pairs per small CSC finish
 constexpr int BNT = 512;           // big-bucket finish workgroups (8 waves)
 constexpr int BIG_LDS = 140 * 1024;   // dynamic LDS of the big-bucket kernels (2 key buffers / 2 + 2 pair buffers)
 constexpr int BIG_WG = 256;        // persistent workgroups of the big-bucket kernels (one per CU)
 constexpr int RB = 8;              // radix digit bits
 constexpr int RBINS = 1 << RB;
-constexpr int TARGET = 2048;       // average entries per bucket
+constexpr int TARGET = TAGAN_CSR_TARGET;   // average entries per bucket
 constexpr int SB_MAX = 8;          // at most 256 rows per bucket
 constexpr int SC_MAX = 8;          // at most 256 buckets per coarse bin
 constexpr int COARSE_PER_SNAPSHOT = 192;
@@ -65,6 +68,20 @@ __device__ __forceinline__ int find_graph(const int64_t* __restrict__ ptr, int G
 __device__ __forceinline__ int64_t node_base(const int64_t* __restrict__ node_ptr, int G, int64_t n) {
     return node_ptr[find_graph(node_ptr, G, n)];
 }
+
+// node_base over the rows [r0, r0 + n) of one bucket: one search for the bucket's first row, another only for rows
+// past the end of that snapshot (a bucket straddles at most a few snapshots)
+struct BucketBase {
+    int64_t base0, end0;
+    const int64_t* node_ptr;
+    int G;
+    __device__ BucketBase(const int64_t* __restrict__ np, int g, int64_t r0) : node_ptr(np), G(g) {
+        const int s = find_graph(np, g, r0);
+        base0 = np[s];
+        end0 = np[s + 1];
+    }
+    __device__ int64_t operator()(int64_t v) const { return v < end0 ? base0 : node_base(node_ptr, G, v); }
+};
 
 struct Geo {
     int64_t N, E, NL;
@@ -828,9 +845,10 @@ __device__ void csr_bucket(const Geo& g, int64_t b, uint32_t* A, uint32_t* B, bo
     const int nv = (int)bucket_rows(b, g.SB, g.N);
     if (!global_bufs)
         for (int i = tid; i < c; i += NTH) A[i] = keys[off + i];
+    const BucketBase nbase(node_ptr, g.G, r0);
     for (int j = tid; j < nv; j += NTH) {     // the bucket's self-loops ("+ eye")
         const int64_t v = r0 + j;
-        A[c + j] = ((uint32_t)j << g.LB) | (uint32_t)(v - node_base(node_ptr, g.G, v));
+        A[c + j] = ((uint32_t)j << g.LB) | (uint32_t)(v - nbase(v));
     }
     __syncthreads();
     const int m = c + nv;
@@ -902,7 +920,8 @@ __device__ void csc_bucket(const Geo& g, int64_t b, uint32_t* K, uint32_t* K2, i
     const int tid = threadIdx.x;
     const int64_t c0 = b << g.SB;
     const int nv = (int)bucket_rows(b, g.SB, g.N);
-    for (int j = tid; j < nv; j += NTH) colbase[j] = (int32_t)node_base(node_ptr, g.G, c0 + j);
+    const BucketBase nbase(node_ptr, g.G, c0);
+    for (int j = tid; j < nv; j += NTH) colbase[j] = (int32_t)nbase(c0 + j);
     __syncthreads();
     if (seg_sort<NTH, true, false>(g, nv, K, K2, V, V2, m, L, sh_sm))
         csc_emit<NTH>(g, b, nv, K, V, m, L, colbase, o, csc_ptr, csc_row, csc_eid, cpos);
@@ -996,8 +1015,9 @@ __global__ void __launch_bounds__(FNT) k_csr_place(Geo g, const int32_t* __restr
     const int64_t r0 = b << g.SB;
     const int nv = (int)bucket_rows(b, g.SB, g.N);
     const int32_t off = bstart[b], u = uoff[b], cnt = uoff[b + 1] - u;
+    const BucketBase nbase(node_ptr, g.G, r0);
     for (int j = threadIdx.x; j < nv; j += FNT) {
-        rb[j] = (int32_t)node_base(node_ptr, g.G, r0 + j);
+        rb[j] = (int32_t)nbase(r0 + j);
         rowptr[r0 + j] += u;
     }
     __syncthreads();

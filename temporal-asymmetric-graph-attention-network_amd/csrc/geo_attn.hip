@@ -196,7 +196,7 @@ struct GeoArgs {
     float* dv;
     int64_t ldd;
     float* delta;
-    float* ds_edge;     // [nnz_cap, heads] dS per edge in CSC order (column-first backward) or null
+    float* ds_edge;     // [nnz_cap, heads] dS per edge in CSR order (column-first backward) or null
     float* prm_partial;
     float* part_m;      // [part_cap, heads]
     float* part_l;      // [part_cap, heads]
@@ -662,7 +662,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
                 pw = keep ? p * A.inv_keep : 0.f;
             }
             const float ds = p * (dp - D[u]);
-            if (A.ds_edge && (L.sl % lph) == 0) A.ds_edge[(int64_t)(e0 + jj + u) * A.heads + h] = ds;   // CSC order
+            if (A.ds_edge && (L.sl % lph) == 0) A.ds_edge[(int64_t)eid[u] * A.heads + h] = ds;   // CSR order
             const Grad g = score_grad<METRIC>(a, b, qq, s, A.inv_sqrt_d, prm);
 #pragma unroll
             for (int c = 0; c < FPL; ++c) {
@@ -710,8 +710,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_delta(GeoArgs A) {
         *(float2*)(A.delta + (row * A.heads + h) * 2) = make_float2(A.lse_in[row * A.heads + h], D);
 }
 
-// Row pass from the stored dS: dq_i = Σ_j dS_ij ∂s/∂q_i, gathering K_j only; dS is read through the CSC
-// position of each CSR entry (the column pass writes it sequentially in CSC order, not scattered).
+// Row pass from the stored dS: dq_i = Σ_j dS_ij ∂s/∂q_i, gathering K_j only; dS is read in CSR order (the column
+// pass stores each edge's dS at its CSR position, csc_eid, so no CSR -> CSC position map is needed).
 template <int METRIC, int LPR, int FPL, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_bwd_row_ds(GeoArgs A) {
     TAGAN_LIVE_SEED(A);
@@ -740,21 +740,19 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_ds(GeoArgs A) {
         float dq[FPL];
 #pragma unroll
         for (int c = 0; c < FPL; ++c) dq[c] = 0.f;
-        int mycol = 0, mypos = 0;
+        int mycol = 0;
         for (int jj = 0; __any(jj < cnt); jj += UN) {
             if ((jj % LPR) == 0) {
                 const bool in = jj + L.sl < cnt;
                 mycol = in ? A.g.col[e0 + jj + L.sl] : 0;
-                mypos = in ? A.g.csr_cpos[e0 + jj + L.sl] : 0;
             }
             float kv[UN][FPL], dsv[UN];
 #pragma unroll
             for (int u = 0; u < UN; ++u) {
                 const int src = L.base + ((jj + u) % LPR);
                 const int j = __shfl(mycol, src, WAVE);
-                const int cp = __shfl(mypos, src, WAVE);
                 ldf<S>(A.k, (int64_t)j * A.ld + f0, kv[u]);
-                dsv[u] = (jj + u < cnt) ? A.ds_edge[(int64_t)cp * A.heads + h] : 0.f;
+                dsv[u] = (jj + u < cnt) ? A.ds_edge[(int64_t)(e0 + jj + u) * A.heads + h] : 0.f;
             }
 #pragma unroll
             for (int u = 0; u < UN; ++u) {
@@ -1170,7 +1168,7 @@ BwdWs bwd_ws(const tagan_graph* g, int heads, int d) {
     w.prm = take((size_t)nprm * heads * 4);
     w.pv = take(lpr ? (size_t)g->part_cap * H * 4 : 0);
     w.pv2 = take(lpr ? (size_t)g->part_cap * 2 * H * 4 : 0);
-    w.col_first = lpr && g->nnz_cap > 0 && g->csr_cpos && col_first_wanted(g->n_nodes, H);
+    w.col_first = lpr && g->nnz_cap > 0 && col_first_wanted(g->n_nodes, H);
     w.ds = take(w.col_first ? (size_t)g->nnz_cap * heads * 4 : 0);
     w.total = off;
     return w;

@@ -69,7 +69,7 @@ class SnapshotGraph:
     chunk_cap: int = 0
     part_cap: int = 0
     nnz_cap: int = 0               # capacity of col / csc arrays (sizes the backward's per-edge dS buffer)
-    csr_cpos: Optional[torch.Tensor] = None   # CSC position of each CSR entry (column-first edge backward)
+    csr_cpos: Optional[torch.Tensor] = None   # CSC position of each CSR entry (only with build(..., cpos=True))
     _struct: object = None
     pending_err: object = None     # (pinned int32 flag, event) of a deferred index validation
 
@@ -94,7 +94,7 @@ class SnapshotGraph:
                                            p(self.csc_row), p(self.csc_eid), self.chunk, self.chunk_cap,
                                            self.part_cap, *[p(t) for t in r], *[p(t) for t in c],
                                            *[None if t is None else p(t) for t in (self.row_order, self.col_order)],
-                                           self.nnz_cap, None if self.csr_cpos is None else p(self.csr_cpos))
+                                           self.nnz_cap)
         return ctypes.byref(self._struct)
 
 
@@ -126,10 +126,6 @@ def _finish(g: SnapshotGraph, nnz_cap: int, chunk: int = CHUNK) -> SnapshotGraph
     g.col_chunks, _, _, g.col_order = _chunk_lists(g.csc_ptr, g.num_nodes, nnz_cap, chunk)
     g.chunk = chunk
     g.nnz_cap = nnz_cap
-    if g.csr_cpos is None:   # tagan_csr_build writes it itself; other builders get the inverse of csc_eid here
-        g.csr_cpos = torch.empty(nnz_cap, dtype=torch.int32, device=g.csc_eid.device)
-        check(lib().tagan_csr_csc_pos(ptr(g.csc_eid), ptr(g.nnz), nnz_cap, ptr(g.csr_cpos), stream_of(g.csc_eid)),
-              "tagan_csr_csc_pos")
     return g
 
 
@@ -167,7 +163,7 @@ def _ptr_table(dev, values):
 
 
 def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], validate=True,
-                chunk: int = CHUNK) -> SnapshotGraph:
+                chunk: int = CHUNK, cpos: bool = False) -> SnapshotGraph:
     """CSR/CSC of the block-diagonal union of snapshot adjacencies (+ self-loops, de-duplicated).
 
     ``edge_indices[g]`` is snapshot g's [2, E_g] edge_index with local node ids.
@@ -175,7 +171,8 @@ def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], va
     ``adj[edge_index[0], edge_index[1]] = 1`` (one device sync, here); "deferred" records the flag and
     ``SnapshotGraph.check_valid()`` raises later (waits only for the CSR build, not the stream); False skips
     it.  An out-of-range edge never enters the CSR either way (tagan_csr_build drops it), so the kernels
-    that follow are safe to launch before the check.
+    that follow are safe to launch before the check.  ``cpos`` also writes ``csr_cpos`` (the CSC position of
+    each CSR entry; a random scatter nothing in the attention path needs).
     """
     require_hip(*edge_indices)
     eis = [e.to(torch.int64) for e in edge_indices]
@@ -183,11 +180,11 @@ def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], va
     e_ptr = [0]
     for e in eis:
         e_ptr.append(e_ptr[-1] + int(e.shape[1]))
-    return build_graph_cat(ei, e_ptr, node_counts, validate, chunk)
+    return build_graph_cat(ei, e_ptr, node_counts, validate, chunk, cpos)
 
 
 def build_graph_cat(ei: torch.Tensor, e_ptr: Sequence[int], node_counts: Sequence[int], validate=True,
-                    chunk: int = CHUNK) -> SnapshotGraph:
+                    chunk: int = CHUNK, cpos: bool = False) -> SnapshotGraph:
     """``build_graph`` on already-concatenated edges: ei [2, ΣE_g] int64 (local ids), snapshot g's edges in
     columns [e_ptr[g], e_ptr[g+1]) (the layout of ``ingest.SnapshotBatch``)."""
     require_hip(ei)
@@ -203,11 +200,11 @@ def build_graph_cat(ei: torch.Tensor, e_ptr: Sequence[int], node_counts: Sequenc
     meta = _ptr_table(dev, list(e_ptr) + n_ptr)
     edge_ptr, node_ptr = meta[:G + 1], meta[G + 1:]
     cap = E + N
-    buf = torch.empty(2 * (N + 1) + 4 * cap, dtype=torch.int32, device=dev)
+    buf = torch.empty(2 * (N + 1) + (4 if cpos else 3) * cap, dtype=torch.int32, device=dev)
     rowptr, csc_ptr = buf[:N + 1], buf[N + 1:2 * (N + 1)]
     o = 2 * (N + 1)
     col, csc_row, csc_eid = buf[o:o + cap], buf[o + cap:o + 2 * cap], buf[o + 2 * cap:o + 3 * cap]
-    cpos = buf[o + 3 * cap:o + 4 * cap]
+    cpos_t = buf[o + 3 * cap:o + 4 * cap] if cpos else None
     scal = torch.empty(2, dtype=torch.int64, device=dev)
     nnz = scal[0:1]
     err = scal[1:2].view(torch.int32)[:1]
@@ -216,10 +213,10 @@ def build_graph_cat(ei: torch.Tensor, e_ptr: Sequence[int], node_counts: Sequenc
     ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=dev)
     check(L.tagan_csr_build(ptr(ei), E, E, ptr(edge_ptr), ptr(node_ptr), G, N,
                             max(n_ptr[i + 1] - n_ptr[i] for i in range(G)), ptr(rowptr), ptr(col),
-                            ptr(csc_ptr), ptr(csc_row), ptr(csc_eid), ptr(nnz), ptr(err), ptr(cpos), ptr(ws),
-                            ws_bytes, stream_of(ei)), "tagan_csr_build")
+                            ptr(csc_ptr), ptr(csc_row), ptr(csc_eid), ptr(nnz), ptr(err),
+                            ptr(cpos_t) if cpos else None, ptr(ws), ws_bytes, stream_of(ei)), "tagan_csr_build")
     g = SnapshotGraph(N, rowptr, col, csc_ptr, csc_row, csc_eid, nnz, list(node_counts))
-    g.csr_cpos = cpos
+    g.csr_cpos = cpos_t
     if validate == "deferred":
         host = torch.empty(1, dtype=torch.int32, pin_memory=True)
         host.copy_(err, non_blocking=True)

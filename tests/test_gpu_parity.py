@@ -31,7 +31,7 @@ def _load(module, sd, dev):
 # ----------------------------------------------------------------------------- CSR builder
 def _check_csr(dev, counts, eis):
     from tagan_amd.kernels import build_graph
-    graph = build_graph([e.to(dev) for e in eis], counts)
+    graph = build_graph([e.to(dev) for e in eis], counts, cpos=True)
     nnz = graph.nnz_host()
     cols, off = [], 0
     rp_all = [0]
@@ -53,7 +53,7 @@ def _check_csr(dev, counts, eis):
     assert torch.equal(want_col[eid], ccol)
     same = ccol[1:] == ccol[:-1]
     assert torch.all(crow.diff()[same] > 0)
-    # the CSR -> CSC position map written by the same build: the inverse of csc_eid
+    # the CSR -> CSC position map written by the same build when asked for: the inverse of csc_eid
     cpos = graph.csr_cpos[:nnz].cpu().long()
     assert torch.equal(cpos[eid], torch.arange(nnz))
     return graph
