@@ -162,6 +162,28 @@ def _ptr_table(dev, values):
     return t
 
 
+def cat_adjacent(ts: Sequence[torch.Tensor], dim: int) -> torch.Tensor:
+    """torch.cat(ts, dim) -- as a zero-copy view when the pieces already lie back to back in one buffer along
+    ``dim`` (the layout of a batch generated or ingested in one allocation), else a real concatenation."""
+    if len(ts) == 1:
+        return ts[0]
+    t0 = ts[0]
+    ok = all(t.dtype == t0.dtype and t.device == t0.device and t.dim() == t0.dim() and t.stride() == t0.stride()
+             and t.untyped_storage().data_ptr() == t0.untyped_storage().data_ptr() for t in ts)
+    if ok:
+        off = t0.storage_offset()
+        for t in ts:
+            if t.storage_offset() != off or any(t.shape[d] != t0.shape[d] for d in range(t.dim()) if d != dim):
+                ok = False
+                break
+            off += t.shape[dim] * t.stride(dim)
+    if not ok:
+        return torch.cat(list(ts), dim)
+    size = list(t0.shape)
+    size[dim] = sum(int(t.shape[dim]) for t in ts)
+    return t0.as_strided(size, t0.stride(), t0.storage_offset())
+
+
 def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], validate=True,
                 chunk: int = CHUNK, cpos: bool = False) -> SnapshotGraph:
     """CSR/CSC of the block-diagonal union of snapshot adjacencies (+ self-loops, de-duplicated).
@@ -176,7 +198,7 @@ def build_graph(edge_indices: List[torch.Tensor], node_counts: Sequence[int], va
     """
     require_hip(*edge_indices)
     eis = [e.to(torch.int64) for e in edge_indices]
-    ei = torch.cat(eis, dim=1) if len(eis) > 1 else eis[0]
+    ei = cat_adjacent(eis, 1)
     e_ptr = [0]
     for e in eis:
         e_ptr.append(e_ptr[-1] + int(e.shape[1]))
@@ -189,8 +211,11 @@ def build_graph_cat(ei: torch.Tensor, e_ptr: Sequence[int], node_counts: Sequenc
     columns [e_ptr[g], e_ptr[g+1]) (the layout of ``ingest.SnapshotBatch``)."""
     require_hip(ei)
     dev = ei.device
-    ei = ei.to(torch.int64).contiguous()
+    ei = ei.to(torch.int64)
+    if ei.stride(1) != 1 or ei.stride(0) < ei.shape[1]:
+        ei = ei.contiguous()
     E = int(ei.shape[1])
+    ld = int(ei.stride(0))
     G = len(node_counts)
     assert len(e_ptr) == G + 1 and e_ptr[0] == 0 and e_ptr[-1] == E
     N = int(sum(node_counts))
@@ -211,7 +236,7 @@ def build_graph_cat(ei: torch.Tensor, e_ptr: Sequence[int], node_counts: Sequenc
     L = lib()
     ws_bytes = L.tagan_csr_build_workspace(E, N)
     ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=dev)
-    check(L.tagan_csr_build(ptr(ei), E, E, ptr(edge_ptr), ptr(node_ptr), G, N,
+    check(L.tagan_csr_build(ptr(ei), ld, E, ptr(edge_ptr), ptr(node_ptr), G, N,
                             max(n_ptr[i + 1] - n_ptr[i] for i in range(G)), ptr(rowptr), ptr(col),
                             ptr(csc_ptr), ptr(csc_row), ptr(csc_eid), ptr(nnz), ptr(err),
                             ptr(cpos_t) if cpos else None, ptr(ws), ws_bytes, stream_of(ei)), "tagan_csr_build")

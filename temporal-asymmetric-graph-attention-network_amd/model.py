@@ -27,7 +27,7 @@ import torch.nn.functional as F
 
 from .fused import precision as precision_ctx
 from .ingest import SnapshotBatch, unpack as _unpack
-from .kernels import build_graph, build_graph_cat, layer_norm, linear, pool_time_major
+from .kernels import build_graph, build_graph_cat, cat_adjacent, layer_norm, linear, pool_time_major
 from .layers.classification import ClassificationModule, TemporalLossModule, fused_head
 from .layers.graph_attention import TAGANGraphAttention
 from .layers.temporal_attention import AsymmetricTemporalAttention, MaskBroadcastError
@@ -112,7 +112,7 @@ class TAGAN(nn.Module):
                 xs.append(x.to(device))
                 eis.append(ei.to(device))
                 counts.append(int(x.shape[0]))
-            x_cat = torch.cat(xs, 0) if len(xs) > 1 else xs[0]
+            x_cat = cat_adjacent(xs, 0)   # a view when the snapshots share one buffer
             graph = build_graph(eis, counts, validate=self.validate_edges)
         h = linear(x_cat, self.node_embedding.weight, self.node_embedding.bias)
         skip = h

@@ -47,16 +47,22 @@ def make_sequence(name: str, device, seed: int = 42, snapshots: int = None,
     if kind == "social":
         ranks = torch.randperm(N, generator=g, device=device).to(torch.float32) + 1.0
         activity = ranks.pow(-1.1)
-    for _ in range(T):
-        x = torch.randn(N, F, generator=g, device=device)
+    # the snapshots' node features and edges are row / column slices of one [T·N, F] and one [2, T·E] buffer (the
+    # batched layout of ingest.SnapshotBatch), so the model's concatenations are views, not copies
+    x_all = torch.empty(T * N, F, device=device)
+    ei_all = torch.empty(2, T * E, dtype=torch.int64, device=device)
+    for t in range(T):
+        x = x_all[t * N:(t + 1) * N]
+        x.copy_(torch.randn(N, F, generator=g, device=device))
         if kind == "social":
             src = torch.multinomial(activity, E, replacement=True, generator=g)
             dst = torch.multinomial(activity, E, replacement=True, generator=g)
             ei = torch.stack([src, dst])
         else:
             ei = torch.randint(0, N, (2, E), generator=g, device=device)
+        ei_all[:, t * E:(t + 1) * E] = ei
         ea = torch.randn(E, De, generator=g, device=device)
-        seq.append((x, ei, ea, list(range(N)) if N <= 100_000 else torch.arange(N)))
+        seq.append((x, ei_all[:, t * E:(t + 1) * E], ea, list(range(N)) if N <= 100_000 else torch.arange(N)))
     return seq
 
 

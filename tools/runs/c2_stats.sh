@@ -9,4 +9,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/s
     python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-roofline --no-alt-precision --no-c1 \
     > $OUT/stats_c2.log 2>&1 || { tail -20 $OUT/stats_c2.log; exit 1; }
 find $OUT/stats_c2 -name "*kernel_trace*" -delete
-python tools/kstats.py $(find $OUT/stats_c2 -name "*kernel_stats.csv" | head -1) 7
+python tools/kstats.py $(find $OUT/stats_c2 -name "*kernel_stats.csv" | head -1)
