@@ -1889,7 +1889,46 @@ __device__ __forceinline__ void v5_static_bias(const TArgs& A, int h, int it, in
         }
 }
 
-template <int TT, int DT, typename S>
+// Fast path (MODE 1: no dropout, 2: dropout) for the common shape: T = TP, no causal flag, no keep-mask, no dense
+// bias (or dense-bias gradient).  Every element is then valid, so the per-element range / mask tests go; the
+// scores are kept in log2 units (log2 e folded into the 1/sqrt(d) scale and the staged bias table: one v_exp_f32
+// per element, no separate multiply); the dropout test is one integer compare of the element's hash against a
+// precomputed threshold -- the same decision as drop_u(...) >= p, bit for bit; the backward carries the keep bit
+// in the sign of the stored probability.  MODE 0 is the general path.
+constexpr float LOG2E_F = 1.4426950408889634f;
+constexpr float LN2_F = 0.6931471805599453f;
+
+// keep an element iff lowbias32(counter ^ key) >= drop_thr(p): (h >> 8) * 2^-24 >= p  <=>  (h >> 8) >= ceil(p 2^24)
+// (exact: p 2^24 is exact in fp32).  Valid for p < 1 - 2^-24 (the host takes MODE 0 otherwise).
+__host__ __device__ __forceinline__ uint32_t drop_thr(float p) {
+    return ((uint32_t)ceilf(p * 16777216.f)) << 8;
+}
+
+bool v5_fast_shape(int T, int TT, int causal, const void* mask, const void* bias_dense, const void* dbias_dense,
+                   float p_drop) {
+    return T == 16 * TT && !causal && !mask && !bias_dense && !dbias_dense &&
+           (p_drop <= 0.f || ceilf(p_drop * 16777216.f) < 16777216.f);
+}
+
+// log2-scaled bias-table values of the lane's elements (fast path: every element valid)
+template <int TT>
+__device__ __forceinline__ void v5_fast_bias(const TArgs& A, int h, int it, int c, int g, float (&bst)[TT][4]) {
+    const int T = A.T, i = it * 16 + c;
+#pragma unroll
+    for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            bst[jt][e] = A.bias_table ? A.bias_table[h * (2 * T - 1) + i - (jt * 16 + 4 * g + e) + T - 1] * LOG2E_F : 0.f;
+}
+
+// the head's table row staged REVERSED and log2-scaled (TT = 8): element (i, j) at Br[T - 1 - i + j], so a lane's
+// elements sit at one per-lane base + compile-time offsets (immediate-offset LDS reads)
+__device__ __forceinline__ void v5_stage_bias_rev(const TArgs& A, int h, float* Br, int nthreads) {
+    const int NB = 2 * A.T - 1;
+    for (int t = threadIdx.x; t < NB; t += nthreads) Br[t] = A.bias_table ? A.bias_table[h * NB + NB - 1 - t] * LOG2E_F : 0.f;
+}
+
+template <int TT, int DT, typename S, int MODE>
 __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float* __restrict__ q,
                                                             const float* __restrict__ k,
                                                             const float* __restrict__ v) {
@@ -1907,11 +1946,15 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
     const int64_t G = gridDim.x / A.heads;
     constexpr bool BREG = TT <= 4;   // as in k_tattn_bwd_v5: at TT = 8 the table row is read from LDS
     float bst[BREG ? TT : 1][4];
-    if constexpr (BREG) {
+    if constexpr (MODE != 0) {
+        if constexpr (BREG) v5_fast_bias<TT>(A, h, w, c0, g0, bst);
+        else v5_stage_bias_rev(A, h, Bt, WAVE * TT);
+    } else if constexpr (BREG) {
         v5_static_bias<TT>(A, h, w, c0, g0, bst);
     } else {
         for (int t = threadIdx.x; t < 2 * T - 1; t += WAVE * TT) Bt[t] = A.bias_table ? A.bias_table[h * (2 * T - 1) + t] : 0.f;
     }
+    const uint32_t thr = MODE == 2 ? drop_thr(A.p_drop) : 0u;
     f4v qv[DT], kv[DT], vv[DT];
     auto load = [&](int64_t rr) {
         const int i = w * 16 + c0;
@@ -1952,6 +1995,37 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
             }
         }
         const uint32_t drk = tkey(A, r, h);
+        float inv_l;
+        if constexpr (MODE != 0) {   // fast path: scores in log2 units, every element valid
+            const float sc2 = A.inv_sqrt_d * LOG2E_F;
+            const int rb = T - 1 - i + 4 * g;
+            float mx = -INFINITY;
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float b2 = BREG ? bst[jt][e] : Bt[rb + jt * 16 + e];
+                    const float sc = fmaf(s[jt][e], sc2, b2);
+                    s[jt][e] = sc;
+                    mx = fmaxf(mx, sc);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, WAVE));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, WAVE));
+            const uint32_t cb = (uint32_t)(i * T + 4 * g);   // dropout counter of element (jt, e): cb + 16 jt + e
+            float l = 0.f;
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float p = __builtin_amdgcn_exp2f(s[jt][e] - mx);
+                    l += p;
+                    s[jt][e] = (MODE == 2 && lowbias32((cb + (uint32_t)(jt * 16 + e)) ^ drk) < thr) ? 0.f : p;
+                }
+            l += __shfl_xor(l, 16, WAVE);
+            l += __shfl_xor(l, 32, WAVE);
+            inv_l = (MODE == 2 ? A.inv_keep : 1.f) / l;
+            if (g == 0) A.lse[(r * A.heads + h) * T + i] = (mx + __log2f(l)) * LN2_F;
+        } else {
         float mx = -INFINITY;
 #pragma unroll
         for (int jt = 0; jt < TT; ++jt)
@@ -1982,8 +2056,9 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
             }
         l += __shfl_xor(l, 16, WAVE);
         l += __shfl_xor(l, 32, WAVE);
-        const float inv_l = (l > 0.f) ? 1.f / l : NAN;
+        inv_l = (l > 0.f) ? 1.f / l : NAN;
         if (g == 0 && i < T) A.lse[(r * A.heads + h) * T + i] = mx + __logf(l);
+        }
         // Oᵀ = Vᵀ·P'ᵀ, two accumulator chains per feature tile
         f4v o[DT][2];
 #pragma unroll
@@ -2004,7 +2079,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
     }
 }
 
-template <int TT, int DT, typename S>
+template <int TT, int DT, typename S, int MODE>
 __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float* __restrict__ q,
                                                             const float* __restrict__ k,
                                                             const float* __restrict__ v,
@@ -2030,13 +2105,17 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
     // bias-table row is read from LDS per element instead
     constexpr bool BREG = TT <= 4;
     float bst[BREG ? TT : 1][4];
-    if constexpr (BREG) {
+    if constexpr (MODE != 0) {
+        if constexpr (BREG) v5_fast_bias<TT>(A, h, w, c0, g0, bst);
+        else v5_stage_bias_rev(A, h, Bt, WAVE * TT);   // (visible after the first unit's staging barrier)
+    } else if constexpr (BREG) {
         v5_static_bias<TT>(A, h, w, c0, g0, bst);
     } else {
         for (int t = threadIdx.x; t < NB; t += WAVE * TT) Bt[t] = A.bias_table ? A.bias_table[h * NB + t] : 0.f;
         // (visible to all waves after the first unit's staging barrier)
     }
     const float msc = A.p_drop > 0.f ? A.inv_keep : 1.f;
+    const uint32_t thr = MODE == 2 ? drop_thr(A.p_drop) : 0u;
     f4v gsum[TT];   // Σ over units of dSᵀ[jt tiles][query tile w]: the bias-table gradient before its diagonal sums
 #pragma unroll
     for (int jt = 0; jt < TT; ++jt) gsum[jt] = f4v{0.f, 0.f, 0.f, 0.f};
@@ -2098,6 +2177,41 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
         }
         if (r + G < A.rows) load(r + G);   // the next unit's rows in flight during the rest of this one
         const uint32_t drk = tkey(A, r, h);
+        if constexpr (MODE != 0) {   // fast path (see v5_fast_shape): log2 units, keep bit in the sign of P
+            const float sc2 = A.inv_sqrt_d * LOG2E_F, lse2 = lse_i * LOG2E_F;
+            const int rb = T - 1 - i + 4 * g;
+            const uint32_t cb = (uint32_t)(i * T + 4 * g);
+            float dl = 0.f;
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float b2 = BREG ? bst[jt][e] : Bt[rb + jt * 16 + e];
+                    const float p = __builtin_amdgcn_exp2f(fmaf(s[jt][e], sc2, b2) - lse2);
+                    float dpv = dp[jt][e];
+                    if constexpr (MODE == 2) {
+                        const bool kp = lowbias32((cb + (uint32_t)(jt * 16 + e)) ^ drk) >= thr;
+                        dpv = kp ? dpv * msc : 0.f;
+                        s[jt][e] = kp ? p : -p;
+                    } else {
+                        s[jt][e] = p;
+                    }
+                    dp[jt][e] = dpv;
+                    dl = fmaf(p, dpv, dl);
+                }
+            dl += __shfl_xor(dl, 16, WAVE);
+            dl += __shfl_xor(dl, 32, WAVE);
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float sv = s[jt][e];
+                    const float dsv = fabsf(sv) * (dp[jt][e] - dl);
+                    dp[jt][e] = dsv;
+                    if constexpr (MODE == 2) s[jt][e] = fmaxf(sv, 0.f) * msc;
+                    X[(jt * 16 + 4 * g + e) * LD + i] = dsv;   // dSᵀ[j][i]
+                }
+        } else {
         uint32_t keep = 0;   // bit jt*4 + e: element kept by the dropout
         float dl = 0.f;
 #pragma unroll
@@ -2134,6 +2248,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
                     A.dbias_dense[((r * A.heads + h) * T + i) * (int64_t)T + j] = dsv;
                 X[j * LD + i] = dsv;   // dSᵀ[j][i]
             }
+        }
         if (A.part) {
 #pragma unroll
             for (int jt = 0; jt < TT; ++jt) gsum[jt] += dp[jt];
@@ -2413,12 +2528,15 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
         const int TT = v5_tiles(T);
         const dim3 g5((unsigned)(v4_groups(rows) * heads));
         const size_t lds = v5_fwd_lds(TT, head_dim / 16);
-#define TAGAN_V5F(TTT, DDT) { auto kern = bf ? k_tattn_fwd_v5<TTT, DDT, bf16s> : k_tattn_fwd_v5<TTT, DDT, float>; \
+        const int mode = v5_fast_shape(T, TT, causal, mask, bias_dense, nullptr, p_drop) ? (p_drop > 0.f ? 2 : 1) : 0;
+#define TAGAN_V5F_M(TTT, DDT, MM) { auto kern = bf ? k_tattn_fwd_v5<TTT, DDT, bf16s, MM> : k_tattn_fwd_v5<TTT, DDT, float, MM>; \
                               rc = lds_optin(kern, lds); if (rc) return rc; kern<<<g5, WAVE * TTT, lds, s>>>(A, qf, kf, vf); }
+#define TAGAN_V5F(TTT, DDT) { if (mode == 2) TAGAN_V5F_M(TTT, DDT, 2) else if (mode == 1) TAGAN_V5F_M(TTT, DDT, 1) else TAGAN_V5F_M(TTT, DDT, 0) }
 #define TAGAN_V5F_D(TTT) if (head_dim == 16) TAGAN_V5F(TTT, 1) else TAGAN_V5F(TTT, 2)
         if (TT == 2) TAGAN_V5F_D(2) else if (TT == 4) TAGAN_V5F_D(4) else TAGAN_V5F_D(8)
 #undef TAGAN_V5F_D
 #undef TAGAN_V5F
+#undef TAGAN_V5F_M
         TAGAN_CHECK_LAUNCH("temporal_attn_fwd_v5");
         return TAGAN_OK;
     }
@@ -2570,12 +2688,15 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
         const int64_t G5 = v4_groups(rows);   // <= nblk: the workspace rows
         const dim3 g5((unsigned)(G5 * heads));
         const size_t lds = v5_bwd_lds(TT, head_dim / 16);
-#define TAGAN_V5B(TTT, DDT) { auto kern = bf ? k_tattn_bwd_v5<TTT, DDT, bf16s> : k_tattn_bwd_v5<TTT, DDT, float>; \
+        const int mode = v5_fast_shape(T, TT, causal, mask, bias_dense, dbias_dense, p_drop) ? (p_drop > 0.f ? 2 : 1) : 0;
+#define TAGAN_V5B_M(TTT, DDT, MM) { auto kern = bf ? k_tattn_bwd_v5<TTT, DDT, bf16s, MM> : k_tattn_bwd_v5<TTT, DDT, float, MM>; \
                               rc = lds_optin(kern, lds); if (rc) return rc; kern<<<g5, WAVE * TTT, lds, s>>>(A, qf, kf, vf, df, lse); }
+#define TAGAN_V5B(TTT, DDT) { if (mode == 2) TAGAN_V5B_M(TTT, DDT, 2) else if (mode == 1) TAGAN_V5B_M(TTT, DDT, 1) else TAGAN_V5B_M(TTT, DDT, 0) }
 #define TAGAN_V5B_D(TTT) if (head_dim == 16) TAGAN_V5B(TTT, 1) else TAGAN_V5B(TTT, 2)
         if (TT == 2) TAGAN_V5B_D(2) else if (TT == 4) TAGAN_V5B_D(4) else TAGAN_V5B_D(8)
 #undef TAGAN_V5B_D
 #undef TAGAN_V5B
+#undef TAGAN_V5B_M
         TAGAN_CHECK_LAUNCH("temporal_attn_bwd_v5");
         if (dbias_table) {
             const int n = heads * (2 * T - 1);
