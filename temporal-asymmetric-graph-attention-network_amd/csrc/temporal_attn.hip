@@ -1996,6 +1996,9 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
         }
         const uint32_t drk = tkey(A, r, h);
         float inv_l;
+        f4v o[DT][2];   // Oᵀ, two accumulator chains per feature tile
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt][0] = o[dt][1] = f4v{0.f, 0.f, 0.f, 0.f};
         if constexpr (MODE != 0) {   // fast path: scores in log2 units, every element valid
             const float sc2 = A.inv_sqrt_d * LOG2E_F;
             const int rb = T - 1 - i + 4 * g;
@@ -2013,14 +2016,34 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
             mx = fmaxf(mx, __shfl_xor(mx, 32, WAVE));
             const uint32_t cb = (uint32_t)(i * T + 4 * g);   // dropout counter of element (jt, e): cb + 16 jt + e
             float l = 0.f;
-#pragma unroll
-            for (int jt = 0; jt < TT; ++jt)
+            auto soft = [&](int jt) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const float p = __builtin_amdgcn_exp2f(s[jt][e] - mx);
                     l += p;
                     s[jt][e] = (MODE == 2 && lowbias32((cb + (uint32_t)(jt * 16 + e)) ^ drk) < thr) ? 0.f : p;
                 }
+            };
+            // Oᵀ = Vᵀ·P'ᵀ: the products of key tile jt issued between the softmax instructions of tile jt+1
+            soft(0);
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt) {
+                if (jt + 1 < TT) soft(jt + 1);
+#pragma unroll
+                for (int dt = 0; dt < DT; ++dt) {
+                    const f4v va = lds4(Vt + (dt * 16 + c) * LT + jt * 16 + 4 * g);   // V[16jt + 4g + e][16dt + c]
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[dt][jt & 1] = mfma4(va[e], s[jt][e], o[dt][jt & 1]);
+                }
+                if (jt + 1 < TT) {
+#pragma unroll
+                    for (int k2 = 0; k2 < 4 * DT; ++k2) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
             l += __shfl_xor(l, 16, WAVE);
             l += __shfl_xor(l, 32, WAVE);
             inv_l = (MODE == 2 ? A.inv_keep : 1.f) / l;
@@ -2058,11 +2081,6 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
         l += __shfl_xor(l, 32, WAVE);
         inv_l = (l > 0.f) ? 1.f / l : NAN;
         if (g == 0 && i < T) A.lse[(r * A.heads + h) * T + i] = mx + __logf(l);
-        }
-        // Oᵀ = Vᵀ·P'ᵀ, two accumulator chains per feature tile
-        f4v o[DT][2];
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) o[dt][0] = o[dt][1] = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
@@ -2071,6 +2089,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
 #pragma unroll
                 for (int e = 0; e < 4; ++e) o[dt][jt & 1] = mfma4(va[e], s[jt][e], o[dt][jt & 1]);
             }
+        }
         if (i < T) {
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt)
