@@ -846,8 +846,15 @@ def main():
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        # every graph is closed (GraphedStep.close: reset before the process group goes), so the ranks only meet
+        # once more and leave.  No destroy_process_group: tearing an RCCL group down after graphs that captured
+        # its collectives aborted the process in a test run (rc 134 after the results were out), and a rank's
+        # exit code is what torchrun reports -- the ranks sync the device, flush and exit directly instead.
+        dist.barrier(group=ctl)
+        torch.cuda.synchronize()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

@@ -947,6 +947,27 @@ constexpr int v4_ld(int TP) { return TP + 8; }
 size_t v4_fwd_lds(int TT, int DT) { return (size_t)(16 * DT * v4_ld(16 * TT)) * 4; }
 size_t v4_bwd_lds(int TT, int DT) { return (size_t)(16 * TT * v4_ld(16 * TT) + 3 * 16 * DT * v4_ld(16 * TT)) * 4; }
 
+// Fast path (MODE 1: no dropout, 2: dropout) for the common shape: T = TP, no causal flag, no keep-mask, no dense
+// bias (or dense-bias gradient).  Every element is then valid, so the per-element range / mask tests go; the
+// scores are kept in log2 units (log2 e folded into the 1/sqrt(d) scale and the staged bias table: one v_exp_f32
+// per element, no separate multiply); the dropout test is one integer compare of the element's hash against a
+// precomputed threshold -- the same decision as drop_u(...) >= p, bit for bit; the backward carries the keep bit
+// in the sign of the stored probability.  MODE 0 is the general path.
+constexpr float LOG2E_F = 1.4426950408889634f;
+constexpr float LN2_F = 0.6931471805599453f;
+
+// keep an element iff lowbias32(counter ^ key) >= drop_thr(p): (h >> 8) * 2^-24 >= p  <=>  (h >> 8) >= ceil(p 2^24)
+// (exact: p 2^24 is exact in fp32).  Valid for p < 1 - 2^-24 (the host takes MODE 0 otherwise).
+__host__ __device__ __forceinline__ uint32_t drop_thr(float p) {
+    return ((uint32_t)ceilf(p * 16777216.f)) << 8;
+}
+
+bool v5_fast_shape(int T, int TT, int causal, const void* mask, const void* bias_dense, const void* dbias_dense,
+                   float p_drop) {
+    return T == 16 * TT && !causal && !mask && !bias_dense && !dbias_dense &&
+           (p_drop <= 0.f || ceilf(p_drop * 16777216.f) < 16777216.f);
+}
+
 // The unit-invariant part of the score of the lane's elements (i = it*16 + c, j = jt*16 + 4g + e):
 // the head's bias-table value, or -inf outside [0, T)² and above the diagonal when causal.  A wave
 // keeps one head, so this lives in registers for the whole kernel (no per-element table lookup).
@@ -962,6 +983,21 @@ __device__ __forceinline__ void v4_static_bias(const TArgs& A, int h, int c, int
                 const int i = it * 16 + c, j = jt * 16 + 4 * g + e;
                 const bool ok = i < T && j < T && !(A.causal && j > i);
                 bst[jt][it][e] = ok ? (A.bias_table ? A.bias_table[h * NB + i - j + T - 1] : 0.f) : -INFINITY;
+            }
+}
+
+// fast path (v5_fast_shape): the log2-scaled table values, every element valid
+template <int TT>
+__device__ __forceinline__ void v4_fast_bias(const TArgs& A, int h, int c, int g, float (&bst)[TT][TT][4]) {
+    const int T = A.T, NB = 2 * T - 1;
+#pragma unroll
+    for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+        for (int it = 0; it < TT; ++it)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int i = it * 16 + c, j = jt * 16 + 4 * g + e;
+                bst[jt][it][e] = A.bias_table ? A.bias_table[h * NB + i - j + T - 1] * LOG2E_F : 0.f;
             }
 }
 
@@ -1119,7 +1155,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_F) k_tattn_fwd_v4(TArgs A, 
     }
 }
 
-template <int TT, int DT, typename S>
+template <int TT, int DT, typename S, int MODE>
 __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, const float* __restrict__ q,
                                                        const float* __restrict__ k,
                                                        const float* __restrict__ v,
@@ -1139,8 +1175,10 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
     float* Qt = Kt + DP * LD;    // [DP][LD] Q transposed
     float* Ot = Qt + DP * LD;    // [DP][LD] dO transposed
     float bst[TT][TT][4];
-    v4_static_bias<TT>(A, h, c0, g0, bst);
+    if constexpr (MODE != 0) v4_fast_bias<TT>(A, h, c0, g0, bst);
+    else v4_static_bias<TT>(A, h, c0, g0, bst);
     const float msc = A.p_drop > 0.f ? A.inv_keep : 1.f;   // drop_scale of a kept element
+    const uint32_t thr = MODE == 2 ? drop_thr(A.p_drop) : 0u;
     // Σ of dSᵀ over this wave's units, in unit order: the bias-table gradient before its diagonal
     // sums, which run once at the end (fixed order: bitwise reproducible)
     f4v gsum[TT][TT];
@@ -1235,6 +1273,42 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
         }   // next unit's rows in flight during this one
         // P = exp(S - lse); dP·m (m = drop_scale); delta_i = Σ_j P·dP·m (= Σ_c dO∘O, so O is not read);
         // dS = P·(dP·m - delta); P' = P·m
+        if constexpr (MODE != 0) {   // fast path (v5_fast_shape): log2 units, keep bit in the sign of P
+            const float sc2 = A.inv_sqrt_d * LOG2E_F;
+#pragma unroll
+            for (int it = 0; it < TT; ++it) {
+                const int i = it * 16 + c;
+                const float lse2 = lse_i[it] * LOG2E_F;
+                const uint32_t cb = (uint32_t)(i * T + 4 * g);
+                float dl = 0.f;
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float p = __builtin_amdgcn_exp2f(fmaf(s[jt][it][e], sc2, bst[jt][it][e]) - lse2);
+                        float dpv = dp[jt][it][e];
+                        if constexpr (MODE == 2) {
+                            const bool kp = lowbias32((cb + (uint32_t)(jt * 16 + e)) ^ drk) >= thr;
+                            dpv = kp ? dpv * msc : 0.f;
+                            s[jt][it][e] = kp ? p : -p;
+                        } else {
+                            s[jt][it][e] = p;
+                        }
+                        dp[jt][it][e] = dpv;
+                        dl = fmaf(p, dpv, dl);
+                    }
+                dl += __shfl_xor(dl, 16, WAVE);
+                dl += __shfl_xor(dl, 32, WAVE);
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float sv = s[jt][it][e];
+                        dp[jt][it][e] = fabsf(sv) * (dp[jt][it][e] - dl);
+                        if constexpr (MODE == 2) s[jt][it][e] = fmaxf(sv, 0.f) * msc;
+                    }
+            }
+        } else {
         uint32_t keep = 0;   // bit (jt*TT + it)*4 + e: element kept by the dropout
 #pragma unroll
         for (int it = 0; it < TT; ++it) {
@@ -1267,6 +1341,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
                     if (A.dbias_dense && i < T && j < T)
                         A.dbias_dense[((r * A.heads + h) * T + i) * (int64_t)T + j] = dsv;
                 }
+        }
         }
         if (A.part) {
 #pragma unroll
@@ -1887,27 +1962,6 @@ __device__ __forceinline__ void v5_static_bias(const TArgs& A, int h, int it, in
             const bool ok = i < T && j < T && !(A.causal && j > i);
             bst[jt][e] = ok ? (A.bias_table ? A.bias_table[h * NB + i - j + T - 1] : 0.f) : -INFINITY;
         }
-}
-
-// Fast path (MODE 1: no dropout, 2: dropout) for the common shape: T = TP, no causal flag, no keep-mask, no dense
-// bias (or dense-bias gradient).  Every element is then valid, so the per-element range / mask tests go; the
-// scores are kept in log2 units (log2 e folded into the 1/sqrt(d) scale and the staged bias table: one v_exp_f32
-// per element, no separate multiply); the dropout test is one integer compare of the element's hash against a
-// precomputed threshold -- the same decision as drop_u(...) >= p, bit for bit; the backward carries the keep bit
-// in the sign of the stored probability.  MODE 0 is the general path.
-constexpr float LOG2E_F = 1.4426950408889634f;
-constexpr float LN2_F = 0.6931471805599453f;
-
-// keep an element iff lowbias32(counter ^ key) >= drop_thr(p): (h >> 8) * 2^-24 >= p  <=>  (h >> 8) >= ceil(p 2^24)
-// (exact: p 2^24 is exact in fp32).  Valid for p < 1 - 2^-24 (the host takes MODE 0 otherwise).
-__host__ __device__ __forceinline__ uint32_t drop_thr(float p) {
-    return ((uint32_t)ceilf(p * 16777216.f)) << 8;
-}
-
-bool v5_fast_shape(int T, int TT, int causal, const void* mask, const void* bias_dense, const void* dbias_dense,
-                   float p_drop) {
-    return T == 16 * TT && !causal && !mask && !bias_dense && !dbias_dense &&
-           (p_drop <= 0.f || ceilf(p_drop * 16777216.f) < 16777216.f);
 }
 
 // log2-scaled bias-table values of the lane's elements (fast path: every element valid)
@@ -2735,11 +2789,14 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
         const int64_t G4 = v4_groups(rows);   // <= nblk: the workspace rows
         const dim3 g4((unsigned)(G4 * heads));
         const size_t lds = v4_bwd_lds(TT, head_dim / 16);
-#define TAGAN_V4B(TTT, DDT) (bf ? k_tattn_bwd_v4<TTT, DDT, bf16s> : k_tattn_bwd_v4<TTT, DDT, float>)<<<g4, WAVE, lds, s>>>(A, qf, kf, vf, df, lse)
+        const int mode4 = v5_fast_shape(T, TT, causal, mask, bias_dense, dbias_dense, p_drop) ? (p_drop > 0.f ? 2 : 1) : 0;
+#define TAGAN_V4B_M(TTT, DDT, MM) (bf ? k_tattn_bwd_v4<TTT, DDT, bf16s, MM> : k_tattn_bwd_v4<TTT, DDT, float, MM>)<<<g4, WAVE, lds, s>>>(A, qf, kf, vf, df, lse)
+#define TAGAN_V4B(TTT, DDT) { if (mode4 == 2) TAGAN_V4B_M(TTT, DDT, 2); else if (mode4 == 1) TAGAN_V4B_M(TTT, DDT, 1); else TAGAN_V4B_M(TTT, DDT, 0); }
 #define TAGAN_V4B_D(TTT) if (head_dim == 16) { TAGAN_V4B(TTT, 1); } else { TAGAN_V4B(TTT, 2); }
         if (TT == 1) { TAGAN_V4B_D(1) } else { TAGAN_V4B_D(2) }
 #undef TAGAN_V4B_D
 #undef TAGAN_V4B
+#undef TAGAN_V4B_M
         TAGAN_CHECK_LAUNCH("temporal_attn_bwd_v4");
         if (dbias_table) {
             const int n = heads * (2 * T - 1);

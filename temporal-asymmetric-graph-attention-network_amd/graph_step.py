@@ -58,8 +58,11 @@ class GraphedStep:
             optimizer.zero_grad(set_to_none=True)
         self.graph = torch.cuda.CUDAGraph()
         # captured on the warm-up stream: autograd nodes that outlive a warm-up step (a loss the caller kept,
-        # AccumulateGrad nodes) then belong to the capture stream, so the backward adds no cross-stream join
-        with torch.cuda.graph(self.graph, stream=side):
+        # AccumulateGrad nodes) then belong to the capture stream, so the backward adds no cross-stream join.
+        # thread_local capture: another thread's runtime calls during the capture (the RCCL process group's
+        # watchdog polling its work events) must not invalidate it -- under the default "global" mode such a
+        # poll aborted the process mid-capture when a process group was live
+        with torch.cuda.graph(self.graph, stream=side, capture_error_mode="thread_local"):
             s = torch.cuda.current_stream(dev)
             check(lib().tagan_seed_counter_step(ptr(self.counter), ctypes.c_void_p(s.cuda_stream)),
                   "tagan_seed_counter_step")
@@ -70,9 +73,13 @@ class GraphedStep:
         return self.loss
 
     def close(self) -> None:
-        """Unregister the seed counter (eager launches use their seeds as passed again)."""
+        """Unregister the seed counter (eager launches use their seeds as passed again) and destroy the graph now
+        (not at garbage collection): a captured RCCL collective must not outlive its process group."""
         lib().tagan_set_seed_counter(None)
         if self.prev_validate is not None:
             self.model.validate_edges = self.prev_validate
+        if self.graph is not None:
+            torch.cuda.synchronize(self.dev)
+            self.graph.reset()
         self.graph = None
         self.loss = None   # releases the captured step's autograd graph (its AccumulateGrad nodes)

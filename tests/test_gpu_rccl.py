@@ -5,8 +5,15 @@ This test makes the RCCL calls themselves run once on the device — the snapsho
 (`sharded._all_to_all`, all_to_all_single on device buffers), the pooling all-reduce, and both gradient
 buckets (`GradBucket.allreduce_mean`, `ShardGradSync.sync`, forced at world size 1) — and checks that a
 one-rank collective leaves every value exactly as the unsharded model computed it (sum over one rank = identity).
+
+Each case runs in a child process (``python tests/test_gpu_rccl.py <case>``) that leaves with os._exit(0) once its
+checks pass, without tearing the RCCL process group down: destroying a group after a HIP graph captured its
+collectives aborted the process in a suite run (bench.py's N > 1 exit does the same).  The parent test asserts
+the child's exit status and its completion marker.
 """
 import os
+import subprocess
+import sys
 
 import pytest
 import torch
@@ -29,7 +36,7 @@ def _setup(dev):
     return model, seq
 
 
-def test_rccl_world1_shard_and_buckets():
+def _case_shard_and_buckets():
     import tagan_amd  # noqa: F401
     from tagan_amd.distributed import GradBucket
     from tagan_amd.sharded import ShardGradSync, SnapshotShardedTAGAN, _all_to_all
@@ -130,27 +137,57 @@ def _init_nccl(dev, tag):
     dist.init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1)
 
 
-def test_rccl_world1_graph_step_small():
+def _case_graph_step_small():
     import tagan_amd  # noqa: F401
     from tagan_amd import synthetic
     dev = torch.device("cuda:0")
     _init_nccl(dev, "gs")
-    try:
-        seq = synthetic.make_sequence("c2", dev, seed=7, snapshots=6, nodes=400, edges=3000)
-        _graph_vs_eager(dev, seq)
-    finally:
-        dist.destroy_process_group()
+    seq = synthetic.make_sequence("c2", dev, seed=7, snapshots=6, nodes=400, edges=3000)
+    _graph_vs_eager(dev, seq)
 
 
-def test_rccl_world1_graph_step_c2():
+def _case_graph_step_c2():
     """The same at the full C2 workload (10k nodes, 100k Zipf edges per snapshot, 32 snapshots): the size at which
     the round-2 split capture (an eager all-reduce between two captured segments) faulted on replay."""
     import tagan_amd  # noqa: F401
     from tagan_amd import synthetic
     dev = torch.device("cuda:0")
     _init_nccl(dev, "gc2")
-    try:
-        seq = synthetic.make_sequence("c2", dev, seed=1000)
-        _graph_vs_eager(dev, seq, steps_eager=7, replays=4)
-    finally:
-        dist.destroy_process_group()
+    seq = synthetic.make_sequence("c2", dev, seed=1000)
+    _graph_vs_eager(dev, seq, steps_eager=7, replays=4)
+
+
+CASES = {"shard_and_buckets": _case_shard_and_buckets, "graph_step_small": _case_graph_step_small,
+         "graph_step_c2": _case_graph_step_c2}
+OK = "RCCL_CASE_OK"
+
+
+def _run_case(name, timeout=240):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), name], capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    tail = (p.stdout[-3000:] + "\n" + p.stderr[-3000:])
+    assert p.returncode == 0 and OK in p.stdout, "case %s: rc %s\n%s" % (name, p.returncode, tail)
+
+
+def test_rccl_world1_shard_and_buckets():
+    _run_case("shard_and_buckets")
+
+
+def test_rccl_world1_graph_step_small():
+    _run_case("graph_step_small")
+
+
+def test_rccl_world1_graph_step_c2():
+    """The graph-step case at the full C2 workload (10k nodes, 100k Zipf edges per snapshot, 32 snapshots): the size
+    at which the round-2 split capture (an eager all-reduce between two captured segments) faulted on replay."""
+    _run_case("graph_step_c2", timeout=280)
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    CASES[sys.argv[1]]()
+    torch.cuda.synchronize()
+    print(OK, flush=True)
+    sys.stderr.flush()
+    os._exit(0)
