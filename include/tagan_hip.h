@@ -332,6 +332,31 @@ int tagan_proj_ln_bwd(int64_t M, int32_t H, int32_t K, const float* da, const fl
                       float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Streaming projection GEMMs on the bf16 matrix cores (csrc/stream_gemm.hip).  Replace the q/k/v and out Linears
+ * of every attention block and their backward (geometric_attention.py:541-596, temporal_attention.py:985-1200:
+ * the nn.Linear forwards, input gradients and weight / bias gradients autograd derives for them).
+ * planes = 3: fp32 operands, each split into three bf16 planes (x = x0 + x1 + x2, RN), six plane products kept
+ *             (terms >= 2^-16 relative), fp32 accumulate: fp32-GEMM accuracy;  planes = 1: bf16 operands.
+ * tagan_sgemm_wprep: B[n][k] = kmajor ? w[k*ldw + n] : w[n*ldw + k] (fp32, N % 16 == 0, K % 32 == 0) ->
+ *   wp, N*K*planes bf16 in MFMA fragment order (the weight operand of tagan_sgemm_nt).
+ * tagan_sgemm_nt:  c[M, N] = a[M, K] · Bᵀ (+ bias[N], fp32, may be NULL); a / c storage TAGAN_F32 or TAGAN_BF16
+ *   (bf16 a needs planes = 1); rows 16-byte aligned.  Shapes: tagan_sgemm_supported.
+ * tagan_sgemm_tn:  dw[n*lddw + k] = Σ_m dy[m][n]·x[m][k] and db[n] = Σ_m dy[m][n] (either output may be NULL),
+ *   dy [M, N], x [M, K] of one storage dtype; workspace tagan_sgemm_tn_workspace bytes; fixed-order reduction
+ *   (bitwise reproducible).  Shapes: tagan_sgemm_tn_supported.
+ * ------------------------------------------------------------------------- */
+int tagan_sgemm_supported(int32_t N, int32_t K, int32_t planes, int32_t a_dtype, int32_t c_dtype);
+int tagan_sgemm_tn_supported(int32_t N, int32_t K, int32_t planes, int32_t dtype);
+int tagan_sgemm_wprep(int32_t N, int32_t K, const float* w, int64_t ldw, int32_t kmajor, int32_t planes, void* wp,
+                      void* stream);
+int tagan_sgemm_nt(int32_t a_dtype, int32_t c_dtype, int64_t M, int32_t N, int32_t K, const void* a, int64_t lda,
+                   const void* wp, int32_t planes, const float* bias, void* c, int64_t ldc, void* stream);
+size_t tagan_sgemm_tn_workspace(int64_t M, int32_t N, int32_t K);
+int tagan_sgemm_tn(int32_t dtype, int64_t M, int32_t N, int32_t K, const void* dy, int64_t ldy, const void* x,
+                   int64_t ldx, int32_t planes, float* dw, int64_t lddw, float* db, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Fused classification head + loss (csrc/head.hip).  Replaces model.py:377-459 after the pooling:
  * graph_features [B, T, H] (row 0 = x0 [T, H], rows 1..B-1 zero, model.py:382-394) ->
  * attention pooling over T (classification.py:912-925: s_t = w2·tanh(W1 x_t + b1), softmax over T,

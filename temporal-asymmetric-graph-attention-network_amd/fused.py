@@ -23,6 +23,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import check, lib, ptr, require_hip, stream_of
+from . import stream_gemm as sg
 from .kernels import TemporalMask, _geo_fwd, colsum, split_rows, weight_grad
 
 
@@ -247,6 +248,28 @@ def _wgrad(dy, x, bf, rows: int = 2048):
 
 
 # ----------------------------------------------------------------------------- the fused block
+# TAGAN_SGEMM=0: the projection GEMMs through torch (hipBLASLt / rocBLAS) instead of the hand-written
+# bf16-matrix-core kernels of csrc/stream_gemm.hip (fp32 mode: three-plane split operands; A/B knob).
+SGEMM = os.environ.get("TAGAN_SGEMM", "1") != "0"
+_SG_OK = {}
+
+
+def _sg_use(H: int, bf: bool, act: bool) -> bool:
+    """The block's six projection products all have a stream_gemm kernel at this H / precision."""
+    if not SGEMM:
+        return False
+    key = (H, bf, act)
+    ok = _SG_OK.get(key)
+    if ok is None:
+        P = 1 if bf else 3
+        ad = torch.bfloat16 if act else torch.float32
+        f32 = torch.float32
+        ok = _SG_OK[key] = (sg.supported(3 * H, H, P, ad, ad) and sg.supported(H, H, P, ad, f32) and
+                            sg.supported(H, H, P, ad, ad) and sg.supported(H, 3 * H, P, ad, f32) and
+                            sg.tn_supported(3 * H, H, P, ad) and sg.tn_supported(H, H, P, ad))
+    return ok
+
+
 # TAGAN_QKV_PACK=0: torch.cat of the q/k/v parameters per block instead of PackQKVFn's one-launch pack (A/B)
 QKV_PACK = os.environ.get("TAGAN_QKV_PACK", "1") != "0"
 # TAGAN_QKV_AUG=0: QKV GEMM with the hipBLASLt bias epilogue instead of the bias-as-weight-column form (A/B)
@@ -406,6 +429,9 @@ class AttnBlockFn(torch.autograd.Function):
         bf = _PREC != "fp32"          # bf16 GEMM operands
         act = _PREC == "bf16"         # bf16 activations between kernels
         proj = _proj_ok(H, bf)
+        if not proj and _sg_use(H, bf, act):
+            return AttnBlockFn._fwd_sgemm(ctx, x, x2, H, bf, act, p1, p2, ln1_w, ln1_b, w_qkv, b_qkv, w_o, b_o,
+                                          ln2_w, ln2_b, core, eps1, eps2, p_out, seed_out, lns_w, lns_b, eps_s, sink)
         if proj and "qkv" in PROJ_SET:
             w_qkv, b_qkv = w_qkv.contiguous(), b_qkv.contiguous()
             qkv, h_aug, mean1, rstd1 = proj_ln_qkv(x2, ln1_w, ln1_b, eps1, w_qkv, b_qkv,
@@ -458,7 +484,64 @@ class AttnBlockFn(torch.autograd.Function):
         return y.view(x.shape)
 
     @staticmethod
+    def _fwd_sgemm(ctx, x, x2, H, bf, act, p1, p2, ln1_w, ln1_b, w_qkv, b_qkv, w_o, b_o, ln2_w, ln2_b, core, eps1,
+                   eps2, p_out, seed_out, lns_w, lns_b, eps_s, sink):
+        """The block with its four forward / input-gradient products on k_sgemm_nt and its two weight-gradient
+        products on k_sgemm_tn (csrc/stream_gemm.hip); LayerNorm, core and dropout as in the library form."""
+        P = 1 if bf else 3
+        adt = torch.bfloat16 if act else torch.float32
+        h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False, y_dtype=adt)
+        qkv = sg.nt(h, sg.wprep(w_qkv, False, P), 3 * H, P, bias=b_qkv.contiguous(), out_dtype=adt)
+        c, saved = core.fwd(qkv, p1, p2)
+        o = sg.nt(c, sg.wprep(w_o, False, P), H, P)          # the bias is added in the closing LayerNorm
+        skip = None
+        if lns_w is not None:
+            y, s2, mean2, rstd2, skip = ln_skip_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, lns_w, lns_b, eps_s,
+                                                    a_bias=b_o)
+        else:
+            y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True, a_bias=b_o)
+        ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
+        ctx.inter = (h, None, mean1, rstd1, qkv, c, c, saved, s2, mean2, rstd2, skip)
+        ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, "sgemm")
+        ctx.sink = sink
+        ctx.packed_aug = False
+        return y.view(x.shape)
+
+    @staticmethod
+    def _bwd_sgemm(ctx, dy):
+        x2, ln1_w, w_qkv, w_o, ln2_w, lns_w = ctx.saved_tensors
+        h, _, mean1, rstd1, qkv, c, _, saved, s2, mean2, rstd2, skip = ctx.inter
+        core, p_out, seed_out, shape, bf, act, _ = ctx.cfg
+        ng = ctx.needs_input_grad
+        H = shape[-1]
+        P = 1 if bf else 3
+        adt = torch.bfloat16 if act else torch.float32
+        dy2 = dy.reshape(-1, H).contiguous()
+        dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True,
+                                         da_dtype=adt)
+        dgs = dbs = None
+        if skip is not None:
+            dres, _, dgs, dbs, _ = ln_bwd(x2, skip[0], skip[1], lns_w, dy2, dres, 0.0, 0, True, False, False)
+        dc = sg.nt(do, sg.wprep(w_o, True, P), H, P, out_dtype=adt)
+        dw_o = sg.tn(do, c, P, want_db=False)[0] if ng[7] else None
+        dqkv, dp1, dp2, db_core = core.bwd(qkv, c, saved, dc, ng[1], ng[2], want_bias_sum=bool(ng[6]))
+        del dc, do
+        dw_qkv = db_qkv = None
+        if ng[5] or (ng[6] and db_core is None):
+            dw_qkv, db_qkv = sg.tn(dqkv, h, P, want_dw=bool(ng[5]), want_db=bool(ng[6]) and db_core is None)
+        if db_core is not None:
+            db_qkv = db_core
+        dh = sg.nt(dqkv, sg.wprep(w_qkv, True, P), H, P)
+        del dqkv
+        dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
+        ctx.inter = None
+        return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
+                None, None, None, None, None, dgs, dbs, None, None, None)
+
+    @staticmethod
     def backward(ctx, dy):
+        if ctx.cfg[-1] == "sgemm":
+            return AttnBlockFn._bwd_sgemm(ctx, dy)
         x2, ln1_w, w_qkv, w_o, ln2_w, lns_w = ctx.saved_tensors
         h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip = ctx.inter
         core, p_out, seed_out, shape, bf, act, proj = ctx.cfg
@@ -568,7 +651,8 @@ def attention_block(x, core, p1: Optional[torch.Tensor], p2: Optional[torch.Tens
     H = q_lin.weight.shape[1]
     w_aug = None
     if QKV_PACK and x.is_cuda and q_lin.weight.dtype == torch.float32 and not WGRAD_ASYNC:
-        aug = QKV_AUG and _PREC == "fp32" and not (_proj_ok(H, False) and "qkv" in PROJ_SET)
+        aug = (QKV_AUG and _PREC == "fp32" and not (_proj_ok(H, False) and "qkv" in PROJ_SET) and
+               not (x.shape[-1] == H and _sg_use(H, False, False)))
         w_qkv, b_qkv, w_aug = PackQKVFn.apply(q_lin.weight, k_lin.weight, v_lin.weight, q_lin.bias, k_lin.bias,
                                               v_lin.bias, aug)
     else:
