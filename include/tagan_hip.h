@@ -356,6 +356,39 @@ int tagan_sgemm_tn(int32_t dtype, int64_t M, int32_t N, int32_t K, const void* d
                    int64_t ldx, int32_t planes, float* dw, int64_t lddw, float* db, void* workspace,
                    size_t workspace_bytes, void* stream);
 
+/* LayerNorm-fused forms of the same kernels (H = 128; each replaces one standalone k_ln_fwd / k_ln_bwd pass of an
+ * attention block: geometric_attention.py:541-542 / 586-596, temporal_attention.py:985-986 / 1190-1200).
+ * tagan_sgemm_ln_supported: op 1 = tagan_sgemm_nt_ln_in + tagan_sgemm_tn_ln, 2 = tagan_sgemm_nt_ln_out,
+ *   3 = tagan_sgemm_nt_ln_bwd exist for (H, planes, activation storage act_dtype).
+ * tagan_sgemm_nt_ln_in:  c = LN(x)·Bᵀ + bias, LN(x) = (x - mean) rstd ln_g + ln_b computed in the GEMM's prologue
+ *   (x fp32 [M, K = H]); the row statistics go to mean / rstd [M]; LN(x) itself is not stored.
+ * tagan_sgemm_tn_ln:     the weight gradient dyᵀ·LN(x) (+ Σ dy) with LN(x) recomputed from x and the forward's
+ *   statistics, bitwise as the prologue made it (x fp32; dy in dtype).
+ * tagan_sgemm_nt_ln_out: s = dropout(a·Bᵀ + bias) + res -> s_out; y = LN(s) (ln_g, ln_b, eps) [+ LN_s(res) when
+ *   gs / bs are given] -> y; statistics -> mean / rstd [/ mean_s / rstd_s] (res, s_out, y fp32 [M, H]).
+ *   The dropout mask is tagan_add_layernorm_fwd's (stream = row, counter = column).
+ * tagan_sgemm_nt_ln_bwd: dh = a·Bᵀ [M, H] (a = dqkv [M, K]) and the LayerNorm backward in the epilogue:
+ *   dx = rstd (g dh - mean(g dh x̂) x̂ - mean(g dh)) + dres (dres may be NULL), dgamma = Σ dh x̂, dbeta = Σ dh
+ *   (fixed-order partial sums: bitwise reproducible); workspace tagan_sgemm_nt_ln_bwd_workspace bytes; M > 0. */
+int tagan_sgemm_ln_supported(int32_t H, int32_t planes, int32_t act_dtype, int32_t op);
+int tagan_sgemm_nt_ln_in(int32_t c_dtype, int64_t M, int32_t N, int32_t K, const float* x, int64_t ldx,
+                         const float* ln_g, const float* ln_b, float eps, const void* wp, int32_t planes,
+                         const float* bias, void* c, int64_t ldc, float* mean, float* rstd, void* stream);
+int tagan_sgemm_tn_ln(int32_t dtype, int64_t M, int32_t N, int32_t K, const void* dy, int64_t ldy, const float* x,
+                      int64_t ldx, const float* ln_g, const float* ln_b, const float* mean, const float* rstd,
+                      int32_t planes, float* dw, int64_t lddw, float* db, void* workspace, size_t workspace_bytes,
+                      void* stream);
+int tagan_sgemm_nt_ln_out(int32_t a_dtype, int64_t M, int32_t H, const void* a, int64_t lda, const void* wp,
+                          int32_t planes, const float* bias, const float* res, float p_drop, uint64_t seed,
+                          const float* ln_g, const float* ln_b, float eps, const float* gs, const float* bs,
+                          float eps_s, float* s_out, float* y, float* mean, float* rstd, float* mean_s,
+                          float* rstd_s, void* stream);
+size_t tagan_sgemm_nt_ln_bwd_workspace(int64_t M, int32_t H, int32_t K);
+int tagan_sgemm_nt_ln_bwd(int32_t a_dtype, int64_t M, int32_t H, int32_t K, const void* a, int64_t lda,
+                          const void* wp, int32_t planes, const float* x, const float* mean, const float* rstd,
+                          const float* gamma, const float* dres, float* dx, float* dgamma, float* dbeta,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Fused classification head + loss (csrc/head.hip).  Replaces model.py:377-459 after the pooling:
  * graph_features [B, T, H] (row 0 = x0 [T, H], rows 1..B-1 zero, model.py:382-394) ->

@@ -90,6 +90,16 @@ _SIGNATURES = {
     "tagan_sgemm_nt": (_c.c_int, [_i32, _i32, _i64, _i32, _i32, _p, _i64, _p, _i32, _p, _p, _i64, _p]),
     "tagan_sgemm_tn_workspace": (_sz, [_i64, _i32, _i32]),
     "tagan_sgemm_tn": (_c.c_int, [_i32, _i64, _i32, _i32, _p, _i64, _p, _i64, _i32, _p, _i64, _p, _p, _sz, _p]),
+    "tagan_sgemm_ln_supported": (_c.c_int, [_i32, _i32, _i32, _i32]),
+    "tagan_sgemm_nt_ln_in": (_c.c_int, [_i32, _i64, _i32, _i32, _p, _i64, _p, _p, _f32, _p, _i32, _p, _p, _i64, _p, _p,
+                                        _p]),
+    "tagan_sgemm_tn_ln": (_c.c_int, [_i32, _i64, _i32, _i32, _p, _i64, _p, _i64, _p, _p, _p, _p, _i32, _p, _i64, _p,
+                                     _p, _sz, _p]),
+    "tagan_sgemm_nt_ln_out": (_c.c_int, [_i32, _i64, _i32, _p, _i64, _p, _i32, _p, _p, _f32, _u64, _p, _p, _f32, _p,
+                                         _p, _f32, _p, _p, _p, _p, _p, _p, _p]),
+    "tagan_sgemm_nt_ln_bwd_workspace": (_sz, [_i64, _i32, _i32]),
+    "tagan_sgemm_nt_ln_bwd": (_c.c_int, [_i32, _i64, _i32, _i32, _p, _i64, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _p,
+                                         _p, _sz, _p]),
     "tagan_head_supported": (_c.c_int, [_i32, _i32, _i32]),
     "tagan_head_saved_floats": (_sz, [_i32, _i32, _i32]),
     "tagan_head_fwd": (_c.c_int, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _f32, _p, _p, _f32, _u64,

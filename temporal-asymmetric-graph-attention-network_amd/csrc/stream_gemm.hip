@@ -116,23 +116,105 @@ struct NtArgs {
     const float* bias;       // [N] or null
     void* c;                 // [M, N] rows, row stride ldc (fp32 or bf16)
     int64_t ldc;
+    // MODE_LN_IN (K = H): a = x fp32 and the staged operand is h = LN(x) = (x - mean) rstd ln_g + ln_b; the row
+    // statistics go to mean / rstd (the LayerNorm backward and the LN-recomputing weight gradient read them)
+    const float* ln_g;
+    const float* ln_b;
+    float eps;
+    float* mean;
+    float* rstd;
+    // MODE_LN_OUT (N = H): v = dropout(acc + bias) + res -> s_out; c = LN(v) (ln_g, ln_b, eps; statistics -> mean,
+    // rstd) [+ LN_s(res) (gs, bs, eps_s; statistics -> mean_s, rstd_s)]
+    // MODE_LN_BWD (N = H): acc = dh, the gradient of h = LN(x) (x = res, statistics mean / rstd as inputs, gamma =
+    // ln_g); c = dx = rstd (g dh - mean(g dh x̂) x̂ - mean(g dh)) + dres; part[blockIdx.x][2H] = Σ dh x̂ | Σ dh
+    const float* res;
+    int64_t ldr;
+    float p_drop, inv_keep;
+    uint64_t seed;
+    const uint64_t* seed_ctr;
+    float* s_out;
+    const float* gs;
+    const float* bs;
+    float eps_s;
+    float* mean_s;
+    float* rstd_s;
+    const float* dres;
+    float* part;
 };
+
+enum { MODE_PLAIN = 0, MODE_LN_IN = 1, MODE_LN_OUT = 2, MODE_LN_BWD = 3 };
+
+// h = LN(x) element: one expression shared by the prologue and the weight gradient's recompute (bitwise equal)
+__device__ __forceinline__ float ln_apply(float x, float m, float rs, float g, float b) {
+    return __builtin_fmaf((x - m) * rs, g, b);
+}
+
+template <int G>
+__device__ __forceinline__ float xsum(float x) {
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+// sum over the four 16-lane groups of a wave (lanes l, l ^ 16, l ^ 32, l ^ 48: same MFMA output row)
+__device__ __forceinline__ float gsum4(float x) {
+    x += __shfl_xor(x, 16, 64);
+    return x + __shfl_xor(x, 32, 64);
+}
 
 // Workgroup: NW waves; wave w owns columns [16 NSUB (NW blockIdx.y + w), +16 NSUB) and keeps their B planes
 // (NSUB x K/32 x P fragments) in registers.  A tile = BM rows x K; thread chunk = 8 consecutive k of one row.
 // LDS image of a tile (per buffer): entry ((p * KK + kk) * J + j) * 64 + slot holds plane p of the B-operand
 // fragment of rows 16 j + (slot & 15), k = 32 kk + 8 (slot >> 4) + [0, 8) — one conflict-free ds_read_b128 per
 // (kk, j, plane) and wave.
-template <int K, int NSUB, int NW, int BM, int P, bool ABF, bool CBF>
-__global__ void __launch_bounds__(NW * 64) k_sgemm_nt(NtArgs g) {
+//
+// MODE_LN_IN maps a tile chunk to (row = c / 16, q = c % 16): the 16 lanes of a DPP row hold one whole row of x, so
+// its LayerNorm statistics are two butterflies in registers (two-pass, like k_ln_fwd).  Those lanes would all hit
+// the same LDS banks in the fragment image, so every mode stores slot (row r, k-group t) of a 64-entry block at
+// 16 t + (r ^ (t + 4 (kk & 3))): a permutation inside each 16-lane group, conflict-free for both chunk maps.
+// MODE_LN_OUT / MODE_LN_BWD need whole output rows: each wave reduces its 16 NSUB columns of a row (two-pass mean
+// and M2 for the forward, plain sums for the backward), the NW wave partials meet in LDS behind one barrier per
+// tile, and the forward merges them with Chan's pairwise formula (no E[x²] - E[x]² cancellation).
+template <int K, int NSUB, int NW, int BM, int P, bool ABF, bool CBF, int MODE, int MINB>
+__global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
     constexpr int KK = K / 32, J = BM / 16, NT = NW * 64, QK = K / 8;
     constexpr int CPT = BM * QK / NT;
     static_assert(BM * QK % NT == 0, "tile chunks must divide over the workgroup");
     static_assert(!ABF || P == 1, "bf16 operands have one plane");
+    static_assert(MODE != MODE_LN_IN || (QK == 16 && !ABF), "LN prologue: K = 128 fp32 rows");
+    constexpr bool EPI = MODE == MODE_LN_OUT || MODE == MODE_LN_BWD;
     constexpr int BUF = P * KK * J * 64;
     extern __shared__ uint4 sg_lds[];
+    float* red = reinterpret_cast<float*>(sg_lds + 2 * BUF);   // EPI: [BM][NW][4] wave partials of the rows
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nsub0 = (blockIdx.y * NW + w) * NSUB;
+    if constexpr (MODE == MODE_LN_OUT) {
+        if (g.seed_ctr) g.seed ^= *g.seed_ctr * 0x9E3779B97F4A7C15ull;   // TAGAN_LIVE_SEED
+    }
+    // LN prologue: gamma | beta in LDS after the two tile buffers (this thread's 8 columns: q = threadIdx.x % 16)
+    float* lgb = reinterpret_cast<float*>(sg_lds + 2 * BUF);
+    if constexpr (MODE == MODE_LN_IN) {
+        for (int i = threadIdx.x; i < 2 * K; i += NT) lgb[i] = i < K ? g.ln_g[i] : g.ln_b[i - K];
+        __syncthreads();
+    }
+    // epilogues: the LayerNorm parameters in LDS after the row partials: [4][HN] = gamma | beta | gamma_s | beta_s
+    // (this lane's columns: 16 (nsub0 + s) + 4 (lane >> 4) + [0, 4))
+    constexpr int HNE = NW * NSUB * 16;
+    const f32x4* eprm = reinterpret_cast<const f32x4*>(red + BM * NW * 4);
+    f32x4 dgacc[MODE == MODE_LN_BWD ? NSUB : 1], dbacc[MODE == MODE_LN_BWD ? NSUB : 1];
+    if constexpr (EPI) {
+        float* ep = red + BM * NW * 4;
+        for (int i = threadIdx.x; i < 4 * HNE; i += NT) {
+            const int q = i / HNE, c = i % HNE;
+            const float* src = q == 0 ? g.ln_g : q == 1 ? g.ln_b : q == 2 ? g.gs : g.bs;
+            ep[i] = (src && (MODE == MODE_LN_OUT || q == 0)) ? src[c] : 0.f;
+        }
+        __syncthreads();
+        if constexpr (MODE == MODE_LN_BWD) {
+#pragma unroll
+            for (int s = 0; s < NSUB; ++s) dgacc[s] = dbacc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    auto eprm_at = [&](int q, int s) { return eprm[(q * HNE + (nsub0 + s) * 16 + 4 * (lane >> 4)) / 4]; };
 
     bf16x8 wr[NSUB][KK][P];
 #pragma unroll
@@ -151,7 +233,7 @@ __global__ void __launch_bounds__(NW * 64) k_sgemm_nt(NtArgs g) {
 
     const int64_t ntiles = (g.M + BM - 1) / BM;
     int64_t tile = blockIdx.x;
-    if (tile >= ntiles) return;   // uniform over the workgroup
+    if (tile >= ntiles) return;   // uniform over the workgroup (the host launches at most ntiles workgroups)
 
     // ---- staging: global -> registers (pf) -> planes in LDS
     float pf[ABF ? 1 : CPT][8];
@@ -160,7 +242,9 @@ __global__ void __launch_bounds__(NW * 64) k_sgemm_nt(NtArgs g) {
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
             const int c = i * NT + threadIdx.x;
-            const int rl = c & 15, q = (c >> 4) % QK, rh = (c >> 4) / QK;
+            const int rl = MODE == MODE_LN_IN ? (c >> 4) & 15 : c & 15;
+            const int q = MODE == MODE_LN_IN ? c & 15 : (c >> 4) % QK;
+            const int rh = MODE == MODE_LN_IN ? c >> 8 : (c >> 4) / QK;
             const int64_t row = t * BM + rh * 16 + rl;
             if constexpr (ABF) {
                 pb[i] = make_uint4(0, 0, 0, 0);
@@ -177,12 +261,29 @@ __global__ void __launch_bounds__(NW * 64) k_sgemm_nt(NtArgs g) {
             }
         }
     };
-    auto stash = [&](uint4* buf) {
+    auto stash = [&](uint4* buf, int64_t t) {
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
             const int c = i * NT + threadIdx.x;
-            const int rl = c & 15, q = (c >> 4) % QK, rh = (c >> 4) / QK;
-            const int e0 = ((q >> 2) * J + rh) * 64 + rl + 16 * (q & 3);
+            const int rl = MODE == MODE_LN_IN ? (c >> 4) & 15 : c & 15;
+            const int q = MODE == MODE_LN_IN ? c & 15 : (c >> 4) % QK;
+            const int rh = MODE == MODE_LN_IN ? c >> 8 : (c >> 4) / QK;
+            const int e0 = ((q >> 2) * J + rh) * 64 + 16 * (q & 3) + (rl ^ ((q & 3) + 4 * ((q >> 2) & 3)));
+            if constexpr (MODE == MODE_LN_IN) {
+                float sm = (pf[i][0] + pf[i][1]) + (pf[i][2] + pf[i][3]) + ((pf[i][4] + pf[i][5]) + (pf[i][6] + pf[i][7]));
+                const float mean = xsum<16>(sm) / (float)K;
+                float sq = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sq += (pf[i][e] - mean) * (pf[i][e] - mean);
+                const float rstd = 1.f / sqrtf(xsum<16>(sq) / (float)K + g.eps);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) pf[i][e] = ln_apply(pf[i][e], mean, rstd, lgb[8 * q + e], lgb[K + 8 * q + e]);
+                const int64_t row = t * BM + rh * 16 + rl;
+                if (q == 0 && row < g.M) {
+                    g.mean[row] = mean;
+                    g.rstd[row] = rstd;
+                }
+            }
             if constexpr (ABF) {
                 buf[e0] = pb[i];
             } else {
@@ -196,12 +297,37 @@ __global__ void __launch_bounds__(NW * 64) k_sgemm_nt(NtArgs g) {
         }
     };
 
+    // fragment slot of this lane in a 64-entry block of k-block kk (the swizzle of stash)
+    int rslot[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rslot[u] = 16 * (lane >> 4) + ((lane & 15) ^ ((lane >> 4) + 4 * u));
+
     load(tile);
-    stash(sg_lds);
+    stash(sg_lds, tile);
     __syncthreads();
     for (int it = 0;; ++it) {
         const int64_t next = tile + gridDim.x;
         if (next < ntiles) load(next);
+        // epilogue operands of this tile (in flight under the MFMAs): the residual rows (LN_OUT: res, LN_BWD: the LN
+        // input x and dres) and the LN_BWD row statistics
+        f32x4 er[EPI ? J : 1][EPI ? NSUB : 1], ed[MODE == MODE_LN_BWD ? J : 1][MODE == MODE_LN_BWD ? NSUB : 1];
+        float em[MODE == MODE_LN_BWD ? J : 1], es[MODE == MODE_LN_BWD ? J : 1];
+        if constexpr (EPI) {
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int64_t row = tile * BM + j * 16 + (lane & 15);
+                const int64_t r = row < g.M ? row : g.M - 1;
+#pragma unroll
+                for (int s = 0; s < NSUB; ++s) {
+                    const int col = (nsub0 + s) * 16 + 4 * (lane >> 4);
+                    er[j][s] = *reinterpret_cast<const f32x4*>(g.res + r * g.ldr + col);
+                }
+                if constexpr (MODE == MODE_LN_BWD) {
+                    em[j] = g.mean[r];
+                    es[j] = g.rstd[r];
+                }
+            }
+        }
         const uint4* buf = sg_lds + (it & 1) * BUF;
         f32x4 acc[J][NSUB];
 #pragma unroll
@@ -215,14 +341,156 @@ __global__ void __launch_bounds__(NW * 64) k_sgemm_nt(NtArgs g) {
                 bf16x8 a[P];
 #pragma unroll
                 for (int p = 0; p < P; ++p)
-                    a[p] = __builtin_bit_cast(bf16x8, buf[((p * KK + kk) * J + j) * 64 + lane]);
+                    a[p] = __builtin_bit_cast(bf16x8, buf[((p * KK + kk) * J + j) * 64 + rslot[kk & 3]]);
 #pragma unroll
                 for (int s = 0; s < NSUB; ++s) acc[j][s] = mfma_planes<P>(wr[s][kk], a, acc[j][s]);
             }
         }
         // stage the next tile first: its loads were issued before this tile's MFMAs, and waiting for them after
         // the output stores would wait for the stores too
-        if (next < ntiles) stash(sg_lds + ((it + 1) & 1) * BUF);
+        if (next < ntiles) stash(sg_lds + ((it + 1) & 1) * BUF, next);
+        if constexpr (EPI) {
+            if constexpr (MODE == MODE_LN_BWD) {   // dres is read in pass 2 only: its loads fly under pass 1
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    const int64_t row = tile * BM + j * 16 + (lane & 15);
+                    const int64_t r = row < g.M ? row : g.M - 1;
+#pragma unroll
+                    for (int s = 0; s < NSUB; ++s)
+                        ed[j][s] = g.dres ? *reinterpret_cast<const f32x4*>(g.dres + r * g.ldc + (nsub0 + s) * 16 +
+                                                                            4 * (lane >> 4))
+                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+            constexpr int HN = NW * NSUB * 16;      // the whole row (gridDim.y == 1 in the LN modes)
+            constexpr float WC = (float)(NSUB * 16);
+            float v[MODE == MODE_LN_OUT ? J : 1][NSUB][4];
+            // pass 1: this wave's share of every row -> red[row][w]
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int64_t row = tile * BM + j * 16 + (lane & 15);
+                const bool live = row < g.M;
+                float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
+                if constexpr (MODE == MODE_LN_OUT) {
+                    const uint32_t key = drop_key(g.seed, (uint64_t)row);
+#pragma unroll
+                    for (int s = 0; s < NSUB; ++s) {
+                        const int col = (nsub0 + s) * 16 + 4 * (lane >> 4);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            float x = acc[j][s][e];
+                            if (g.p_drop > 0.f) x = drop_u(key, (uint32_t)(col + e)) >= g.p_drop ? x * g.inv_keep : 0.f;
+                            x += er[j][s][e];
+                            v[j][s][e] = x;
+                            p0 += x;
+                            p2 += er[j][s][e];
+                        }
+                        if (live) *reinterpret_cast<f32x4*>(g.s_out + row * g.ldc + col) =
+                                      f32x4{v[j][s][0], v[j][s][1], v[j][s][2], v[j][s][3]};
+                    }
+                    const float mw = gsum4(p0) / WC, ms = gsum4(p2) / WC;
+#pragma unroll
+                    for (int s = 0; s < NSUB; ++s)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            p1 += (v[j][s][e] - mw) * (v[j][s][e] - mw);
+                            p3 += (er[j][s][e] - ms) * (er[j][s][e] - ms);
+                        }
+                    p0 = mw; p1 = gsum4(p1); p2 = ms; p3 = gsum4(p3);
+                } else {
+                    const float m = em[j], rs = es[j];
+#pragma unroll
+                    for (int s = 0; s < NSUB; ++s)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float d = acc[j][s][e];
+                            const float xv = (er[j][s][e] - m) * rs, gd = d * eprm_at(0, s)[e];
+                            p0 += gd * xv;
+                            p1 += gd;
+                            if (live) {
+                                dgacc[s][e] += d * xv;
+                                dbacc[s][e] += d;
+                            }
+                        }
+                    p0 = gsum4(p0); p1 = gsum4(p1);
+                }
+                if ((lane >> 4) == 0) {
+                    float* rp = red + ((j * 16 + (lane & 15)) * NW + w) * 4;
+                    rp[0] = p0; rp[1] = p1; rp[2] = p2; rp[3] = p3;
+                }
+            }
+            lds_barrier();
+            // pass 2: whole-row statistics, outputs
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int64_t row = tile * BM + j * 16 + (lane & 15);
+                const bool live = row < g.M;
+                const float* rp = red + (j * 16 + (lane & 15)) * NW * 4;
+                if constexpr (MODE == MODE_LN_OUT) {
+                    float mean = 0.f, means = 0.f;
+#pragma unroll
+                    for (int ww = 0; ww < NW; ++ww) { mean += rp[ww * 4]; means += rp[ww * 4 + 2]; }
+                    mean /= (float)NW;
+                    means /= (float)NW;
+                    float m2 = 0.f, m2s = 0.f;
+#pragma unroll
+                    for (int ww = 0; ww < NW; ++ww) {
+                        const float d = rp[ww * 4] - mean, ds = rp[ww * 4 + 2] - means;
+                        m2 += rp[ww * 4 + 1] + WC * d * d;
+                        m2s += rp[ww * 4 + 3] + WC * ds * ds;
+                    }
+                    const float rstd = 1.f / sqrtf(m2 / (float)HN + g.eps);
+                    const float rstds = 1.f / sqrtf(m2s / (float)HN + g.eps_s);
+                    if (!live) continue;
+#pragma unroll
+                    for (int s = 0; s < NSUB; ++s) {
+                        const int col = (nsub0 + s) * 16 + 4 * (lane >> 4);
+                        f32x4 y;
+                        const f32x4 eg = eprm_at(0, s), eb = eprm_at(1, s);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) y[e] = (v[j][s][e] - mean) * rstd * eg[e] + eb[e];
+                        if (g.gs) {
+                            const f32x4 egs = eprm_at(2, s), ebs = eprm_at(3, s);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) y[e] += (er[j][s][e] - means) * rstds * egs[e] + ebs[e];
+                        }
+                        *reinterpret_cast<f32x4*>((float*)g.c + row * g.ldc + col) = y;
+                    }
+                    if ((lane >> 4) == 0 && w == 0) {
+                        g.mean[row] = mean;
+                        g.rstd[row] = rstd;
+                        if (g.gs) {
+                            g.mean_s[row] = means;
+                            g.rstd_s[row] = rstds;
+                        }
+                    }
+                } else {
+                    float c1 = 0.f, c2 = 0.f;
+#pragma unroll
+                    for (int ww = 0; ww < NW; ++ww) { c1 += rp[ww * 4]; c2 += rp[ww * 4 + 1]; }
+                    c1 /= (float)HN;
+                    c2 /= (float)HN;
+                    if (!live) continue;
+                    const float rs = es[j];
+#pragma unroll
+                    for (int s = 0; s < NSUB; ++s) {
+                        const int col = (nsub0 + s) * 16 + 4 * (lane >> 4);
+                        f32x4 dx;
+                        const f32x4 eg = eprm_at(0, s);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float xv = (er[j][s][e] - em[j]) * rs, gd = acc[j][s][e] * eg[e];
+                            dx[e] = rs * (gd - c1 * xv - c2) + ed[j][s][e];
+                        }
+                        *reinterpret_cast<f32x4*>((float*)g.c + row * g.ldc + col) = dx;
+                    }
+                }
+            }
+            if (next >= ntiles) break;
+            lds_barrier();
+            tile = next;
+            continue;
+        }
         // D[n][m] of the MFMA = C[m][n]: lane holds C[row 16 j + (lane & 15)][4 consecutive n]
 #pragma unroll
         for (int j = 0; j < J; ++j) {
@@ -245,6 +513,20 @@ __global__ void __launch_bounds__(NW * 64) k_sgemm_nt(NtArgs g) {
         lds_barrier();
         tile = next;
     }
+    if constexpr (MODE == MODE_LN_BWD) {
+        // Σ over this workgroup's rows of dh x̂ and dh for the lane's columns: lanes l ^ 1..8 share them
+#pragma unroll
+        for (int s = 0; s < NSUB; ++s)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float a = xsum<16>(dgacc[s][e]), b = xsum<16>(dbacc[s][e]);
+                if ((lane & 15) == 0) {
+                    const int col = (nsub0 + s) * 16 + 4 * (lane >> 4) + e;
+                    g.part[(int64_t)blockIdx.x * 2 * NW * NSUB * 16 * gridDim.y + col] = a;
+                    g.part[(int64_t)blockIdx.x * 2 * NW * NSUB * 16 * gridDim.y + NW * NSUB * 16 * gridDim.y + col] = b;
+                }
+            }
+    }
 }
 
 // ------------------------------------------------------------------------------------------- TN: dW = dYᵀ·X
@@ -256,6 +538,12 @@ struct TnArgs {
     int64_t ldx;
     int64_t tiles_per_wg;    // 32-row tiles per workgroup (contiguous range)
     float* part;             // [gridDim.x][N * K + N] partial dW | db
+    // LNX: x is the fp32 LayerNorm input and the X operand is h = LN(x), recomputed from the forward's row
+    // statistics exactly as the LN prologue of k_sgemm_nt made it (ln_apply)
+    const float* ln_g;
+    const float* ln_b;
+    const float* mean;
+    const float* rstd;
 };
 
 // One 32-row tile per step.  Workgroup (blockIdx.x, blockIdx.y): rows of m-group blockIdx.x, dY columns
@@ -265,7 +553,7 @@ struct TnArgs {
 // for BOTH operands (a permutation of the sum), so each ds_read_b64_tr_b16 of a 32-lane half covers 8 adjacent rows:
 // conflict-free.  Wave w owns n-subtiles [NSN w, NSN (w + 1)) and all K / 16 k-subtiles; db comes from one more
 // MFMA per plane against a fragment of ones.
-template <int N, int K, int NSN, int NW, int NG, int P, bool ABF, int MINB>
+template <int N, int K, int NSN, int NW, int NG, int P, bool ABF, int MINB, bool LNX>
 __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_tn(TnArgs g) {
     constexpr int NL = N / NG;
     static_assert(NL == NW * NSN * 16, "waves must cover the workgroup's columns");
@@ -296,16 +584,31 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_tn(TnArgs g) {
     const int64_t t0 = (int64_t)blockIdx.x * g.tiles_per_wg;
     const int64_t t1 = min(t0 + g.tiles_per_wg, (g.M + 31) / 32);
 
-    float4 pf[ABF ? 1 : CPT];
+    // LNX: an x chunk's 4 columns are fixed per thread (NT and the dY part of a tile are multiples of K / 4)
+    static_assert(!LNX || (NT % (K / 4) == 0 && (8 * NL) % (K / 4) == 0), "LNX: thread-fixed x columns");
+    float4 lng = make_float4(0.f, 0.f, 0.f, 0.f), lnb = lng;
+    if constexpr (LNX) {
+        const int col = 4 * (threadIdx.x % (K / 4));
+        lng = *reinterpret_cast<const float4*>(g.ln_g + col);
+        lnb = *reinterpret_cast<const float4*>(g.ln_b + col);
+    }
+    // LNX: chunks [0, CY) are dY's, [CY, CPT) X's (compile-time split)
+    constexpr int CY = LNX ? 8 * NL / NT : 0, CX = LNX ? CPT - CY : 1;
+    static_assert(!LNX || (8 * NL % NT == 0 && Q4 % NT == 0), "LNX: whole chunk rounds per operand");
+    float4 pf[(ABF && !LNX) ? 1 : CPT];
     uint2 pb[ABF ? CPT : 1];
+    float pm[CX], pr[CX];
     auto load = [&](int64_t t) {
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
             const int c = i * NT + threadIdx.x;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             uint2 u = make_uint2(0, 0);
+            if constexpr (LNX) {
+                if (i >= CY) { pm[i - CY] = 0.f; pr[i - CY] = 0.f; }
+            }
             if (c < Q4) {
-                const bool isy = c < 32 * NL / 4;
+                const bool isy = LNX ? i < CY : c < 32 * NL / 4;
                 const int cc = isy ? c : c - 32 * NL / 4;
                 const int W4 = (isy ? NL : K) / 4;
                 const int r = cc / W4, col = 4 * (cc % W4);
@@ -314,11 +617,19 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_tn(TnArgs g) {
                     const void* base = isy ? g.dy : g.x;
                     const int64_t ld = isy ? g.ldy : g.ldx;
                     const int64_t o = row * ld + col + (isy ? ncol0 : 0);
-                    if constexpr (ABF) u = *reinterpret_cast<const uint2*>((const uint16_t*)base + o);
-                    else v = *reinterpret_cast<const float4*>((const float*)base + o);
+                    if (LNX && !isy) {
+                        v = *reinterpret_cast<const float4*>((const float*)base + o);
+                        pm[LNX ? i - CY : 0] = g.mean[row];
+                        pr[LNX ? i - CY : 0] = g.rstd[row];
+                    } else if constexpr (ABF) {
+                        u = *reinterpret_cast<const uint2*>((const uint16_t*)base + o);
+                    } else {
+                        v = *reinterpret_cast<const float4*>((const float*)base + o);
+                    }
                 }
             }
-            if constexpr (ABF) pb[i] = u; else pf[i] = v;
+            if constexpr (ABF) pb[i] = u;
+            if constexpr (!ABF || LNX) pf[i] = v;
         }
     };
     auto stash = [&]() {
@@ -326,13 +637,21 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_tn(TnArgs g) {
         for (int i = 0; i < CPT; ++i) {
             const int c = i * NT + threadIdx.x;
             if (c < Q4) {
-                const bool isy = c < 32 * NL / 4;
+                const bool isy = LNX ? i < CY : c < 32 * NL / 4;
                 const int cc = isy ? c : c - 32 * NL / 4;
                 const int W4 = (isy ? NL : K) / 4;
                 const int r = cc / W4, col = 4 * (cc % W4);
                 uint16_t* dst = isy ? ly + r * SY + col : lx + r * SX + col;
                 const int pstride = isy ? PY : PX;
-                if constexpr (ABF) {
+                if (LNX && !isy) {
+                    const float4 x = pf[i];
+                    const float m = pm[LNX ? i - CY : 0], rs = pr[LNX ? i - CY : 0];
+                    uint32_t lo[P], hi[P];
+                    split2<P>(ln_apply(x.x, m, rs, lng.x, lnb.x), ln_apply(x.y, m, rs, lng.y, lnb.y), lo);
+                    split2<P>(ln_apply(x.z, m, rs, lng.z, lnb.z), ln_apply(x.w, m, rs, lng.w, lnb.w), hi);
+#pragma unroll
+                    for (int p = 0; p < P; ++p) *reinterpret_cast<uint2*>(dst + p * pstride) = make_uint2(lo[p], hi[p]);
+                } else if constexpr (ABF) {
                     *reinterpret_cast<uint2*>(dst) = pb[i];
                 } else {
                     uint32_t lo[P], hi[P];
@@ -432,17 +751,22 @@ int num_cu() {
 
 typedef void (*nt_fn)(NtArgs);
 struct NtCfg {
-    int K, N, P, abf, cbf;   // shape / storage key
+    int K, N, P, abf, cbf, mode;   // shape / storage / fusion key
     nt_fn fn;
     int nw, nsub, bm;
     size_t lds;
     int wg_per_cu;
 };
 
-template <int K, int NSUB, int NW, int BM, int P, bool ABF, bool CBF>
+// MINB: waves per SIMD the register allocation must allow (4 = two 8-wave workgroups per CU: the LN epilogues
+// serialise each workgroup's memory and matrix phases, a second workgroup per CU overlaps them)
+template <int K, int NSUB, int NW, int BM, int P, bool ABF, bool CBF, int MODE = MODE_PLAIN, int MINB = 1>
 constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
-    return NtCfg{K, N, P, ABF, CBF, k_sgemm_nt<K, NSUB, NW, BM, P, ABF, CBF>, NW, NSUB, BM,
-                 (size_t)2 * P * (K / 32) * (BM / 16) * 64 * 16, wg_per_cu};
+    return NtCfg{K, N, P, ABF, CBF, MODE, k_sgemm_nt<K, NSUB, NW, BM, P, ABF, CBF, MODE, MINB>, NW, NSUB, BM,
+                 (size_t)2 * P * (K / 32) * (BM / 16) * 64 * 16 +
+                     ((MODE == MODE_LN_OUT || MODE == MODE_LN_BWD) ? (size_t)(BM * NW * 4 + 4 * N) * 4 : 0) +
+                     (MODE == MODE_LN_IN ? (size_t)2 * K * 4 : 0),
+                 wg_per_cu};
 }
 
 // (K, N) of the attention blocks at H = 128: QKV forward (128, 384), out-projection forward and its input
@@ -459,12 +783,26 @@ constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
     nt_cfg<128, 3, 8, 64, 1, ABF, CBF>(384, 1), nt_cfg<128, 3, 8, 32, 1, ABF, CBF>(384, 1),                   \
     nt_cfg<128, 1, 8, 128, 1, ABF, CBF>(128, 2), nt_cfg<128, 1, 8, 32, 1, ABF, CBF>(128, 2),                   \
     nt_cfg<384, 1, 8, 64, 1, ABF, CBF>(128, 1), nt_cfg<384, 1, 8, 32, 1, ABF, CBF>(128, 1)
+// The LayerNorm-fused forms (H = 128): LN1 prologue of the QKV projection (x fp32 in; qkv fp32, or bf16 in the
+// bf16 activation mode), dropout + residual + LN2 [+ skip LN] epilogue of the out-projection (y fp32), LN1 backward
+// epilogue of the QKV input gradient (dx fp32).
+#define NT_SETLN                                                                                             \
+    nt_cfg<128, 3, 8, 32, 3, false, false, MODE_LN_IN>(384, 1),                                                 \
+    nt_cfg<128, 3, 8, 64, 1, false, true, MODE_LN_IN>(384, 1), nt_cfg<128, 3, 8, 32, 1, false, true, MODE_LN_IN, 4>(384, 2), \
+    nt_cfg<128, 3, 8, 64, 1, false, false, MODE_LN_IN>(384, 1),                                                 \
+    nt_cfg<128, 1, 8, 32, 3, false, false, MODE_LN_OUT>(128, 1),                                                \
+    nt_cfg<128, 1, 8, 32, 1, true, false, MODE_LN_OUT, 4>(128, 2), nt_cfg<128, 1, 8, 64, 1, true, false, MODE_LN_OUT>(128, 1), \
+    nt_cfg<128, 1, 8, 32, 1, false, false, MODE_LN_OUT, 4>(128, 2),                                             \
+    nt_cfg<384, 1, 8, 32, 3, false, false, MODE_LN_BWD>(128, 1),                                                \
+    nt_cfg<384, 1, 8, 64, 1, true, false, MODE_LN_BWD>(128, 1), nt_cfg<384, 1, 8, 64, 1, false, false, MODE_LN_BWD>(128, 1)
 const NtCfg NT_TABLE[] = {
     NT_SET3,
     NT_SET1(false, false),
     NT_SET1(true, false),
     NT_SET1(true, true),
+    NT_SETLN,
 };
+#undef NT_SETLN
 #undef NT_SET3
 #undef NT_SET1
 
@@ -478,11 +816,11 @@ int sgemm_variant() {
     return v;
 }
 
-const NtCfg* nt_find(int K, int N, int P, int abf, int cbf) {
+const NtCfg* nt_find(int K, int N, int P, int abf, int cbf, int mode = MODE_PLAIN) {
     const NtCfg* first = nullptr;
     int seen = 0;
     for (const NtCfg& c : NT_TABLE)
-        if (c.K == K && c.N == N && c.P == P && c.abf == abf && c.cbf == cbf) {
+        if (c.K == K && c.N == N && c.P == P && c.abf == abf && c.cbf == cbf && c.mode == mode) {
             if (!first) first = &c;
             if (seen++ == sgemm_variant()) return &c;
         }
@@ -491,17 +829,18 @@ const NtCfg* nt_find(int K, int N, int P, int abf, int cbf) {
 
 typedef void (*tn_fn)(TnArgs);
 struct TnCfg {
-    int N, K, P, abf;
+    int N, K, P, abf, lnx;
     tn_fn fn;
     int nw, ng;
     size_t lds;
     int wg_per_cu;
 };
-template <int N, int K, int NSN, int NW, int NG, int P, bool ABF>
+template <int N, int K, int NSN, int NW, int NG, int P, bool ABF, bool LNX = false>
 constexpr TnCfg tn_cfg(int wg_per_cu) {
-    return TnCfg{N, K, P, ABF, k_sgemm_tn<N, K, NSN, NW, NG, P, ABF, NW == 4 ? 2 : 1>, NW, NG,
+    return TnCfg{N, K, P, ABF, LNX, k_sgemm_tn<N, K, NSN, NW, NG, P, ABF, NW == 4 ? 2 : 1, LNX>, NW, NG,
                  (size_t)P * 32 * ((N / NG + 16) + (K + 16)) * 2, wg_per_cu};
 }
+// abf = dY stored bf16 (and X too, unless lnx: X = LN(x) from the fp32 LayerNorm input)
 const TnCfg TN_TABLE[] = {
     tn_cfg<384, 128, 3, 4, 2, 3, false>(2), tn_cfg<384, 128, 3, 8, 1, 3, false>(1),
     tn_cfg<128, 128, 1, 8, 1, 3, false>(2), tn_cfg<128, 128, 1, 8, 1, 3, false>(1),
@@ -509,12 +848,15 @@ const TnCfg TN_TABLE[] = {
     tn_cfg<128, 128, 1, 8, 1, 1, false>(2), tn_cfg<128, 128, 1, 8, 1, 1, false>(1),
     tn_cfg<384, 128, 3, 8, 1, 1, true>(1),  tn_cfg<384, 128, 3, 4, 2, 1, true>(2),
     tn_cfg<128, 128, 1, 8, 1, 1, true>(2),  tn_cfg<128, 128, 1, 8, 1, 1, true>(1),
+    tn_cfg<384, 128, 3, 8, 1, 3, false, true>(1), tn_cfg<384, 128, 3, 4, 2, 3, false, true>(2),
+    tn_cfg<384, 128, 3, 8, 1, 1, true, true>(1),  tn_cfg<384, 128, 3, 4, 2, 1, true, true>(2),
+    tn_cfg<384, 128, 3, 8, 1, 1, false, true>(1),
 };
-const TnCfg* tn_find(int N, int K, int P, int abf) {
+const TnCfg* tn_find(int N, int K, int P, int abf, int lnx = 0) {
     const TnCfg* first = nullptr;
     int seen = 0;
     for (const TnCfg& c : TN_TABLE)
-        if (c.N == N && c.K == K && c.P == P && c.abf == abf) {
+        if (c.N == N && c.K == K && c.P == P && c.abf == abf && c.lnx == lnx) {
             if (!first) first = &c;
             if (seen++ == sgemm_variant()) return &c;
         }
@@ -526,6 +868,25 @@ int64_t tn_groups(int64_t M, const TnCfg* cfg) {
     const int64_t tiles = (M + 31) / 32;
     const int64_t g = (int64_t)num_cu() * cfg->wg_per_cu / cfg->ng;
     return tiles < g ? (tiles > 0 ? tiles : 1) : g;
+}
+
+// workgroups of an NT launch along the rows (grid.x): one per CU slot, at most one per tile
+int64_t nt_groups(int64_t M, const NtCfg* cfg, int gy) {
+    const int64_t tiles = (M + cfg->bm - 1) / cfg->bm;
+    int64_t gx = (int64_t)num_cu() * cfg->wg_per_cu / gy;
+    if (gx > tiles) gx = tiles;
+    return gx < 1 ? 1 : gx;
+}
+
+bool lds_ok(const void* fn, size_t lds);
+
+int nt_launch(const NtCfg* cfg, const NtArgs& g, int N, void* stream, const char* what) {
+    TAGAN_REQUIRE(lds_ok((const void*)cfg->fn, cfg->lds), TAGAN_ERR_LAUNCH, "%s: LDS attribute", what);
+    const int gy = N / (cfg->nw * cfg->nsub * 16);
+    const int64_t gx = nt_groups(g.M, cfg, gy);
+    hipLaunchKernelGGL(cfg->fn, dim3((unsigned)gx, (unsigned)gy), dim3(cfg->nw * 64), cfg->lds, as_stream(stream), g);
+    TAGAN_CHECK_LAUNCH(what);
+    return TAGAN_OK;
 }
 
 bool lds_ok(const void* fn, size_t lds) {
@@ -579,15 +940,94 @@ extern "C" int tagan_sgemm_nt(int32_t a_dtype, int32_t c_dtype, int64_t M, int32
     TAGAN_REQUIRE(((uintptr_t)a % 16 == 0) && (lda * es) % 16 == 0 && ((uintptr_t)c % 8 == 0) &&
                       (ldc * ec) % 8 == 0 && (!bias || (uintptr_t)bias % 16 == 0),
                   TAGAN_ERR_ARG, "tagan_sgemm_nt: operands must be 16-byte aligned rows");
-    TAGAN_REQUIRE(lds_ok((const void*)cfg->fn, cfg->lds), TAGAN_ERR_LAUNCH, "tagan_sgemm_nt: LDS attribute");
-    const int gy = N / (cfg->nw * cfg->nsub * 16);
-    const int64_t tiles = (M + cfg->bm - 1) / cfg->bm;
-    int64_t gx = (int64_t)num_cu() * cfg->wg_per_cu / gy;
-    if (gx > tiles) gx = tiles;
-    if (gx < 1) gx = 1;
-    NtArgs g{M, a, lda, (const uint4*)wp, bias, c, ldc};
-    hipLaunchKernelGGL(cfg->fn, dim3((unsigned)gx, (unsigned)gy), dim3(cfg->nw * 64), cfg->lds, as_stream(stream), g);
-    TAGAN_CHECK_LAUNCH("tagan_sgemm_nt");
+    NtArgs g{};
+    g.M = M; g.a = a; g.lda = lda; g.wp = (const uint4*)wp; g.bias = bias; g.c = c; g.ldc = ldc;
+    return nt_launch(cfg, g, N, stream, "tagan_sgemm_nt");
+}
+
+extern "C" int tagan_sgemm_ln_supported(int32_t H, int32_t planes, int32_t act_dtype, int32_t op) {
+    const int ab = act_dtype == TAGAN_BF16;
+    switch (op) {
+        case 1: return nt_find(H, 3 * H, planes, 0, ab, MODE_LN_IN) && tn_find(3 * H, H, planes, ab, 1);
+        case 2: return nt_find(H, H, planes, ab, 0, MODE_LN_OUT) != nullptr;
+        case 3: return nt_find(3 * H, H, planes, ab, 0, MODE_LN_BWD) != nullptr;
+        default: return 0;
+    }
+}
+
+extern "C" int tagan_sgemm_nt_ln_in(int32_t c_dtype, int64_t M, int32_t N, int32_t K, const float* x, int64_t ldx,
+                                    const float* ln_g, const float* ln_b, float eps, const void* wp, int32_t planes,
+                                    const float* bias, void* c, int64_t ldc, float* mean, float* rstd, void* stream) {
+    const NtCfg* cfg = nt_find(K, N, planes, 0, c_dtype == TAGAN_BF16, MODE_LN_IN);
+    TAGAN_REQUIRE(cfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt_ln_in: no kernel for N=%d K=%d planes=%d", N, K, planes);
+    TAGAN_REQUIRE(M >= 0 && wp && ln_g && ln_b, TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_in: bad arguments");
+    if (M == 0) return TAGAN_OK;
+    TAGAN_REQUIRE(x && c && mean && rstd && ldx >= K && ldc >= N, TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_in: bad operands");
+    const int ec = c_dtype == TAGAN_BF16 ? 2 : 4;
+    TAGAN_REQUIRE((uintptr_t)x % 16 == 0 && (ldx * 4) % 16 == 0 && (uintptr_t)c % 8 == 0 && (ldc * ec) % 8 == 0 &&
+                      (!bias || (uintptr_t)bias % 16 == 0),
+                  TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_in: operands must be 16-byte aligned rows");
+    NtArgs g{};
+    g.M = M; g.a = x; g.lda = ldx; g.wp = (const uint4*)wp; g.bias = bias; g.c = c; g.ldc = ldc;
+    g.ln_g = ln_g; g.ln_b = ln_b; g.eps = eps; g.mean = mean; g.rstd = rstd;
+    return nt_launch(cfg, g, N, stream, "tagan_sgemm_nt_ln_in");
+}
+
+extern "C" int tagan_sgemm_nt_ln_out(int32_t a_dtype, int64_t M, int32_t H, const void* a, int64_t lda, const void* wp,
+                                     int32_t planes, const float* bias, const float* res, float p_drop, uint64_t seed,
+                                     const float* ln_g, const float* ln_b, float eps, const float* gs, const float* bs,
+                                     float eps_s, float* s_out, float* y, float* mean, float* rstd, float* mean_s,
+                                     float* rstd_s, void* stream) {
+    const NtCfg* cfg = nt_find(H, H, planes, a_dtype == TAGAN_BF16, 0, MODE_LN_OUT);
+    TAGAN_REQUIRE(cfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt_ln_out: no kernel for H=%d planes=%d", H, planes);
+    TAGAN_REQUIRE(M >= 0 && wp && ln_g && ln_b && p_drop >= 0.f && p_drop < 1.f && (!gs == !bs) &&
+                      (!gs || (mean_s && rstd_s)),
+                  TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_out: bad arguments");
+    if (M == 0) return TAGAN_OK;
+    TAGAN_REQUIRE(a && res && s_out && y && mean && rstd && lda >= H, TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_out: bad operands");
+    const int es = a_dtype == TAGAN_BF16 ? 2 : 4;
+    TAGAN_REQUIRE((uintptr_t)a % 16 == 0 && (lda * es) % 16 == 0 && (uintptr_t)res % 16 == 0 &&
+                      (uintptr_t)s_out % 16 == 0 && (uintptr_t)y % 16 == 0 && (!bias || (uintptr_t)bias % 16 == 0),
+                  TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_out: operands must be 16-byte aligned rows");
+    NtArgs g{};
+    g.M = M; g.a = a; g.lda = lda; g.wp = (const uint4*)wp; g.bias = bias; g.c = y; g.ldc = H;
+    g.ln_g = ln_g; g.ln_b = ln_b; g.eps = eps; g.mean = mean; g.rstd = rstd;
+    g.res = res; g.ldr = H; g.p_drop = p_drop; g.inv_keep = 1.f / (1.f - p_drop); g.seed = seed;
+    g.seed_ctr = seed_counter(); g.s_out = s_out;
+    g.gs = gs; g.bs = bs; g.eps_s = eps_s; g.mean_s = mean_s; g.rstd_s = rstd_s;
+    return nt_launch(cfg, g, H, stream, "tagan_sgemm_nt_ln_out");
+}
+
+extern "C" size_t tagan_sgemm_nt_ln_bwd_workspace(int64_t M, int32_t H, int32_t K) {
+    int64_t g = 1;
+    for (const NtCfg& c : NT_TABLE)
+        if (c.mode == MODE_LN_BWD && c.N == H && c.K == K) g = std::max(g, nt_groups(M, &c, 1));
+    return (size_t)g * 2 * H * sizeof(float);
+}
+
+extern "C" int tagan_sgemm_nt_ln_bwd(int32_t a_dtype, int64_t M, int32_t H, int32_t K, const void* a, int64_t lda,
+                                     const void* wp, int32_t planes, const float* x, const float* mean,
+                                     const float* rstd, const float* gamma, const float* dres, float* dx, float* dgamma,
+                                     float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+    const NtCfg* cfg = nt_find(K, H, planes, a_dtype == TAGAN_BF16, 0, MODE_LN_BWD);
+    TAGAN_REQUIRE(cfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt_ln_bwd: no kernel for H=%d K=%d planes=%d", H, K, planes);
+    TAGAN_REQUIRE(M >= 0 && wp && gamma && dgamma && dbeta, TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_bwd: bad arguments");
+    TAGAN_REQUIRE(M > 0, TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_bwd: M must be positive (no rows: dgamma = dbeta = 0)");
+    TAGAN_REQUIRE(a && x && mean && rstd && dx && lda >= K, TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_bwd: bad operands");
+    const int es = a_dtype == TAGAN_BF16 ? 2 : 4;
+    TAGAN_REQUIRE((uintptr_t)a % 16 == 0 && (lda * es) % 16 == 0 && (uintptr_t)x % 16 == 0 &&
+                      (uintptr_t)dx % 16 == 0 && (!dres || (uintptr_t)dres % 16 == 0),
+                  TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_bwd: operands must be 16-byte aligned rows");
+    const int64_t G = nt_groups(M, cfg, 1);
+    TAGAN_REQUIRE(ws && ws_bytes >= (size_t)G * 2 * H * sizeof(float), TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_bwd: workspace");
+    NtArgs g{};
+    g.M = M; g.a = a; g.lda = lda; g.wp = (const uint4*)wp; g.bias = nullptr; g.c = dx; g.ldc = H;
+    g.ln_g = gamma; g.mean = (float*)mean; g.rstd = (float*)rstd; g.res = x; g.ldr = H; g.dres = dres;
+    g.part = (float*)ws;
+    const int rc = nt_launch(cfg, g, H, stream, "tagan_sgemm_nt_ln_bwd");
+    if (rc != TAGAN_OK) return rc;
+    launch_colsum((const float*)ws, (int)G, 2 * H, dgamma, dbeta, H, as_stream(stream), 1.f, 2 * H);
+    TAGAN_CHECK_LAUNCH("tagan_sgemm_nt_ln_bwd_sum");
     return TAGAN_OK;
 }
 
@@ -599,10 +1039,32 @@ extern "C" size_t tagan_sgemm_tn_workspace(int64_t M, int32_t N, int32_t K) {
     return (size_t)g * ((size_t)N * K + N) * sizeof(float);
 }
 
+static int tn_run(int32_t dtype, int64_t M, int32_t N, int32_t K, const void* dy, int64_t ldy, const void* x,
+                  int64_t ldx, int32_t planes, float* dw, int64_t lddw, float* db, void* ws, size_t ws_bytes,
+                  void* stream, const float* ln_g, const float* ln_b, const float* mean, const float* rstd);
+
 extern "C" int tagan_sgemm_tn(int32_t dtype, int64_t M, int32_t N, int32_t K, const void* dy, int64_t ldy,
                               const void* x, int64_t ldx, int32_t planes, float* dw, int64_t lddw, float* db,
                               void* ws, size_t ws_bytes, void* stream) {
-    const TnCfg* cfg = tn_find(N, K, planes, dtype == TAGAN_BF16);
+    return tn_run(dtype, M, N, K, dy, ldy, x, ldx, planes, dw, lddw, db, ws, ws_bytes, stream, nullptr, nullptr,
+                  nullptr, nullptr);
+}
+
+extern "C" int tagan_sgemm_tn_ln(int32_t dtype, int64_t M, int32_t N, int32_t K, const void* dy, int64_t ldy,
+                                 const float* x, int64_t ldx, const float* ln_g, const float* ln_b, const float* mean,
+                                 const float* rstd, int32_t planes, float* dw, int64_t lddw, float* db, void* ws,
+                                 size_t ws_bytes, void* stream) {
+    TAGAN_REQUIRE(ln_g && ln_b && mean && rstd, TAGAN_ERR_ARG, "tagan_sgemm_tn_ln: null LayerNorm operand");
+    TAGAN_REQUIRE((uintptr_t)x % 16 == 0 && (ldx * 4) % 16 == 0, TAGAN_ERR_ARG,
+                  "tagan_sgemm_tn_ln: x must be 16-byte aligned rows");
+    return tn_run(dtype, M, N, K, dy, ldy, x, ldx, planes, dw, lddw, db, ws, ws_bytes, stream, ln_g, ln_b, mean, rstd);
+}
+
+static int tn_run(int32_t dtype, int64_t M, int32_t N, int32_t K, const void* dy, int64_t ldy, const void* x,
+                  int64_t ldx, int32_t planes, float* dw, int64_t lddw, float* db, void* ws, size_t ws_bytes,
+                  void* stream, const float* ln_g, const float* ln_b, const float* mean, const float* rstd) {
+    const int lnx = ln_g != nullptr;
+    const TnCfg* cfg = tn_find(N, K, planes, dtype == TAGAN_BF16, lnx);
     TAGAN_REQUIRE(cfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_tn: no kernel for N=%d K=%d planes=%d dtype %d", N, K,
                   planes, dtype);
     TAGAN_REQUIRE(M >= 0 && (M == 0 || (dy && x)) && (dw || db), TAGAN_ERR_ARG, "tagan_sgemm_tn: bad arguments");
@@ -615,7 +1077,7 @@ extern "C" int tagan_sgemm_tn(int32_t dtype, int64_t M, int32_t N, int32_t K, co
     TAGAN_REQUIRE(lds_ok((const void*)cfg->fn, cfg->lds), TAGAN_ERR_LAUNCH, "tagan_sgemm_tn: LDS attribute");
     const int64_t G = tn_groups(M, cfg);
     const int64_t tiles = (M + 31) / 32;
-    TnArgs g{M, dy, ldy, x, ldx, (tiles + G - 1) / G, (float*)ws};
+    TnArgs g{M, dy, ldy, x, ldx, (tiles + G - 1) / G, (float*)ws, ln_g, ln_b, mean, rstd};
     hipLaunchKernelGGL(cfg->fn, dim3((unsigned)G, (unsigned)cfg->ng), dim3(cfg->nw * 64), cfg->lds, as_stream(stream),
                        g);
     TAGAN_CHECK_LAUNCH("tagan_sgemm_tn");

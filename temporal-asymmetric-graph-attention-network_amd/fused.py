@@ -270,6 +270,34 @@ def _sg_use(H: int, bf: bool, act: bool) -> bool:
     return ok
 
 
+# TAGAN_SG_LN=0: the stream_gemm block with standalone LayerNorm kernels instead of the LayerNorm-fused GEMMs (LN1 in
+# the QKV projection's prologue, dropout + residual + LN2 [+ skip LN] in the out-projection's epilogue, LN1's backward
+# in the QKV input gradient's epilogue, h = LN1(x) recomputed inside the QKV weight gradient; A/B knob)
+# TAGAN_SG_LN = comma list of the fused ops ("in", "out", "bwd"), "all", "0"/"none", or "auto" (default): the
+# measured-best set per precision.  Interleaved C2 A/B on one MI355X (tools/runs/sgln_check.sh,
+# profiles/r3c_sgln_ab.txt), ms per step fp32 / bf16: none 7.16 / 5.64, in 6.93 / 5.57, in+out 7.01 / 5.49,
+# all 7.43 / 5.67.  The epilogue forms need a whole output row per workgroup, so each workgroup alternates a
+# matrix phase and a memory phase split by a barrier; with the fp32 (three-plane) weights resident in registers
+# only one workgroup fits a CU and nothing overlaps those phases (out: +0.08 ms in fp32, -0.08 ms in bf16 where two
+# fit; bwd: +0.4 ms, its K = 384 weight fragments alone take 144 VGPRs).
+_SG_LN_ENV = os.environ.get("TAGAN_SG_LN", "auto").strip().lower()
+SG_LN_SET = (set() if _SG_LN_ENV in ("0", "none", "") else
+             {"in", "out", "bwd"} if _SG_LN_ENV in ("1", "all") else
+             None if _SG_LN_ENV == "auto" else set(_SG_LN_ENV.split(",")))
+_SG_LN_OK = {}
+
+
+def _sg_ln_use(H: int, bf: bool, act: bool, op: str) -> bool:
+    ops = SG_LN_SET if SG_LN_SET is not None else ({"in", "out"} if bf else {"in"})
+    if op not in ops:
+        return False
+    key = (H, bf, act, op)
+    ok = _SG_LN_OK.get(key)
+    if ok is None:
+        ok = _SG_LN_OK[key] = sg.ln_supported(H, 1 if bf else 3, act, op)
+    return ok
+
+
 # TAGAN_QKV_PACK=0: torch.cat of the q/k/v parameters per block instead of PackQKVFn's one-launch pack (A/B)
 QKV_PACK = os.environ.get("TAGAN_QKV_PACK", "1") != "0"
 # TAGAN_QKV_AUG=0: QKV GEMM with the hipBLASLt bias epilogue instead of the bias-as-weight-column form (A/B)
@@ -490,18 +518,29 @@ class AttnBlockFn(torch.autograd.Function):
         products on k_sgemm_tn (csrc/stream_gemm.hip); LayerNorm, core and dropout as in the library form."""
         P = 1 if bf else 3
         adt = torch.bfloat16 if act else torch.float32
-        h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False, y_dtype=adt)
-        qkv = sg.nt(h, sg.wprep(w_qkv, False, P), 3 * H, P, bias=b_qkv.contiguous(), out_dtype=adt)
-        c, saved = core.fwd(qkv, p1, p2)
-        o = sg.nt(c, sg.wprep(w_o, False, P), H, P)          # the bias is added in the closing LayerNorm
-        skip = None
-        if lns_w is not None:
-            y, s2, mean2, rstd2, skip = ln_skip_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, lns_w, lns_b, eps_s,
-                                                    a_bias=b_o)
+        lnf = _sg_ln_use(H, bf, act, "in")
+        ln_out = _sg_ln_use(H, bf, act, "out")
+        if lnf:   # LN1 in the QKV projection's prologue: h is never stored
+            h = None
+            qkv, mean1, rstd1 = sg.nt_ln_in(x2, ln1_w, ln1_b, eps1, sg.wprep(w_qkv, False, P), 3 * H, P,
+                                            bias=b_qkv.contiguous(), out_dtype=adt)
         else:
-            y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True, a_bias=b_o)
+            h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False, y_dtype=adt)
+            qkv = sg.nt(h, sg.wprep(w_qkv, False, P), 3 * H, P, bias=b_qkv.contiguous(), out_dtype=adt)
+        c, saved = core.fwd(qkv, p1, p2)
+        if ln_out:   # dropout + residual + LN2 (+ the skip LayerNorm) in the out-projection's epilogue
+            y, s2, mean2, rstd2, skip = sg.nt_ln_out(c, sg.wprep(w_o, False, P), P, b_o.contiguous(), x2, p_out,
+                                                     seed_out, ln2_w, ln2_b, eps2, lns_w, lns_b, eps_s)
+        else:
+            o = sg.nt(c, sg.wprep(w_o, False, P), H, P)          # the bias is added in the closing LayerNorm
+            skip = None
+            if lns_w is not None:
+                y, s2, mean2, rstd2, skip = ln_skip_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, lns_w, lns_b,
+                                                        eps_s, a_bias=b_o)
+            else:
+                y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True, a_bias=b_o)
         ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
-        ctx.inter = (h, None, mean1, rstd1, qkv, c, c, saved, s2, mean2, rstd2, skip)
+        ctx.inter = (h, ln1_b if lnf else None, mean1, rstd1, qkv, c, c, saved, s2, mean2, rstd2, skip)
         ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, "sgemm")
         ctx.sink = sink
         ctx.packed_aug = False
@@ -510,8 +549,9 @@ class AttnBlockFn(torch.autograd.Function):
     @staticmethod
     def _bwd_sgemm(ctx, dy):
         x2, ln1_w, w_qkv, w_o, ln2_w, lns_w = ctx.saved_tensors
-        h, _, mean1, rstd1, qkv, c, _, saved, s2, mean2, rstd2, skip = ctx.inter
+        h, ln1_b, mean1, rstd1, qkv, c, _, saved, s2, mean2, rstd2, skip = ctx.inter
         core, p_out, seed_out, shape, bf, act, _ = ctx.cfg
+        lnf = h is None   # the LayerNorm-fused form (h = LN1(x) recomputed where it is needed)
         ng = ctx.needs_input_grad
         H = shape[-1]
         P = 1 if bf else 3
@@ -528,12 +568,20 @@ class AttnBlockFn(torch.autograd.Function):
         del dc, do
         dw_qkv = db_qkv = None
         if ng[5] or (ng[6] and db_core is None):
-            dw_qkv, db_qkv = sg.tn(dqkv, h, P, want_dw=bool(ng[5]), want_db=bool(ng[6]) and db_core is None)
+            if lnf:
+                dw_qkv, db_qkv = sg.tn_ln(dqkv, x2, ln1_w, ln1_b, mean1, rstd1, P, want_dw=bool(ng[5]),
+                                          want_db=bool(ng[6]) and db_core is None)
+            else:
+                dw_qkv, db_qkv = sg.tn(dqkv, h, P, want_dw=bool(ng[5]), want_db=bool(ng[6]) and db_core is None)
         if db_core is not None:
             db_qkv = db_core
-        dh = sg.nt(dqkv, sg.wprep(w_qkv, True, P), H, P)
-        del dqkv
-        dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
+        if _sg_ln_use(H, bf, act, "bwd"):   # dh = dqkv·W_qkv and LN1's backward in one kernel
+            dx, dg1, db1 = sg.nt_ln_bwd(dqkv, sg.wprep(w_qkv, True, P), P, x2, mean1, rstd1, ln1_w, dres)
+            del dqkv
+        else:
+            dh = sg.nt(dqkv, sg.wprep(w_qkv, True, P), H, P)
+            del dqkv
+            dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
         ctx.inter = None
         return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
                 None, None, None, None, None, dgs, dbs, None, None, None)

@@ -63,3 +63,83 @@ def tn(dy: torch.Tensor, x: torch.Tensor, planes: int, want_dw=True, want_db=Tru
                            ptr(dw) if want_dw else None, dw.stride(0) if want_dw else K,
                            ptr(db) if want_db else None, ptr(ws), wsb, stream_of(dy)), "tagan_sgemm_tn")
     return (dw if want_dw else None), (db if want_db else None)
+
+
+# ----------------------------------------------------------------------------- LayerNorm-fused forms (H = 128)
+LN_OPS = {"in": 1, "out": 2, "bwd": 3}
+
+
+def ln_supported(H: int, planes: int, act_bf16: bool, op: str = "in") -> bool:
+    """The LN-fused kernel(s) of one op exist at this H / precision (tagan_sgemm_ln_supported): "in" = LN1 prologue
+    of the QKV projection + its LN-recomputing weight gradient, "out" = out-projection + LN2 epilogue, "bwd" = QKV
+    input gradient + LN1-backward epilogue."""
+    return bool(lib().tagan_sgemm_ln_supported(H, planes, TAGAN_BF16 if act_bf16 else 0, LN_OPS[op]))
+
+
+def nt_ln_in(x, ln_w, ln_b, eps, wp, N: int, planes: int, bias=None, out_dtype=torch.float32):
+    """out = LN(x)·Bᵀ + bias with LN in the GEMM prologue; returns out [M, N], mean [M], rstd [M]."""
+    M, K = x.shape
+    assert x.dtype == torch.float32 and x.stride(1) == 1
+    out = torch.empty(M, N, dtype=out_dtype, device=x.device)
+    st = torch.empty(2, M, device=x.device)
+    check(lib().tagan_sgemm_nt_ln_in(dtype_code(out), M, N, K, ptr(x), x.stride(0), ptr(ln_w), ptr(ln_b), float(eps),
+                                     ptr(wp), planes, ptr(bias), ptr(out), out.stride(0), ptr(st[0]), ptr(st[1]),
+                                     stream_of(x)), "tagan_sgemm_nt_ln_in")
+    return out, st[0], st[1]
+
+
+def tn_ln(dy, x, ln_w, ln_b, mean, rstd, planes: int, want_dw=True, want_db=True):
+    """dw = dyᵀ·LN(x), db = Σ_rows dy with LN(x) recomputed from x and the forward's statistics."""
+    M, N = dy.shape
+    K = x.shape[1]
+    assert x.shape[0] == M and x.dtype == torch.float32 and x.stride(1) == 1
+    if dy.stride(1) != 1:
+        dy = dy.contiguous()
+    L = lib()
+    dw = torch.empty(N, K, device=dy.device) if want_dw else None
+    db = torch.empty(N, device=dy.device) if want_db else None
+    wsb = int(L.tagan_sgemm_tn_workspace(M, N, K))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dy.device)
+    check(L.tagan_sgemm_tn_ln(dtype_code(dy), M, N, K, ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(ln_w),
+                              ptr(ln_b), ptr(mean), ptr(rstd), planes, ptr(dw), K, ptr(db), ptr(ws), wsb,
+                              stream_of(dy)), "tagan_sgemm_tn_ln")
+    return dw, db
+
+
+def nt_ln_out(a, wp, planes: int, bias, res, p_drop: float, seed: int, ln_w, ln_b, eps, gs=None, bs=None,
+              eps_s: float = 1e-5):
+    """y = LN(dropout(a·Bᵀ + bias) + res) [+ LN_s(res)]; returns y, s (the LN input), mean, rstd, skip stats."""
+    M, H = res.shape
+    if a.stride(1) != 1:
+        a = a.contiguous()
+    dev = res.device
+    y = torch.empty(M, H, device=dev)
+    s = torch.empty(M, H, device=dev)
+    st = torch.empty(4 if gs is not None else 2, M, device=dev)
+    skip = (st[2], st[3]) if gs is not None else None
+    check(lib().tagan_sgemm_nt_ln_out(dtype_code(a), M, H, ptr(a), a.stride(0), ptr(wp), planes, ptr(bias), ptr(res),
+                                      float(p_drop), seed, ptr(ln_w), ptr(ln_b), float(eps), ptr(gs), ptr(bs),
+                                      float(eps_s), ptr(s), ptr(y), ptr(st[0]), ptr(st[1]),
+                                      ptr(skip[0]) if skip else None, ptr(skip[1]) if skip else None, stream_of(res)),
+          "tagan_sgemm_nt_ln_out")
+    return y, s, st[0], st[1], skip
+
+
+def nt_ln_bwd(a, wp, planes: int, x, mean, rstd, gamma, dres=None):
+    """dh = a·Bᵀ and the LayerNorm backward of h = LN(x) in the epilogue; returns dx, dgamma, dbeta."""
+    M, K = a.shape
+    H = x.shape[1]
+    dev = x.device
+    if M == 0:
+        return torch.empty(0, H, device=dev), torch.zeros(H, device=dev), torch.zeros(H, device=dev)
+    if a.stride(1) != 1:
+        a = a.contiguous()
+    dx = torch.empty(M, H, device=dev)
+    dgb = torch.empty(2, H, device=dev)
+    L = lib()
+    wsb = int(L.tagan_sgemm_nt_ln_bwd_workspace(M, H, K))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    check(L.tagan_sgemm_nt_ln_bwd(dtype_code(a), M, H, K, ptr(a), a.stride(0), ptr(wp), planes, ptr(x), ptr(mean),
+                                  ptr(rstd), ptr(gamma), ptr(dres), ptr(dx), ptr(dgb[0]), ptr(dgb[1]), ptr(ws), wsb,
+                                  stream_of(a)), "tagan_sgemm_nt_ln_bwd")
+    return dx, dgb[0], dgb[1]

@@ -1,0 +1,203 @@
+"""LayerNorm-fused projection GEMMs (csrc/stream_gemm.hip MODE_LN_IN / MODE_LN_OUT / MODE_LN_BWD and the LN-recomputing
+weight gradient) through the C-ABI, against fp64 restatements of the unfused chain they replace:
+
+  LN1 + QKV projection        geometric_attention.py:541-548 / temporal_attention.py:985-990
+  out-projection + dropout + residual + LN2 (+ skip LN)  geometric_attention.py:586-596, model.py:258-262
+  their backward (LN1 backward after the QKV input gradient; the QKV weight gradient of h = LN1(x)).
+
+fp32 mode (three bf16 planes): outputs within 2e-5 of max|ref| elementwise and 1e-5 normwise (fp32-GEMM accuracy
+on O(1) LayerNorm outputs).  bf16 planes: within 1e-2 normwise.  The dropout mask of the out-projection epilogue
+must be the standalone LayerNorm kernel's (same hash, stream = row, counter = column): checked by running both on
+the same inputs.  Statistics (mean, rstd) to 1e-5 relative.  dgamma / dbeta are fixed-order sums (bitwise
+reproducible).  Rows: ragged counts (1, 15, 33, 1000, 40961)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+H = 128
+ROWS = [1, 15, 33, 1000, 40961]
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import tagan_amd  # noqa: F401
+    return torch.device("cuda:0")
+
+
+def _nerr(x, ref):
+    return float((x.double() - ref).norm() / ref.norm().clamp_min(1e-300))
+
+
+def _merr(x, ref):
+    return float((x.double() - ref).abs().max() / ref.abs().max().clamp_min(1e-300))
+
+
+def _ln64(x, g, b, eps):
+    x = x.double()
+    m = x.mean(1, keepdim=True)
+    v = ((x - m) ** 2).mean(1, keepdim=True)
+    rs = 1.0 / torch.sqrt(v + eps)
+    return (x - m) * rs * g.double() + b.double(), m[:, 0], rs[:, 0]
+
+
+def _params(dev, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    ln_w = 1.0 + 0.1 * torch.randn(H, device=dev, generator=g)
+    ln_b = 0.1 * torch.randn(H, device=dev, generator=g)
+    return g, ln_w, ln_b
+
+
+@pytest.mark.parametrize("M", ROWS)
+@pytest.mark.parametrize("planes,store", [(3, "fp32"), (1, "bf16")])
+def test_ln_in_qkv(M, planes, store):
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    g, ln_w, ln_b = _params(dev, M + planes)
+    x = 0.5 + 2.0 * torch.randn(M, H, device=dev, generator=g)
+    w = torch.randn(3 * H, H, device=dev, generator=g) / H ** 0.5
+    bias = torch.randn(3 * H, device=dev, generator=g)
+    dt = torch.bfloat16 if store == "bf16" else torch.float32
+    out, mean, rstd = sg.nt_ln_in(x, ln_w, ln_b, 1e-5, sg.wprep(w, False, planes), 3 * H, planes, bias=bias,
+                                  out_dtype=dt)
+    h, m64, rs64 = _ln64(x, ln_w, ln_b, 1e-5)
+    ref = h @ w.double().t() + bias.double()
+    assert out.dtype == dt
+    assert _merr(mean, m64) <= 1e-5 and _merr(rstd, rs64) <= 1e-5
+    if planes == 3:
+        assert _merr(out, ref) <= 2e-5 and _nerr(out, ref) <= 1e-5, (_merr(out, ref), _nerr(out, ref))
+    else:
+        assert _nerr(out, ref) < 1e-2
+    # the weight gradient of h = LN(x), h recomputed from x and the statistics just written
+    dq = torch.randn(M, 3 * H, device=dev, generator=g).to(dt)
+    dw, db = sg.tn_ln(dq, x, ln_w, ln_b, mean, rstd, planes)
+    refw = dq.double().t() @ h
+    if planes == 3:
+        assert _merr(dw, refw) <= 2e-5, _merr(dw, refw)
+    else:
+        assert _nerr(dw, refw) < 1e-2
+    assert _merr(db, dq.double().sum(0)) <= (2e-6 if planes == 3 else 1e-3)
+    dw2, db2 = sg.tn_ln(dq, x, ln_w, ln_b, mean, rstd, planes)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+def test_ln_in_recompute_matches_stored_h():
+    """The weight gradient over the recomputed h equals the plain weight gradient over a stored LN(x) computed with
+    the same statistics (bf16 plane: the same rounding of the same fp32 value)."""
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    g, ln_w, ln_b = _params(dev, 5)
+    M = 5000
+    x = torch.randn(M, H, device=dev, generator=g)
+    w = torch.randn(3 * H, H, device=dev, generator=g) / H ** 0.5
+    _, mean, rstd = sg.nt_ln_in(x, ln_w, ln_b, 1e-5, sg.wprep(w, False, 1), 3 * H, 1, out_dtype=torch.bfloat16)
+    # fma(t, g, b) with t = (x - m) rs in fp32: the fp64 t·g + b rounded once to fp32 (t·g is exact in fp64)
+    t = (x - mean[:, None]) * rstd[:, None]
+    h = (t.double() * ln_w.double() + ln_b.double()).float()
+    dq = torch.randn(M, 3 * H, device=dev, generator=g).to(torch.bfloat16)
+    dw_a, _ = sg.tn_ln(dq, x, ln_w, ln_b, mean, rstd, 1)
+    dw_b, _ = sg.tn(dq, h.to(torch.bfloat16), 1)
+    assert _merr(dw_a, dw_b.double()) <= 1e-5
+
+
+@pytest.mark.parametrize("M", ROWS)
+@pytest.mark.parametrize("planes,store", [(3, "fp32"), (1, "bf16")])
+@pytest.mark.parametrize("skip", [False, True])
+def test_ln_out(M, planes, store, skip):
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    g, ln_w, ln_b = _params(dev, 100 + M + planes)
+    dt = torch.bfloat16 if store == "bf16" else torch.float32
+    a = torch.randn(M, H, device=dev, generator=g).to(dt)
+    res = torch.randn(M, H, device=dev, generator=g)
+    w = torch.randn(H, H, device=dev, generator=g) / H ** 0.5
+    bias = torch.randn(H, device=dev, generator=g)
+    gs = bs = None
+    if skip:
+        gs = 1.0 + 0.1 * torch.randn(H, device=dev, generator=g)
+        bs = 0.1 * torch.randn(H, device=dev, generator=g)
+    y, s, mean, rstd, sk = sg.nt_ln_out(a, sg.wprep(w, False, planes), planes, bias, res, 0.0, 0, ln_w, ln_b, 1e-5,
+                                        gs, bs, 1e-5)
+    s64 = a.double() @ w.double().t() + bias.double() + res.double()
+    y64, m64, rs64 = _ln64(s64, ln_w, ln_b, 1e-5)
+    if skip:
+        ys, ms64, rss64 = _ln64(res, gs, bs, 1e-5)
+        y64 = y64 + ys
+        assert _merr(sk[0], ms64) <= 1e-5 and _merr(sk[1], rss64) <= 1e-5
+    tol = (2e-5, 1e-5) if planes == 3 else (5e-2, 1e-2)
+    assert _merr(s, s64) <= tol[0] and _nerr(s, s64) <= tol[1], (_merr(s, s64), _nerr(s, s64))
+    assert _merr(y, y64) <= tol[0] and _nerr(y, y64) <= tol[1], (_merr(y, y64), _nerr(y, y64))
+    assert _merr(mean, m64) <= (1e-5 if planes == 3 else 1e-2) and _merr(rstd, rs64) <= (1e-5 if planes == 3 else 1e-2)
+
+
+@pytest.mark.parametrize("skip", [False, True])
+def test_ln_out_dropout_matches_layernorm_kernel(skip):
+    """The epilogue's dropout decisions and LayerNorm equal the standalone chain on the same o = a·Wᵀ."""
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    from tagan_amd.fused import ln_fwd, ln_skip_fwd
+    g, ln_w, ln_b = _params(dev, 77)
+    M = 3001
+    a = torch.randn(M, H, device=dev, generator=g)
+    res = torch.randn(M, H, device=dev, generator=g)
+    w = torch.randn(H, H, device=dev, generator=g) / H ** 0.5
+    bias = torch.randn(H, device=dev, generator=g)
+    gs = 1.0 + 0.1 * torch.randn(H, device=dev, generator=g) if skip else None
+    bs = 0.1 * torch.randn(H, device=dev, generator=g) if skip else None
+    wp = sg.wprep(w, False, 3)
+    y, s, mean, rstd, sk = sg.nt_ln_out(a, wp, 3, bias, res, 0.1, 1234, ln_w, ln_b, 1e-5, gs, bs, 1e-5)
+    o = sg.nt(a, wp, H, 3)
+    if skip:
+        y2, s2, m2, r2, sk2 = ln_skip_fwd(o, res, 0.1, 1234, ln_w, ln_b, 1e-5, gs, bs, 1e-5, a_bias=bias)
+    else:
+        y2, s2, m2, r2 = ln_fwd(o, res, 0.1, 1234, ln_w, ln_b, 1e-5, True, a_bias=bias)
+    dropped = (s - res).abs() < 1e-30
+    dropped2 = (s2 - res).abs() < 1e-30
+    assert torch.equal(dropped, dropped2)
+    assert 0.05 < float(dropped.float().mean()) < 0.15
+    assert _merr(s, s2.double()) <= 1e-5 and _merr(y, y2.double()) <= 1e-5
+    assert _merr(mean, m2.double()) <= 1e-5 and _merr(rstd, r2.double()) <= 1e-5
+
+
+@pytest.mark.parametrize("M", ROWS)
+@pytest.mark.parametrize("planes,store", [(3, "fp32"), (1, "bf16")])
+@pytest.mark.parametrize("with_dres", [True, False])
+def test_ln_bwd(M, planes, store, with_dres):
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    g, ln_w, ln_b = _params(dev, 300 + M + planes)
+    dt = torch.bfloat16 if store == "bf16" else torch.float32
+    x = 0.3 + torch.randn(M, H, device=dev, generator=g)
+    _, m64, rs64 = _ln64(x, ln_w, ln_b, 1e-5)
+    mean, rstd = m64.float(), rs64.float()
+    dq = torch.randn(M, 3 * H, device=dev, generator=g).to(dt)
+    wq = torch.randn(3 * H, H, device=dev, generator=g) / H ** 0.5          # nn.Linear weight [3H, H]
+    dres = torch.randn(M, H, device=dev, generator=g) if with_dres else None
+    dx, dg, db = sg.nt_ln_bwd(dq, sg.wprep(wq, True, planes), planes, x, mean, rstd, ln_w, dres)
+    dh = dq.double() @ wq.double()
+    xh = (x.double() - mean.double()[:, None]) * rstd.double()[:, None]
+    gd = dh * ln_w.double()
+    c1 = (gd * xh).mean(1, keepdim=True)
+    c2 = gd.mean(1, keepdim=True)
+    ref = rstd.double()[:, None] * (gd - c1 * xh - c2)
+    if with_dres:
+        ref = ref + dres.double()
+    rdg = (dh * xh).sum(0)
+    rdb = dh.sum(0)
+    if planes == 3:
+        assert _merr(dx, ref) <= 2e-5 and _nerr(dx, ref) <= 1e-5, (_merr(dx, ref), _nerr(dx, ref))
+        assert _merr(dg, rdg) <= 2e-5 and _merr(db, rdb) <= 2e-5
+    else:
+        assert _nerr(dx, ref) < 1e-2 and _nerr(dg, rdg) < 1e-2 and _nerr(db, rdb) < 1e-2
+    dx2, dg2, db2 = sg.nt_ln_bwd(dq, sg.wprep(wq, True, planes), planes, x, mean, rstd, ln_w, dres)
+    assert torch.equal(dx, dx2) and torch.equal(dg, dg2) and torch.equal(db, db2)
+
+
+def test_ln_supported_shapes():
+    _dev()
+    from tagan_amd import stream_gemm as sg
+    for op in ("in", "out", "bwd"):
+        assert sg.ln_supported(128, 3, False, op) and sg.ln_supported(128, 1, True, op)
+        assert sg.ln_supported(128, 1, False, op)
+        assert not sg.ln_supported(256, 3, False, op)
