@@ -790,8 +790,9 @@ def main():
                  if gemm_table else "library-default heuristic")
     if _fused._sg_use(H, args.precision != "fp32", args.precision == "bf16"):
         lib_gemms = ("attention-block projections: hand-written bf16-matrix-core kernels (csrc/stream_gemm.hip; "
-                     "fp32 mode as three bf16 planes, six plane products, fp32 accumulate; LN1 fused into the QKV "
-                     "projection's prologue, in bf16 mode dropout + residual + LN2 into the out-projection's "
+                     "fp32 mode as three bf16 planes, six plane products, fp32 accumulate; the N = 128 products on "
+                     "row-owner kernels; LN1 fused into the QKV projection's prologue, dropout + residual + LN2 into "
+                     "the out-projection's epilogue, in bf16 mode also LN1's backward into the QKV input gradient's "
                      "epilogue); node embedding, head and GRU GEMMs: " + lib_gemms)
     rec["config"]["gemms"] = lib_gemms
     rec["launch"] = (("hip-graph (one replay per step)" if world == 1 else

@@ -245,13 +245,16 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
             const int rl = MODE == MODE_LN_IN ? (c >> 4) & 15 : c & 15;
             const int q = MODE == MODE_LN_IN ? c & 15 : (c >> 4) % QK;
             const int rh = MODE == MODE_LN_IN ? c >> 8 : (c >> 4) / QK;
-            const int64_t row = t * BM + rh * 16 + rl;
+            // rows past M reload row M - 1: they only feed output rows that are never stored, and an unconditional
+            // load needs no zero-filled destination (a conditional one made the compiler drain every store of the
+            // previous tile -- s_waitcnt vmcnt(0) -- before this prefetch could issue)
+            const int64_t row0 = t * BM + rh * 16 + rl;
+            const int64_t row = row0 < g.M ? row0 : g.M - 1;
             if constexpr (ABF) {
-                pb[i] = make_uint4(0, 0, 0, 0);
-                if (row < g.M) pb[i] = *reinterpret_cast<const uint4*>((const uint16_t*)g.a + row * g.lda + 8 * q);
+                pb[i] = *reinterpret_cast<const uint4*>((const uint16_t*)g.a + row * g.lda + 8 * q);
             } else {
-                float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
-                if (row < g.M) {
+                float4 v0, v1;
+                {
                     const float* src = (const float*)g.a + row * g.lda + 8 * q;
                     v0 = *reinterpret_cast<const float4*>(src);
                     v1 = *reinterpret_cast<const float4*>(src + 4);
@@ -307,7 +310,12 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
     __syncthreads();
     for (int it = 0;; ++it) {
         const int64_t next = tile + gridDim.x;
-        if (next < ntiles) load(next);
+        // the prefetch is unconditional (the last tile re-stages itself into the idle buffer): with a conditional
+        // one the compiler could not prove the loads drained at the back edge and waited for every store of the
+        // tile (s_waitcnt vmcnt(0)) before the next prefetch could issue
+        const int64_t pre = next < ntiles ? next : tile;
+        load(pre);
+        __builtin_amdgcn_sched_barrier(0);
         // epilogue operands of this tile (in flight under the MFMAs): the residual rows (LN_OUT: res, LN_BWD: the LN
         // input x and dres) and the LN_BWD row statistics
         f32x4 er[EPI ? J : 1][EPI ? NSUB : 1], ed[MODE == MODE_LN_BWD ? J : 1][MODE == MODE_LN_BWD ? NSUB : 1];
@@ -347,8 +355,25 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
             }
         }
         // stage the next tile first: its loads were issued before this tile's MFMAs, and waiting for them after
-        // the output stores would wait for the stores too
-        if (next < ntiles) stash(sg_lds + ((it + 1) & 1) * BUF, next);
+        // the output stores would wait for the stores too.  Scheduling barriers pin the order prefetch -> MFMAs ->
+        // stash: otherwise the scheduler sinks the prefetch loads to their use or hoists the stash (it writes the
+        // other LDS buffer) above the MFMAs, and either way the loads no longer overlap the matrix work; the empty
+        // asm statements keep the IR passes from moving the plane split of the prefetched values up to the loads
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int s = 0; s < NSUB; ++s) asm volatile("" : "+v"(acc[j][s]));
+        if constexpr (ABF) {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) asm volatile("" : "+v"(pb[i].x), "+v"(pb[i].y), "+v"(pb[i].z), "+v"(pb[i].w));
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) asm volatile("" : "+v"(pf[i][e]));
+        }
+        stash(sg_lds + ((it + 1) & 1) * BUF, pre);
         if constexpr (EPI) {
             if constexpr (MODE == MODE_LN_BWD) {   // dres is read in pass 2 only: its loads fly under pass 1
 #pragma unroll
@@ -526,6 +551,226 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
                     g.part[(int64_t)blockIdx.x * 2 * NW * NSUB * 16 * gridDim.y + NW * NSUB * 16 * gridDim.y + col] = b;
                 }
             }
+    }
+}
+
+// ------------------------------------------------------------------------------------------- row-owner NT (N = 128)
+// For the N = H = 128 products (out-projection forward, its input gradient, the QKV input gradient) and their
+// LayerNorm-fused forms: ONE WAVE OWNS WHOLE 16-ROW OUTPUT TILES.  B's bf16 planes sit in LDS (staged once per
+// workgroup in k_sgemm_wprep's fragment order, read back with one conflict-free ds_read_b128 per fragment); each wave
+// loads its A fragments straight from HBM into MFMA operand registers (lane (c, t): row c, k = 32 kk + 8 t + [0, 8):
+// 32 or 16 contiguous bytes), splits them into planes in registers, and runs 8 n-subtiles x K/32 x (6 | 1) MFMAs.
+// The finished row is then entirely inside the wave (lanes c, c ^ 16, c ^ 32, c ^ 48 hold 4 columns of each
+// n-subtile), so a LayerNorm's row statistics are two shuffles: no LDS hand-off and no workgroup barrier in the tile
+// loop -- the W waves of a CU run their tiles independently and overlap each other's memory and matrix phases (the
+// weight-stationary k_sgemm_nt needs one barrier per tile for a row-wide epilogue and measured slower there).
+template <int K, int P, bool ABF, bool CBF, int MODE, int W>
+__global__ void __launch_bounds__(W * 64) k_rowgemm(NtArgs g) {
+    constexpr int NS = 8, N = 128, KK = K / 32;
+    constexpr int NB = NS * KK * P * 64;             // B fragments (uint4) in LDS
+    static_assert(!ABF || P == 1, "bf16 operands have one plane");
+    extern __shared__ uint4 sg_lds[];
+    float* prm = reinterpret_cast<float*>(sg_lds + NB);   // [5][N]: gamma | beta | gamma_s | beta_s | bias
+    float* wred = prm + 5 * N;                            // LN_BWD: [W][2N] wave partials of dgamma | dbeta
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 15, gq = lane >> 4;
+    for (int i = threadIdx.x; i < NB; i += W * 64) sg_lds[i] = g.wp[i];
+    for (int i = threadIdx.x; i < 5 * N; i += W * 64) {
+        const int q = i / N, col = i % N;
+        const float* src = q == 0 ? g.ln_g : q == 1 ? g.ln_b : q == 2 ? g.gs : q == 3 ? g.bs : g.bias;
+        prm[i] = (src && (q == 4 || (MODE == MODE_LN_OUT) || (MODE == MODE_LN_BWD && q == 0))) ? src[col] : 0.f;
+    }
+    __syncthreads();
+    if constexpr (MODE == MODE_LN_OUT) {
+        if (g.seed_ctr) g.seed ^= *g.seed_ctr * 0x9E3779B97F4A7C15ull;   // TAGAN_LIVE_SEED
+    }
+    auto pv = [&](int q, int s) { return *reinterpret_cast<const f32x4*>(prm + q * N + 16 * s + 4 * gq); };
+    f32x4 dgacc[MODE == MODE_LN_BWD ? NS : 1], dbacc[MODE == MODE_LN_BWD ? NS : 1];
+    if constexpr (MODE == MODE_LN_BWD) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) dgacc[s] = dbacc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int64_t ntiles = (g.M + 15) / 16;
+    for (int64_t t = (int64_t)blockIdx.x * W + w; t < ntiles; t += (int64_t)gridDim.x * W) {
+        const int64_t row0 = t * 16 + c;
+        const bool live = row0 < g.M;
+        const int64_t row = live ? row0 : g.M - 1;   // dead rows recompute row M - 1 and store nothing
+        // B's LDS reads are the same every tile: behind an opaque copy of the lane index the compiler cannot hoist
+        // them out of the tile loop (it would hold every fragment in registers and spill)
+        int lb = lane;
+        asm volatile("" : "+v"(lb));
+        uint4 ar[ABF ? KK : 1];
+        float4 af[ABF ? 1 : KK][2];
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+            if constexpr (ABF) {
+                ar[kk] = *reinterpret_cast<const uint4*>((const uint16_t*)g.a + row * g.lda + 32 * kk + 8 * gq);
+            } else {
+                const float* src = (const float*)g.a + row * g.lda + 32 * kk + 8 * gq;
+                af[kk][0] = *reinterpret_cast<const float4*>(src);
+                af[kk][1] = *reinterpret_cast<const float4*>(src + 4);
+            }
+        }
+        f32x4 acc[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) acc[s] = pv(4, s);
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+            bf16x8 ap[P];
+            if constexpr (ABF) {
+                ap[0] = __builtin_bit_cast(bf16x8, ar[kk]);
+            } else {
+                uint32_t pl[4][P];
+                split2<P>(af[kk][0].x, af[kk][0].y, pl[0]);
+                split2<P>(af[kk][0].z, af[kk][0].w, pl[1]);
+                split2<P>(af[kk][1].x, af[kk][1].y, pl[2]);
+                split2<P>(af[kk][1].z, af[kk][1].w, pl[3]);
+#pragma unroll
+                for (int p = 0; p < P; ++p)
+                    ap[p] = __builtin_bit_cast(bf16x8, make_uint4(pl[0][p], pl[1][p], pl[2][p], pl[3][p]));
+            }
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                bf16x8 bp[P];
+#pragma unroll
+                for (int p = 0; p < P; ++p) bp[p] = __builtin_bit_cast(bf16x8, sg_lds[((s * KK + kk) * P + p) * 64 + lb]);
+                acc[s] = mfma_planes<P>(bp, ap, acc[s]);
+            }
+        }
+        // lane holds C[row][16 s + 4 gq + e], e = 0..3, for every n-subtile s
+        if constexpr (MODE == MODE_PLAIN) {
+            if (live) {
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    const int64_t off = row * g.ldc + 16 * s + 4 * gq;
+                    if constexpr (CBF) {
+                        *reinterpret_cast<uint2*>((uint16_t*)g.c + off) = make_uint2(pk_bf16(acc[s][0], acc[s][1]),
+                                                                                     pk_bf16(acc[s][2], acc[s][3]));
+                    } else {
+                        *reinterpret_cast<f32x4*>((float*)g.c + off) = acc[s];
+                    }
+                }
+            }
+        } else if constexpr (MODE == MODE_LN_OUT) {
+            const uint32_t key = drop_key(g.seed, (uint64_t)row0);
+            float sm = 0.f, sr = 0.f;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const int col = 16 * s + 4 * gq;
+                const f32x4 r = *reinterpret_cast<const f32x4*>(g.res + row * g.ldr + col);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float x = acc[s][e];
+                    if (g.p_drop > 0.f) x = drop_u(key, (uint32_t)(col + e)) >= g.p_drop ? x * g.inv_keep : 0.f;
+                    x += r[e];
+                    acc[s][e] = x;
+                    sm += x;
+                    sr += r[e];
+                }
+                if (live) *reinterpret_cast<f32x4*>(g.s_out + row * g.ldc + col) = acc[s];
+            }
+            const float mean = gsum4(sm) / (float)N;
+            float sq = 0.f;
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sq += (acc[s][e] - mean) * (acc[s][e] - mean);
+            const float rstd = 1.f / sqrtf(gsum4(sq) / (float)N + g.eps);
+            float means = 0.f, rstds = 0.f;
+            if (g.gs) {   // skip branch: statistics of the residual rows (re-read: L1 / L2 hits)
+                means = gsum4(sr) / (float)N;
+                float sqs = 0.f;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    const f32x4 r = *reinterpret_cast<const f32x4*>(g.res + row * g.ldr + 16 * s + 4 * gq);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) sqs += (r[e] - means) * (r[e] - means);
+                }
+                rstds = 1.f / sqrtf(gsum4(sqs) / (float)N + g.eps_s);
+            }
+            if (live) {
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    const int col = 16 * s + 4 * gq;
+                    const f32x4 ga = pv(0, s), be = pv(1, s);
+                    f32x4 y;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) y[e] = (acc[s][e] - mean) * rstd * ga[e] + be[e];
+                    if (g.gs) {
+                        const f32x4 r = *reinterpret_cast<const f32x4*>(g.res + row * g.ldr + col);
+                        const f32x4 gs = pv(2, s), bs = pv(3, s);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) y[e] += (r[e] - means) * rstds * gs[e] + bs[e];
+                    }
+                    *reinterpret_cast<f32x4*>((float*)g.c + row * g.ldc + col) = y;
+                }
+                if (gq == 0) {
+                    g.mean[row] = mean;
+                    g.rstd[row] = rstd;
+                    if (g.gs) {
+                        g.mean_s[row] = means;
+                        g.rstd_s[row] = rstds;
+                    }
+                }
+            }
+        } else {   // MODE_LN_BWD: acc = dh
+            const float m = g.mean[row], rs = g.rstd[row];
+            float c1 = 0.f, c2 = 0.f;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const f32x4 x = *reinterpret_cast<const f32x4*>(g.res + row * g.ldr + 16 * s + 4 * gq);
+                const f32x4 ga = pv(0, s);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float xv = (x[e] - m) * rs, gd = acc[s][e] * ga[e];
+                    c1 += gd * xv;
+                    c2 += gd;
+                    if (live) {
+                        dgacc[s][e] += acc[s][e] * xv;
+                        dbacc[s][e] += acc[s][e];
+                    }
+                }
+            }
+            c1 = gsum4(c1) / (float)N;
+            c2 = gsum4(c2) / (float)N;
+            if (live) {
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    const int col = 16 * s + 4 * gq;
+                    const f32x4 x = *reinterpret_cast<const f32x4*>(g.res + row * g.ldr + col);
+                    const f32x4 d = g.dres ? *reinterpret_cast<const f32x4*>(g.dres + row * g.ldc + col)
+                                           : f32x4{0.f, 0.f, 0.f, 0.f};
+                    const f32x4 ga = pv(0, s);
+                    f32x4 dx;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float xv = (x[e] - m) * rs, gd = acc[s][e] * ga[e];
+                        dx[e] = rs * (gd - c1 * xv - c2) + d[e];
+                    }
+                    *reinterpret_cast<f32x4*>((float*)g.c + row * g.ldc + col) = dx;
+                }
+            }
+        }
+    }
+    if constexpr (MODE == MODE_LN_BWD) {
+        // Σ over the wave's rows (lanes c = 0..15 share the columns), the waves' sums in wave order -> one partial
+        // row per workgroup (fixed order: bitwise reproducible)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float a = xsum<16>(dgacc[s][e]), b = xsum<16>(dbacc[s][e]);
+                if (c == 0) {
+                    wred[w * 2 * N + 16 * s + 4 * gq + e] = a;
+                    wred[w * 2 * N + N + 16 * s + 4 * gq + e] = b;
+                }
+            }
+        __syncthreads();
+        for (int i = threadIdx.x; i < 2 * N; i += W * 64) {
+            float a = 0.f;
+            for (int ww = 0; ww < W; ++ww) a += wred[ww * 2 * N + i];
+            g.part[(int64_t)blockIdx.x * 2 * N + i] = a;
+        }
     }
 }
 
@@ -855,7 +1100,7 @@ constexpr TnCfg tn_cfg(int wg_per_cu) {
 }
 // abf = dY stored bf16 (and X too, unless lnx: X = LN(x) from the fp32 LayerNorm input)
 const TnCfg TN_TABLE[] = {
-    tn_cfg<384, 128, 3, 4, 2, 3, false>(2), tn_cfg<384, 128, 3, 8, 1, 3, false>(1),
+    tn_cfg<384, 128, 3, 8, 1, 3, false>(1), tn_cfg<384, 128, 3, 4, 2, 3, false>(2),
     tn_cfg<128, 128, 1, 8, 1, 3, false>(2), tn_cfg<128, 128, 1, 8, 1, 3, false>(1),
     tn_cfg<384, 128, 3, 8, 1, 1, false>(1), tn_cfg<384, 128, 3, 4, 2, 1, false>(2),
     tn_cfg<128, 128, 1, 8, 1, 1, false>(2), tn_cfg<128, 128, 1, 8, 1, 1, false>(1),
@@ -881,6 +1126,59 @@ int64_t tn_groups(int64_t M, const TnCfg* cfg) {
     const int64_t tiles = (M + 31) / 32;
     const int64_t g = (int64_t)num_cu() * cfg->wg_per_cu / cfg->ng;
     return tiles < g ? (tiles > 0 ? tiles : 1) : g;
+}
+
+struct RgCfg {
+    int K, P, abf, cbf, mode, w;
+    nt_fn fn;
+    size_t lds;
+};
+template <int K, int P, bool ABF, bool CBF, int MODE, int W = 16>
+constexpr RgCfg rg_cfg() {
+    return RgCfg{K, P, ABF, CBF, MODE, W, k_rowgemm<K, P, ABF, CBF, MODE, W>,
+                 (size_t)8 * (K / 32) * P * 64 * 16 + (size_t)(5 * 128 + (MODE == MODE_LN_BWD ? W * 2 * 128 : 0)) * 4};
+}
+// N = 128 only; B's planes must fit the LDS (K = 384 in fp32 would need 288 KB: k_sgemm_nt keeps that shape)
+const RgCfg RG_TABLE[] = {
+    rg_cfg<128, 3, false, false, MODE_PLAIN>(), rg_cfg<128, 1, false, false, MODE_PLAIN>(),
+    rg_cfg<128, 1, true, false, MODE_PLAIN>(),  rg_cfg<128, 1, true, true, MODE_PLAIN>(),
+    rg_cfg<384, 1, true, false, MODE_PLAIN>(),  rg_cfg<384, 1, false, false, MODE_PLAIN>(),
+    rg_cfg<128, 3, false, false, MODE_LN_OUT>(), rg_cfg<128, 1, true, false, MODE_LN_OUT>(),
+    rg_cfg<128, 1, false, false, MODE_LN_OUT>(),
+    rg_cfg<384, 1, true, false, MODE_LN_BWD, 8>(), rg_cfg<384, 1, false, false, MODE_LN_BWD, 8>(),
+};
+
+// TAGAN_SG_ROW=0: the N = 128 products on k_sgemm_nt instead of k_rowgemm (A/B knob, read once)
+bool rowgemm_on() {
+    static const int on = [] {
+        const char* e = getenv("TAGAN_SG_ROW");
+        return e ? atoi(e) : 1;
+    }();
+    return on != 0;
+}
+
+const RgCfg* rg_find(int K, int N, int P, int abf, int cbf, int mode) {
+    if (N != 128 || !rowgemm_on()) return nullptr;
+    for (const RgCfg& c : RG_TABLE)
+        if (c.K == K && c.P == P && c.abf == abf && c.cbf == cbf && c.mode == mode) return &c;
+    return nullptr;
+}
+
+int64_t rg_groups(int64_t M, const RgCfg* cfg) {
+    const int64_t tiles = (M + 15) / 16;
+    int64_t gx = std::min<int64_t>(num_cu(), (tiles + cfg->w - 1) / cfg->w);
+    return gx < 1 ? 1 : gx;
+}
+
+bool lds_ok(const void* fn, size_t lds);
+
+int rg_launch(const RgCfg* cfg, const NtArgs& g, void* stream, const char* what, int64_t* groups = nullptr) {
+    TAGAN_REQUIRE(lds_ok((const void*)cfg->fn, cfg->lds), TAGAN_ERR_LAUNCH, "%s: LDS attribute", what);
+    const int64_t gx = rg_groups(g.M, cfg);
+    if (groups) *groups = gx;
+    hipLaunchKernelGGL(cfg->fn, dim3((unsigned)gx), dim3(cfg->w * 64), cfg->lds, as_stream(stream), g);
+    TAGAN_CHECK_LAUNCH(what);
+    return TAGAN_OK;
 }
 
 // workgroups of an NT launch along the rows (grid.x): one per CU slot, at most one per tile
@@ -918,7 +1216,8 @@ bool lds_ok(const void* fn, size_t lds) {
 using namespace tagan;
 
 extern "C" int tagan_sgemm_supported(int32_t N, int32_t K, int32_t planes, int32_t a_dtype, int32_t c_dtype) {
-    return nt_find(K, N, planes, a_dtype == TAGAN_BF16, c_dtype == TAGAN_BF16) != nullptr;
+    const int ab = a_dtype == TAGAN_BF16, cb = c_dtype == TAGAN_BF16;
+    return nt_find(K, N, planes, ab, cb) != nullptr || rg_find(K, N, planes, ab, cb, MODE_PLAIN) != nullptr;
 }
 
 extern "C" int tagan_sgemm_tn_supported(int32_t N, int32_t K, int32_t planes, int32_t dtype) {
@@ -941,9 +1240,10 @@ extern "C" int tagan_sgemm_wprep(int32_t N, int32_t K, const float* w, int64_t l
 extern "C" int tagan_sgemm_nt(int32_t a_dtype, int32_t c_dtype, int64_t M, int32_t N, int32_t K, const void* a,
                               int64_t lda, const void* wp, int32_t planes, const float* bias, void* c, int64_t ldc,
                               void* stream) {
+    const RgCfg* rcfg = rg_find(K, N, planes, a_dtype == TAGAN_BF16, c_dtype == TAGAN_BF16, MODE_PLAIN);
     const NtCfg* cfg = nt_find(K, N, planes, a_dtype == TAGAN_BF16, c_dtype == TAGAN_BF16);
-    TAGAN_REQUIRE(cfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt: no kernel for N=%d K=%d planes=%d dtypes %d/%d", N, K,
-                  planes, a_dtype, c_dtype);
+    TAGAN_REQUIRE(cfg || rcfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt: no kernel for N=%d K=%d planes=%d dtypes %d/%d",
+                  N, K, planes, a_dtype, c_dtype);
     TAGAN_REQUIRE(M >= 0 && wp, TAGAN_ERR_ARG, "tagan_sgemm_nt: bad arguments");
     if (M == 0) return TAGAN_OK;
     TAGAN_REQUIRE(a && c, TAGAN_ERR_ARG, "tagan_sgemm_nt: null operand");
@@ -955,6 +1255,7 @@ extern "C" int tagan_sgemm_nt(int32_t a_dtype, int32_t c_dtype, int64_t M, int32
                   TAGAN_ERR_ARG, "tagan_sgemm_nt: operands must be 16-byte aligned rows");
     NtArgs g{};
     g.M = M; g.a = a; g.lda = lda; g.wp = (const uint4*)wp; g.bias = bias; g.c = c; g.ldc = ldc;
+    if (rcfg) return rg_launch(rcfg, g, stream, "tagan_sgemm_nt");
     return nt_launch(cfg, g, N, stream, "tagan_sgemm_nt");
 }
 
@@ -962,8 +1263,8 @@ extern "C" int tagan_sgemm_ln_supported(int32_t H, int32_t planes, int32_t act_d
     const int ab = act_dtype == TAGAN_BF16;
     switch (op) {
         case 1: return nt_find(H, 3 * H, planes, 0, ab, MODE_LN_IN) && tn_find(3 * H, H, planes, ab, 1);
-        case 2: return nt_find(H, H, planes, ab, 0, MODE_LN_OUT) != nullptr;
-        case 3: return nt_find(3 * H, H, planes, ab, 0, MODE_LN_BWD) != nullptr;
+        case 2: return nt_find(H, H, planes, ab, 0, MODE_LN_OUT) || rg_find(H, H, planes, ab, 0, MODE_LN_OUT);
+        case 3: return nt_find(3 * H, H, planes, ab, 0, MODE_LN_BWD) || rg_find(3 * H, H, planes, ab, 0, MODE_LN_BWD);
         default: return 0;
     }
 }
@@ -991,8 +1292,9 @@ extern "C" int tagan_sgemm_nt_ln_out(int32_t a_dtype, int64_t M, int32_t H, cons
                                      const float* ln_g, const float* ln_b, float eps, const float* gs, const float* bs,
                                      float eps_s, float* s_out, float* y, float* mean, float* rstd, float* mean_s,
                                      float* rstd_s, void* stream) {
+    const RgCfg* rcfg = rg_find(H, H, planes, a_dtype == TAGAN_BF16, 0, MODE_LN_OUT);
     const NtCfg* cfg = nt_find(H, H, planes, a_dtype == TAGAN_BF16, 0, MODE_LN_OUT);
-    TAGAN_REQUIRE(cfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt_ln_out: no kernel for H=%d planes=%d", H, planes);
+    TAGAN_REQUIRE(cfg || rcfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt_ln_out: no kernel for H=%d planes=%d", H, planes);
     TAGAN_REQUIRE(M >= 0 && wp && ln_g && ln_b && p_drop >= 0.f && p_drop < 1.f && (!gs == !bs) &&
                       (!gs || (mean_s && rstd_s)),
                   TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_out: bad arguments");
@@ -1008,6 +1310,7 @@ extern "C" int tagan_sgemm_nt_ln_out(int32_t a_dtype, int64_t M, int32_t H, cons
     g.res = res; g.ldr = H; g.p_drop = p_drop; g.inv_keep = 1.f / (1.f - p_drop); g.seed = seed;
     g.seed_ctr = seed_counter(); g.s_out = s_out;
     g.gs = gs; g.bs = bs; g.eps_s = eps_s; g.mean_s = mean_s; g.rstd_s = rstd_s;
+    if (rcfg) return rg_launch(rcfg, g, stream, "tagan_sgemm_nt_ln_out");
     return nt_launch(cfg, g, H, stream, "tagan_sgemm_nt_ln_out");
 }
 
@@ -1015,6 +1318,9 @@ extern "C" size_t tagan_sgemm_nt_ln_bwd_workspace(int64_t M, int32_t H, int32_t 
     int64_t g = 1;
     for (const NtCfg& c : NT_TABLE)
         if (c.mode == MODE_LN_BWD && c.N == H && c.K == K) g = std::max(g, nt_groups(M, &c, 1));
+    if (H == 128)
+        for (const RgCfg& c : RG_TABLE)
+            if (c.mode == MODE_LN_BWD && c.K == K) g = std::max(g, rg_groups(M, &c));
     return (size_t)g * 2 * H * sizeof(float);
 }
 
@@ -1022,8 +1328,10 @@ extern "C" int tagan_sgemm_nt_ln_bwd(int32_t a_dtype, int64_t M, int32_t H, int3
                                      const void* wp, int32_t planes, const float* x, const float* mean,
                                      const float* rstd, const float* gamma, const float* dres, float* dx, float* dgamma,
                                      float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+    const RgCfg* rcfg = rg_find(K, H, planes, a_dtype == TAGAN_BF16, 0, MODE_LN_BWD);
     const NtCfg* cfg = nt_find(K, H, planes, a_dtype == TAGAN_BF16, 0, MODE_LN_BWD);
-    TAGAN_REQUIRE(cfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt_ln_bwd: no kernel for H=%d K=%d planes=%d", H, K, planes);
+    TAGAN_REQUIRE(cfg || rcfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt_ln_bwd: no kernel for H=%d K=%d planes=%d", H, K,
+                  planes);
     TAGAN_REQUIRE(M >= 0 && wp && gamma && dgamma && dbeta, TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_bwd: bad arguments");
     TAGAN_REQUIRE(M > 0, TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_bwd: M must be positive (no rows: dgamma = dbeta = 0)");
     TAGAN_REQUIRE(a && x && mean && rstd && dx && lda >= K, TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_bwd: bad operands");
@@ -1031,13 +1339,14 @@ extern "C" int tagan_sgemm_nt_ln_bwd(int32_t a_dtype, int64_t M, int32_t H, int3
     TAGAN_REQUIRE((uintptr_t)a % 16 == 0 && (lda * es) % 16 == 0 && (uintptr_t)x % 16 == 0 &&
                       (uintptr_t)dx % 16 == 0 && (!dres || (uintptr_t)dres % 16 == 0),
                   TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_bwd: operands must be 16-byte aligned rows");
-    const int64_t G = nt_groups(M, cfg, 1);
+    const int64_t G = rcfg ? rg_groups(M, rcfg) : nt_groups(M, cfg, 1);
     TAGAN_REQUIRE(ws && ws_bytes >= (size_t)G * 2 * H * sizeof(float), TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_bwd: workspace");
     NtArgs g{};
     g.M = M; g.a = a; g.lda = lda; g.wp = (const uint4*)wp; g.bias = nullptr; g.c = dx; g.ldc = H;
     g.ln_g = gamma; g.mean = (float*)mean; g.rstd = (float*)rstd; g.res = x; g.ldr = H; g.dres = dres;
     g.part = (float*)ws;
-    const int rc = nt_launch(cfg, g, H, stream, "tagan_sgemm_nt_ln_bwd");
+    const int rc = rcfg ? rg_launch(rcfg, g, stream, "tagan_sgemm_nt_ln_bwd") :
+                          nt_launch(cfg, g, H, stream, "tagan_sgemm_nt_ln_bwd");
     if (rc != TAGAN_OK) return rc;
     launch_colsum((const float*)ws, (int)G, 2 * H, dgamma, dbeta, H, as_stream(stream), 1.f, 2 * H);
     TAGAN_CHECK_LAUNCH("tagan_sgemm_nt_ln_bwd_sum");

@@ -273,22 +273,21 @@ def _sg_use(H: int, bf: bool, act: bool) -> bool:
 # TAGAN_SG_LN=0: the stream_gemm block with standalone LayerNorm kernels instead of the LayerNorm-fused GEMMs (LN1 in
 # the QKV projection's prologue, dropout + residual + LN2 [+ skip LN] in the out-projection's epilogue, LN1's backward
 # in the QKV input gradient's epilogue, h = LN1(x) recomputed inside the QKV weight gradient; A/B knob)
-# TAGAN_SG_LN = comma list of the fused ops ("in", "out", "bwd"), "all", "0"/"none", or "auto" (default): the
-# measured-best set per precision.  Interleaved C2 A/B on one MI355X (tools/runs/sgln_check.sh,
-# profiles/r3c_sgln_ab.txt), ms per step fp32 / bf16: none 7.16 / 5.64, in 6.93 / 5.57, in+out 7.01 / 5.49,
-# all 7.43 / 5.67.  The epilogue forms need a whole output row per workgroup, so each workgroup alternates a
-# matrix phase and a memory phase split by a barrier; with the fp32 (three-plane) weights resident in registers
-# only one workgroup fits a CU and nothing overlaps those phases (out: +0.08 ms in fp32, -0.08 ms in bf16 where two
-# fit; bwd: +0.4 ms, its K = 384 weight fragments alone take 144 VGPRs).
+# TAGAN_SG_LN = list of the fused ops ("in", "out", "bwd"; separated by , + or :), "all", "0"/"none", or "auto"
+# (default): the measured-best set per precision.  Same-process interleaved graph-replay A/B on one MI355X
+# (tools/ab_step.py, profiles/r3d_ab_step.txt), ms per C2 step with the row-owner N = 128 kernels (k_rowgemm):
+#   fp32  none 6.99  in 6.82  in+out 6.75  all 6.99   (fp32 "bwd" runs on k_sgemm_nt: its K = 384 three-plane weight
+#                                                      fragments do not fit a row-owner kernel's LDS, 288 KB)
+#   bf16  none 5.62  in 5.50  in+out 5.41  all 5.26
 _SG_LN_ENV = os.environ.get("TAGAN_SG_LN", "auto").strip().lower()
 SG_LN_SET = (set() if _SG_LN_ENV in ("0", "none", "") else
              {"in", "out", "bwd"} if _SG_LN_ENV in ("1", "all") else
-             None if _SG_LN_ENV == "auto" else set(_SG_LN_ENV.split(",")))
+             None if _SG_LN_ENV == "auto" else set(_SG_LN_ENV.replace("+", ",").replace(":", ",").split(",")))
 _SG_LN_OK = {}
 
 
 def _sg_ln_use(H: int, bf: bool, act: bool, op: str) -> bool:
-    ops = SG_LN_SET if SG_LN_SET is not None else ({"in", "out"} if bf else {"in"})
+    ops = SG_LN_SET if SG_LN_SET is not None else ({"in", "out", "bwd"} if bf else {"in", "out"})
     if op not in ops:
         return False
     key = (H, bf, act, op)

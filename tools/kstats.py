@@ -9,7 +9,7 @@ import re
 import sys
 
 FAMILIES = [
-    ("sgemm (hand-written)", r"k_sgemm"),
+    ("sgemm (hand-written)", r"k_sgemm|k_rowgemm"),
     ("gemm", r"^Cijk_|gemm|Gemm"),
     ("geo", r"k_geo_"),
     ("temporal", r"k_tattn"),
