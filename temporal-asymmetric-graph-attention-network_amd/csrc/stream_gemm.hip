@@ -611,6 +611,12 @@ __global__ void __launch_bounds__(W * 64) k_rowgemm(NtArgs g) {
                 af[kk][1] = *reinterpret_cast<const float4*>(src + 4);
             }
         }
+        // LN_OUT: the residual row is read with the A fragments (in flight under the MFMAs)
+        f32x4 er[MODE == MODE_LN_OUT ? NS : 1];
+        if constexpr (MODE == MODE_LN_OUT) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) er[s] = *reinterpret_cast<const f32x4*>(g.res + row * g.ldr + 16 * s + 4 * gq);
+        }
         f32x4 acc[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) acc[s] = pv(4, s);
@@ -657,7 +663,7 @@ __global__ void __launch_bounds__(W * 64) k_rowgemm(NtArgs g) {
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
                 const int col = 16 * s + 4 * gq;
-                const f32x4 r = *reinterpret_cast<const f32x4*>(g.res + row * g.ldr + col);
+                const f32x4 r = er[s];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     float x = acc[s][e];
@@ -681,11 +687,9 @@ __global__ void __launch_bounds__(W * 64) k_rowgemm(NtArgs g) {
                 means = gsum4(sr) / (float)N;
                 float sqs = 0.f;
 #pragma unroll
-                for (int s = 0; s < NS; ++s) {
-                    const f32x4 r = *reinterpret_cast<const f32x4*>(g.res + row * g.ldr + 16 * s + 4 * gq);
+                for (int s = 0; s < NS; ++s)
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) sqs += (r[e] - means) * (r[e] - means);
-                }
+                    for (int e = 0; e < 4; ++e) sqs += (er[s][e] - means) * (er[s][e] - means);
                 rstds = 1.f / sqrtf(gsum4(sqs) / (float)N + g.eps_s);
             }
             if (live) {
@@ -697,10 +701,9 @@ __global__ void __launch_bounds__(W * 64) k_rowgemm(NtArgs g) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) y[e] = (acc[s][e] - mean) * rstd * ga[e] + be[e];
                     if (g.gs) {
-                        const f32x4 r = *reinterpret_cast<const f32x4*>(g.res + row * g.ldr + col);
                         const f32x4 gs = pv(2, s), bs = pv(3, s);
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) y[e] += (r[e] - means) * rstds * gs[e] + bs[e];
+                        for (int e = 0; e < 4; ++e) y[e] += (er[s][e] - means) * rstds * gs[e] + bs[e];
                     }
                     *reinterpret_cast<f32x4*>((float*)g.c + row * g.ldc + col) = y;
                 }
@@ -1148,17 +1151,21 @@ const RgCfg RG_TABLE[] = {
     rg_cfg<384, 1, true, false, MODE_LN_BWD, 8>(), rg_cfg<384, 1, false, false, MODE_LN_BWD, 8>(),
 };
 
-// TAGAN_SG_ROW=0: the N = 128 products on k_sgemm_nt instead of k_rowgemm (A/B knob, read once)
-bool rowgemm_on() {
-    static const int on = [] {
+// TAGAN_SG_ROW (A/B knob, read once): 1 (default) = the LayerNorm-fused N = 128 products on k_rowgemm, 0 = all on
+// k_sgemm_nt, 2 = the plain N = 128 products on k_rowgemm too.  Plain products measured faster on k_sgemm_nt (C2
+// kernel stats, profiles/r3d_sgemm_table_fp32.md: fp32 K = 128 62 vs 77 us, bf16 41 vs 46 us, bf16 K = 384 70 vs
+// 78 us): without a row-wide epilogue the weight-stationary kernel's register-resident B wins.
+int rowgemm_level() {
+    static const int lv = [] {
         const char* e = getenv("TAGAN_SG_ROW");
         return e ? atoi(e) : 1;
     }();
-    return on != 0;
+    return lv;
 }
 
 const RgCfg* rg_find(int K, int N, int P, int abf, int cbf, int mode) {
-    if (N != 128 || !rowgemm_on()) return nullptr;
+    const int lv = rowgemm_level();
+    if (N != 128 || lv == 0 || (mode == MODE_PLAIN && lv < 2)) return nullptr;
     for (const RgCfg& c : RG_TABLE)
         if (c.K == K && c.P == P && c.abf == abf && c.cbf == cbf && c.mode == mode) return &c;
     return nullptr;
