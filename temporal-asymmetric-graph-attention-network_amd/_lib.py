@@ -77,6 +77,8 @@ _SIGNATURES = {
     "tagan_layernorm_bwd_workspace": (_sz, [_i64, _i32]),
     "tagan_layernorm_bwd": (_c.c_int, [_c.c_int, _i64, _i32, _p, _p, _p, _p, _p, _p, _f32, _u64, _p, _p, _p, _p,
                                        _p, _p, _sz, _p]),
+    "tagan_layernorm_skip_bwd_workspace": (_sz, [_i64, _i32]),
+    "tagan_layernorm_skip_bwd": (_c.c_int, [_c.c_int, _i64, _i32] + [_p] * 8 + [_p, _f32, _u64] + [_p] * 8 + [_sz, _p]),
     "tagan_proj_supported": (_c.c_int, [_i32]),
     "tagan_ln_qkv_fwd": (_c.c_int, [_i64, _i32, _i32, _p, _p, _p, _f32, _p, _p, _p, _i64, _p, _i64, _p, _p, _p]),
     "tagan_proj_ln_fwd": (_c.c_int, [_i64, _i32, _p, _p, _p, _p, _f32, _u64, _p, _p, _f32, _p, _p, _f32, _p, _p, _p,

@@ -20,7 +20,10 @@ namespace {
 constexpr int HB = 1024;     // threads: NG = HB / H groups of H feature threads
 constexpr int HU = 8;        // steps per thread in the [T, H] products (ceil(T / NG); T·H <= 8192)
 constexpr int HC = 16;       // max classes
-constexpr int KC = 32;       // weight rows / columns staged per LDS chunk
+constexpr int KC = 32;       // weight rows / columns staged per LDS chunk (H > 128; the whole matrix at H <= 128)
+// staging width: at H <= 128 the whole H x H weight fits the LDS next to the [T, H] tiles, so a product stages it in
+// ONE pass (one global-load latency instead of H / KC dependent rounds)
+__host__ __device__ inline int kstep(int H) { return H <= 128 ? H : KC; }
 constexpr int NWV = HB / 64; // waves
 
 struct HeadArgs {
@@ -64,7 +67,7 @@ __device__ float block_sum(float v, float* red) {
 struct HeadLds {
     float *xs, *zs, *wt, *part, *va, *vd, *vp, *vu, *vg, *vh, *vl, *red;
     __device__ HeadLds(float* sm, int T, int H) {
-        xs = sm; zs = xs + T * H; wt = zs + T * H; part = wt + KC * (H + 1); va = part + HB; vd = va + 128;
+        xs = sm; zs = xs + T * H; wt = zs + T * H; part = wt + kstep(H) * (H + 1); va = part + HB; vd = va + 128;
         vp = vd + 128; vu = vp + 256; vg = vu + 256; vh = vg + 256; vl = vh + 256; red = vl + 16;
     }
 };
@@ -76,8 +79,9 @@ __device__ __forceinline__ void xw_t(const float* __restrict__ W, const float* x
                                      bool act, int grp, int j, float (&acc)[HU]) {
 #pragma unroll
     for (int u = 0; u < HU; ++u) acc[u] = 0.f;
-    for (int kc = 0; kc < H; kc += KC) {
-        const int kn = min(KC, H - kc);
+    const int KS = kstep(H);
+    for (int kc = 0; kc < H; kc += KS) {
+        const int kn = min(KS, H - kc);
         __syncthreads();   // the previous chunk's reads are done
         for (int e = threadIdx.x; e < H * kn; e += HB) {
             const int jj = e / kn, kk = e % kn;
@@ -164,14 +168,25 @@ __global__ void __launch_bounds__(HB) k_head_fwd(HeadArgs A) {
         }
         __syncthreads();
         // u = Wc1 p + bc1: one wave per output row, lanes over the (coalesced) row
-        for (int jo = w; jo < H; jo += NWV) {
-            float s = 0.f;
-            for (int k = lane * 4; k < H; k += 256) {
-                const float4 wv = *reinterpret_cast<const float4*>(A.Wc1 + (int64_t)jo * H + k);
-                s += (wv.x * L.vp[k] + wv.y * L.vp[k + 1]) + (wv.z * L.vp[k + 2] + wv.w * L.vp[k + 3]);
+        {   // every row's load first (H <= 256: <= 16 rows per wave, one float4 per lane and row), then the sums
+            constexpr int MR = 256 / NWV;
+            float4 wv[MR];
+            const int k = lane * 4;
+#pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                const int jo = w + r * NWV;
+                wv[r] = (jo < H && k < H) ? *reinterpret_cast<const float4*>(A.Wc1 + (int64_t)jo * H + k)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
             }
-            s = wave_sum(s);
-            if (lane == 0) L.vu[jo] = s + A.bc1[jo];
+#pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                const int jo = w + r * NWV;
+                if (jo >= H) break;
+                float s = 0.f;
+                if (k < H) s = (wv[r].x * L.vp[k] + wv[r].y * L.vp[k + 1]) + (wv[r].z * L.vp[k + 2] + wv[r].w * L.vp[k + 3]);
+                s = wave_sum(s);
+                if (lane == 0) L.vu[jo] = s + A.bc1[jo];
+            }
         }
         __syncthreads();
         // LayerNorm ; ReLU ; dropout
@@ -301,6 +316,7 @@ __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
         // dpooled[k] = Σ_j du_j Wc1[j][k]: thread (grp, k) over j = grp, grp + NG, ..., then the groups in order
         if (act) {
             float g = 0.f;
+#pragma unroll 8
             for (int jj = grp; jj < H; jj += NG) g += vq[jj] * A.Wc1[(int64_t)jj * H + j];
             L.part[grp * H + j] = g;
         }
@@ -353,8 +369,9 @@ __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
             float acc[HU];
 #pragma unroll
             for (int u = 0; u < HU; ++u) acc[u] = 0.f;
-            for (int jc = 0; jc < H; jc += KC) {
-                const int jn = min(KC, H - jc);
+            const int KS = kstep(H);
+            for (int jc = 0; jc < H; jc += KS) {
+                const int jn = min(KS, H - jc);
                 __syncthreads();
                 for (int e = tid; e < jn * H; e += HB) L.wt[(e / H) * (H + 1) + e % H] = A.W1[(int64_t)jc * H + e];
                 __syncthreads();
@@ -382,7 +399,7 @@ __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
 }
 
 size_t head_lds(int T, int H) {
-    return (size_t)(2 * T * H + KC * (H + 1) + HB + 2 * 128 + 4 * 256 + 16 + 32) * sizeof(float);
+    return (size_t)(2 * T * H + kstep(H) * (H + 1) + HB + 2 * 128 + 4 * 256 + 16 + 32) * sizeof(float);
 }
 
 int head_lds_optin(size_t bytes) {

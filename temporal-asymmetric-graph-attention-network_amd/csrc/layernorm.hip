@@ -176,36 +176,48 @@ __global__ void __launch_bounds__(BLK) k_ln_fwd(LnArgs A) {
     }
 }
 
-template <int LPR, int NV, int U, typename S>
+// SK: the skip branch of model.py:258-262 in the same pass -- y = LN(s) + LN_s(b) shares dy, so ds gets LN_s's
+// input gradient too (b = A.b with statistics A.mean_s / A.rstd_s and gamma A.gamma_s), and the partial rows carry
+// its dgamma_s | dbeta_s (5H per block instead of 3H).  One read of dy and one write of ds instead of two.
+template <int LPR, int NV, int U, typename S, bool SK = false>
 __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
     TAGAN_LIVE_SEED(A);
-    constexpr int RPW = WAVE / LPR;
-    __shared__ float red[BLK / WAVE][RPW][3 * 4 * NV * LPR];
+    constexpr int RPW = WAVE / LPR, NP = SK ? 5 : 3;
+    __shared__ float red[BLK / WAVE][RPW][NP * 4 * NV * LPR];
     const int lane = threadIdx.x & (WAVE - 1), sl = lane % LPR, sub = lane / LPR, w = threadIdx.x >> 6;
     const int H = A.H;
-    float4 dg[NV], db[NV], dsa[NV];
+    float4 dg[NV], db[NV], dsa[NV], dgs[SK ? NV : 1], dbs[SK ? NV : 1];
 #pragma unroll
     for (int n = 0; n < NV; ++n) {
         dg[n] = make_float4(0.f, 0.f, 0.f, 0.f);
         db[n] = make_float4(0.f, 0.f, 0.f, 0.f);
         dsa[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (SK) {
+            dgs[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+            dbs[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
     const int64_t nwaves = (int64_t)gridDim.x * (BLK / WAVE);
     for (int64_t wave = blockIdx.x * (int64_t)(BLK / WAVE) + w; wave * (RPW * U) < A.M; wave += nwaves) {
-        float4 sv[U][NV], dv[U][NV], ev[U][NV];
-        float mean[U], rstd[U];
+        float4 sv[U][NV], dv[U][NV], ev[U][NV], bv[SK ? U : 1][NV];
+        float mean[U], rstd[U], mean_s[SK ? U : 1], rstd_s[SK ? U : 1];
 #pragma unroll
         for (int u = 0; u < U; ++u) {        // every load of the U row groups first
             const int64_t row = wave * (RPW * U) + u * RPW + sub;
             const int64_t r = row < A.M ? row : A.M - 1;
             mean[u] = A.mean[r];
             rstd[u] = A.rstd[r];
+            if constexpr (SK) {
+                mean_s[u] = A.mean_s[r];
+                rstd_s[u] = A.rstd_s[r];
+            }
 #pragma unroll
             for (int n = 0; n < NV; ++n) {
                 const int c = (n * LPR + sl) * 4;
                 sv[u][n] = ld4(A.s_in + r * H + c);
                 dv[u][n] = ld4(A.dy + r * H + c);
                 ev[u][n] = (A.ds && A.dres) ? ld4(A.dres + r * H + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+                if constexpr (SK) bv[u][n] = ld4(A.b + r * H + c);
             }
         }
 #pragma unroll
@@ -230,6 +242,27 @@ __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
             }
             c1 = row_sum<LPR>(c1) / (float)H;
             c2 = row_sum<LPR>(c2) / (float)H;
+            // skip branch: x̂_s, g_s·dy and its two row sums
+            float4 xs[SK ? NV : 1], gs[SK ? NV : 1];
+            float c1s = 0.f, c2s = 0.f;
+            if constexpr (SK) {
+#pragma unroll
+                for (int n = 0; n < NV; ++n) {
+                    const int c = (n * LPR + sl) * 4;
+                    const float4 b = bv[u][n], d = dv[u][n], g = ld4(A.gamma_s + c);
+                    const float m = mean_s[u], rs = rstd_s[u];
+                    xs[n] = make_float4((b.x - m) * rs, (b.y - m) * rs, (b.z - m) * rs, (b.w - m) * rs);
+                    gs[n] = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
+                    c1s += (gs[n].x * xs[n].x + gs[n].y * xs[n].y) + (gs[n].z * xs[n].z + gs[n].w * xs[n].w);
+                    c2s += (gs[n].x + gs[n].y) + (gs[n].z + gs[n].w);
+                    if (live) {
+                        dgs[n].x += d.x * xs[n].x; dgs[n].y += d.y * xs[n].y; dgs[n].z += d.z * xs[n].z; dgs[n].w += d.w * xs[n].w;
+                        dbs[n].x += d.x; dbs[n].y += d.y; dbs[n].z += d.z; dbs[n].w += d.w;
+                    }
+                }
+                c1s = row_sum<LPR>(c1s) / (float)H;
+                c2s = row_sum<LPR>(c2s) / (float)H;
+            }
             if (!live) continue;
             const float rs = rstd[u];
 #pragma unroll
@@ -248,6 +281,13 @@ __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
                 if (A.ds) {
                     const float4 e = ev[u][n];
                     o.x += e.x; o.y += e.y; o.z += e.z; o.w += e.w;
+                    if constexpr (SK) {   // + LN_s's input gradient (same rounding order as the two-pass form)
+                        const float r2 = rstd_s[u];
+                        o.x += r2 * (gs[n].x - c1s * xs[n].x - c2s);
+                        o.y += r2 * (gs[n].y - c1s * xs[n].y - c2s);
+                        o.z += r2 * (gs[n].z - c1s * xs[n].z - c2s);
+                        o.w += r2 * (gs[n].w - c1s * xs[n].w - c2s);
+                    }
                     st4(A.ds + row * H + c, o);
                 }
             }
@@ -260,13 +300,17 @@ __global__ void __launch_bounds__(BLK) k_ln_bwd(LnArgs A) {
             st4(&red[w][sub][c], dg[n]);
             st4(&red[w][sub][H + c], db[n]);
             st4(&red[w][sub][2 * H + c], dsa[n]);
+            if constexpr (SK) {
+                st4(&red[w][sub][3 * H + c], dgs[n]);
+                st4(&red[w][sub][4 * H + c], dbs[n]);
+            }
         }
         __syncthreads();
-        for (int x = threadIdx.x; x < 3 * H; x += BLK) {
+        for (int x = threadIdx.x; x < NP * H; x += BLK) {
             float s = 0.f;
             for (int ww = 0; ww < BLK / WAVE; ++ww)
                 for (int ss = 0; ss < RPW; ++ss) s += red[ww][ss][x];
-            A.part[(int64_t)blockIdx.x * 3 * H + x] = s;
+            A.part[(int64_t)blockIdx.x * NP * H + x] = s;
         }
     }
 }
@@ -304,6 +348,14 @@ int ln_rows(int nv) {
     }();
     const int u = env ? env : 2;
     return nv == 2 && u > 2 ? 2 : u;
+}
+
+// the fused LN2 + skip-LN backward (H = 128: LPR 32, NV 1; any U)
+template <typename S>
+void launch_ln_skip_bwd(int u, dim3 g, hipStream_t s, const LnArgs& A) {
+    if (u == 1) k_ln_bwd<32, 1, 1, S, true><<<g, BLK, 0, s>>>(A);
+    else if (u == 2) k_ln_bwd<32, 1, 2, S, true><<<g, BLK, 0, s>>>(A);
+    else k_ln_bwd<32, 1, 4, S, true><<<g, BLK, 0, s>>>(A);
 }
 
 template <typename S, bool FWD>
@@ -423,6 +475,48 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, cons
         launch_colsum(A.part + 2 * H, nblk, H, dsum_a, nullptr, H, s, 1.f, 3 * H);
         TAGAN_CHECK_LAUNCH("layernorm_bwd_sum_a");
     }
+    return TAGAN_OK;
+}
+
+size_t tagan_layernorm_skip_bwd_workspace(int64_t M, int32_t H) {
+    (void)M;
+    return (size_t)tagan::ln_bwd_blocks() * 5 * H * sizeof(float);
+}
+
+int tagan_layernorm_skip_bwd(int dtype, int64_t M, int32_t H, const float* s_in, const float* mean, const float* rstd,
+                             const float* gamma, const float* b, const float* mean_s, const float* rstd_s,
+                             const float* gamma_s, const float* dy, float p_drop, uint64_t seed, float* ds, float* da,
+                             float* dgamma, float* dbeta, float* dsum_a, float* dgamma_s, float* dbeta_s,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+    using namespace tagan;
+    TAGAN_REQUIRE(dtype == TAGAN_F32 || dtype == TAGAN_BF16, TAGAN_ERR_UNSUPPORTED, "layernorm: dtype %d", dtype);
+    TAGAN_REQUIRE(H == 128, TAGAN_ERR_UNSUPPORTED, "layernorm_skip_bwd: H=%d (H = 128 only)", H);
+    TAGAN_REQUIRE(M > 0 && s_in && mean && rstd && gamma && b && mean_s && rstd_s && gamma_s && dy && ds && da &&
+                      dgamma && dbeta && dsum_a && dgamma_s && dbeta_s,
+                  TAGAN_ERR_ARG, "layernorm_skip_bwd: bad args");
+    TAGAN_REQUIRE(workspace && workspace_bytes >= tagan_layernorm_skip_bwd_workspace(M, H), TAGAN_ERR_WORKSPACE,
+                  "layernorm_skip_bwd: workspace");
+    LnArgs A{};
+    A.M = M; A.H = H; A.gamma = gamma; A.s_in = s_in; A.mean = (float*)mean; A.rstd = (float*)rstd; A.dy = dy;
+    A.b = b; A.mean_s = (float*)mean_s; A.rstd_s = (float*)rstd_s; A.gamma_s = gamma_s;
+    A.dres = nullptr; A.ds = ds; A.da = da; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed;
+    A.seed_ctr = seed_counter();
+    A.part = (float*)workspace;
+    A.want_dsa = 1;
+    const int u = ln_rows(1);
+    const int64_t rpw = (WAVE / 32) * u;
+    const int64_t need = ((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE);
+    const int nblk = (int)std::min<int64_t>(need, ln_bwd_blocks());
+    hipStream_t s = as_stream(stream);
+    if (dtype == TAGAN_BF16) launch_ln_skip_bwd<bf16s>(u, dim3(nblk), s, A);
+    else launch_ln_skip_bwd<float>(u, dim3(nblk), s, A);
+    TAGAN_CHECK_LAUNCH("layernorm_skip_bwd");
+    launch_colsum(A.part, nblk, 2 * H, dgamma, dbeta, H, s, 1.f, 5 * H);
+    TAGAN_CHECK_LAUNCH("layernorm_skip_bwd_sum");
+    launch_colsum(A.part + 2 * H, nblk, H, dsum_a, nullptr, H, s, 1.f, 5 * H);
+    TAGAN_CHECK_LAUNCH("layernorm_skip_bwd_sum_a");
+    launch_colsum(A.part + 3 * H, nblk, 2 * H, dgamma_s, dbeta_s, H, s, 1.f, 5 * H);
+    TAGAN_CHECK_LAUNCH("layernorm_skip_bwd_sum_s");
     return TAGAN_OK;
 }
 

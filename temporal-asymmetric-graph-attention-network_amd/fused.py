@@ -76,6 +76,42 @@ def ln_bwd(s, mean, rstd, gamma, dy2, dres, p_drop, seed, want_ds, want_da, want
     return ds, da, dg, dbt, dsa
 
 
+def ln_skip_bwd(s, mean, rstd, gamma, b, mean_s, rstd_s, gamma_s, dy2, p_drop, seed, da_dtype=torch.float32):
+    """Backward of y = LN(dropout-sum s) + LN_s(b) in one pass: ds (incl. LN_s's input gradient), da, dgamma, dbeta,
+    dsum_a, dgamma_s, dbeta_s (the two-call ln_bwd chain's values to fp32 rounding, the same dropout decisions)."""
+    M, H = dy2.shape
+    dev = dy2.device
+    ds = torch.empty_like(dy2)
+    da = torch.empty(M, H, device=dev, dtype=da_dtype)
+    out = torch.empty(5, H, device=dev)
+    L = lib()
+    wsb = L.tagan_layernorm_skip_bwd_workspace(M, H)
+    ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
+    check(L.tagan_layernorm_skip_bwd(_lib.dtype_code(da), M, H, ptr(s), ptr(mean), ptr(rstd), ptr(gamma), ptr(b),
+                                     ptr(mean_s), ptr(rstd_s), ptr(gamma_s), ptr(dy2), float(p_drop), seed, ptr(ds),
+                                     ptr(da), ptr(out[0]), ptr(out[1]), ptr(out[2]), ptr(out[3]), ptr(out[4]), ptr(ws),
+                                     wsb, stream_of(dy2)), "tagan_layernorm_skip_bwd")
+    return ds, da, out[0], out[1], out[2], out[3], out[4]
+
+
+# TAGAN_LN_SKIP_BWD=0: the skip block's LN2 and LN_s backward as two passes (A/B knob)
+LN_SKIP_BWD = os.environ.get("TAGAN_LN_SKIP_BWD", "1") != "0"
+
+
+def _ln2_bwd(s2, mean2, rstd2, ln2_w, dy2, skip, x2, lns_w, p_out, seed_out, da_dtype):
+    """LN2's backward of a block (and, for the skip block, LN_s's): dres, do, dg2, db2, dbo, dgs, dbs."""
+    M, H = dy2.shape
+    if skip is not None and LN_SKIP_BWD and H == 128:
+        return ln_skip_bwd(s2, mean2, rstd2, ln2_w, x2, skip[0], skip[1], lns_w, dy2, p_out, seed_out,
+                           da_dtype=da_dtype)
+    dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True,
+                                     da_dtype=da_dtype)
+    dgs = dbs = None
+    if skip is not None:       # skip branch: LN_s backward with the residual gradient added in-kernel
+        dres, _, dgs, dbs, _ = ln_bwd(x2, skip[0], skip[1], lns_w, dy2, dres, 0.0, 0, True, False, False)
+    return dres, do, dg2, db2, dbo, dgs, dbs
+
+
 # ----------------------------------------------------------------------------- attention cores
 class GeoCore:
     """Edge-softmax attention over a SnapshotGraph (csrc/geo_attn.hip); qkv2 [N, 3H] -> ctx [N, H]."""
@@ -556,11 +592,8 @@ class AttnBlockFn(torch.autograd.Function):
         P = 1 if bf else 3
         adt = torch.bfloat16 if act else torch.float32
         dy2 = dy.reshape(-1, H).contiguous()
-        dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True,
-                                         da_dtype=adt)
-        dgs = dbs = None
-        if skip is not None:
-            dres, _, dgs, dbs, _ = ln_bwd(x2, skip[0], skip[1], lns_w, dy2, dres, 0.0, 0, True, False, False)
+        dres, do, dg2, db2, dbo, dgs, dbs = _ln2_bwd(s2, mean2, rstd2, ln2_w, dy2, skip, x2, lns_w, p_out, seed_out,
+                                                     adt)
         dc = sg.nt(do, sg.wprep(w_o, True, P), H, P, out_dtype=adt)
         dw_o = sg.tn(do, c, P, want_db=False)[0] if ng[7] else None
         dqkv, dp1, dp2, db_core = core.bwd(qkv, c, saved, dc, ng[1], ng[2], want_bias_sum=bool(ng[6]))
@@ -598,11 +631,8 @@ class AttnBlockFn(torch.autograd.Function):
         aw = (_AsyncWGrad(ctx.sink, dy.device) if (WGRAD_ASYNC and ctx.sink is not None and dy.is_cuda and not bf
                                                     and not proj and h_aug is not None and WGRAD_BIAS_AUG
                                                     and ng[5] and ng[6] and ng[7]) else None)
-        dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True,
-                                         da_dtype=torch.bfloat16 if bf else torch.float32)
-        dgs = dbs = None
-        if skip is not None:       # skip branch: LN_s backward with the residual gradient added in-kernel
-            dres, _, dgs, dbs, _ = ln_bwd(x2, skip[0], skip[1], lns_w, dy2, dres, 0.0, 0, True, False, False)
+        dres, do, dg2, db2, dbo, dgs, dbs = _ln2_bwd(s2, mean2, rstd2, ln2_w, dy2, skip, x2, lns_w, p_out, seed_out,
+                                                     torch.bfloat16 if bf else torch.float32)
         dc = proj_mm(do, w_o.contiguous(), True) if (proj and "dc" in PROJ_SET) else _mm(do, w_o, bf, out_bf16=act)
         if aw is not None:
             aw.dw_o = aw.run(lambda a, b: _wgrad(a, b, bf), do, cg)

@@ -117,3 +117,20 @@ def test_every_header_symbol_has_a_ctypes_signature():
     """A missing argtypes entry turns float arguments into ctypes errors at call time."""
     missing = [s for s in _lib.header_symbols() if s not in _lib._SIGNATURES]
     assert not missing, missing
+
+
+def test_ctypes_signatures_match_header_arity():
+    """Every ctypes signature has as many arguments as its declaration in include/tagan_hip.h (a miscounted
+    argtypes list only fails at call time, on the GPU)."""
+    import re
+    with open(_lib.HEADER_PATH) as f:
+        src = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    bad = []
+    for name, (_res, args) in _lib._SIGNATURES.items():
+        m = re.search(r"\b%s\s*\(([^;{]*?)\)\s*;" % re.escape(name), src)
+        assert m, "no declaration of %s" % name
+        params = m.group(1).strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        if n != len(args):
+            bad.append((name, n, len(args)))
+    assert not bad, bad

@@ -87,3 +87,31 @@ def test_layernorm_dropout_mask_shared(dev, M):
     ds, da, _, _, _ = ln_bwd(s, mean, rstd, gamma, dy, None, p, seed, True, True, False)
     assert torch.all(da[drop] == 0)
     torch.testing.assert_close(da[~drop], ds[~drop] / (1 - p), atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("M", MS + (320000,))
+@pytest.mark.parametrize("da_bf16", [False, True])
+def test_skip_bwd_fused_equals_two_passes(dev, M, da_bf16):
+    """tagan_layernorm_skip_bwd (the skip block's LN2 + LN_s backward in one pass) against the two-pass chain it
+    replaces (LN2's backward, then LN_s's with that ds as dres), with dropout: the same dropout decisions (da zero
+    exactly where the chain's is) and the same values to fp32 rounding -- the compiler contracts the fused pass's
+    multiply-adds differently (observed 1 ulp), so the bound is 4 ulp of the tensor's scale, not bit equality."""
+    from tagan_amd.fused import ln_bwd, ln_skip_bwd, ln_skip_fwd
+    H = 128
+    a, b, ab, g2, b2, _, dy = _inputs(dev, M, H, seed=11)
+    gs, bs = 1.0 + 0.1 * torch.randn(H, device=dev), 0.1 * torch.randn(H, device=dev)
+    y, s, mean, rstd, (ms, rss) = ln_skip_fwd(a, b, 0.1, 99, g2, b2, 1e-5, gs, bs, 1e-5, a_bias=ab)
+    dt = torch.bfloat16 if da_bf16 else torch.float32
+    ds1, da1, dg1, db1, dsa1 = ln_bwd(s, mean, rstd, g2, dy, None, 0.1, 99, True, True, True, da_dtype=dt)
+    ds1, _, dgs1, dbs1, _ = ln_bwd(b, ms, rss, gs, dy, ds1, 0.0, 0, True, False, False)
+    ds2, da2, dg2, db2, dsa2, dgs2, dbs2 = ln_skip_bwd(s, mean, rstd, g2, b, ms, rss, gs, dy, 0.1, 99, da_dtype=dt)
+    for n, x1, x2 in (("ds", ds1, ds2), ("da", da1, da2), ("dgamma", dg1, dg2), ("dbeta", db1, db2),
+                      ("dsum_a", dsa1, dsa2), ("dgamma_s", dgs1, dgs2), ("dbeta_s", dbs1, dbs2)):
+        err = float((x1.double() - x2.double()).abs().max())
+        scale = max(1.0, float(x1.double().abs().max()))
+        if n in ("ds", "da"):   # elementwise: a few fp32 ulp (one bf16 ulp where da is stored in bf16)
+            tol = (2.0 ** -7 if x1.dtype == torch.bfloat16 else 8 * 2.0 ** -23) * scale
+        else:                   # column sums over M rows of those elements
+            tol = 1e-5 * scale
+        assert err <= tol, (n, err, tol)
+    assert torch.equal(da1 == 0, da2 == 0)

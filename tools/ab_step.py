@@ -43,8 +43,11 @@ def main():
 
     graphs = {}
     for v in args.variants:
-        fused.SG_LN_SET = (set() if v == "none" else {"in", "out", "bwd"} if v == "all" else
-                           None if v == "auto" else set(v.replace("+", ",").split(",")))
+        # "<ln ops>[/skip0]": TAGAN_SG_LN op set; "/skip0" = the skip block's LN backward as two passes
+        ln, _, flag = v.partition("/")
+        fused.SG_LN_SET = (set() if ln == "none" else {"in", "out", "bwd"} if ln == "all" else
+                           None if ln == "auto" else set(ln.replace("+", ",").split(",")))
+        fused.LN_SKIP_BWD = flag != "skip0"
         graphs[v] = bench.graphed(model, opt, cfg, fwd)
     times = {v: [] for v in args.variants}
     st = torch.cuda.current_stream()
