@@ -167,20 +167,21 @@ __global__ void __launch_bounds__(HB) k_head_fwd(HeadArgs A) {
             L.vp[tid] = p;
         }
         __syncthreads();
-        // u = Wc1 p + bc1: one wave per output row, lanes over the (coalesced) row
-        {   // every row's load first (H <= 256: <= 16 rows per wave, one float4 per lane and row), then the sums
-            constexpr int MR = 256 / NWV;
+        // u = Wc1 p + bc1: one wave per output row, lanes over the row (H <= 256: one float4 per lane); the loads of
+        // MR rows are issued together before their sums (one latency per batch instead of one per row)
+        for (int r0 = 0; r0 * NWV < H; r0 += 4) {
+            constexpr int MR = 4;
             float4 wv[MR];
             const int k = lane * 4;
 #pragma unroll
             for (int r = 0; r < MR; ++r) {
-                const int jo = w + r * NWV;
+                const int jo = w + (r0 + r) * NWV;
                 wv[r] = (jo < H && k < H) ? *reinterpret_cast<const float4*>(A.Wc1 + (int64_t)jo * H + k)
                                           : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
             for (int r = 0; r < MR; ++r) {
-                const int jo = w + r * NWV;
+                const int jo = w + (r0 + r) * NWV;
                 if (jo >= H) break;
                 float s = 0.f;
                 if (k < H) s = (wv[r].x * L.vp[k] + wv[r].y * L.vp[k + 1]) + (wv[r].z * L.vp[k + 2] + wv[r].w * L.vp[k + 3]);

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round-end rehearsal: full GPU suite (parity maxima logged), smoke(), default bench line, rocprof kernel stats of the
+# C2 fp32 step, the stream-GEMM table.  bash tools/runs/round_end.sh <tag>
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/${1:-rend}
+mkdir -p $OUT
+TAGAN_PARITY_LOG=$OUT/parity_errors.json timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 \
+    --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }
+tail -1 $OUT/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
+timeout -k 10 500 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+python -c "import json;d=json.load(open('$OUT/bench.json'));print(d['value'], d['ms_per_step'], d['alt_precision']['ms_per_step'], d['roofline']['frac'], d['temporal_kernels'][1]['frac_bwd'])"
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_c2 -o run -- \
+    python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-roofline --no-alt-precision --no-c1 \
+    > $OUT/stats_c2.log 2>&1 || { tail -20 $OUT/stats_c2.log; exit 1; }
+find $OUT/stats_c2 -name "*kernel_trace*" -delete
+f=$(find $OUT/stats_c2 -name "*kernel_stats.csv" | head -1)
+python tools/kstats.py $f | sed -n 1,14p
+python tools/sgemm_table.py $f
