@@ -360,6 +360,11 @@ int tagan_sgemm_supported(int32_t N, int32_t K, int32_t planes, int32_t a_dtype,
 int tagan_sgemm_tn_supported(int32_t N, int32_t K, int32_t planes, int32_t dtype);
 int tagan_sgemm_wprep(int32_t N, int32_t K, const float* w, int64_t ldw, int32_t kmajor, int32_t planes, void* wp,
                       void* stream);
+/* tagan_sgemm_wprep_block: an attention block's four weight preparations in one launch -- wq_nt = wprep(w_qkv [3H, H],
+ * kmajor 0), wo_nt = wprep(w_o [H, H], 0), wo_km = wprep(w_o, 1), wq_km = wprep(w_qkv, 1) -- each bitwise equal to
+ * the tagan_sgemm_wprep call it stands for. */
+int tagan_sgemm_wprep_block(int32_t H, const float* w_qkv, int64_t ld_qkv, const float* w_o, int64_t ld_o,
+                            int32_t planes, void* wq_nt, void* wo_nt, void* wo_km, void* wq_km, void* stream);
 int tagan_sgemm_nt(int32_t a_dtype, int32_t c_dtype, int64_t M, int32_t N, int32_t K, const void* a, int64_t lda,
                    const void* wp, int32_t planes, const float* bias, void* c, int64_t ldc, void* stream);
 size_t tagan_sgemm_tn_workspace(int64_t M, int32_t N, int32_t K);

@@ -89,6 +89,7 @@ _SIGNATURES = {
     "tagan_sgemm_supported": (_c.c_int, [_i32, _i32, _i32, _i32, _i32]),
     "tagan_sgemm_tn_supported": (_c.c_int, [_i32, _i32, _i32, _i32]),
     "tagan_sgemm_wprep": (_c.c_int, [_i32, _i32, _p, _i64, _i32, _i32, _p, _p]),
+    "tagan_sgemm_wprep_block": (_c.c_int, [_i32, _p, _i64, _p, _i64, _i32, _p, _p, _p, _p, _p]),
     "tagan_sgemm_nt": (_c.c_int, [_i32, _i32, _i64, _i32, _i32, _p, _i64, _p, _i32, _p, _p, _i64, _p]),
     "tagan_sgemm_tn_workspace": (_sz, [_i64, _i32, _i32]),
     "tagan_sgemm_tn": (_c.c_int, [_i32, _i64, _i32, _i32, _p, _i64, _p, _i64, _i32, _p, _i64, _p, _p, _sz, _p]),

@@ -107,6 +107,40 @@ __global__ void k_sgemm_wprep(int N, int K, const float* __restrict__ w, int64_t
         wp[((int64_t)(ns * KK + kk) * P + p) * 64 + lane] = make_uint4(pl[p][0], pl[p][1], pl[p][2], pl[p][3]);
 }
 
+// the four weight preparations of an attention block in one launch (blockIdx.y = job): the forward operands of
+// the QKV and out projections and the transposed (k-major) operands of their input gradients
+struct PrepJob {
+    int N, K, kmajor;
+    const float* w;
+    int64_t ldw;
+    uint4* wp;
+};
+struct PrepJobs {
+    PrepJob j[4];
+};
+__global__ void k_sgemm_wprep4(PrepJobs J, int P) {
+    const PrepJob& jb = J.j[blockIdx.y];
+    const int KK = jb.K / 32;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)(jb.N / 16) * KK * 64) return;
+    const int lane = (int)(idx & 63);
+    const int64_t f = idx >> 6;
+    const int kk = (int)(f % KK), ns = (int)(f / KK);
+    const int n = ns * 16 + (lane & 15), k0 = kk * 32 + 8 * (lane >> 4);
+    float x[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = jb.kmajor ? jb.w[(int64_t)(k0 + e) * jb.ldw + n] : jb.w[(int64_t)n * jb.ldw + k0 + e];
+    uint32_t pl[3][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        uint32_t t[3];
+        split2<3>(x[2 * e], x[2 * e + 1], t);
+        pl[0][e] = t[0]; pl[1][e] = t[1]; pl[2][e] = t[2];
+    }
+    for (int p = 0; p < P; ++p)
+        jb.wp[((int64_t)(ns * KK + kk) * P + p) * 64 + lane] = make_uint4(pl[p][0], pl[p][1], pl[p][2], pl[p][3]);
+}
+
 // ------------------------------------------------------------------------------------------- NT: C = A·Bᵀ
 struct NtArgs {
     int64_t M;
@@ -1241,6 +1275,24 @@ extern "C" int tagan_sgemm_wprep(int32_t N, int32_t K, const float* w, int64_t l
     k_sgemm_wprep<<<(unsigned)((total + 255) / 256), 256, 0, as_stream(stream)>>>(N, K, w, ldw, kmajor, planes,
                                                                                    (uint4*)wp);
     TAGAN_CHECK_LAUNCH("tagan_sgemm_wprep");
+    return TAGAN_OK;
+}
+
+extern "C" int tagan_sgemm_wprep_block(int32_t H, const float* w_qkv, int64_t ld_qkv, const float* w_o, int64_t ld_o,
+                                       int32_t planes, void* wq_nt, void* wo_nt, void* wo_km, void* wq_km,
+                                       void* stream) {
+    TAGAN_REQUIRE(H > 0 && H % 32 == 0, TAGAN_ERR_ARG, "tagan_sgemm_wprep_block: H %% 32 must be 0 (H=%d)", H);
+    TAGAN_REQUIRE(planes == 1 || planes == 3, TAGAN_ERR_ARG, "tagan_sgemm_wprep_block: planes must be 1 or 3");
+    TAGAN_REQUIRE(w_qkv && w_o && wq_nt && wo_nt && wo_km && wq_km && ld_qkv >= H && ld_o >= H, TAGAN_ERR_ARG,
+                  "tagan_sgemm_wprep_block: bad arguments");
+    PrepJobs J;
+    J.j[0] = PrepJob{3 * H, H, 0, w_qkv, ld_qkv, (uint4*)wq_nt};   // QKV forward: B = W_qkv [3H, H]
+    J.j[1] = PrepJob{H, H, 0, w_o, ld_o, (uint4*)wo_nt};           // out forward: B = W_o [H, H]
+    J.j[2] = PrepJob{H, H, 1, w_o, ld_o, (uint4*)wo_km};           // dC = dO·W_o: B = W_oᵀ
+    J.j[3] = PrepJob{H, 3 * H, 1, w_qkv, ld_qkv, (uint4*)wq_km};   // dh = dqkv·W_qkv: B = W_qkvᵀ
+    const int64_t most = (int64_t)(3 * H / 16) * (H / 32) * 64;
+    k_sgemm_wprep4<<<dim3((unsigned)((most + 255) / 256), 4), 256, 0, as_stream(stream)>>>(J, planes);
+    TAGAN_CHECK_LAUNCH("tagan_sgemm_wprep_block");
     return TAGAN_OK;
 }
 

@@ -555,19 +555,21 @@ class AttnBlockFn(torch.autograd.Function):
         adt = torch.bfloat16 if act else torch.float32
         lnf = _sg_ln_use(H, bf, act, "in")
         ln_out = _sg_ln_use(H, bf, act, "out")
+        # the block's four weight operands in one launch; the transposed pair waits in ctx for the backward
+        wq_nt, wo_nt, wo_km, wq_km = sg.wprep_block(w_qkv, w_o, P)
         if lnf:   # LN1 in the QKV projection's prologue: h is never stored
             h = None
-            qkv, mean1, rstd1 = sg.nt_ln_in(x2, ln1_w, ln1_b, eps1, sg.wprep(w_qkv, False, P), 3 * H, P,
+            qkv, mean1, rstd1 = sg.nt_ln_in(x2, ln1_w, ln1_b, eps1, wq_nt, 3 * H, P,
                                             bias=b_qkv.contiguous(), out_dtype=adt)
         else:
             h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False, y_dtype=adt)
-            qkv = sg.nt(h, sg.wprep(w_qkv, False, P), 3 * H, P, bias=b_qkv.contiguous(), out_dtype=adt)
+            qkv = sg.nt(h, wq_nt, 3 * H, P, bias=b_qkv.contiguous(), out_dtype=adt)
         c, saved = core.fwd(qkv, p1, p2)
         if ln_out:   # dropout + residual + LN2 (+ the skip LayerNorm) in the out-projection's epilogue
-            y, s2, mean2, rstd2, skip = sg.nt_ln_out(c, sg.wprep(w_o, False, P), P, b_o.contiguous(), x2, p_out,
+            y, s2, mean2, rstd2, skip = sg.nt_ln_out(c, wo_nt, P, b_o.contiguous(), x2, p_out,
                                                      seed_out, ln2_w, ln2_b, eps2, lns_w, lns_b, eps_s)
         else:
-            o = sg.nt(c, sg.wprep(w_o, False, P), H, P)          # the bias is added in the closing LayerNorm
+            o = sg.nt(c, wo_nt, H, P)          # the bias is added in the closing LayerNorm
             skip = None
             if lns_w is not None:
                 y, s2, mean2, rstd2, skip = ln_skip_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, lns_w, lns_b,
@@ -577,6 +579,7 @@ class AttnBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
         ctx.inter = (h, ln1_b if lnf else None, mean1, rstd1, qkv, c, c, saved, s2, mean2, rstd2, skip)
         ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, "sgemm")
+        ctx.wkm = (wo_km, wq_km)
         ctx.sink = sink
         ctx.packed_aug = False
         return y.view(x.shape)
@@ -587,6 +590,7 @@ class AttnBlockFn(torch.autograd.Function):
         h, ln1_b, mean1, rstd1, qkv, c, _, saved, s2, mean2, rstd2, skip = ctx.inter
         core, p_out, seed_out, shape, bf, act, _ = ctx.cfg
         lnf = h is None   # the LayerNorm-fused form (h = LN1(x) recomputed where it is needed)
+        wo_km, wq_km = ctx.wkm
         ng = ctx.needs_input_grad
         H = shape[-1]
         P = 1 if bf else 3
@@ -594,7 +598,7 @@ class AttnBlockFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, H).contiguous()
         dres, do, dg2, db2, dbo, dgs, dbs = _ln2_bwd(s2, mean2, rstd2, ln2_w, dy2, skip, x2, lns_w, p_out, seed_out,
                                                      adt)
-        dc = sg.nt(do, sg.wprep(w_o, True, P), H, P, out_dtype=adt)
+        dc = sg.nt(do, wo_km, H, P, out_dtype=adt)
         dw_o = sg.tn(do, c, P, want_db=False)[0] if ng[7] else None
         dqkv, dp1, dp2, db_core = core.bwd(qkv, c, saved, dc, ng[1], ng[2], want_bias_sum=bool(ng[6]))
         del dc, do
@@ -608,13 +612,14 @@ class AttnBlockFn(torch.autograd.Function):
         if db_core is not None:
             db_qkv = db_core
         if _sg_ln_use(H, bf, act, "bwd"):   # dh = dqkv·W_qkv and LN1's backward in one kernel
-            dx, dg1, db1 = sg.nt_ln_bwd(dqkv, sg.wprep(w_qkv, True, P), P, x2, mean1, rstd1, ln1_w, dres)
+            dx, dg1, db1 = sg.nt_ln_bwd(dqkv, wq_km, P, x2, mean1, rstd1, ln1_w, dres)
             del dqkv
         else:
-            dh = sg.nt(dqkv, sg.wprep(w_qkv, True, P), H, P)
+            dh = sg.nt(dqkv, wq_km, H, P)
             del dqkv
             dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
         ctx.inter = None
+        ctx.wkm = None
         return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
                 None, None, None, None, None, dgs, dbs, None, None, None)
 

@@ -31,6 +31,24 @@ def wprep(w: torch.Tensor, kmajor: bool, planes: int) -> torch.Tensor:
     return wp
 
 
+def wprep_block(w_qkv: torch.Tensor, w_o: torch.Tensor, planes: int):
+    """The four operands of an attention block in one launch: (W_qkv, W_o) for the forward products and (W_oᵀ,
+    W_qkvᵀ) for the input gradients (= wprep(w_qkv, False), wprep(w_o, False), wprep(w_o, True), wprep(w_qkv, True))."""
+    assert w_qkv.dtype == torch.float32 and w_o.dtype == torch.float32
+    if w_qkv.stride(1) != 1:
+        w_qkv = w_qkv.contiguous()
+    if w_o.stride(1) != 1:
+        w_o = w_o.contiguous()
+    H = w_o.shape[0]
+    assert w_qkv.shape == (3 * H, H) and w_o.shape == (H, H)
+    buf = torch.empty(8 * H * H * planes, dtype=torch.bfloat16, device=w_o.device)
+    wq_nt, wo_nt, wo_km, wq_km = torch.split(buf, [3 * H * H * planes, H * H * planes, H * H * planes,
+                                                   3 * H * H * planes])
+    check(lib().tagan_sgemm_wprep_block(H, ptr(w_qkv), w_qkv.stride(0), ptr(w_o), w_o.stride(0), planes, ptr(wq_nt),
+                                        ptr(wo_nt), ptr(wo_km), ptr(wq_km), stream_of(w_o)), "tagan_sgemm_wprep_block")
+    return wq_nt, wo_nt, wo_km, wq_km
+
+
 def nt(a: torch.Tensor, wp: torch.Tensor, N: int, planes: int, bias=None, out_dtype=torch.float32, out=None):
     """out[M, N] = a[M, K] · Bᵀ (+ bias) with B prepared by ``wprep``."""
     M, K = a.shape

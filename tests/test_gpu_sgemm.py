@@ -131,3 +131,18 @@ def test_unsupported_shape_reported():
     with pytest.raises(RuntimeError):
         sg.nt(torch.randn(10, 64, device="cuda"), torch.empty(96 * 64 * 3, dtype=torch.bfloat16, device="cuda"),
               96, 3)
+
+
+@pytest.mark.parametrize("planes", [1, 3])
+def test_wprep_block_equals_single_preps(planes):
+    """tagan_sgemm_wprep_block's four operands are bitwise the four tagan_sgemm_wprep calls they stand for."""
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    g = torch.Generator(device=dev).manual_seed(31)
+    wq = torch.randn(384, 128, device=dev, generator=g)
+    wo = torch.randn(128, 128, device=dev, generator=g)
+    got = sg.wprep_block(wq, wo, planes)
+    want = (sg.wprep(wq, False, planes), sg.wprep(wo, False, planes), sg.wprep(wo, True, planes),
+            sg.wprep(wq, True, planes))
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
