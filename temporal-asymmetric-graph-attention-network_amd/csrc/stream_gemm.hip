@@ -598,9 +598,15 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
 // n-subtile), so a LayerNorm's row statistics are two shuffles: no LDS hand-off and no workgroup barrier in the tile
 // loop -- the W waves of a CU run their tiles independently and overlap each other's memory and matrix phases (the
 // weight-stationary k_sgemm_nt needs one barrier per tile for a row-wide epilogue and measured slower there).
-template <int K, int P, bool ABF, bool CBF, int MODE, int W>
+//
+// MODE_LN_IN (N = 3H = 384, one plane: the bf16 QKV projection): LN1 in the prologue -- the lane's 32 values of x
+// (row c, k = 32 kk + 8 t + [0, 8)) and the other three lane groups hold the whole row, so its two-pass statistics
+// are in-lane sums and two shuffles; h = ln_apply(x) exactly as k_sgemm_nt's prologue makes it.
+template <int K, int P, bool ABF, bool CBF, int MODE, int W, int NN = 128>
 __global__ void __launch_bounds__(W * 64) k_rowgemm(NtArgs g) {
-    constexpr int NS = 8, N = 128, KK = K / 32;
+    constexpr int N = NN, NS = N / 16, KK = K / 32;
+    static_assert(MODE != MODE_LN_IN || (!ABF && K == 128), "LN prologue: fp32 rows of K = 128");
+    static_assert(MODE == MODE_LN_IN || N == 128, "row-wide epilogues: N = 128");
     constexpr int NB = NS * KK * P * 64;             // B fragments (uint4) in LDS
     static_assert(!ABF || P == 1, "bf16 operands have one plane");
     extern __shared__ uint4 sg_lds[];
@@ -612,7 +618,9 @@ __global__ void __launch_bounds__(W * 64) k_rowgemm(NtArgs g) {
     for (int i = threadIdx.x; i < 5 * N; i += W * 64) {
         const int q = i / N, col = i % N;
         const float* src = q == 0 ? g.ln_g : q == 1 ? g.ln_b : q == 2 ? g.gs : q == 3 ? g.bs : g.bias;
-        prm[i] = (src && (q == 4 || (MODE == MODE_LN_OUT) || (MODE == MODE_LN_BWD && q == 0))) ? src[col] : 0.f;
+        const bool use = q == 4 || MODE == MODE_LN_OUT || (MODE == MODE_LN_BWD && q == 0) ||
+                         (MODE == MODE_LN_IN && q < 2 && col < K);
+        prm[i] = (src && use) ? src[col] : 0.f;
     }
     __syncthreads();
     if constexpr (MODE == MODE_LN_OUT) {
@@ -651,6 +659,39 @@ __global__ void __launch_bounds__(W * 64) k_rowgemm(NtArgs g) {
 #pragma unroll
             for (int s = 0; s < NS; ++s) er[s] = *reinterpret_cast<const f32x4*>(g.res + row * g.ldr + 16 * s + 4 * gq);
         }
+        if constexpr (MODE == MODE_LN_IN) {   // h = LN1(x) in place
+            float sm = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk)
+                sm += (af[kk][0].x + af[kk][0].y) + (af[kk][0].z + af[kk][0].w) +
+                      ((af[kk][1].x + af[kk][1].y) + (af[kk][1].z + af[kk][1].w));
+            const float mean = gsum4(sm) / (float)K;
+            float sq = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float4 v = af[kk][h];
+                    sq += ((v.x - mean) * (v.x - mean) + (v.y - mean) * (v.y - mean)) +
+                          ((v.z - mean) * (v.z - mean) + (v.w - mean) * (v.w - mean));
+                }
+            const float rstd = 1.f / sqrtf(gsum4(sq) / (float)K + g.eps);
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int k0 = 32 * kk + 8 * gq + 4 * h;
+                    float4& v = af[kk][h];
+                    v.x = ln_apply(v.x, mean, rstd, prm[k0], prm[N + k0]);
+                    v.y = ln_apply(v.y, mean, rstd, prm[k0 + 1], prm[N + k0 + 1]);
+                    v.z = ln_apply(v.z, mean, rstd, prm[k0 + 2], prm[N + k0 + 2]);
+                    v.w = ln_apply(v.w, mean, rstd, prm[k0 + 3], prm[N + k0 + 3]);
+                }
+            if (live && gq == 0) {
+                g.mean[row] = mean;
+                g.rstd[row] = rstd;
+            }
+        }
         f32x4 acc[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) acc[s] = pv(4, s);
@@ -678,7 +719,7 @@ __global__ void __launch_bounds__(W * 64) k_rowgemm(NtArgs g) {
             }
         }
         // lane holds C[row][16 s + 4 gq + e], e = 0..3, for every n-subtile s
-        if constexpr (MODE == MODE_PLAIN) {
+        if constexpr (MODE == MODE_PLAIN || MODE == MODE_LN_IN) {
             if (live) {
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
@@ -1169,11 +1210,13 @@ struct RgCfg {
     int K, P, abf, cbf, mode, w;
     nt_fn fn;
     size_t lds;
+    int n;
 };
-template <int K, int P, bool ABF, bool CBF, int MODE, int W = 16>
+template <int K, int P, bool ABF, bool CBF, int MODE, int W = 16, int NN = 128>
 constexpr RgCfg rg_cfg() {
-    return RgCfg{K, P, ABF, CBF, MODE, W, k_rowgemm<K, P, ABF, CBF, MODE, W>,
-                 (size_t)8 * (K / 32) * P * 64 * 16 + (size_t)(5 * 128 + (MODE == MODE_LN_BWD ? W * 2 * 128 : 0)) * 4};
+    return RgCfg{K, P, ABF, CBF, MODE, W, k_rowgemm<K, P, ABF, CBF, MODE, W, NN>,
+                 (size_t)(NN / 16) * (K / 32) * P * 64 * 16 + (size_t)(5 * NN + (MODE == MODE_LN_BWD ? W * 2 * NN : 0)) * 4,
+                 NN};
 }
 // N = 128 only; B's planes must fit the LDS (K = 384 in fp32 would need 288 KB: k_sgemm_nt keeps that shape)
 const RgCfg RG_TABLE[] = {
@@ -1183,10 +1226,11 @@ const RgCfg RG_TABLE[] = {
     rg_cfg<128, 3, false, false, MODE_LN_OUT>(), rg_cfg<128, 1, true, false, MODE_LN_OUT>(),
     rg_cfg<128, 1, false, false, MODE_LN_OUT>(),
     rg_cfg<384, 1, true, false, MODE_LN_BWD, 8>(), rg_cfg<384, 1, false, false, MODE_LN_BWD, 8>(),
+    rg_cfg<128, 1, false, true, MODE_LN_IN, 8, 384>(), rg_cfg<128, 1, false, false, MODE_LN_IN, 8, 384>(),
 };
 
 // TAGAN_SG_ROW (A/B knob, read once): 1 (default) = the LayerNorm-fused N = 128 products on k_rowgemm, 0 = all on
-// k_sgemm_nt, 2 = the plain N = 128 products on k_rowgemm too.  Plain products measured faster on k_sgemm_nt (C2
+// k_sgemm_nt, 2 = the plain N = 128 products on k_rowgemm too, 3 = also the one-plane LN1 + QKV forward (N = 384).  Plain products measured faster on k_sgemm_nt (C2
 // kernel stats, profiles/r3d_sgemm_table_fp32.md: fp32 K = 128 62 vs 77 us, bf16 41 vs 46 us, bf16 K = 384 70 vs
 // 78 us): without a row-wide epilogue the weight-stationary kernel's register-resident B wins.
 int rowgemm_level() {
@@ -1199,9 +1243,9 @@ int rowgemm_level() {
 
 const RgCfg* rg_find(int K, int N, int P, int abf, int cbf, int mode) {
     const int lv = rowgemm_level();
-    if (N != 128 || lv == 0 || (mode == MODE_PLAIN && lv < 2)) return nullptr;
+    if (lv == 0 || (mode == MODE_PLAIN && lv < 2) || (mode == MODE_LN_IN && lv < 3)) return nullptr;
     for (const RgCfg& c : RG_TABLE)
-        if (c.K == K && c.P == P && c.abf == abf && c.cbf == cbf && c.mode == mode) return &c;
+        if (c.n == N && c.K == K && c.P == P && c.abf == abf && c.cbf == cbf && c.mode == mode) return &c;
     return nullptr;
 }
 
@@ -1331,8 +1375,10 @@ extern "C" int tagan_sgemm_ln_supported(int32_t H, int32_t planes, int32_t act_d
 extern "C" int tagan_sgemm_nt_ln_in(int32_t c_dtype, int64_t M, int32_t N, int32_t K, const float* x, int64_t ldx,
                                     const float* ln_g, const float* ln_b, float eps, const void* wp, int32_t planes,
                                     const float* bias, void* c, int64_t ldc, float* mean, float* rstd, void* stream) {
+    const RgCfg* rcfg = rg_find(K, N, planes, 0, c_dtype == TAGAN_BF16, MODE_LN_IN);
     const NtCfg* cfg = nt_find(K, N, planes, 0, c_dtype == TAGAN_BF16, MODE_LN_IN);
-    TAGAN_REQUIRE(cfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt_ln_in: no kernel for N=%d K=%d planes=%d", N, K, planes);
+    TAGAN_REQUIRE(cfg || rcfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt_ln_in: no kernel for N=%d K=%d planes=%d", N, K,
+                  planes);
     TAGAN_REQUIRE(M >= 0 && wp && ln_g && ln_b, TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_in: bad arguments");
     if (M == 0) return TAGAN_OK;
     TAGAN_REQUIRE(x && c && mean && rstd && ldx >= K && ldc >= N, TAGAN_ERR_ARG, "tagan_sgemm_nt_ln_in: bad operands");
@@ -1343,6 +1389,7 @@ extern "C" int tagan_sgemm_nt_ln_in(int32_t c_dtype, int64_t M, int32_t N, int32
     NtArgs g{};
     g.M = M; g.a = x; g.lda = ldx; g.wp = (const uint4*)wp; g.bias = bias; g.c = c; g.ldc = ldc;
     g.ln_g = ln_g; g.ln_b = ln_b; g.eps = eps; g.mean = mean; g.rstd = rstd;
+    if (rcfg) return rg_launch(rcfg, g, stream, "tagan_sgemm_nt_ln_in");
     return nt_launch(cfg, g, N, stream, "tagan_sgemm_nt_ln_in");
 }
 
@@ -1377,9 +1424,8 @@ extern "C" size_t tagan_sgemm_nt_ln_bwd_workspace(int64_t M, int32_t H, int32_t 
     int64_t g = 1;
     for (const NtCfg& c : NT_TABLE)
         if (c.mode == MODE_LN_BWD && c.N == H && c.K == K) g = std::max(g, nt_groups(M, &c, 1));
-    if (H == 128)
-        for (const RgCfg& c : RG_TABLE)
-            if (c.mode == MODE_LN_BWD && c.K == K) g = std::max(g, rg_groups(M, &c));
+    for (const RgCfg& c : RG_TABLE)
+        if (c.mode == MODE_LN_BWD && c.n == H && c.K == K) g = std::max(g, rg_groups(M, &c));
     return (size_t)g * 2 * H * sizeof(float);
 }
 
