@@ -2486,12 +2486,12 @@ int lds_optin(K* kern, size_t bytes) {
 
 // waves: G partial rows x heads (G <= grid_rows(rows), the bias-gradient workspace rows)
 // (a multiple of 8 from 8 rows up, for the XCD-aware wave map)
-// TAGAN_V4_G=<n> overrides the 1024 row groups (grid-size sweeps; capped at 1024 = the workspace rows)
+// TAGAN_V4_G=<n> overrides the 1024 row groups (grid-size sweeps, up to 8192; the workspace follows: ws_rows)
 int64_t v4_groups(int64_t rows) {
     static const int64_t cap = [] {
         const char* e = getenv("TAGAN_V4_G");
         const int64_t v = e ? atoll(e) : 0;
-        return (v >= 8 && v <= 1024) ? v : (int64_t)1024;
+        return (v >= 8 && v <= 8192) ? v : (int64_t)1024;
     }();
     return rows >= 8 ? std::min<int64_t>(rows, cap) & ~(int64_t)7 : rows;
 }
@@ -2516,6 +2516,8 @@ int pick_D(int d) {
 }
 
 int grid_rows(int64_t rows) { return (int)std::min<int64_t>(rows, 256 * 4); }
+// partial rows of the backward workspace: every kernel generation's row groups fit
+int64_t ws_rows(int64_t rows) { return std::max<int64_t>(grid_rows(rows), v4_groups(rows)); }
 
 int check(int dtype, int64_t rows, int T, int heads, int d, float p_drop) {
     TAGAN_REQUIRE(dtype == TAGAN_F32 || dtype == TAGAN_BF16, TAGAN_ERR_UNSUPPORTED, "temporal_attn: dtype %d",
@@ -2667,8 +2669,8 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
 size_t tagan_temporal_attn_bwd_workspace(int64_t rows, int32_t T, int32_t heads, int32_t head_dim) {
     using namespace tagan;
     if (rows <= 0 || T <= 0 || heads <= 0 || head_dim <= 0) return 0;
-    return align_up((size_t)grid_rows(rows) * heads * (2 * T - 1) * sizeof(float), 256) +
-           align_up((size_t)grid_rows(rows) * 3 * heads * head_dim * sizeof(float), 256);
+    return align_up((size_t)ws_rows(rows) * heads * (2 * T - 1) * sizeof(float), 256) +
+           align_up((size_t)ws_rows(rows) * 3 * heads * head_dim * sizeof(float), 256);
 }
 
 int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim, const void* q,
@@ -2714,7 +2716,7 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
         if (dbias_table) A.part = (float*)workspace;
         if (dsum_qkv)
             A.qkv_part = (float*)((char*)workspace +
-                                  align_up((size_t)nblk * heads * (2 * T - 1) * sizeof(float), 256));
+                                  align_up((size_t)ws_rows(rows) * heads * (2 * T - 1) * sizeof(float), 256));
     }
     hipStream_t s = as_stream(stream);
     const dim3 g(nblk);
