@@ -23,11 +23,23 @@ There is deliberately no split form (an eager segment between two captured ones)
 that form faulted and why the collective lives inside the one graph instead.
 """
 import ctypes
+import time
 from typing import Callable
 
 import torch
 
 from ._lib import check, lib, ptr
+
+
+def _nccl_live() -> bool:
+    """A process group with an RCCL ("nccl") backend is initialised (its watchdog thread polls work events)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    try:
+        return "nccl" in str(dist.get_backend()).lower()
+    except Exception:
+        return False
 
 
 class GraphedStep:
@@ -56,6 +68,13 @@ class GraphedStep:
         torch.cuda.current_stream(dev).wait_stream(side)
         if optimizer is not None:
             optimizer.zero_grad(set_to_none=True)
+        if _nccl_live():
+            # the RCCL process group's watchdog polls the end events of the warm-up steps' collectives; if one is
+            # still queued when the capture starts, the event can be recycled into the captured all-reduce and the
+            # poll then fails with hipErrorCapturedEvent (an abort seen once in five full suites, C2 graph step).
+            # Drain the device and give the watchdog (100-ms poll) time to retire that work first.
+            torch.cuda.synchronize(dev)
+            time.sleep(0.3)
         self.graph = torch.cuda.CUDAGraph()
         # captured on the warm-up stream: autograd nodes that outlive a warm-up step (a loss the caller kept,
         # AccumulateGrad nodes) then belong to the capture stream, so the backward adds no cross-stream join.
