@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--no-c1", action="store_true", help="skip the GPU C1 line beside the C1 CPU baselines")
     ap.add_argument("--launch", default="auto", choices=("auto", "graph", "eager"),
                     help="graph: replay the step as a HIP graph (graph_step.py); eager: launch every kernel from "
-                         "Python; auto (default): time a short trial of both and keep the faster (--shard: eager)")
+                         "Python; auto (default): time a short trial of both and keep the faster; --shard always launches eagerly")
     ap.add_argument("--no-graph", action="store_true", help="same as --launch eager")
     ap.add_argument("--sub-records", default="auto",
                     help="BASELINE multi-GPU workloads measured beside the headline: auto (c3_dp at N = 2, 4; "
@@ -590,7 +590,7 @@ def c5_shard_record(dev, rank, world, ctl, backend, steps=5, warmup=3):
     opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay, fused=True)
     t0, t1 = blocks(T, world)[rank]
     full = synthetic.make_sequence("c5", dev, seed=5000)   # the same sequence on every rank; keep this rank's block
-    seq = full[t0:t1]
+    seq = synthetic.take(full, t0, t1)
     del full
     counts_all = [N] * T
     sharded = SnapshotShardedTAGAN.for_model(model)
@@ -642,10 +642,11 @@ def main():
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
+        from tagan_amd.distributed import init_process_group   # RCCL event recycling off (graph capture)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
-            dist.init_process_group(backend)
+            init_process_group(backend)
         assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -666,7 +667,8 @@ def main():
     # every form of the step is captured whole (the RCCL all-reduce inside the graph); only a gloo data plane
     # (the one-GPU rehearsal knob) cannot be captured and launches eagerly
     capturable = world == 1 or backend == "nccl"
-    launch = "eager" if (args.no_graph or not capturable) else args.launch
+    # --shard launches eagerly: no test captures the sharded step (all-to-all + segment reduce + static grad sync)
+    launch = "eager" if (args.no_graph or not capturable or args.shard) else args.launch
     use_graph = launch != "eager"   # capturable optimizer whenever a graph may be captured
     torch.manual_seed(0)
     model = TAGAN(cfg, precision=args.precision).to(dev).train()
@@ -681,7 +683,7 @@ def main():
         full = synthetic.make_sequence(args.config, dev, seed=1000)
         counts_all = [int(x.shape[0]) for x, _, _, _ in full]
         t0, t1 = blocks(len(full), world)[rank]
-        seq = full[t0:t1]
+        seq = synthetic.take(full, t0, t1)
         del full
         sharded = SnapshotShardedTAGAN.for_model(model)
         sync = ShardGradSync(list(model.named_parameters()))

@@ -56,6 +56,10 @@ enum tagan_metric {
 };
 
 const char* tagan_last_error(void);
+/* 1 when the library is the bounds-check build (`make debug`: device checks on gather indices, chunk ranges and
+ * partial slots; a failing check skips its access and the next launch check returns TAGAN_ERR_LAUNCH with the
+ * source line in tagan_last_error(); eager launches only), 0 for the shipped build. */
+int tagan_debug_build(void);
 int tagan_version(void);
 int tagan_device_arch(char* buf, int len);   /* e.g. "gfx950"; needs a device */
 
@@ -302,45 +306,6 @@ int tagan_layernorm_skip_bwd(int dtype, int64_t M, int32_t H, const float* s, co
                              const float* gamma_s, const float* dy, float p_drop, uint64_t seed, float* ds, float* da,
                              float* dgamma, float* dbeta, float* dsum_a, float* dgamma_s, float* dbeta_s,
                              void* workspace, size_t workspace_bytes, void* stream);
-
-/* ---------------------------------------------------------------------------
- * Fused projection GEMMs of an attention block (csrc/proj_gemm.hip), fp32 on the
- * f32 matrix cores (v_mfma_f32_32x32x2_f32), H = 128 (tagan_proj_supported).
- * Replace, per GeometricAttention / temporal layer (geometric_attention.py:541-596,
- * temporal_attention.py:985-1200): layer_norm1 + the q/k/v Linears, the out Linear +
- * output_dropout + residual + layer_norm2, and in the backward the q/k/v input
- * gradient + layer_norm1's backward (the autograd graph of those ops).  All operands
- * fp32, row-major, 16-byte aligned; weights in nn.Linear layout [out, in].
- *
- * tagan_ln_qkv_fwd:  h = LN(x; gamma, beta, eps) (x [M,H]);  out[M,N] = h·wᵀ + bias
- *   (w [N,H], N = 3H, out row stride ldo); mean/rstd [M] for the backward; h_out
- *   (optional, row stride ldh) receives h, plus (1,0,0,0) at columns H..H+3 when
- *   ldh >= H + 4 (the augmented operand of the weight-gradient GEMM).
- * tagan_proj_ln_fwd:  s = dropout(a·wᵀ + bias; p_drop, seed) + res  (element (r,c):
- *   stream r, counter c — the same mask as tagan_add_layernorm_fwd),
- *   y = LN(s; gamma, beta, eps) [+ LN_s(res; gamma_s, beta_s, eps_s) when gamma_s];
- *   s_out, mean/rstd (and mean_s/rstd_s) are kept for tagan_layernorm_bwd.
- * tagan_proj_gemm:  out[M,H] = a[M,K]·B, K = H or 3H (a row stride lda);
- *   B = w ([K,H], w_kmajor = 1) or wᵀ (w [H,K], w_kmajor = 0).
- * tagan_proj_ln_bwd:  dh = da[M,K]·w (w [K,H], K = H or 3H: the input gradient of
- *   the projection whose weight is w), then LN's backward with LN's forward input x
- *   and statistics mean/rstd:  dx = rstd·(g − mean(g·x̂)·x̂ − mean(g)) + dres,
- *   g = dh·gamma;  dgamma = Σ dh·x̂, dbeta = Σ dh (ordered per-block partials).
- * ------------------------------------------------------------------------- */
-int tagan_proj_supported(int32_t H);
-int tagan_ln_qkv_fwd(int64_t M, int32_t H, int32_t N, const float* x, const float* gamma, const float* beta,
-                     float eps, const float* w, const float* bias, float* out, int64_t ldo, float* h_out,
-                     int64_t ldh, float* mean, float* rstd, void* stream);
-int tagan_proj_ln_fwd(int64_t M, int32_t H, const float* a, const float* w, const float* bias, const float* res,
-                      float p_drop, uint64_t seed, const float* gamma, const float* beta, float eps,
-                      const float* gamma_s, const float* beta_s, float eps_s, float* s_out, float* y,
-                      float* mean, float* rstd, float* mean_s, float* rstd_s, void* stream);
-int tagan_proj_gemm(int64_t M, int32_t H, int32_t K, const float* a, int64_t lda, const float* w, int w_kmajor,
-                    float* out, int64_t ldo, void* stream);
-size_t tagan_proj_ln_bwd_workspace(int64_t M, int32_t H);
-int tagan_proj_ln_bwd(int64_t M, int32_t H, int32_t K, const float* da, const float* w, const float* x,
-                      const float* mean, const float* rstd, const float* gamma, const float* dres, float* dx,
-                      float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Streaming projection GEMMs on the bf16 matrix cores (csrc/stream_gemm.hip).  Replace the q/k/v and out Linears

@@ -35,6 +35,7 @@ _i32, _i64, _u64, _f32, _sz = _c.c_int32, _c.c_int64, _c.c_uint64, _c.c_float, _
 _SIGNATURES = {
     "tagan_last_error": (_c.c_char_p, []),
     "tagan_version": (_c.c_int, []),
+    "tagan_debug_build": (_c.c_int, []),
     "tagan_device_arch": (_c.c_int, [_c.c_char_p, _c.c_int]),
     "tagan_uniform": (_f32, [_u64, _u64, _c.c_uint32]),
     "tagan_set_seed_counter": (None, [_p]),
@@ -79,13 +80,6 @@ _SIGNATURES = {
                                        _p, _p, _sz, _p]),
     "tagan_layernorm_skip_bwd_workspace": (_sz, [_i64, _i32]),
     "tagan_layernorm_skip_bwd": (_c.c_int, [_c.c_int, _i64, _i32] + [_p] * 8 + [_p, _f32, _u64] + [_p] * 8 + [_sz, _p]),
-    "tagan_proj_supported": (_c.c_int, [_i32]),
-    "tagan_ln_qkv_fwd": (_c.c_int, [_i64, _i32, _i32, _p, _p, _p, _f32, _p, _p, _p, _i64, _p, _i64, _p, _p, _p]),
-    "tagan_proj_ln_fwd": (_c.c_int, [_i64, _i32, _p, _p, _p, _p, _f32, _u64, _p, _p, _f32, _p, _p, _f32, _p, _p, _p,
-                                     _p, _p, _p, _p]),
-    "tagan_proj_gemm": (_c.c_int, [_i64, _i32, _i32, _p, _i64, _p, _c.c_int, _p, _i64, _p]),
-    "tagan_proj_ln_bwd_workspace": (_sz, [_i64, _i32]),
-    "tagan_proj_ln_bwd": (_c.c_int, [_i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
     "tagan_sgemm_supported": (_c.c_int, [_i32, _i32, _i32, _i32, _i32]),
     "tagan_sgemm_tn_supported": (_c.c_int, [_i32, _i32, _i32, _i32]),
     "tagan_sgemm_wprep": (_c.c_int, [_i32, _i32, _p, _i64, _i32, _i32, _p, _p]),

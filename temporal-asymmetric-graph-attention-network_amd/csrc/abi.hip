@@ -29,6 +29,14 @@ const char* tagan_last_error(void) { return tagan::g_err; }
 
 int tagan_version(void) { return 1; }
 
+int tagan_debug_build(void) {
+#ifdef TAGAN_DEBUG
+    return 1;
+#else
+    return 0;
+#endif
+}
+
 int tagan_device_arch(char* buf, int len) {
     TAGAN_REQUIRE(buf != nullptr && len > 0, TAGAN_ERR_ARG, "tagan_device_arch: null buffer");
     int dev = 0;

@@ -21,6 +21,52 @@ void set_error(const char* fmt, ...);
         }                                        \
     } while (0)
 
+// ---------------------------------------------------------------- bounds-check debug build
+// `make debug` (= EXTRA=-DTAGAN_DEBUG into build_debug/ and libtagan_hip_debug.so; never the shipped library)
+// compiles the device checks TAGAN_DBAD(cond, a, b) in: a failing check records (line, a, b) in this translation
+// unit's device word, prints the first failure, and evaluates to true so the caller SKIPS the access it guards (no
+// out-of-bounds access, no trap: a check must not take the GPU down).  Every TAGAN_CHECK_LAUNCH then synchronises
+// the device and turns a recorded failure into TAGAN_ERR_LAUNCH with the file / line / values in tagan_last_error().
+// The per-launch synchronisation makes the debug build eager-only (no HIP-graph capture).  In the default build the
+// checks compile to `false` and cost nothing.
+#ifdef TAGAN_DEBUG
+static __device__ unsigned int g_tagan_dbg[4];   // per translation unit: {failures, line, a, b}
+__device__ __noinline__ static bool tagan_dbg_record(const char* file, int line, long long a, long long b) {
+    if (atomicAdd(&g_tagan_dbg[0], 1u) == 0u) {
+        g_tagan_dbg[1] = (unsigned)line;
+        g_tagan_dbg[2] = (unsigned)a;
+        g_tagan_dbg[3] = (unsigned)b;
+        printf("TAGAN_DEBUG %s:%d: check failed (a=%lld b=%lld)\n", file, line, a, b);
+    }
+    return true;
+}
+#define TAGAN_DBAD(cond, a, b) (!(cond) && tagan_dbg_record(__FILE__, __LINE__, (long long)(a), (long long)(b)))
+static inline int tagan_dbg_poll(const char* what) {
+    unsigned int h[4] = {0, 0, 0, 0};
+    if (hipDeviceSynchronize() != hipSuccess) {
+        ::tagan::set_error("%s: device error (debug build)", what);
+        return TAGAN_ERR_LAUNCH;
+    }
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_tagan_dbg), sizeof(h)) != hipSuccess) return TAGAN_OK;
+    if (h[0] == 0) return TAGAN_OK;
+    const unsigned int z[4] = {0, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tagan_dbg), z, sizeof(z));
+    ::tagan::set_error("%s: TAGAN_DEBUG check failed %u time(s), first at line %u of the kernel source (a=%d b=%d)",
+                       what, h[0], h[1], (int)h[2], (int)h[3]);
+    return TAGAN_ERR_LAUNCH;
+}
+#define TAGAN_DBG_POLL(what)                     \
+    do {                                         \
+        const int d_ = ::tagan::tagan_dbg_poll(what);     \
+        if (d_ != TAGAN_OK) return d_;           \
+    } while (0)
+#else
+#define TAGAN_DBAD(cond, a, b) false
+#define TAGAN_DBG_POLL(what) \
+    do {                     \
+    } while (0)
+#endif
+
 #define TAGAN_CHECK_LAUNCH(what)                                                       \
     do {                                                                               \
         hipError_t e_ = hipGetLastError();                                             \
@@ -28,6 +74,7 @@ void set_error(const char* fmt, ...);
             ::tagan::set_error("%s: launch failed: %s", what, hipGetErrorString(e_));  \
             return TAGAN_ERR_LAUNCH;                                                   \
         }                                                                              \
+        TAGAN_DBG_POLL(what);                                                          \
     } while (0)
 
 #define TAGAN_CHECK_HIP(call, what)                                                    \

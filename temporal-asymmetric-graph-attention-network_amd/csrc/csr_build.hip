@@ -1025,6 +1025,8 @@ __global__ void __launch_bounds__(FNT) k_csr_place(Geo g, const int32_t* __restr
     for (int i = threadIdx.x; i < cnt; i += FNT) {
         const uint32_t k = keys[off + i];
         const int j = (int)(k >> g.LB);
+        if (TAGAN_DBAD(j < nv && u + i < g.E + g.N, j, u + i)) continue;   // row of the bucket, CSR capacity
+        if (TAGAN_DBAD(rb[j] + (int64_t)(k & lmask) < g.N, rb[j], k & lmask)) continue;   // column id
         col[u + i] = rb[j] + (int32_t)(k & lmask);
         sloc[u + i] = (int32_t)(r0 + j) - rb[j];
     }

@@ -308,6 +308,8 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
     if (valid) {
         row = A.g.row_chunk_seg[L.chunk];
         e0 = A.g.row_chunk_beg[L.chunk];
+        if (TAGAN_DBAD(row >= 0 && row < A.g.n_nodes && e0 >= A.g.rowptr[row] && e0 <= A.g.rowptr[row + 1], row, e0))
+            row = e0 = 0;
         cnt = min(A.g.chunk, A.g.rowptr[row + 1] - e0);
     }
     if (!__any(valid)) return;
@@ -327,6 +329,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
     int mycol = 0;
     for (int jj = 0; __any(jj < cnt); jj += UN) {
         if ((jj % LPR) == 0) mycol = (jj + L.sl < cnt) ? A.g.col[e0 + jj + L.sl] : 0;
+        if (TAGAN_DBAD(mycol >= 0 && mycol < A.g.n_nodes, mycol, row)) mycol = 0;   // gather index
         float kv[UN][FPL], vv[UN][FPL];
 #pragma unroll
         for (int u = 0; u < UN; ++u) {
@@ -356,6 +359,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
     }
     if (!valid) return;
     const int part = A.g.row_chunk_part[L.chunk];
+    if (TAGAN_DBAD(part < A.g.part_cap, part, A.g.part_cap)) return;   // partial slot
     if (part < 0) {
         const float inv = (l > 0.f) ? 1.f / l : NAN;
 #pragma unroll
@@ -443,6 +447,7 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_merge(GeoArgs A) {
                 const int cc = c + u * nph;
                 if (cc < c1) {
                     const int part = A.g.row_chunk_part[cc];
+                    if (TAGAN_DBAD(part >= 0 && part < A.g.part_cap, part, A.g.part_cap)) continue;   // partial slot
                     SoftState y;
                     y.m = A.part_m[(int64_t)part * A.heads + h];
                     y.l = A.part_l[(int64_t)part * A.heads + h];
@@ -475,6 +480,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
     if (valid) {
         row = A.g.row_chunk_seg[L.chunk];
         e0 = A.g.row_chunk_beg[L.chunk];
+        if (TAGAN_DBAD(row >= 0 && row < A.g.n_nodes && e0 >= A.g.rowptr[row] && e0 <= A.g.rowptr[row + 1], row, e0))
+            row = e0 = 0;
         cnt = min(A.g.chunk, A.g.rowptr[row + 1] - e0);
     }
     const int lph = A.d / FPL;
@@ -498,6 +505,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
         int mycol = 0;
         for (int jj = 0; __any(jj < cnt); jj += UN) {
             if ((jj % LPR) == 0) mycol = (jj + L.sl < cnt) ? A.g.col[e0 + jj + L.sl] : 0;
+            if (TAGAN_DBAD(mycol >= 0 && mycol < A.g.n_nodes, mycol, row)) mycol = 0;   // gather index
             float kv[UN][FPL], vv[UN][FPL];
 #pragma unroll
             for (int u = 0; u < UN; ++u) {
@@ -532,7 +540,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
         }
         if (valid) {
             const int part = A.g.row_chunk_part[L.chunk];
-            if (part < 0) stf<S>(A.dq, (int64_t)row * A.ldd + f0, dq);
+            if (TAGAN_DBAD(part < A.g.part_cap, part, A.g.part_cap)) {   // partial slot (no return: a barrier follows)
+            } else if (part < 0) stf<S>(A.dq, (int64_t)row * A.ldd + f0, dq);
             else stf<float>(A.part_v, (int64_t)part * A.H + f0, dq);
             if ((L.sl % lph) == 0 && A.g.row_chunk_ptr[row] == L.chunk)   // packed {lse, delta} per (row, head)
                 *(float2*)(A.delta + ((int64_t)row * A.heads + h) * 2) = make_float2(lse, D);
@@ -579,7 +588,8 @@ __global__ void __launch_bounds__(BLK) k_geo_sum_parts(const int32_t* __restrict
 #pragma unroll
                 for (int u = 0; u < MG; ++u) {
                     const int cc = c + u * nph;
-                    if (cc < c1) acc[u] = f4add(acc[u], ld4(part + (int64_t)chunk_part[cc] * width + f0));
+                    if (cc < c1 && !TAGAN_DBAD(chunk_part[cc] >= 0, chunk_part[cc], cc))   // partial slot
+                        acc[u] = f4add(acc[u], ld4(part + (int64_t)chunk_part[cc] * width + f0));
                 }
             }
             float4 sum = f4add(f4add(acc[0], acc[1]), f4add(acc[2], acc[3]));
@@ -605,6 +615,9 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
     if (valid) {
         colj = A.g.col_chunk_seg[L.chunk];
         e0 = A.g.col_chunk_beg[L.chunk];
+        if (TAGAN_DBAD(colj >= 0 && colj < A.g.n_nodes && e0 >= A.g.csc_ptr[colj] && e0 <= A.g.csc_ptr[colj + 1], colj,
+                       e0))
+            colj = e0 = 0;
         cnt = min(A.g.chunk, A.g.csc_ptr[colj + 1] - e0);
     }
     if (!__any(valid)) return;
@@ -625,6 +638,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
             const bool in = jj + L.sl < cnt;
             myrow = in ? A.g.csc_row[e0 + jj + L.sl] : 0;
             myeid = in ? A.g.csc_eid[e0 + jj + L.sl] : 0;
+            if (TAGAN_DBAD(myrow >= 0 && myrow < A.g.n_nodes, myrow, colj)) myrow = 0;   // gather index
+            if (TAGAN_DBAD(myeid >= 0 && (A.g.nnz_cap <= 0 || myeid < A.g.nnz_cap), myeid, A.g.nnz_cap)) myeid = 0;
         }
         float qv[UN][FPL], dov[UN][FPL];
         float lse[UN], D[UN];
@@ -676,6 +691,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
     }
     if (!valid) return;
     const int part = A.g.col_chunk_part[L.chunk];
+    if (TAGAN_DBAD(part < A.g.part_cap, part, A.g.part_cap)) return;   // partial slot
     if (part < 0) {
         stf<S>(A.dk, (int64_t)colj * A.ldd + f0, dk);
         stf<S>(A.dv, (int64_t)colj * A.ldd + f0, dv);
@@ -725,6 +741,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_ds(GeoArgs A) {
     if (valid) {
         row = A.g.row_chunk_seg[L.chunk];
         e0 = A.g.row_chunk_beg[L.chunk];
+        if (TAGAN_DBAD(row >= 0 && row < A.g.n_nodes && e0 >= A.g.rowptr[row] && e0 <= A.g.rowptr[row + 1], row, e0))
+            row = e0 = 0;
         cnt = min(A.g.chunk, A.g.rowptr[row + 1] - e0);
     }
     const int lph = A.d / FPL;
@@ -745,6 +763,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_ds(GeoArgs A) {
             if ((jj % LPR) == 0) {
                 const bool in = jj + L.sl < cnt;
                 mycol = in ? A.g.col[e0 + jj + L.sl] : 0;
+                if (TAGAN_DBAD(mycol >= 0 && mycol < A.g.n_nodes, mycol, row)) mycol = 0;   // gather index
             }
             float kv[UN][FPL], dsv[UN];
 #pragma unroll
@@ -777,7 +796,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_ds(GeoArgs A) {
         }
         if (valid) {
             const int part = A.g.row_chunk_part[L.chunk];
-            if (part < 0) stf<S>(A.dq, (int64_t)row * A.ldd + f0, dq);
+            if (TAGAN_DBAD(part < A.g.part_cap, part, A.g.part_cap)) {   // partial slot (no return: a barrier follows)
+            } else if (part < 0) stf<S>(A.dq, (int64_t)row * A.ldd + f0, dq);
             else stf<float>(A.part_v, (int64_t)part * A.H + f0, dq);
         }
     }
@@ -1139,13 +1159,10 @@ struct BwdWs {
 // gathers at the price of a node pass over O and dO and a dS round trip; it pays where the gathers miss the caches:
 // C4 backward 8.8 -> 7.7 ms, while at C2 (its K|V rows mostly served by L2 / Infinity Cache) it measured 0.04 ms per
 // layer slower (profiles/r2_geo_bwd_order_ab.txt).  Default: column-first when the graph's K|V rows at fp32
-// (N·H·8 bytes) exceed 512 MB, twice the 256-MB Infinity Cache.  TAGAN_GEO_BWD_ORDER=row|col forces an order
-// (A/B; read at load time) and tagan_geo_set_bwd_order() sets it.  The choice depends on the graph and H only,
+// (N·H·8 bytes) exceed 512 MB, twice the 256-MB Infinity Cache.  tagan_geo_set_bwd_order() forces an order (A/B
+// runs and the order-equivalence test).  The choice depends on the graph and H only,
 // so the workspace query agrees with the call.
-int g_bwd_order = [] {
-    const char* e = getenv("TAGAN_GEO_BWD_ORDER");
-    return (e && strcmp(e, "row") == 0) ? 0 : (e && strcmp(e, "col") == 0) ? 1 : 2;
-}();
+int g_bwd_order = 2;
 
 bool col_first_wanted(int64_t N, int H) {
     const int mode = __atomic_load_n(&g_bwd_order, __ATOMIC_RELAXED);

@@ -881,18 +881,14 @@ int gru_mfma_optin(int hc) {
 
 // Rows per workgroup of the matrix-core kernels: 16 while that still leaves < 2 workgroups per CU at 32 (more
 // of them in flight: C2's 10k rows 3.58 -> 3.00 ms intended forward), 32 above (halves the weight reads from
-// L2).  TAGAN_GRU_MR=16|32 overrides.
+// L2).
 int gru_mfma_rows(int64_t N, bool bwd = false) {
-    const char* em = getenv("TAGAN_GRU_MR");
-    if (em) return atoi(em) == 16 ? 16 : 32;
     // the backward measured faster at 16 at every size (C4: 211 vs 264 ms, profiles/r2_gru_mfma_ab.txt)
     return (bwd || N <= 32 * 512) ? 16 : 32;
 }
 
-// TAGAN_GRU_MFMA=0 keeps the VALU kernels (A/B, parity of the two forms)
+// the VALU kernels take the other widths (hc 16 / 32)
 bool gru_mfma_ok(int hc, int64_t N) {
-    const char* e = getenv("TAGAN_GRU_MFMA");
-    if (e && e[0] == '0') return false;
     return (hc == 64 || hc == 128 || hc == 256) && N * 3 * hc < ((int64_t)1 << 31);   // 32-bit row offsets
 }
 

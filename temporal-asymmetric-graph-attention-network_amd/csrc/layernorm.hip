@@ -327,28 +327,12 @@ bool geometry(int H, int& lpr, int& nv) {
     }
 }
 
-// Backward grid (persistent blocks, one [3H] partial row each); TAGAN_LN_BWD_BLOCKS overrides it for
-// A/B probes (read once; 256..8192).
-int ln_bwd_blocks() {
-    static const int n = [] {
-        const char* e = getenv("TAGAN_LN_BWD_BLOCKS");
-        const int v = e ? atoi(e) : 0;
-        return (v >= 256 && v <= 8192) ? v : 1024;
-    }();
-    return n;
-}
+// Backward grid (persistent blocks, one [3H] partial row each): 1024 blocks (4 waves / SIMD); 1280 / 2048 / 4096 were
+// 3 / 10 / 27 % slower on the full backward (profiles/r1_ln_bwd_blocks_ab.txt).
+int ln_bwd_blocks() { return 1024; }
 
-// Row groups per wave (U).  Default 2 (best of 1/2/4 at C2 in tools/ln_probe.py); TAGAN_LN_ROWS = 1|2|4 overrides it
-// for A/B probes (read once).
-int ln_rows(int nv) {
-    static const int env = [] {
-        const char* e = getenv("TAGAN_LN_ROWS");
-        const int v = e ? atoi(e) : 0;
-        return (v == 1 || v == 2 || v == 4) ? v : 0;
-    }();
-    const int u = env ? env : 2;
-    return nv == 2 && u > 2 ? 2 : u;
-}
+// Row groups per wave (U): 2, the best of 1 / 2 / 4 at C2 (tools/ln_probe.py, profiles/r1_ln_rows_ab.txt).
+int ln_rows(int /*nv*/) { return 2; }
 
 // the fused LN2 + skip-LN backward (H = 128: LPR 32, NV 1; any U)
 template <typename S>

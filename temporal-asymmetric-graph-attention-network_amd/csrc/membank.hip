@@ -212,6 +212,7 @@ __global__ void __launch_bounds__(BLK) k_gather(tagan_membank B, const int32_t* 
         const int64_t i = x / B.H;
         const int c = (int)(x - i * B.H);
         const int s = slots[i];
+        if (TAGAN_DBAD(s < B.cap, s, B.cap)) continue;   // slot table index
         out[x] = s >= 0 ? B.states[(int64_t)s * B.H + c] : 0.f;
     }
 }

@@ -1142,25 +1142,10 @@ const NtCfg NT_TABLE[] = {
 #undef NT_SET3
 #undef NT_SET1
 
-int sgemm_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TAGAN_SGEMM_VARIANT");
-        v = e ? atoi(e) : 0;
-        if (v < 0) v = 0;
-    }
-    return v;
-}
-
 const NtCfg* nt_find(int K, int N, int P, int abf, int cbf, int mode = MODE_PLAIN) {
-    const NtCfg* first = nullptr;
-    int seen = 0;
     for (const NtCfg& c : NT_TABLE)
-        if (c.K == K && c.N == N && c.P == P && c.abf == abf && c.cbf == cbf && c.mode == mode) {
-            if (!first) first = &c;
-            if (seen++ == sgemm_variant()) return &c;
-        }
-    return first;
+        if (c.K == K && c.N == N && c.P == P && c.abf == abf && c.cbf == cbf && c.mode == mode) return &c;
+    return nullptr;
 }
 
 typedef void (*tn_fn)(TnArgs);
@@ -1189,14 +1174,9 @@ const TnCfg TN_TABLE[] = {
     tn_cfg<384, 128, 3, 8, 1, 1, false, true>(1),
 };
 const TnCfg* tn_find(int N, int K, int P, int abf, int lnx = 0) {
-    const TnCfg* first = nullptr;
-    int seen = 0;
     for (const TnCfg& c : TN_TABLE)
-        if (c.N == N && c.K == K && c.P == P && c.abf == abf && c.lnx == lnx) {
-            if (!first) first = &c;
-            if (seen++ == sgemm_variant()) return &c;
-        }
-    return first;
+        if (c.N == N && c.K == K && c.P == P && c.abf == abf && c.lnx == lnx) return &c;
+    return nullptr;
 }
 
 // m-groups of a weight-gradient launch (grid.x): one workgroup per CU slot, each over a contiguous row range
@@ -1229,21 +1209,12 @@ const RgCfg RG_TABLE[] = {
     rg_cfg<128, 1, false, true, MODE_LN_IN, 8, 384>(), rg_cfg<128, 1, false, false, MODE_LN_IN, 8, 384>(),
 };
 
-// TAGAN_SG_ROW (A/B knob, read once): 1 (default) = the LayerNorm-fused N = 128 products on k_rowgemm, 0 = all on
-// k_sgemm_nt, 2 = the plain N = 128 products on k_rowgemm too, 3 = also the one-plane LN1 + QKV forward (N = 384).  Plain products measured faster on k_sgemm_nt (C2
-// kernel stats, profiles/r3d_sgemm_table_fp32.md: fp32 K = 128 62 vs 77 us, bf16 41 vs 46 us, bf16 K = 384 70 vs
-// 78 us): without a row-wide epilogue the weight-stationary kernel's register-resident B wins.
-int rowgemm_level() {
-    static const int lv = [] {
-        const char* e = getenv("TAGAN_SG_ROW");
-        return e ? atoi(e) : 1;
-    }();
-    return lv;
-}
-
+// Row-owner kernels take the LayerNorm-fused N = 128 products only.  The plain products measured faster on the
+// weight-stationary k_sgemm_nt (C2 kernel stats, profiles/r3d_sgemm_table_fp32.md: fp32 K = 128 62 vs 77 us, bf16 41
+// vs 46 us, bf16 K = 384 70 vs 78 us: without a row-wide epilogue the register-resident B wins), and so did the
+// one-plane LN1 + QKV forward (bf16 step 5.18 vs 5.23-5.25 ms).
 const RgCfg* rg_find(int K, int N, int P, int abf, int cbf, int mode) {
-    const int lv = rowgemm_level();
-    if (lv == 0 || (mode == MODE_PLAIN && lv < 2) || (mode == MODE_LN_IN && lv < 3)) return nullptr;
+    if (mode == MODE_PLAIN || mode == MODE_LN_IN) return nullptr;
     for (const RgCfg& c : RG_TABLE)
         if (c.n == N && c.K == K && c.P == P && c.abf == abf && c.cbf == cbf && c.mode == mode) return &c;
     return nullptr;

@@ -2486,13 +2486,10 @@ int lds_optin(K* kern, size_t bytes) {
 
 // waves: G partial rows x heads (G <= grid_rows(rows), the bias-gradient workspace rows)
 // (a multiple of 8 from 8 rows up, for the XCD-aware wave map)
-// TAGAN_V4_G=<n> overrides the 1024 row groups (grid-size sweeps, up to 8192; the workspace follows: ws_rows)
+// 1024 row groups: 2048 / 4096 / 8192 measured 0.344 / 0.359 / 0.401 ms against 0.346 ms for the C2 backward
+// 
 int64_t v4_groups(int64_t rows) {
-    static const int64_t cap = [] {
-        const char* e = getenv("TAGAN_V4_G");
-        const int64_t v = e ? atoll(e) : 0;
-        return (v >= 8 && v <= 8192) ? v : (int64_t)1024;
-    }();
+    constexpr int64_t cap = 1024;
     return rows >= 8 ? std::min<int64_t>(rows, cap) & ~(int64_t)7 : rows;
 }
 

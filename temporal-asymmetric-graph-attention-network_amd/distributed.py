@@ -9,12 +9,34 @@ so one collective beats per-tensor calls); parameters whose grad is None on
 every rank (edge_embedding, temporal_propagation.*, time_encoding — dead in the
 shipped forward) are skipped identically on all ranks.
 """
+import os
 import time
 from contextlib import contextmanager
 from typing import Dict, Iterable, List, Optional
 
 import torch
 import torch.distributed as dist
+
+
+# ProcessGroupNCCL's per-device CUDA-event cache (on by default in this torch) hands a retired collective's end event
+# to the next collective.  With the step's all-reduce captured into a HIP graph, such an event can end up recorded in
+# the capturing stream while the watchdog thread still polls it through an earlier Work: the poll then fails with
+# hipErrorCapturedEvent and the watchdog aborts the process (seen once in five round-3 suites).  With the cache off
+# every Work owns its event, so an event the watchdog polls is never recorded by a capture.  The flag is read when a
+# process group is constructed: it must be set before init_process_group / new_group.
+EVENT_CACHE_ENV = "TORCH_NCCL_CUDA_EVENT_CACHE"
+
+
+def graph_safe_env() -> None:
+    """Switch ProcessGroupNCCL's event recycling off for the process groups created from here on."""
+    os.environ[EVENT_CACHE_ENV] = "0"
+
+
+def init_process_group(backend: str, **kw) -> None:
+    """``torch.distributed.init_process_group`` with ``graph_safe_env()`` applied first (any backend: a later RCCL
+    group created with ``new_group`` reads the same flag)."""
+    graph_safe_env()
+    dist.init_process_group(backend, **kw)
 
 
 def _staged(t: torch.Tensor, group) -> bool:

@@ -94,14 +94,10 @@ def ln_skip_bwd(s, mean, rstd, gamma, b, mean_s, rstd_s, gamma_s, dy2, p_drop, s
     return ds, da, out[0], out[1], out[2], out[3], out[4]
 
 
-# TAGAN_LN_SKIP_BWD=0: the skip block's LN2 and LN_s backward as two passes (A/B knob)
-LN_SKIP_BWD = os.environ.get("TAGAN_LN_SKIP_BWD", "1") != "0"
-
-
 def _ln2_bwd(s2, mean2, rstd2, ln2_w, dy2, skip, x2, lns_w, p_out, seed_out, da_dtype):
     """LN2's backward of a block (and, for the skip block, LN_s's): dres, do, dg2, db2, dbo, dgs, dbs."""
     M, H = dy2.shape
-    if skip is not None and LN_SKIP_BWD and H == 128:
+    if skip is not None and H == 128:   # one pass for both LayerNorms (150 vs 2 x 118 us at C2)
         return ln_skip_bwd(s2, mean2, rstd2, ln2_w, x2, skip[0], skip[1], lns_w, dy2, p_out, seed_out,
                            da_dtype=da_dtype)
     dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True,
@@ -306,25 +302,19 @@ def _sg_use(H: int, bf: bool, act: bool) -> bool:
     return ok
 
 
-# TAGAN_SG_LN=0: the stream_gemm block with standalone LayerNorm kernels instead of the LayerNorm-fused GEMMs (LN1 in
-# the QKV projection's prologue, dropout + residual + LN2 [+ skip LN] in the out-projection's epilogue, LN1's backward
-# in the QKV input gradient's epilogue, h = LN1(x) recomputed inside the QKV weight gradient; A/B knob)
-# TAGAN_SG_LN = list of the fused ops ("in", "out", "bwd"; separated by , + or :), "all", "0"/"none", or "auto"
-# (default): the measured-best set per precision.  Same-process interleaved graph-replay A/B on one MI355X
-# (tools/ab_step.py, profiles/r3d_ab_step.txt), ms per C2 step with the row-owner N = 128 kernels (k_rowgemm):
+# LayerNorm-fused stream-GEMM ops per precision ("in": LN1 in the QKV projection's prologue, h = LN1(x) recomputed
+# inside the QKV weight gradient; "out": dropout + residual + LN2 [+ skip LN] in the out-projection's epilogue; "bwd":
+# LN1's backward in the QKV input gradient's epilogue).  Same-process interleaved graph-replay A/B on one MI355X
+# (tools/ab_step.py, profiles/r3d_ab_step.txt), ms per C2 step:
 #   fp32  none 6.99  in 6.82  in+out 6.75  all 6.99   (fp32 "bwd" runs on k_sgemm_nt: its K = 384 three-plane weight
 #                                                      fragments do not fit a row-owner kernel's LDS, 288 KB)
 #   bf16  none 5.62  in 5.50  in+out 5.41  all 5.26
-_SG_LN_ENV = os.environ.get("TAGAN_SG_LN", "auto").strip().lower()
-SG_LN_SET = (set() if _SG_LN_ENV in ("0", "none", "") else
-             {"in", "out", "bwd"} if _SG_LN_ENV in ("1", "all") else
-             None if _SG_LN_ENV == "auto" else set(_SG_LN_ENV.replace("+", ",").replace(":", ",").split(",")))
+SG_LN_OPS = {False: frozenset({"in", "out"}), True: frozenset({"in", "out", "bwd"})}
 _SG_LN_OK = {}
 
 
 def _sg_ln_use(H: int, bf: bool, act: bool, op: str) -> bool:
-    ops = SG_LN_SET if SG_LN_SET is not None else ({"in", "out", "bwd"} if bf else {"in", "out"})
-    if op not in ops:
+    if op not in SG_LN_OPS[bf]:
         return False
     key = (H, bf, act, op)
     ok = _SG_LN_OK.get(key)
@@ -333,150 +323,21 @@ def _sg_ln_use(H: int, bf: bool, act: bool, op: str) -> bool:
     return ok
 
 
-# TAGAN_QKV_PACK=0: torch.cat of the q/k/v parameters per block instead of PackQKVFn's one-launch pack (A/B)
-QKV_PACK = os.environ.get("TAGAN_QKV_PACK", "1") != "0"
-# TAGAN_QKV_AUG=0: QKV GEMM with the hipBLASLt bias epilogue instead of the bias-as-weight-column form (A/B)
-QKV_AUG = os.environ.get("TAGAN_QKV_AUG", "1") != "0"
-# TAGAN_OUT_BIAS_LN=0: out-projection bias in the GEMM epilogue instead of the closing LayerNorm (A/B)
-OUT_BIAS_LN = os.environ.get("TAGAN_OUT_BIAS_LN", "1") != "0"
-# split-K slice height of the QKV weight gradient (3H outputs): taller slices than the out-projection's
-# 2048 (-> 2560 at C2) measured faster for N_out = 384 (tools/wgrad_probe.py); TAGAN_WGRAD_ROWS_QKV overrides
-WGRAD_ROWS_QKV = int(os.environ.get("TAGAN_WGRAD_ROWS_QKV", "8192"))
-# TAGAN_WGRAD_BIAS_AUG=0: QKV bias gradient by a column-sum pass over dqkv instead of the ones column of
-# LN1's augmented output riding through the weight-gradient GEMM (fp32 QKV_AUG form only; A/B)
-WGRAD_BIAS_AUG = os.environ.get("TAGAN_WGRAD_BIAS_AUG", "1") != "0"
-# Fused matrix-core projection kernels of csrc/proj_gemm.hip (fp32, H = 128), per GEMM of the block:
-#   "qkv": LN1 as the QKV GEMM's prologue;  "out": dropout + residual + LN2 as the out-projection's epilogue;
-#   "dc":  the out-projection's input gradient;  "dh": LN1's backward as the epilogue of the QKV input gradient.
-# TAGAN_PROJ = comma list of those, "all", or "0"/"none" (default).  Interleaved C2 A/B on one MI355X
-# (tools/runs/ab_proj.sh, profiles/r2_proj_ab.txt): none 8.40-8.42 ms, "out,dc" 8.48-8.52, all 8.66-8.73 — at
-# C2 each fused kernel is bound by HBM traffic and MFMA issue that its two waves per SIMD do not overlap, so it
-# lands at parity with the TunableOp-tuned hipBLASLt GEMM + the standalone LayerNorm kernel it replaces and the
-# default keeps the latter.
-_PROJ_ENV = os.environ.get("TAGAN_PROJ", "0").strip().lower()
-PROJ_SET = (set() if _PROJ_ENV in ("0", "none", "") else
-            {"qkv", "out", "dc", "dh"} if _PROJ_ENV in ("1", "all") else set(_PROJ_ENV.split(",")))
-PROJ = bool(PROJ_SET)
+# Library-GEMM form of the block (widths without a stream_gemm kernel):
+# * fp32: LN1 writes [h | 1 0 0 0] (row stride H + 4) and the QKV bias rides in the GEMM as a weight column -- one
+#   GEMM over K = H + 4 without a bias epilogue (tools/runs/qkv_aug.sh: ~1 % of the C2 step on hipBLASLt); the weight
+#   gradient over the same augmented operand gives the bias gradient as its column H (+66 us of GEMM against a 491-MB
+#   column-sum pass, profiles/r1_wgrad_bias_aug_ab.txt);
+# * the out-projection bias is added in the closing LayerNorm (no GEMM epilogue);
+# * split-K slice height of the QKV weight gradient (3H outputs): taller than the out-projection's 2048 rows
+#   (tools/wgrad_probe.py).
+WGRAD_ROWS_QKV = 8192
 
 
-def _proj_ok(H: int, bf: bool) -> bool:
-    return PROJ and not bf and bool(lib().tagan_proj_supported(H))
-
-
-def proj_ln_qkv(x2, ln1_w, ln1_b, eps1, w_qkv, b_qkv, want_h: bool):
-    """LN1 + QKV projection in one kernel: qkv [M, 3H], h_aug [M, H + 4] (LN1 output + ones column) or None."""
-    M, H = x2.shape
-    dev = x2.device
-    qkv = torch.empty(M, 3 * H, device=dev)
-    st = torch.empty(2, M, device=dev)
-    h_aug = torch.empty(M, H + 4, device=dev) if want_h else None
-    check(lib().tagan_ln_qkv_fwd(M, H, 3 * H, ptr(x2), ptr(ln1_w), ptr(ln1_b), float(eps1), ptr(w_qkv), ptr(b_qkv),
-                                 ptr(qkv), 3 * H, ptr(h_aug), H + 4 if want_h else 0, ptr(st[0]), ptr(st[1]),
-                                 stream_of(x2)), "tagan_ln_qkv_fwd")
-    return qkv, h_aug, st[0], st[1]
-
-
-def proj_ln_out(c, w_o, b_o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, lns_w=None, lns_b=None, eps_s=1e-5):
-    """y = LN2(dropout(c·w_oᵀ + b_o) + x2) [+ LN_s(x2)] in one kernel; returns y, s, mean, rstd, skip stats."""
-    M, H = x2.shape
-    dev = x2.device
-    y = torch.empty(M, H, device=dev)
-    s2 = torch.empty(M, H, device=dev)
-    st = torch.empty(4 if lns_w is not None else 2, M, device=dev)
-    skip = (st[2], st[3]) if lns_w is not None else None
-    check(lib().tagan_proj_ln_fwd(M, H, ptr(c), ptr(w_o), ptr(b_o), ptr(x2), float(p_out), seed_out, ptr(ln2_w),
-                                  ptr(ln2_b), float(eps2), ptr(lns_w), ptr(lns_b), float(eps_s), ptr(s2), ptr(y),
-                                  ptr(st[0]), ptr(st[1]), ptr(skip[0]) if skip else None,
-                                  ptr(skip[1]) if skip else None, stream_of(x2)), "tagan_proj_ln_fwd")
-    return y, s2, st[0], st[1], skip
-
-
-def proj_mm(a, w, kmajor: bool):
-    """a[M, K] · (w if kmajor else wᵀ) -> [M, H] on the matrix-core kernel (K = H or 3H)."""
-    M, K = a.shape
-    H = w.shape[1] if kmajor else w.shape[0]
-    out = torch.empty(M, H, device=a.device)
-    check(lib().tagan_proj_gemm(M, H, K, ptr(a), a.stride(0), ptr(w), int(kmajor), ptr(out), H, stream_of(a)),
-          "tagan_proj_gemm")
-    return out
-
-
-def proj_ln_bwd(da, w, x2, mean, rstd, gamma, dres):
-    """dx = LNᵀ(da·w) + dres with dgamma, dbeta (w [K, H] = the projection's nn.Linear weight)."""
-    M, K = da.shape
-    H = x2.shape[1]
-    dev = da.device
-    dx = torch.empty(M, H, device=dev)
-    dgb = torch.empty(2, H, device=dev)
-    L = lib()
-    wsb = L.tagan_proj_ln_bwd_workspace(M, H)
-    ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
-    check(L.tagan_proj_ln_bwd(M, H, K, ptr(da), ptr(w), ptr(x2), ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), ptr(dx),
-                              ptr(dgb[0]), ptr(dgb[1]), ptr(ws), wsb, stream_of(da)), "tagan_proj_ln_bwd")
-    return dx, dgb[0], dgb[1]
-
-# TAGAN_WGRAD_ASYNC=1: the block's weight-gradient GEMMs (dW_out, dW_qkv and the QKV bias column) run on a side
-# stream, overlapping the rest of the backward (the next layer's HBM-bound edge / LayerNorm kernels); nothing in
-# the backward reads them, so they are handed to the parameters by an end-of-backward callback after the main
-# stream has joined the side stream (HIP-graph capturable: fork / join through stream waits).  Measured at C2
-# (profiles/r2_wgrad_async_ab.txt): 8.56-8.61 ms against 8.19-8.22 ms synchronous -- the hipBLASLt GEMMs and the
-# edge / LayerNorm kernels slow each other down more than they overlap, so the default stays synchronous.
-WGRAD_ASYNC = os.environ.get("TAGAN_WGRAD_ASYNC", "0") == "1"
-_SIDE = {}
-
-
-def _side_stream(dev):
-    st = _SIDE.get(dev.index)
-    if st is None:
-        st = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
-    return st
-
-
-class WGradSink:
-    """Parameters of one attention block whose weight gradients may arrive asynchronously (TAGAN_WGRAD_ASYNC)."""
-
-    def __init__(self, q_lin, k_lin, v_lin, out_lin):
-        self.qkv = (q_lin, k_lin, v_lin)
-        self.out = out_lin
-
-
-def _give(p, g):
-    if p.grad is None:
-        p.grad = g
-    else:
-        p.grad.add_(g)
-
-
-class _AsyncWGrad:
-    """Side-stream weight gradients of one backward call, joined and assigned at the end of the backward."""
-
-    def __init__(self, sink, dev):
-        self.sink, self.main, self.side = sink, torch.cuda.current_stream(dev), _side_stream(dev)
-        self.keep, self.dw_o, self.dw_qkv, self.db_qkv = [], None, None, None
-        torch.autograd.Variable._execution_engine.queue_callback(self.finish)
-
-    def run(self, fn, *inputs):
-        self.side.wait_stream(self.main)   # the inputs are complete on the main stream
-        self.keep.extend(inputs)           # alive until the main stream has joined the side stream
-        with torch.cuda.stream(self.side):
-            return fn(*inputs)
-
-    def finish(self):
-        self.main.wait_stream(self.side)
-        with torch.cuda.stream(self.main):
-            H = self.sink.out.weight.shape[1]
-            if self.dw_o is not None:
-                _give(self.sink.out.weight, self.dw_o)
-            for i, lin in enumerate(self.sink.qkv):
-                if self.dw_qkv is not None:
-                    _give(lin.weight, self.dw_qkv[i * H:(i + 1) * H])
-                if self.db_qkv is not None:
-                    _give(lin.bias, self.db_qkv[i * H:(i + 1) * H])
-        if not torch.cuda.is_current_stream_capturing():
-            for t in (self.dw_o, self.dw_qkv, self.db_qkv):
-                if t is not None:
-                    t.record_stream(self.main)   # allocated on the side stream, read on the main one
-        self.keep.clear()
+def _aligned(*ts) -> bool:
+    """Every tensor starts on a 16-byte boundary (the stream_gemm C-ABI's row-alignment contract; a parameter that
+    is a view into a flat buffer at an odd offset takes the library GEMMs instead)."""
+    return all(t is None or t.data_ptr() % 16 == 0 for t in ts)
 
 
 class AttnBlockFn(torch.autograd.Function):
@@ -484,26 +345,18 @@ class AttnBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, p1, p2, ln1_w, ln1_b, w_qkv, b_qkv, w_o, b_o, ln2_w, ln2_b, core, eps1: float,
-                eps2: float, p_out: float, seed_out: int, lns_w=None, lns_b=None, eps_s: float = 1e-5, sink=None,
+                eps2: float, p_out: float, seed_out: int, lns_w=None, lns_b=None, eps_s: float = 1e-5,
                 w_aug_packed=None):
         require_hip(x)
         H = x.shape[-1]
         x2 = x.reshape(-1, H).contiguous()
         bf = _PREC != "fp32"          # bf16 GEMM operands
         act = _PREC == "bf16"         # bf16 activations between kernels
-        proj = _proj_ok(H, bf)
-        if not proj and _sg_use(H, bf, act):
+        if _sg_use(H, bf, act) and _aligned(x2, b_qkv, b_o, ln1_w, ln1_b, ln2_w, ln2_b, lns_w, lns_b):
             return AttnBlockFn._fwd_sgemm(ctx, x, x2, H, bf, act, p1, p2, ln1_w, ln1_b, w_qkv, b_qkv, w_o, b_o,
-                                          ln2_w, ln2_b, core, eps1, eps2, p_out, seed_out, lns_w, lns_b, eps_s, sink)
-        if proj and "qkv" in PROJ_SET:
-            w_qkv, b_qkv = w_qkv.contiguous(), b_qkv.contiguous()
-            qkv, h_aug, mean1, rstd1 = proj_ln_qkv(x2, ln1_w, ln1_b, eps1, w_qkv, b_qkv,
-                                                   want_h=any(ctx.needs_input_grad))
-            h = h_aug[:, :H] if h_aug is not None else None
-        elif QKV_AUG and not bf:
-            # fp32: LN1 writes [h | 1 0 0 0] (row stride H + 4) and the QKV bias rides in the GEMM as a weight
-            # column -- one GEMM over K = H + 4 without the bias epilogue, ≈1 % of the C2 step faster on
-            # hipBLASLt (tools/runs/qkv_aug.sh); with bf16 operands the epilogue form is the faster one
+                                          ln2_w, ln2_b, core, eps1, eps2, p_out, seed_out, lns_w, lns_b, eps_s)
+        if not bf:
+            # fp32: LN1 writes [h | 1 0 0 0] (row stride H + 4) and the QKV bias rides in the GEMM as a weight column
             h_aug = torch.empty(x2.shape[0], H + 4, device=x2.device)
             _, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False, y=h_aug)
             w_aug = w_aug_packed   # [W | b | 0 0 0] from PackQKVFn, else concatenated here
@@ -515,42 +368,28 @@ class AttnBlockFn(torch.autograd.Function):
             h_aug = None
             h, _, mean1, rstd1 = ln_fwd(x2, None, 0.0, 0, ln1_w, ln1_b, eps1, False,
                                         y_dtype=torch.bfloat16 if act else torch.float32)
-            if bf:
-                h = _b(h)
+            h = _b(h)
             qkv = _addmm(b_qkv, h, w_qkv, bf, out_bf16=act)
         c, saved = core.fwd(qkv, p1, p2)
         cg = _b(c) if bf else c
-        if proj and "out" in PROJ_SET:
-            y, s2, mean2, rstd2, skip = proj_ln_out(c, w_o.contiguous(), b_o, x2, p_out, seed_out, ln2_w, ln2_b, eps2,
-                                                    lns_w, lns_b, eps_s)
-            ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
-            ctx.inter = (h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
-            ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, proj)
-            ctx.sink = sink
-            ctx.packed_aug = False
-            return y.view(x.shape)
-        if OUT_BIAS_LN:   # out-projection bias added in the closing LayerNorm (no GEMM epilogue)
-            o, b_o_ln = _mm(cg, w_o.t(), bf), b_o
-        else:
-            o, b_o_ln = _addmm(b_o, cg, w_o, bf), None
+        o = _mm(cg, w_o.t(), bf)   # the out-projection bias is added in the closing LayerNorm
         skip = None
         if lns_w is not None:      # y = LN2(drop(o) + x) + LN_s(x) in one pass (model.py:258-262)
             y, s2, mean2, rstd2, skip = ln_skip_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, lns_w, lns_b, eps_s,
-                                                    a_bias=b_o_ln)
+                                                    a_bias=b_o)
         else:
-            y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True, a_bias=b_o_ln)
+            y, s2, mean2, rstd2 = ln_fwd(o, x2, p_out, seed_out, ln2_w, ln2_b, eps2, True, a_bias=b_o)
         ctx.save_for_backward(x2, ln1_w, w_qkv, w_o, ln2_w, lns_w)
         ctx.inter = (h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip)
-        ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, False)
-        ctx.sink = sink
+        ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, "library")
         ctx.packed_aug = h_aug is not None and w_aug_packed is not None
         return y.view(x.shape)
 
     @staticmethod
     def _fwd_sgemm(ctx, x, x2, H, bf, act, p1, p2, ln1_w, ln1_b, w_qkv, b_qkv, w_o, b_o, ln2_w, ln2_b, core, eps1,
-                   eps2, p_out, seed_out, lns_w, lns_b, eps_s, sink):
-        """The block with its four forward / input-gradient products on k_sgemm_nt and its two weight-gradient
-        products on k_sgemm_tn (csrc/stream_gemm.hip); LayerNorm, core and dropout as in the library form."""
+                   eps2, p_out, seed_out, lns_w, lns_b, eps_s):
+        """The block with its four forward / input-gradient products on k_sgemm_nt / k_rowgemm and its two
+        weight-gradient products on k_sgemm_tn (csrc/stream_gemm.hip); LayerNorm fused where SG_LN_OPS says."""
         P = 1 if bf else 3
         adt = torch.bfloat16 if act else torch.float32
         lnf = _sg_ln_use(H, bf, act, "in")
@@ -580,7 +419,6 @@ class AttnBlockFn(torch.autograd.Function):
         ctx.inter = (h, ln1_b if lnf else None, mean1, rstd1, qkv, c, c, saved, s2, mean2, rstd2, skip)
         ctx.cfg = (core, p_out, seed_out, x.shape, bf, act, "sgemm")
         ctx.wkm = (wo_km, wq_km)
-        ctx.sink = sink
         ctx.packed_aug = False
         return y.view(x.shape)
 
@@ -621,7 +459,7 @@ class AttnBlockFn(torch.autograd.Function):
         ctx.inter = None
         ctx.wkm = None
         return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
-                None, None, None, None, None, dgs, dbs, None, None, None)
+                None, None, None, None, None, dgs, dbs, None, None)
 
     @staticmethod
     def backward(ctx, dy):
@@ -629,36 +467,17 @@ class AttnBlockFn(torch.autograd.Function):
             return AttnBlockFn._bwd_sgemm(ctx, dy)
         x2, ln1_w, w_qkv, w_o, ln2_w, lns_w = ctx.saved_tensors
         h, h_aug, mean1, rstd1, qkv, c, cg, saved, s2, mean2, rstd2, skip = ctx.inter
-        core, p_out, seed_out, shape, bf, act, proj = ctx.cfg
+        core, p_out, seed_out, shape, bf, act, _ = ctx.cfg
         ng = ctx.needs_input_grad
         dy2 = dy.reshape(-1, shape[-1]).contiguous()
-        # weight gradients on the side stream: only for the default fp32 QKV_AUG form (bias from the ones column)
-        aw = (_AsyncWGrad(ctx.sink, dy.device) if (WGRAD_ASYNC and ctx.sink is not None and dy.is_cuda and not bf
-                                                    and not proj and h_aug is not None and WGRAD_BIAS_AUG
-                                                    and ng[5] and ng[6] and ng[7]) else None)
         dres, do, dg2, db2, dbo, dgs, dbs = _ln2_bwd(s2, mean2, rstd2, ln2_w, dy2, skip, x2, lns_w, p_out, seed_out,
                                                      torch.bfloat16 if bf else torch.float32)
-        dc = proj_mm(do, w_o.contiguous(), True) if (proj and "dc" in PROJ_SET) else _mm(do, w_o, bf, out_bf16=act)
-        if aw is not None:
-            aw.dw_o = aw.run(lambda a, b: _wgrad(a, b, bf), do, cg)
-            dw_o = None
-        else:
-            dw_o = _wgrad(do, cg, bf) if ng[7] else None
+        dc = _mm(do, w_o, bf, out_bf16=act)
+        dw_o = _wgrad(do, cg, bf) if ng[7] else None
         dqkv, dp1, dp2, db_core = core.bwd(qkv, c, saved, dc, ng[1], ng[2], want_bias_sum=bool(ng[6]))
         del dc, do
         H = shape[-1]
-        if aw is not None:
-            if db_core is None:
-                def qkv_aug(a, b):
-                    dw = _wgrad(a, b, bf, WGRAD_ROWS_QKV)
-                    return dw[:, :H].contiguous(), dw[:, H].contiguous()
-                aw.dw_qkv, aw.db_qkv = aw.run(qkv_aug, dqkv, h_aug)
-                db_qkv = None
-            else:
-                aw.dw_qkv = aw.run(lambda a, b: _wgrad(a, b, bf, WGRAD_ROWS_QKV), dqkv, h)
-                db_qkv = db_core
-            dw_qkv = None
-        elif db_core is None and ng[5] and ng[6] and h_aug is not None and WGRAD_BIAS_AUG:
+        if db_core is None and ng[5] and ng[6] and h_aug is not None:
             # dqkvᵀ·[h | 1 0 0 0]: column H of the product is the column sum of dqkv (the bias gradient)
             # -- 4 more GEMM columns instead of a 491 MB column-sum pass at C2
             dw_aug = _wgrad(dqkv, h_aug, bf, WGRAD_ROWS_QKV)
@@ -668,23 +487,16 @@ class AttnBlockFn(torch.autograd.Function):
         else:
             db_qkv = (db_core if db_core is not None else colsum(dqkv)) if ng[6] else None
             dw_qkv = None
-        if proj and "dh" in PROJ_SET:
-            if dw_qkv is None and ng[5]:
-                dw_qkv = _wgrad(dqkv, h, bf, WGRAD_ROWS_QKV)
-            dx, dg1, db1 = proj_ln_bwd(dqkv, w_qkv, x2, mean1, rstd1, ln1_w, dres)
-            ctx.inter = None
-            return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
-                    None, None, None, None, None, dgs, dbs, None, None, None)
         if bf:
             dqkv = _b(dqkv)
         dh = _mm(dqkv, w_qkv, bf)
-        if dw_qkv is None and ng[5] and aw is None:
+        if dw_qkv is None and ng[5]:
             dw_qkv = _wgrad(dqkv, h, bf, WGRAD_ROWS_QKV)
         del dqkv
         dx, _, dg1, db1, _ = ln_bwd(x2, mean1, rstd1, ln1_w, dh, dres, 0.0, 0, True, False, False)
         ctx.inter = None
         return (dx.view(shape), dp1, dp2, dg1, db1, dw_qkv, db_qkv, dw_o, dbo, dg2, db2,
-                None, None, None, None, None, dgs, dbs, None, None, None)
+                None, None, None, None, None, dgs, dbs, None, None)
 
 
 class PackQKVFn(torch.autograd.Function):
@@ -732,22 +544,21 @@ def attention_block(x, core, p1: Optional[torch.Tensor], p2: Optional[torch.Tens
     (TAGAN's first geometric layer, model.py:258-262), fused into the closing LayerNorm."""
     H = q_lin.weight.shape[1]
     w_aug = None
-    if QKV_PACK and x.is_cuda and q_lin.weight.dtype == torch.float32 and not WGRAD_ASYNC:
-        aug = (QKV_AUG and _PREC == "fp32" and not (_proj_ok(H, False) and "qkv" in PROJ_SET) and
-               not (x.shape[-1] == H and _sg_use(H, False, False)))
+    if x.is_cuda and q_lin.weight.dtype == torch.float32:
+        # [W_q; W_k; W_v] in one launch; the fp32 library form also takes [W | b | 0 0 0] from the same launch
+        aug = _PREC == "fp32" and not (x.shape[-1] == H and _sg_use(H, False, False))
         w_qkv, b_qkv, w_aug = PackQKVFn.apply(q_lin.weight, k_lin.weight, v_lin.weight, q_lin.bias, k_lin.bias,
                                               v_lin.bias, aug)
     else:
         w_qkv = torch.cat([q_lin.weight, k_lin.weight, v_lin.weight], 0)
         b_qkv = torch.cat([q_lin.bias, k_lin.bias, v_lin.bias], 0)
-    sink = WGradSink(q_lin, k_lin, v_lin, out_lin) if WGRAD_ASYNC else None
     if skip_ln is not None:
         return AttnBlockFn.apply(x, p1, p2, ln1.weight, ln1.bias, w_qkv, b_qkv, out_lin.weight, out_lin.bias,
                                  ln2.weight, ln2.bias, core, ln1.eps, ln2.eps, float(p_out), seed_out,
-                                 skip_ln.weight, skip_ln.bias, skip_ln.eps, sink, w_aug)
+                                 skip_ln.weight, skip_ln.bias, skip_ln.eps, w_aug)
     return AttnBlockFn.apply(x, p1, p2, ln1.weight, ln1.bias, w_qkv, b_qkv, out_lin.weight, out_lin.bias,
                              ln2.weight, ln2.bias, core, ln1.eps, ln2.eps, float(p_out), seed_out,
-                             None, None, 1e-5, sink, w_aug)
+                             None, None, 1e-5, w_aug)
 
 
 def fusable(x: torch.Tensor, use_layer_norm: bool) -> bool:

@@ -23,7 +23,7 @@ There is deliberately no split form (an eager segment between two captured ones)
 that form faulted and why the collective lives inside the one graph instead.
 """
 import ctypes
-import time
+import os
 from typing import Callable
 
 import torch
@@ -69,12 +69,16 @@ class GraphedStep:
         if optimizer is not None:
             optimizer.zero_grad(set_to_none=True)
         if _nccl_live():
-            # the RCCL process group's watchdog polls the end events of the warm-up steps' collectives; if one is
-            # still queued when the capture starts, the event can be recycled into the captured all-reduce and the
-            # poll then fails with hipErrorCapturedEvent (an abort seen once in five full suites, C2 graph step).
-            # Drain the device and give the watchdog (100-ms poll) time to retire that work first.
+            # the RCCL group's watchdog polls the end events of the warm-up steps' collectives; with ProcessGroupNCCL's
+            # event cache on, a retired Work's event can be handed to the captured all-reduce and recorded in the
+            # capture while an earlier Work of the watchdog still references it (hipErrorCapturedEvent, an abort).
+            # distributed.init_process_group switches the cache off before the group exists; refuse to capture a
+            # collective without that guarantee instead of racing.
+            from .distributed import EVENT_CACHE_ENV
+            if os.environ.get(EVENT_CACHE_ENV) != "0":
+                raise RuntimeError("GraphedStep with a live RCCL process group needs %s=0 set before the group is "
+                                   "created (tagan_amd.distributed.init_process_group does it)" % EVENT_CACHE_ENV)
             torch.cuda.synchronize(dev)
-            time.sleep(0.3)
         self.graph = torch.cuda.CUDAGraph()
         # captured on the warm-up stream: autograd nodes that outlive a warm-up step (a loss the caller kept,
         # AccumulateGrad nodes) then belong to the capture stream, so the backward adds no cross-stream join.

@@ -167,6 +167,9 @@ def cat_adjacent(ts: Sequence[torch.Tensor], dim: int) -> torch.Tensor:
     ``dim`` (the layout of a batch generated or ingested in one allocation), else a real concatenation."""
     if len(ts) == 1:
         return ts[0]
+    if torch.is_grad_enabled() and any(t.requires_grad for t in ts):
+        # as_strided's backward is taken with respect to ts[0]'s geometry: the other pieces would get no gradient
+        return torch.cat(list(ts), dim)
     t0 = ts[0]
     ok = all(t.dtype == t0.dtype and t.device == t0.device and t.dim() == t0.dim() and t.stride() == t0.stride()
              and t.untyped_storage().data_ptr() == t0.untyped_storage().data_ptr() for t in ts)

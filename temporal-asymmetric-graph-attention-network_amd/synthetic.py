@@ -66,6 +66,24 @@ def make_sequence(name: str, device, seed: int = 42, snapshots: int = None,
     return seq
 
 
+def take(seq: List[Tuple], t0: int, t1: int) -> List[Tuple]:
+    """Snapshots [t0, t1) of a ``make_sequence`` sequence repacked into buffers of their own (one [ΣN, F] and one
+    [2, ΣE] buffer again, so the model's concatenations stay views): a rank's block of a sharded sequence then does
+    not keep the whole sequence's buffers alive."""
+    part = seq[t0:t1]
+    if not part:
+        return []
+    x_all = torch.cat([x for x, _, _, _ in part], 0)
+    ei_all = torch.cat([ei for _, ei, _, _ in part], 1)
+    out, r, c = [], 0, 0
+    for x, ei, ea, ids in part:
+        n, e = x.shape[0], ei.shape[1]
+        out.append((x_all[r:r + n], ei_all[:, c:c + e], ea.clone() if ea is not None else None, ids))
+        r += n
+        c += e
+    return out
+
+
 def config_for(name: str, **over):
     from .utils.config import TAGANConfig
     N, E, T, H, h, F, De, _ = CONFIGS[name]

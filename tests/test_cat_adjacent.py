@@ -32,3 +32,16 @@ def test_non_adjacent_falls_back_to_cat():
         out = cat_adjacent(parts, dim)
         assert torch.equal(out, want)
         assert out.data_ptr() != base.data_ptr() or parts[0].data_ptr() != base.data_ptr()
+
+
+def test_pieces_that_require_grad_get_their_gradients():
+    """Adjacent views of one leaf that requires grad: every piece's rows get their gradient (torch.cat semantics; an
+    as_strided view of the first piece would drop the others')."""
+    leaf = torch.randn(10, 3, requires_grad=True)
+    parts = [leaf[0:4], leaf[4:7], leaf[7:10]]
+    w = torch.randn(10, 3)
+    (cat_adjacent(parts, 0) * w).sum().backward()
+    assert torch.equal(leaf.grad, w)
+    with torch.no_grad():
+        out = cat_adjacent([p.detach() for p in parts], 0)
+    assert out.data_ptr() == leaf.data_ptr()

@@ -6,10 +6,12 @@ This test makes the RCCL calls themselves run once on the device — the snapsho
 buckets (`GradBucket.allreduce_mean`, `ShardGradSync.sync`, forced at world size 1) — and checks that a
 one-rank collective leaves every value exactly as the unsharded model computed it (sum over one rank = identity).
 
-Each case runs in a child process (``python tests/test_gpu_rccl.py <case>``) that leaves with os._exit(0) once its
-checks pass, without tearing the RCCL process group down: destroying a group after a HIP graph captured its
-collectives aborted the process in a suite run (bench.py's N > 1 exit does the same).  The parent test asserts
-the child's exit status and its completion marker.
+Each case runs in a child process (``python tests/test_gpu_rccl.py <case>``).  The graph cases close the captured
+step (``GraphedStep.close``: graph reset first) and then destroy the process group and exit normally -- the order whose
+absence aborted a round-3 suite run after a graph had captured the group's collective.  The
+graph cases create the group through ``tagan_amd.distributed.init_process_group`` (ProcessGroupNCCL's event cache
+off, the deterministic fix of the watchdog's hipErrorCapturedEvent abort).  The parent test asserts the child's exit
+status and its completion marker.
 """
 import os
 import subprocess
@@ -44,7 +46,8 @@ def _case_shard_and_buckets():
     torch.cuda.set_device(dev)
     import tempfile
     store = os.path.join(tempfile.mkdtemp(prefix="tagan_rccl_"), "store")   # file rendezvous: no TCP port race
-    dist.init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1)
+    from tagan_amd.distributed import init_process_group
+    init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1)
     try:
         assert dist.get_backend() == "nccl"
         # raw all_to_all_single over device buffers
@@ -134,7 +137,8 @@ def _init_nccl(dev, tag):
     import tempfile
     torch.cuda.set_device(dev)
     store = os.path.join(tempfile.mkdtemp(prefix="tagan_rccl_%s_" % tag), "store")
-    dist.init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1)
+    from tagan_amd.distributed import init_process_group   # RCCL event recycling off before the group exists
+    init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1)
 
 
 def _case_graph_step_small():
@@ -144,6 +148,7 @@ def _case_graph_step_small():
     _init_nccl(dev, "gs")
     seq = synthetic.make_sequence("c2", dev, seed=7, snapshots=6, nodes=400, edges=3000)
     _graph_vs_eager(dev, seq)
+    dist.destroy_process_group()
 
 
 def _case_graph_step_c2():
@@ -155,6 +160,7 @@ def _case_graph_step_c2():
     _init_nccl(dev, "gc2")
     seq = synthetic.make_sequence("c2", dev, seed=1000)
     _graph_vs_eager(dev, seq, steps_eager=7, replays=4)
+    dist.destroy_process_group()
 
 
 CASES = {"shard_and_buckets": _case_shard_and_buckets, "graph_step_small": _case_graph_step_small,
@@ -189,5 +195,3 @@ if __name__ == "__main__":
     CASES[sys.argv[1]]()
     torch.cuda.synchronize()
     print(OK, flush=True)
-    sys.stderr.flush()
-    os._exit(0)

@@ -1,10 +1,10 @@
 """Same-process A/B of fused-LayerNorm variants of the C2 training step (graph replays, interleaved).
 
-Each variant sets ``fused.SG_LN_SET`` (the ops of the LN-fused stream GEMMs) before its own HIP-graph capture of the
+Each variant sets ``fused.SG_LN_OPS`` (the ops of the LN-fused stream GEMMs) before its own HIP-graph capture of the
 bench step; the graphs are then replayed round-robin, HIP events around each block of replays, and the median per
 variant is reported.  Box-to-box (DVFS) differences cancel, which separate-process A/Bs do not guarantee.
 
-    python tools/ab_step.py [--precision fp32|bf16] [--rounds 7] [--reps 10] none in in,out all
+    python tools/ab_step.py [--precision fp32|bf16] [--rounds 7] [--reps 10] none in in+out all default
 """
 import argparse
 import os
@@ -41,13 +41,16 @@ def main():
     def fwd():
         return model(seq, labels=labels)
 
+    DEFAULT_OPS = dict(fused.SG_LN_OPS)
     graphs = {}
     for v in args.variants:
-        # "<ln ops>[/skip0]": TAGAN_SG_LN op set; "/skip0" = the skip block's LN backward as two passes
-        ln, _, flag = v.partition("/")
-        fused.SG_LN_SET = (set() if ln == "none" else {"in", "out", "bwd"} if ln == "all" else
-                           None if ln == "auto" else set(ln.replace("+", ",").split(",")))
-        fused.LN_SKIP_BWD = flag != "skip0"
+        # "<ln ops>": the LayerNorm-fused stream-GEMM op set of this precision (fused.SG_LN_OPS) for this variant's
+        # capture: none, all, default, or a "+"-list of in / out / bwd
+        bf = args.precision != "fp32"
+        default = DEFAULT_OPS[bf]
+        fused.SG_LN_OPS[bf] = (frozenset() if v == "none" else frozenset({"in", "out", "bwd"}) if v == "all" else
+                               default if v == "default" else frozenset(v.replace("+", ",").split(",")))
+        fused._SG_LN_OK.clear()
         graphs[v] = bench.graphed(model, opt, cfg, fwd)
     times = {v: [] for v in args.variants}
     st = torch.cuda.current_stream()
