@@ -574,22 +574,24 @@ def c3_dp_record(dev, rank, world, ctl, backend, steps=5, warmup=3):
     return rec
 
 
-def c5_shard_record(dev, rank, world, ctl, backend, steps=5, warmup=3):
+def c5_shard_record(dev, rank, world, ctl, backend, steps=5, warmup=3, nodes=None, edges=None):
     """BASELINE configs[4] over N ranks: ONE sequence of 128 snapshots (100k nodes / 2M edges each, hidden 256,
     16 heads, fp32) sharded by snapshot (sharded.py): the geometric stage on each rank's 128/N snapshots, one
     all-to-all to node rows, the temporal stage on the rank's rows, one pooling all-reduce, one flagged gradient
-    all-reduce; eager launches."""
+    all-reduce; eager launches.  ``nodes`` / ``edges`` shrink the snapshots (same T, H, heads) for a rehearsal of
+    several ranks on one GPU (tests/test_gpu_sharded.py)."""
     from tagan_amd import TAGAN, synthetic
     from tagan_amd.distributed import broadcast_parameters
     from tagan_amd.sharded import ShardGradSync, SnapshotShardedTAGAN, blocks
     cfg = synthetic.config_for("c5")
     N, E, T, H, heads = synthetic.CONFIGS["c5"][:5]
+    N, E = nodes or N, edges or E
     torch.manual_seed(0)
     model = TAGAN(cfg).to(dev).train()
     broadcast_parameters(model)
     opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay, fused=True)
     t0, t1 = blocks(T, world)[rank]
-    full = synthetic.make_sequence("c5", dev, seed=5000)   # the same sequence on every rank; keep this rank's block
+    full = synthetic.make_sequence("c5", dev, seed=5000, nodes=N, edges=E)   # the same sequence on every rank
     seq = synthetic.take(full, t0, t1)
     del full
     counts_all = [N] * T

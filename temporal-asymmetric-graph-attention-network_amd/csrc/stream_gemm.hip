@@ -174,6 +174,9 @@ struct NtArgs {
     float* rstd_s;
     const float* dres;
     float* part;
+    // MODE_PLAIN split-K: B's fragments are k-blocks [kk0, kk0 + K / 32) of a panel prepared with kkt k-blocks per
+    // n-subtile (kkt = 0: K / 32), and accum = 1 adds the product to the fp32 C already there
+    int kkt, kk0, accum;
 };
 
 enum { MODE_PLAIN = 0, MODE_LN_IN = 1, MODE_LN_OUT = 2, MODE_LN_BWD = 3 };
@@ -257,7 +260,8 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
         for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
             for (int p = 0; p < P; ++p)
-                wr[s][kk][p] = __builtin_bit_cast(bf16x8, g.wp[((int64_t)((nsub0 + s) * KK + kk) * P + p) * 64 + lane]);
+                wr[s][kk][p] = __builtin_bit_cast(
+                    bf16x8, g.wp[((int64_t)((nsub0 + s) * (g.kkt ? g.kkt : KK) + g.kk0 + kk) * P + p) * 64 + lane]);
     f32x4 bias[NSUB];
 #pragma unroll
     for (int s = 0; s < NSUB; ++s) {
@@ -558,7 +562,10 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
 #pragma unroll
                 for (int s = 0; s < NSUB; ++s) {
                     const int64_t off = row * g.ldc + (nsub0 + s) * 16 + 4 * (lane >> 4);
-                    const f32x4 v = acc[j][s];
+                    f32x4 v = acc[j][s];
+                    if constexpr (!CBF && MODE == MODE_PLAIN) {
+                        if (g.accum) v += *reinterpret_cast<const f32x4*>((const float*)g.c + off);
+                    }
                     if constexpr (CBF) {
                         *reinterpret_cast<uint2*>((uint16_t*)g.c + off) = make_uint2(pk_bf16(v[0], v[1]),
                                                                                      pk_bf16(v[2], v[3]));
@@ -1111,26 +1118,33 @@ constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
 // the v-th where one exists.
 // fp32 (three planes): MFMA-bound, tiles sized by the registers the weight fragments leave; one plane: HBM-bound,
 // taller tiles so that more bytes are in flight per workgroup.
+// H = 256 (C3, C5): a K = 256 three-plane panel is 96 VGPRs per 16 columns, so one n-subtile per wave and the
+// columns spread over grid.y (N / 128 workgroup columns; each re-reads A, mostly from L2); K = 768 three-plane (the
+// QKV input gradient, 288 VGPRs per 16 columns) runs as two K = 384 halves, the second accumulating into C
+// (tagan_sgemm_nt splits it).  H = 64 (C1): 4-wave workgroups cover N = 192 / 64 in one grid column.
 #define NT_SET3                                                                                              \
-    nt_cfg<128, 3, 8, 32, 3, false, false>(384, 1), nt_cfg<128, 2, 12, 48, 3, false, false>(384, 1),           \
-    nt_cfg<128, 1, 8, 32, 3, false, false>(128, 2), nt_cfg<128, 1, 8, 64, 3, false, false>(128, 1),            \
-    nt_cfg<384, 1, 8, 32, 3, false, false>(128, 1)
+    nt_cfg<128, 3, 8, 32, 3, false, false>(384, 1), nt_cfg<128, 1, 8, 32, 3, false, false>(128, 2),            \
+    nt_cfg<384, 1, 8, 32, 3, false, false>(128, 1),                                                            \
+    nt_cfg<256, 1, 8, 32, 3, false, false>(768, 1), nt_cfg<256, 1, 8, 32, 3, false, false>(256, 1),            \
+    nt_cfg<384, 1, 8, 32, 3, false, false>(256, 1),                                                            \
+    nt_cfg<64, 3, 4, 32, 3, false, false>(192, 1), nt_cfg<64, 1, 4, 32, 3, false, false>(64, 2),               \
+    nt_cfg<192, 1, 4, 32, 3, false, false>(64, 2)
 #define NT_SET1(ABF, CBF)                                                                                    \
-    nt_cfg<128, 3, 8, 64, 1, ABF, CBF>(384, 1), nt_cfg<128, 3, 8, 32, 1, ABF, CBF>(384, 1),                   \
-    nt_cfg<128, 1, 8, 128, 1, ABF, CBF>(128, 2), nt_cfg<128, 1, 8, 32, 1, ABF, CBF>(128, 2),                   \
-    nt_cfg<384, 1, 8, 64, 1, ABF, CBF>(128, 1), nt_cfg<384, 1, 8, 32, 1, ABF, CBF>(128, 1)
+    nt_cfg<128, 3, 8, 64, 1, ABF, CBF>(384, 1), nt_cfg<128, 1, 8, 128, 1, ABF, CBF>(128, 2),                  \
+    nt_cfg<384, 1, 8, 64, 1, ABF, CBF>(128, 1),                                                                \
+    nt_cfg<256, 2, 8, 64, 1, ABF, CBF>(768, 1), nt_cfg<256, 2, 8, 64, 1, ABF, CBF>(256, 1),                   \
+    nt_cfg<768, 1, 8, 32, 1, ABF, CBF>(256, 1),                                                                \
+    nt_cfg<64, 3, 4, 64, 1, ABF, CBF>(192, 1), nt_cfg<64, 1, 4, 64, 1, ABF, CBF>(64, 2),                      \
+    nt_cfg<192, 1, 4, 64, 1, ABF, CBF>(64, 2)
 // The LayerNorm-fused forms (H = 128): LN1 prologue of the QKV projection (x fp32 in; qkv fp32, or bf16 in the
 // bf16 activation mode), dropout + residual + LN2 [+ skip LN] epilogue of the out-projection (y fp32), LN1 backward
 // epilogue of the QKV input gradient (dx fp32).
+// (The LN2 epilogue and the one-plane LN1-backward epilogue run on the row-owner kernels, RG_TABLE.)
 #define NT_SETLN                                                                                             \
     nt_cfg<128, 3, 8, 32, 3, false, false, MODE_LN_IN>(384, 1),                                                 \
-    nt_cfg<128, 3, 8, 64, 1, false, true, MODE_LN_IN>(384, 1), nt_cfg<128, 3, 8, 32, 1, false, true, MODE_LN_IN, 4>(384, 2), \
+    nt_cfg<128, 3, 8, 64, 1, false, true, MODE_LN_IN>(384, 1),                                                  \
     nt_cfg<128, 3, 8, 64, 1, false, false, MODE_LN_IN>(384, 1),                                                 \
-    nt_cfg<128, 1, 8, 32, 3, false, false, MODE_LN_OUT>(128, 1),                                                \
-    nt_cfg<128, 1, 8, 32, 1, true, false, MODE_LN_OUT, 4>(128, 2), nt_cfg<128, 1, 8, 64, 1, true, false, MODE_LN_OUT>(128, 1), \
-    nt_cfg<128, 1, 8, 32, 1, false, false, MODE_LN_OUT, 4>(128, 2),                                             \
-    nt_cfg<384, 1, 8, 32, 3, false, false, MODE_LN_BWD>(128, 1),                                                \
-    nt_cfg<384, 1, 8, 64, 1, true, false, MODE_LN_BWD>(128, 1), nt_cfg<384, 1, 8, 64, 1, false, false, MODE_LN_BWD>(128, 1)
+    nt_cfg<384, 1, 8, 32, 3, false, false, MODE_LN_BWD>(128, 1)
 const NtCfg NT_TABLE[] = {
     NT_SET3,
     NT_SET1(false, false),
@@ -1162,17 +1176,19 @@ constexpr TnCfg tn_cfg(int wg_per_cu) {
                  (size_t)P * 32 * ((N / NG + 16) + (K + 16)) * 2, wg_per_cu};
 }
 // abf = dY stored bf16 (and X too, unless lnx: X = LN(x) from the fp32 LayerNorm input)
+// H = 256: one n-subtile per wave (the K = 256 accumulator row is 64 VGPRs), grid.y = N / 128 column groups.
+// H = 64: 4-wave workgroups over the whole N.
+#define TN_SETP(P, ABF)                                                                                      \
+    tn_cfg<384, 128, 3, 8, 1, P, ABF>(1), tn_cfg<128, 128, 1, 8, 1, P, ABF>(2),                               \
+    tn_cfg<768, 256, 1, 8, 6, P, ABF>(1), tn_cfg<256, 256, 1, 8, 2, P, ABF>(1),                               \
+    tn_cfg<192, 64, 3, 4, 1, P, ABF>(2), tn_cfg<64, 64, 1, 4, 1, P, ABF>(2)
 const TnCfg TN_TABLE[] = {
-    tn_cfg<384, 128, 3, 8, 1, 3, false>(1), tn_cfg<384, 128, 3, 4, 2, 3, false>(2),
-    tn_cfg<128, 128, 1, 8, 1, 3, false>(2), tn_cfg<128, 128, 1, 8, 1, 3, false>(1),
-    tn_cfg<384, 128, 3, 8, 1, 1, false>(1), tn_cfg<384, 128, 3, 4, 2, 1, false>(2),
-    tn_cfg<128, 128, 1, 8, 1, 1, false>(2), tn_cfg<128, 128, 1, 8, 1, 1, false>(1),
-    tn_cfg<384, 128, 3, 8, 1, 1, true>(1),  tn_cfg<384, 128, 3, 4, 2, 1, true>(2),
-    tn_cfg<128, 128, 1, 8, 1, 1, true>(2),  tn_cfg<128, 128, 1, 8, 1, 1, true>(1),
-    tn_cfg<384, 128, 3, 8, 1, 3, false, true>(1), tn_cfg<384, 128, 3, 4, 2, 3, false, true>(2),
-    tn_cfg<384, 128, 3, 8, 1, 1, true, true>(1),  tn_cfg<384, 128, 3, 4, 2, 1, true, true>(2),
+    TN_SETP(3, false), TN_SETP(1, false), TN_SETP(1, true),
+    tn_cfg<384, 128, 3, 8, 1, 3, false, true>(1),
+    tn_cfg<384, 128, 3, 8, 1, 1, true, true>(1),
     tn_cfg<384, 128, 3, 8, 1, 1, false, true>(1),
 };
+#undef TN_SETP
 const TnCfg* tn_find(int N, int K, int P, int abf, int lnx = 0) {
     for (const TnCfg& c : TN_TABLE)
         if (c.N == N && c.K == K && c.P == P && c.abf == abf && c.lnx == lnx) return &c;
@@ -1200,19 +1216,15 @@ constexpr RgCfg rg_cfg() {
 }
 // N = 128 only; B's planes must fit the LDS (K = 384 in fp32 would need 288 KB: k_sgemm_nt keeps that shape)
 const RgCfg RG_TABLE[] = {
-    rg_cfg<128, 3, false, false, MODE_PLAIN>(), rg_cfg<128, 1, false, false, MODE_PLAIN>(),
-    rg_cfg<128, 1, true, false, MODE_PLAIN>(),  rg_cfg<128, 1, true, true, MODE_PLAIN>(),
-    rg_cfg<384, 1, true, false, MODE_PLAIN>(),  rg_cfg<384, 1, false, false, MODE_PLAIN>(),
     rg_cfg<128, 3, false, false, MODE_LN_OUT>(), rg_cfg<128, 1, true, false, MODE_LN_OUT>(),
     rg_cfg<128, 1, false, false, MODE_LN_OUT>(),
     rg_cfg<384, 1, true, false, MODE_LN_BWD, 8>(), rg_cfg<384, 1, false, false, MODE_LN_BWD, 8>(),
-    rg_cfg<128, 1, false, true, MODE_LN_IN, 8, 384>(), rg_cfg<128, 1, false, false, MODE_LN_IN, 8, 384>(),
 };
 
 // Row-owner kernels take the LayerNorm-fused N = 128 products only.  The plain products measured faster on the
 // weight-stationary k_sgemm_nt (C2 kernel stats, profiles/r3d_sgemm_table_fp32.md: fp32 K = 128 62 vs 77 us, bf16 41
 // vs 46 us, bf16 K = 384 70 vs 78 us: without a row-wide epilogue the register-resident B wins), and so did the
-// one-plane LN1 + QKV forward (bf16 step 5.18 vs 5.23-5.25 ms).
+// one-plane LN1 + QKV forward (bf16 step 5.18 vs 5.23-5.25 ms); those forms are not built.
 const RgCfg* rg_find(int K, int N, int P, int abf, int cbf, int mode) {
     if (mode == MODE_PLAIN || mode == MODE_LN_IN) return nullptr;
     for (const RgCfg& c : RG_TABLE)
@@ -1266,6 +1278,13 @@ bool lds_ok(const void* fn, size_t lds) {
     return true;
 }
 
+// split-K form of a plain fp32-output product without a kernel of its own: two K / 2 halves, the second accumulating
+// into C (K = 768 three-plane: the H = 256 QKV input gradient)
+const NtCfg* nt_find_half(int K, int N, int P, int abf, int cbf) {
+    if (cbf || K % 64 != 0 || nt_find(K, N, P, abf, cbf)) return nullptr;
+    return nt_find(K / 2, N, P, abf, cbf);
+}
+
 }  // namespace
 }  // namespace tagan
 
@@ -1273,7 +1292,8 @@ using namespace tagan;
 
 extern "C" int tagan_sgemm_supported(int32_t N, int32_t K, int32_t planes, int32_t a_dtype, int32_t c_dtype) {
     const int ab = a_dtype == TAGAN_BF16, cb = c_dtype == TAGAN_BF16;
-    return nt_find(K, N, planes, ab, cb) != nullptr || rg_find(K, N, planes, ab, cb, MODE_PLAIN) != nullptr;
+    return nt_find(K, N, planes, ab, cb) != nullptr || rg_find(K, N, planes, ab, cb, MODE_PLAIN) != nullptr ||
+           nt_find_half(K, N, planes, ab, cb) != nullptr;
 }
 
 extern "C" int tagan_sgemm_tn_supported(int32_t N, int32_t K, int32_t planes, int32_t dtype) {
@@ -1316,8 +1336,9 @@ extern "C" int tagan_sgemm_nt(int32_t a_dtype, int32_t c_dtype, int64_t M, int32
                               void* stream) {
     const RgCfg* rcfg = rg_find(K, N, planes, a_dtype == TAGAN_BF16, c_dtype == TAGAN_BF16, MODE_PLAIN);
     const NtCfg* cfg = nt_find(K, N, planes, a_dtype == TAGAN_BF16, c_dtype == TAGAN_BF16);
-    TAGAN_REQUIRE(cfg || rcfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_nt: no kernel for N=%d K=%d planes=%d dtypes %d/%d",
-                  N, K, planes, a_dtype, c_dtype);
+    const NtCfg* half = (cfg || rcfg) ? nullptr : nt_find_half(K, N, planes, a_dtype == TAGAN_BF16, c_dtype == TAGAN_BF16);
+    TAGAN_REQUIRE(cfg || rcfg || half, TAGAN_ERR_UNSUPPORTED,
+                  "tagan_sgemm_nt: no kernel for N=%d K=%d planes=%d dtypes %d/%d", N, K, planes, a_dtype, c_dtype);
     TAGAN_REQUIRE(M >= 0 && wp, TAGAN_ERR_ARG, "tagan_sgemm_nt: bad arguments");
     if (M == 0) return TAGAN_OK;
     TAGAN_REQUIRE(a && c, TAGAN_ERR_ARG, "tagan_sgemm_nt: null operand");
@@ -1330,6 +1351,16 @@ extern "C" int tagan_sgemm_nt(int32_t a_dtype, int32_t c_dtype, int64_t M, int32
     NtArgs g{};
     g.M = M; g.a = a; g.lda = lda; g.wp = (const uint4*)wp; g.bias = bias; g.c = c; g.ldc = ldc;
     if (rcfg) return rg_launch(rcfg, g, stream, "tagan_sgemm_nt");
+    if (half) {   // C = A[:, :K/2]·B[:, :K/2]ᵀ + bias, then C += A[:, K/2:]·B[:, K/2:]ᵀ
+        g.kkt = K / 32;
+        const int rc = nt_launch(half, g, N, stream, "tagan_sgemm_nt (first K half)");
+        if (rc != TAGAN_OK) return rc;
+        g.a = (const char*)a + (size_t)(K / 2) * es;
+        g.bias = nullptr;
+        g.kk0 = K / 64;
+        g.accum = 1;
+        return nt_launch(half, g, N, stream, "tagan_sgemm_nt (second K half)");
+    }
     return nt_launch(cfg, g, N, stream, "tagan_sgemm_nt");
 }
 

@@ -221,6 +221,44 @@ def test_c2_bf16_vs_oracle(dev):
     print("bf16 C2: worst normwise / bound = %.3f (%s)" % worst)
 
 
+# ----------------------------------------------------------------------------- C3 / C5 geometry, whole model
+# The full T / hidden / heads of C3 (T 64, H 256, 8 heads) and C5 (T 128, H 256, 16 heads) with the node count cut
+# (degree kept at 20) so the fp64 oracle runs the whole model: every layer (both geometric layers on the H = 256
+# stream GEMMs, the v5 temporal kernel, pooling, head, loss) forward and backward against it at the north_star's
+# 1e-4, like the C2 test above.
+GEOMETRY = {"c3": (1500, 30_000), "c5": (800, 16_000)}
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_geometry_whole_model_vs_oracle(dev, name):
+    from tagan_amd import synthetic
+    nodes, edges = GEOMETRY[name]
+    cfg, model = _model(name, dev)
+    seq = synthetic.make_sequence(name, dev, seed=2024, nodes=nodes, edges=edges)
+    seq = [(x.clone().requires_grad_(True), ei, ea, ids) for x, ei, ea, ids in seq]
+    labels = torch.tensor([1.0], device=dev)
+    out = model(seq, labels=labels)
+    out["loss"].backward()
+    P = _p64(model)
+    seq64 = [(x.detach().cpu().double().requires_grad_(True), ei.cpu(), None, ids) for x, ei, _, ids in seq]
+    ref = oracle.tagan_forward(P, cfg.to_dict(), seq64, labels.cpu().double())
+    ref["loss"].backward()
+    G.assert_close("%s logits" % name, out["logits"], ref["logits"].detach(), OUT_ATOL, OUT_RTOL)
+    G.assert_close("%s loss" % name, out["loss"].reshape(1), ref["loss"].detach().reshape(1), OUT_ATOL, OUT_RTOL)
+    n_checked = 0
+    for pname, p in model.named_parameters():
+        want = P[pname].grad
+        if want is not None:
+            _close_grad("grad " + pname, p.grad, want)
+            n_checked += 1
+        else:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, pname
+    assert n_checked >= 30
+    for t, ((x, _, _, _), (x64, _, _, _)) in enumerate(zip(seq, seq64)):
+        _close_grad("grad x.%d" % t, x.grad, x64.grad)
+
+
 # ----------------------------------------------------------------------------- C3-C5 sampled checks
 FULL = {
     # name: snapshots on this GPU for the geometric stage (C5: one rank's share of the 8-GPU shard)

@@ -28,8 +28,11 @@ def _merr(x, ref):
     return float((x.double() - ref).abs().max() / ref.abs().max().clamp_min(1e-300))
 
 
-# (N, K, kmajor): QKV forward, out-projection forward, out-projection input gradient, QKV input gradient
-NT_SHAPES = [(384, 128, False), (128, 128, False), (128, 128, True), (128, 384, True)]
+# (N, K, kmajor): QKV forward, out-projection forward, out-projection input gradient, QKV input gradient at every
+# hidden width BASELINE names (H = 128: C2 / C4, H = 256: C3 / C5, H = 64: C1); (256, 768, True) in fp32 runs as two
+# K = 384 halves, the second accumulating into C
+NT_SHAPES = [(3 * H, H, False) for H in (128, 256, 64)] + [(H, H, False) for H in (128, 256, 64)] + \
+            [(H, H, True) for H in (128, 256, 64)] + [(H, 3 * H, True) for H in (128, 256, 64)]
 ROWS = [1, 15, 33, 1000, 40961]
 
 
@@ -68,7 +71,7 @@ def test_nt_strided_and_zero_rows():
     assert z.shape == (0, 384)
 
 
-@pytest.mark.parametrize("N,K", [(384, 128), (128, 128)])
+@pytest.mark.parametrize("N,K", [(384, 128), (128, 128), (768, 256), (256, 256), (192, 64), (64, 64)])
 @pytest.mark.parametrize("M", ROWS + [0])
 def test_tn_fp32_planes(N, K, M):
     dev = _dev()
@@ -104,23 +107,46 @@ def test_tn_column_views():
     assert _merr(db, dq[:, 128:256].double().sum(0)) <= 2e-6
 
 
+@pytest.mark.parametrize("H", [128, 256, 64])
 @pytest.mark.parametrize("store", ["fp32", "bf16"])
-def test_bf16_plane(store):
+def test_bf16_plane(store, H):
+    """One-plane products of a block at width H: QKV forward, its input gradient (K = 3H) and both weight
+    gradients."""
     dev = _dev()
     from tagan_amd import stream_gemm as sg
-    g = torch.Generator(device=dev).manual_seed(21)
+    g = torch.Generator(device=dev).manual_seed(21 + H)
     dt = torch.bfloat16 if store == "bf16" else torch.float32
-    a = torch.randn(3001, 128, device=dev, generator=g).to(dt)
-    w = torch.randn(384, 128, device=dev, generator=g) / 128 ** 0.5
-    bias = torch.randn(384, device=dev, generator=g)
-    c = sg.nt(a, sg.wprep(w, False, 1), 384, 1, bias=bias, out_dtype=dt)
+    a = torch.randn(3001, H, device=dev, generator=g).to(dt)
+    w = torch.randn(3 * H, H, device=dev, generator=g) / H ** 0.5
+    bias = torch.randn(3 * H, device=dev, generator=g)
+    c = sg.nt(a, sg.wprep(w, False, 1), 3 * H, 1, bias=bias, out_dtype=dt)
     ref = a.double() @ w.double().t() + bias.double()
     assert c.dtype == dt
     assert _nerr(c, ref) < 1e-2
-    dq = torch.randn(3001, 384, device=dev, generator=g).to(dt)
+    dq = torch.randn(3001, 3 * H, device=dev, generator=g).to(dt)
+    dh = sg.nt(dq, sg.wprep(w, True, 1), H, 1)
+    assert _nerr(dh, dq.double() @ w.double()) < 1e-2
     dw, db = sg.tn(dq, a, 1)
     assert _nerr(dw, dq.double().t() @ a.double()) < 1e-2
     assert _nerr(db, dq.double().sum(0)) < 1e-2
+    dw2, db2 = sg.tn(dq[:, :H], a, 1)
+    assert _nerr(dw2, dq[:, :H].double().t() @ a.double()) < 1e-2
+
+
+def test_split_k_accumulates_exactly_twice():
+    """The K = 768 three-plane product (two K = 384 halves, the second accumulating into C) equals the sum of the
+    two half products computed separately, up to one fp32 rounding per element."""
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    g = torch.Generator(device=dev).manual_seed(77)
+    dq = torch.randn(4099, 768, device=dev, generator=g)
+    w = torch.randn(768, 256, device=dev, generator=g) / 768 ** 0.5      # dh = dq·w: B = wᵀ (k-major)
+    full = sg.nt(dq, sg.wprep(w, True, 3), 256, 3)
+    lo = sg.nt(dq[:, :384], sg.wprep(w[:384], True, 3), 256, 3)
+    hi = sg.nt(dq[:, 384:], sg.wprep(w[384:], True, 3), 256, 3)
+    assert (full - (lo + hi)).abs().max() <= 1e-6 * full.abs().max()
+    ref = dq.double() @ w.double()
+    assert _merr(full, ref) <= 1e-6
 
 
 def test_unsupported_shape_reported():
@@ -128,19 +154,21 @@ def test_unsupported_shape_reported():
     from tagan_amd import stream_gemm as sg
     assert not sg.supported(96, 64, 3)
     assert not sg.tn_supported(96, 64, 3)
+    assert not sg.supported(768, 1536, 3) and not sg.tn_supported(1536, 512, 3)
     with pytest.raises(RuntimeError):
         sg.nt(torch.randn(10, 64, device="cuda"), torch.empty(96 * 64 * 3, dtype=torch.bfloat16, device="cuda"),
               96, 3)
 
 
+@pytest.mark.parametrize("H", [128, 256, 64])
 @pytest.mark.parametrize("planes", [1, 3])
-def test_wprep_block_equals_single_preps(planes):
+def test_wprep_block_equals_single_preps(planes, H):
     """tagan_sgemm_wprep_block's four operands are bitwise the four tagan_sgemm_wprep calls they stand for."""
     dev = _dev()
     from tagan_amd import stream_gemm as sg
     g = torch.Generator(device=dev).manual_seed(31)
-    wq = torch.randn(384, 128, device=dev, generator=g)
-    wo = torch.randn(128, 128, device=dev, generator=g)
+    wq = torch.randn(3 * H, H, device=dev, generator=g)
+    wo = torch.randn(H, H, device=dev, generator=g)
     got = sg.wprep_block(wq, wo, planes)
     want = (sg.wprep(wq, False, planes), sg.wprep(wo, False, planes), sg.wprep(wo, True, planes),
             sg.wprep(wq, True, planes))
