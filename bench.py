@@ -841,7 +841,7 @@ def main():
         # BASELINE's multi-GPU workloads beside the C2 headline (DESIGN.md §4 'sub-records'): every rank takes part
         if gstep is not None:
             gstep.close()
-        del step, gstep
+        step = gstep = None
         torch.cuda.empty_cache()
         for name in subs:
             fn = {"c3_dp": c3_dp_record, "c5_shard": c5_shard_record}[name]
@@ -861,15 +861,13 @@ def main():
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:
-        # every graph is closed (GraphedStep.close: reset before the process group goes), so the ranks only meet
-        # once more and leave.  No destroy_process_group: tearing an RCCL group down after graphs that captured
-        # its collectives aborted the process in a test run (rc 134 after the results were out), and a rank's
-        # exit code is what torchrun reports -- the ranks sync the device, flush and exit directly instead.
+        # every graph that captured a collective is closed (GraphedStep.close resets it) before the process group
+        # is destroyed: the order tests/test_gpu_rccl.py's graph cases run
+        if gstep is not None:
+            gstep.close()
         dist.barrier(group=ctl)
         torch.cuda.synchronize()
-        sys.stdout.flush()
-        sys.stderr.flush()
-        os._exit(0)
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

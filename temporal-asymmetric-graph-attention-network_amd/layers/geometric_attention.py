@@ -5,9 +5,14 @@ initialisation order and forward signature (geometric_attention.py:228-607), so
 reference ``state_dict``s load unchanged and ``torch.manual_seed(s)`` yields the
 same initial weights.  The forward runs:
 
-  LN1 (HIP) -> one fused QKV GEMM (hipBLASLt) -> ``tagan_geo_attn_fwd``
+  LN1 fused into the prologue of the QKV projection (hand-written bf16-matrix-core
+  GEMM, csrc/stream_gemm.hip; fp32 as three bf16 planes) -> ``tagan_geo_attn_fwd``
   (metric score, edge-softmax, attn-dropout, A·V over the mask's CSR; HIP)
-  -> out-proj GEMM -> fused dropout + residual + LN2 (HIP)
+  -> out-projection GEMM with dropout + residual + LN2 in its epilogue (HIP)
+
+(widths without a stream-GEMM kernel -- none of BASELINE's 64 / 128 / 256 -- take
+hipBLASLt and the standalone LayerNorm kernels; at H = 64 / 256 the LayerNorms run
+as their own kernels beside the stream GEMMs).
 
 Dense masks become CSR (``graph_from_dense_mask``); TAGANGraphAttention hands in
 a prebuilt snapshot CSR through ``forward_graph``.  There is no CPU path.

@@ -2,10 +2,11 @@
 
 ``TimeEncoding``, ``TemporalAttention`` and ``AsymmetricTemporalAttention`` keep
 the reference constructors, parameter names/shapes and initialisation order.
-Forward = LN1 (HIP) -> fused QKV GEMM (hipBLASLt) -> ``tagan_temporal_attn_fwd``
-(QKᵀ/√d + folded relative-position/asymmetric-kernel bias table [+ time bias]
--> masks -> softmax -> attn-dropout -> A·V per node row, HIP) -> out-proj GEMM
--> fused dropout + residual + LN2 (HIP).
+Forward = LN1 + QKV projection (hand-written stream GEMM, csrc/stream_gemm.hip; LN1 in
+its prologue at H = 128) -> ``tagan_temporal_attn_fwd`` (QKᵀ/√d + folded
+relative-position/asymmetric-kernel bias table [+ time bias] -> masks -> softmax ->
+attn-dropout -> A·V per node row, HIP) -> out-projection stream GEMM with dropout +
+residual + LN2 in its epilogue at H = 128 (standalone LayerNorm kernels at H = 64 / 256).
 
 Snapshot lists are kept **time-major** ([T, N_max, H], the natural result of
 stacking snapshots) — the kernel takes strides, so the reference's

@@ -23,3 +23,8 @@ PY
 bash tools/sq_counters.sh ${1:-r4b} python tools/sgemm_probe.py --H 128 --M 320000 > $OUT/sq.log 2>&1 || { tail -20 $OUT/sq.log; exit 1; }
 cp gpurun_out/sq_${1:-r4b}/table.txt $OUT/pmc_table.txt
 grep -A 20 "k_sgemm" $OUT/pmc_table.txt | head -120
+# the round-4 tests added beside the GEMM work: C5-geometry two-rank shard (gloo on one GPU), C3/C5-geometry whole
+# model against the fp64 oracle
+timeout -k 10 900 python -u -m pytest tests/test_gpu_sharded.py::test_sharded_hip_matches_unsharded_c5_geometry \
+    "tests/test_gpu_fullsize.py::test_geometry_whole_model_vs_oracle" -v --timeout 850 --timeout-method thread \
+    > $OUT/new_tests.log 2>&1; echo "new tests rc=$?"; grep -E "PASS|FAIL|Error|error" $OUT/new_tests.log | head -20
