@@ -181,6 +181,11 @@ struct NtArgs {
 
 enum { MODE_PLAIN = 0, MODE_LN_IN = 1, MODE_LN_OUT = 2, MODE_LN_BWD = 3 };
 
+// k_sgemm_nt A-tile load map (compile-time A/B switch: make variant NAME=x EXTRA=-DNT_ROWLOAD=0): 1 = whole rows
+#ifndef NT_ROWLOAD
+#define NT_ROWLOAD 1
+#endif
+
 // h = LN(x) element: one expression shared by the prologue and the weight gradient's recompute (bitwise equal)
 __device__ __forceinline__ float ln_apply(float x, float m, float rs, float g, float b) {
     return __builtin_fmaf((x - m) * rs, g, b);
@@ -227,7 +232,7 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
     if constexpr (MODE == MODE_LN_OUT) {
         if (g.seed_ctr) g.seed ^= *g.seed_ctr * 0x9E3779B97F4A7C15ull;   // TAGAN_LIVE_SEED
     }
-    // LN prologue: gamma | beta in LDS after the two tile buffers (this thread's 8 columns: q = threadIdx.x % 16)
+    // LN prologue: gamma | beta in LDS after the two tile buffers
     float* lgb = reinterpret_cast<float*>(sg_lds + 2 * BUF);
     if constexpr (MODE == MODE_LN_IN) {
         for (int i = threadIdx.x; i < 2 * K; i += NT) lgb[i] = i < K ? g.ln_g[i] : g.ln_b[i - K];
@@ -274,22 +279,48 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
     if (tile >= ntiles) return;   // uniform over the workgroup (the host launches at most ntiles workgroups)
 
     // ---- staging: global -> registers (pf) -> planes in LDS
+    // NT_ROWLOAD: the workgroup's loads walk whole rows -- consecutive lanes take consecutive 16-byte pieces of a row
+    // (fp32: 32 lanes per 512-B row; bf16: 16 lanes per 256-B row), so one wave instruction reads 1 KB of contiguous
+    // lines; a fp32 float4 is half a fragment chunk and goes to LDS as an 8-byte half slot.  (0: the round-3 map, a
+    // lane loads a whole 8-k chunk and the 64 lanes of an instruction spread over 16 rows at half-line granularity.)
+    constexpr bool RL = NT_ROWLOAD != 0;
+    constexpr int C4 = BM * K / 4 / NT;   // fp32 float4 pieces per thread (= 2 CPT)
     float pf[ABF ? 1 : CPT][8];
     uint4 pb[ABF ? CPT : 1];
-    auto load = [&](int64_t t) {
-#pragma unroll
-        for (int i = 0; i < CPT; ++i) {
+    // (row in tile, 8-k chunk q, half h) of piece i: fp32 row loads (RL) walk float4 pieces, else whole chunks
+    auto piece = [&](int i, int& r, int& q, int& h) {
+        if constexpr (RL && !ABF) {
+            const int c = i * NT + threadIdx.x, c4 = c % (K / 4);
+            r = c / (K / 4); q = c4 >> 1; h = c4 & 1;
+        } else if constexpr (RL) {
+            const int c = i * NT + threadIdx.x;
+            r = c / QK; q = c % QK; h = 0;
+        } else {
             const int c = i * NT + threadIdx.x;
             const int rl = MODE == MODE_LN_IN ? (c >> 4) & 15 : c & 15;
-            const int q = MODE == MODE_LN_IN ? c & 15 : (c >> 4) % QK;
-            const int rh = MODE == MODE_LN_IN ? c >> 8 : (c >> 4) / QK;
+            q = MODE == MODE_LN_IN ? c & 15 : (c >> 4) % QK;
+            r = (MODE == MODE_LN_IN ? c >> 8 : (c >> 4) / QK) * 16 + rl;
+            h = 0;
+        }
+    };
+    constexpr int NPC = (RL && !ABF) ? C4 : CPT;   // pieces per thread
+    auto pf4 = [&](int i) -> float* { return (RL && !ABF) ? &pf[i >> 1][4 * (i & 1)] : pf[i]; };
+    auto load = [&](int64_t t) {
+#pragma unroll
+        for (int i = 0; i < NPC; ++i) {
+            int r, q, h;
+            piece(i, r, q, h);
             // rows past M reload row M - 1: they only feed output rows that are never stored, and an unconditional
             // load needs no zero-filled destination (a conditional one made the compiler drain every store of the
             // previous tile -- s_waitcnt vmcnt(0) -- before this prefetch could issue)
-            const int64_t row0 = t * BM + rh * 16 + rl;
+            const int64_t row0 = t * BM + r;
             const int64_t row = row0 < g.M ? row0 : g.M - 1;
             if constexpr (ABF) {
                 pb[i] = *reinterpret_cast<const uint4*>((const uint16_t*)g.a + row * g.lda + 8 * q);
+            } else if constexpr (RL) {
+                const float4 v = *reinterpret_cast<const float4*>((const float*)g.a + row * g.lda + 8 * q + 4 * h);
+                float* d = pf4(i);
+                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
             } else {
                 float4 v0, v1;
                 {
@@ -302,40 +333,55 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
             }
         }
     };
-    auto stash = [&](uint4* buf, int64_t t) {
-#pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const int c = i * NT + threadIdx.x;
-            const int rl = MODE == MODE_LN_IN ? (c >> 4) & 15 : c & 15;
-            const int q = MODE == MODE_LN_IN ? c & 15 : (c >> 4) % QK;
-            const int rh = MODE == MODE_LN_IN ? c >> 8 : (c >> 4) / QK;
+    auto stash_one = [&](uint4* buf, int64_t t, int i) {
+        constexpr int W = (RL && !ABF) ? 4 : 8;   // values per piece
+        {
+            int r, q, h;
+            piece(i, r, q, h);
+            const int rh = r >> 4, rl = r & 15;
             const int e0 = ((q >> 2) * J + rh) * 64 + 16 * (q & 3) + (rl ^ ((q & 3) + 4 * ((q >> 2) & 3)));
-            if constexpr (MODE == MODE_LN_IN) {
-                float sm = (pf[i][0] + pf[i][1]) + (pf[i][2] + pf[i][3]) + ((pf[i][4] + pf[i][5]) + (pf[i][6] + pf[i][7]));
-                const float mean = xsum<16>(sm) / (float)K;
+            float* v = pf4(i);
+            if constexpr (MODE == MODE_LN_IN) {   // the row's pieces sit in K / W consecutive lanes
+                constexpr int G = K / W;
+                float sm = 0.f;
+#pragma unroll
+                for (int e = 0; e < W; ++e) sm += v[e];
+                const float mean = xsum<G>(sm) / (float)K;
                 float sq = 0.f;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) sq += (pf[i][e] - mean) * (pf[i][e] - mean);
-                const float rstd = 1.f / sqrtf(xsum<16>(sq) / (float)K + g.eps);
+                for (int e = 0; e < W; ++e) sq += (v[e] - mean) * (v[e] - mean);
+                const float rstd = 1.f / sqrtf(xsum<G>(sq) / (float)K + g.eps);
+                const int k0 = 8 * q + 4 * h;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) pf[i][e] = ln_apply(pf[i][e], mean, rstd, lgb[8 * q + e], lgb[K + 8 * q + e]);
-                const int64_t row = t * BM + rh * 16 + rl;
-                if (q == 0 && row < g.M) {
+                for (int e = 0; e < W; ++e) v[e] = ln_apply(v[e], mean, rstd, lgb[k0 + e], lgb[K + k0 + e]);
+                const int64_t row = t * BM + r;
+                if (q == 0 && h == 0 && row < g.M) {
                     g.mean[row] = mean;
                     g.rstd[row] = rstd;
                 }
             }
             if constexpr (ABF) {
                 buf[e0] = pb[i];
+            } else if constexpr (RL) {
+                uint32_t lo[P], hi[P];
+                split2<P>(v[0], v[1], lo);
+                split2<P>(v[2], v[3], hi);
+#pragma unroll
+                for (int p = 0; p < P; ++p)
+                    reinterpret_cast<uint2*>(buf + p * KK * J * 64 + e0)[h] = make_uint2(lo[p], hi[p]);
             } else {
                 uint32_t pl[4][P];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) split2<P>(pf[i][2 * e], pf[i][2 * e + 1], pl[e]);
+                for (int e = 0; e < 4; ++e) split2<P>(v[2 * e], v[2 * e + 1], pl[e]);
 #pragma unroll
                 for (int p = 0; p < P; ++p)
                     buf[p * KK * J * 64 + e0] = make_uint4(pl[0][p], pl[1][p], pl[2][p], pl[3][p]);
             }
         }
+    };
+    auto stash = [&](uint4* buf, int64_t t) {
+#pragma unroll
+        for (int i = 0; i < NPC; ++i) stash_one(buf, t, i);
     };
 
     // fragment slot of this lane in a 64-entry block of k-block kk (the swizzle of stash)
@@ -345,12 +391,12 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
 
     load(tile);
     stash(sg_lds, tile);
+    // the prefetch is unconditional (the last tile re-stages itself into the idle buffer): with a conditional one
+    // the compiler could not prove the loads drained at the back edge and waited for every store of the tile
+    // (s_waitcnt vmcnt(0)) before the next prefetch could issue
     __syncthreads();
     for (int it = 0;; ++it) {
         const int64_t next = tile + gridDim.x;
-        // the prefetch is unconditional (the last tile re-stages itself into the idle buffer): with a conditional
-        // one the compiler could not prove the loads drained at the back edge and waited for every store of the
-        // tile (s_waitcnt vmcnt(0)) before the next prefetch could issue
         const int64_t pre = next < ntiles ? next : tile;
         load(pre);
         __builtin_amdgcn_sched_barrier(0);
@@ -1042,201 +1088,6 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_tn(TnArgs g) {
     }
 }
 
-// TN, second form (fp32 operands): dY goes straight from HBM into MFMA operand registers and only X goes through LDS.
-// Wave w owns NSN interleaved n-subtiles of dY columns: subtile s holds columns base_w + NSN m + s (m = 0..15), so a
-// lane's NSN values of one row are one contiguous NSN-float load (16 lanes x NSN floats of a row per instruction),
-// and each dY element is split into planes exactly once, by the wave that multiplies it.  The reduction index of
-// both operands is the tile row 4 grp + (e & 3) + 16 (e >> 2) (element e of lane group grp), the order the
-// transposed LDS reads of X produce.  X (or h = LN(x), recomputed from the forward's row statistics: LNX) is split
-// into planes once per workgroup and double-buffered in LDS: ONE barrier per 32-row tile, and the next tile's dY and
-// X loads are in flight under this tile's MFMAs.
-template <int N, int K, int NSN, int NW, int NG, int P, bool LNX, int MINB>
-__global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_tn2(TnArgs g) {
-    constexpr int NL = N / NG;
-    static_assert(NL == NW * NSN * 16, "waves must cover the workgroup's columns");
-    static_assert(NSN >= 2 && NSN <= 4, "dY row loads of 2, 3 or 4 floats");
-    constexpr int NT = NW * 64, KS = K / 16;
-    constexpr int SX = K + 16, PX = 32 * SX, BUFX = P * PX;   // bf16 elements: row stride, plane, buffer
-    constexpr int XQ = 32 * K / 4;                            // float4 chunks of an X tile
-    constexpr int XC = (XQ + NT - 1) / NT;
-    static_assert(!LNX || NT % (K / 4) == 0, "LNX: thread-fixed x columns");
-    extern __shared__ uint4 sg_lds[];
-    uint16_t* lx = reinterpret_cast<uint16_t*>(sg_lds);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int grp = lane >> 4, li = lane & 15;
-    const int cw = blockIdx.y * NL + w * NSN * 16;            // the wave's first dY column
-
-    f32x4 acc[NSN][KS];
-    float dbs[NSN];   // db: fp32 sums of the lane's dY values (its 8 rows of each tile), lane groups summed at the end
-#pragma unroll
-    for (int s = 0; s < NSN; ++s) {
-        dbs[s] = 0.f;
-#pragma unroll
-        for (int k = 0; k < KS; ++k) acc[s][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-
-    const int64_t t0 = (int64_t)blockIdx.x * g.tiles_per_wg;
-    const int64_t t1 = min(t0 + g.tiles_per_wg, (g.M + 31) / 32);
-    if (t0 >= t1) {   // no rows for this group: zero partials (the reduction reads every group)
-        float* part = g.part + (int64_t)blockIdx.x * (N * K + N);
-        for (int i = threadIdx.x; i < NL * K; i += NT) part[(int64_t)(blockIdx.y * NL + i / K) * K + i % K] = 0.f;
-        for (int i = threadIdx.x; i < NL; i += NT) part[N * K + blockIdx.y * NL + i] = 0.f;
-        return;
-    }
-    // LNX: gamma | beta in LDS after the two X buffers (read at stash time: no registers held across the loop)
-    float* lgb = reinterpret_cast<float*>(lx + 2 * BUFX);
-    if constexpr (LNX) {
-        for (int i = threadIdx.x; i < 2 * K; i += NT) lgb[i] = i < K ? g.ln_g[i] : g.ln_b[i - K];
-        __syncthreads();
-    }
-
-    // ---- addressing: a uniform tile base (scalar registers) plus loop-invariant 32-bit lane offsets, so a full
-    // tile's loads cost no vector address arithmetic; the partial last tile (if any) is peeled off the pipelined loop
-    int yoff[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) yoff[e] = (4 * grp + (e & 3) + 16 * (e >> 2)) * (int)g.ldy + cw + NSN * li;
-    int xoff[XC];
-    auto xrow = [&](int i) { return (i * NT + (int)threadIdx.x) / (K / 4); };
-    auto xcol = [&](int i) { return 4 * ((i * NT + (int)threadIdx.x) % (K / 4)); };
-#pragma unroll
-    for (int i = 0; i < XC; ++i) xoff[i] = xrow(i) * (int)g.ldx + xcol(i);
-    const float* gy = (const float*)g.dy;
-    const float* gx = (const float*)g.x;
-
-    // ---- dY: raw rows of tile t -> yr; planes -> ya
-    float yr[8][NSN];
-    auto load_row = [&](const float* src, int e) {
-        if constexpr (NSN == 2) {
-            const float2 v = *reinterpret_cast<const float2*>(src);
-            yr[e][0] = v.x; yr[e][1] = v.y;
-        } else if constexpr (NSN == 4) {
-            const float4 v = *reinterpret_cast<const float4*>(src);
-            yr[e][0] = v.x; yr[e][1] = v.y; yr[e][2] = v.z; yr[e][3] = v.w;
-        } else {
-#pragma unroll
-            for (int s = 0; s < NSN; ++s) yr[e][s] = src[s];
-        }
-    };
-    auto load_y = [&](int64_t t, bool full) {
-        const float* b = gy + t * 32 * g.ldy;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            if (full) {
-                load_row(b + yoff[e], e);
-            } else if (t * 32 + 4 * grp + (e & 3) + 16 * (e >> 2) < g.M) {
-                load_row(b + yoff[e], e);
-            } else {
-#pragma unroll
-                for (int s = 0; s < NSN; ++s) yr[e][s] = 0.f;
-            }
-        }
-    };
-    bf16x8 ya[NSN][P];
-    auto split_y = [&]() {
-#pragma unroll
-        for (int s = 0; s < NSN; ++s) {
-            dbs[s] += ((yr[0][s] + yr[1][s]) + (yr[2][s] + yr[3][s])) + ((yr[4][s] + yr[5][s]) + (yr[6][s] + yr[7][s]));
-            uint32_t pl[4][P];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) split2<P>(yr[2 * e][s], yr[2 * e + 1][s], pl[e]);
-#pragma unroll
-            for (int p = 0; p < P; ++p) ya[s][p] = __builtin_bit_cast(bf16x8, make_uint4(pl[0][p], pl[1][p], pl[2][p], pl[3][p]));
-        }
-    };
-    // ---- X: XC float4 chunks per thread -> planes in LDS buffer b (rows past M: zero)
-    float4 xr[XC];
-    float xm[LNX ? XC : 1], xs[LNX ? XC : 1];
-    auto load_x = [&](int64_t t, bool full) {
-        const float* b = gx + t * 32 * g.ldx;
-#pragma unroll
-        for (int i = 0; i < XC; ++i) {
-            if (XQ % NT == 0 || i * NT + (int)threadIdx.x < XQ) {
-                const bool live = full || t * 32 + xrow(i) < g.M;
-                xr[i] = live ? *reinterpret_cast<const float4*>(b + xoff[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
-                if constexpr (LNX) {
-                    xm[i] = live ? g.mean[t * 32 + xrow(i)] : 0.f;
-                    xs[i] = live ? g.rstd[t * 32 + xrow(i)] : 0.f;
-                }
-            }
-        }
-    };
-    auto stash_x = [&](uint16_t* buf, int64_t t, bool full) {
-#pragma unroll
-        for (int i = 0; i < XC; ++i) {
-            if (XQ % NT == 0 || i * NT + (int)threadIdx.x < XQ) {
-                const int col = xcol(i);
-                float4 v = xr[i];
-                if constexpr (LNX) {   // rows past M stay 0 (their dY is 0 too); h of a live row as the prologue made it
-                    if (full || t * 32 + xrow(i) < g.M) {
-                        const float4 lg = *reinterpret_cast<const float4*>(lgb + col);
-                        const float4 lb = *reinterpret_cast<const float4*>(lgb + K + col);
-                        v.x = ln_apply(v.x, xm[i], xs[i], lg.x, lb.x);
-                        v.y = ln_apply(v.y, xm[i], xs[i], lg.y, lb.y);
-                        v.z = ln_apply(v.z, xm[i], xs[i], lg.z, lb.z);
-                        v.w = ln_apply(v.w, xm[i], xs[i], lg.w, lb.w);
-                    }
-                }
-                uint32_t lo[P], hi[P];
-                split2<P>(v.x, v.y, lo);
-                split2<P>(v.z, v.w, hi);
-#pragma unroll
-                for (int p = 0; p < P; ++p)
-                    *reinterpret_cast<uint2*>(buf + p * PX + xrow(i) * SX + col) = make_uint2(lo[p], hi[p]);
-            }
-        }
-    };
-    auto frag = [&](const uint16_t* plane, int c0) {
-        const int q = li >> 2, p4 = li & 3;
-        const uint16_t* a0 = plane + (4 * grp + q) * SX + c0 + 4 * p4;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 16 * SX));
-        const short __attribute__((ext_vector_type(8))) v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        return __builtin_bit_cast(bf16x8, v);
-    };
-    auto mfmas = [&](const uint16_t* bx) {
-#pragma unroll
-        for (int k = 0; k < KS; ++k) {
-            bf16x8 xb[P];
-#pragma unroll
-            for (int p = 0; p < P; ++p) xb[p] = frag(bx + p * PX, k * 16);
-#pragma unroll
-            for (int s = 0; s < NSN; ++s) acc[s][k] = mfma_planes<P>(ya[s], xb, acc[s][k]);
-        }
-    };
-
-    const int64_t tf = min(t1, g.M / 32);   // tiles [t0, tf) are whole; at most one partial tile follows
-    load_y(t0, t0 < tf);
-    load_x(t0, t0 < tf);
-    split_y();
-    stash_x(lx, t0, t0 < tf);
-    lds_barrier();
-    for (int64_t t = t0; t < t1; ++t) {
-        const int cur = (int)((t - t0) & 1);
-        const bool more = t + 1 < t1;
-        if (more) {   // next tile in flight under this tile's MFMAs
-            load_y(t + 1, t + 1 < tf);
-            load_x(t + 1, t + 1 < tf);
-        }
-        mfmas(lx + cur * BUFX);
-        if (more) {
-            split_y();
-            stash_x(lx + (cur ^ 1) * BUFX, t + 1, t + 1 < tf);
-            lds_barrier();   // the other buffer is complete; this one's reads are done before it is rewritten
-        }
-    }
-    // D[m][k]: lane holds subtile rows m = 4 grp + r (dY column cw + NSN m + s), column k = 16 kk + li
-    float* part = g.part + (int64_t)blockIdx.x * (N * K + N);
-#pragma unroll
-    for (int s = 0; s < NSN; ++s) {
-#pragma unroll
-        for (int k = 0; k < KS; ++k)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) part[(int64_t)(cw + NSN * (4 * grp + r) + s) * K + 16 * k + li] = acc[s][k][r];
-        const float d = gsum4(dbs[s]);   // the four lane groups hold the tile's other rows of column m = li
-        if (grp == 0) part[N * K + cw + NSN * li + s] = d;
-    }
-}
-
 // dw[n * lddw + k] = Σ_g part[g][n K + k], db[n] likewise.  A 256-thread block owns 64 consecutive outputs; its four
 // waves sum the four quarters of the partial range (g ascending, 4 interleaved accumulators each: 16 loads in
 // flight per lane) and the quarters meet in LDS in a fixed order (bitwise reproducible).  One thread per output
@@ -1334,12 +1185,12 @@ constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
 // The LayerNorm-fused forms (H = 128): LN1 prologue of the QKV projection (x fp32 in; qkv fp32, or bf16 in the
 // bf16 activation mode), dropout + residual + LN2 [+ skip LN] epilogue of the out-projection (y fp32), LN1 backward
 // epilogue of the QKV input gradient (dx fp32).
-// (The LN2 epilogue and the one-plane LN1-backward epilogue run on the row-owner kernels, RG_TABLE.)
+// (The LN2 epilogue and the one-plane LN1-backward epilogue run on the row-owner kernels, RG_TABLE; the three-plane
+// LN1-backward epilogue lost its A/B -- fp32 step 6.99 vs 6.75 ms, profiles/r3d_ab_step.txt -- and is not built.)
 #define NT_SETLN                                                                                             \
     nt_cfg<128, 3, 8, 32, 3, false, false, MODE_LN_IN>(384, 1),                                                 \
     nt_cfg<128, 3, 8, 64, 1, false, true, MODE_LN_IN>(384, 1),                                                  \
-    nt_cfg<128, 3, 8, 64, 1, false, false, MODE_LN_IN>(384, 1),                                                 \
-    nt_cfg<384, 1, 8, 32, 3, false, false, MODE_LN_BWD>(128, 1)
+    nt_cfg<128, 3, 8, 64, 1, false, false, MODE_LN_IN>(384, 1)
 const NtCfg NT_TABLE[] = {
     NT_SET3,
     NT_SET1(false, false),
@@ -1387,27 +1238,6 @@ const TnCfg TN_TABLE[] = {
 const TnCfg* tn_find(int N, int K, int P, int abf, int lnx = 0) {
     for (const TnCfg& c : TN_TABLE)
         if (c.N == N && c.K == K && c.P == P && c.abf == abf && c.lnx == lnx) return &c;
-    return nullptr;
-}
-
-// the second TN form (fp32 operands; tn_run prefers it when dY's rows allow NSN-float loads)
-template <int N, int K, int NSN, int NW, int NG, int P, bool LNX = false, int MINB = 1>
-constexpr TnCfg tn2_cfg(int wg_per_cu) {
-    return TnCfg{N, K, P, 0, LNX, k_sgemm_tn2<N, K, NSN, NW, NG, P, LNX, MINB>, NW, NG,
-                 (size_t)2 * P * 32 * (K + 16) * 2 + (LNX ? 2 * K * 4 : 0), wg_per_cu};
-}
-const TnCfg TN2_TABLE[] = {
-    tn2_cfg<384, 128, 2, 12, 1, 3>(1), tn2_cfg<128, 128, 2, 4, 1, 3, false, 2>(2),
-    tn2_cfg<384, 128, 3, 8, 1, 3, true>(1),
-    tn2_cfg<768, 256, 2, 8, 3, 3>(1),  tn2_cfg<256, 256, 2, 8, 1, 3>(1),
-    tn2_cfg<384, 128, 2, 12, 1, 1>(1), tn2_cfg<128, 128, 2, 4, 1, 1, false, 3>(3),
-    tn2_cfg<384, 128, 2, 12, 1, 1, true>(1),
-    tn2_cfg<768, 256, 2, 8, 3, 1>(1),  tn2_cfg<256, 256, 2, 8, 1, 1>(1),
-};
-const TnCfg* tn2_find(int N, int K, int P, int abf, int lnx) {
-    if (abf) return nullptr;
-    for (const TnCfg& c : TN2_TABLE)
-        if (c.N == N && c.K == K && c.P == P && c.lnx == lnx) return &c;
     return nullptr;
 }
 
@@ -1681,8 +1511,6 @@ extern "C" size_t tagan_sgemm_tn_workspace(int64_t M, int32_t N, int32_t K) {
     int64_t g = 1;
     for (const TnCfg& c : TN_TABLE)
         if (c.N == N && c.K == K) g = std::max(g, tn_groups(M, &c));
-    for (const TnCfg& c : TN2_TABLE)
-        if (c.N == N && c.K == K) g = std::max(g, tn_groups(M, &c));
     return (size_t)g * ((size_t)N * K + N) * sizeof(float);
 }
 
@@ -1712,9 +1540,6 @@ static int tn_run(int32_t dtype, int64_t M, int32_t N, int32_t K, const void* dy
                   void* stream, const float* ln_g, const float* ln_b, const float* mean, const float* rstd) {
     const int lnx = ln_g != nullptr;
     const TnCfg* cfg = tn_find(N, K, planes, dtype == TAGAN_BF16, lnx);
-    const TnCfg* cfg2 = tn2_find(N, K, planes, dtype == TAGAN_BF16, lnx);
-    if (cfg2 && (uintptr_t)dy % 16 == 0 && ldy % 4 == 0 && (uintptr_t)x % 16 == 0 && ldx % 4 == 0)
-        cfg = cfg2;   // 16-byte rows: dY as NSN-float loads, X as float4 (other strides: the first form)
     TAGAN_REQUIRE(cfg, TAGAN_ERR_UNSUPPORTED, "tagan_sgemm_tn: no kernel for N=%d K=%d planes=%d dtype %d", N, K,
                   planes, dtype);
     TAGAN_REQUIRE(M >= 0 && (M == 0 || (dy && x)) && (dw || db), TAGAN_ERR_ARG, "tagan_sgemm_tn: bad arguments");

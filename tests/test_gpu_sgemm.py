@@ -174,24 +174,3 @@ def test_wprep_block_equals_single_preps(planes, H):
             sg.wprep(wq, True, planes))
     for a, b in zip(got, want):
         assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("N,K", [(384, 128), (128, 128), (768, 256)])
-def test_tn_both_forms_agree(N, K):
-    """fp32 weight gradients run on k_sgemm_tn2 (dY straight into MFMA registers) when the rows are 16-byte aligned,
-    on k_sgemm_tn otherwise (row stride N + 2 here): both within fp32-GEMM accuracy of fp64 and of each other."""
-    dev = _dev()
-    from tagan_amd import stream_gemm as sg
-    g = torch.Generator(device=dev).manual_seed(N + K)
-    M = 20001
-    wide = torch.randn(M, N + 2, device=dev, generator=g)
-    x = torch.randn(M, K, device=dev, generator=g)
-    dy_odd = wide[:, :N]                       # row stride N + 2: the first form
-    dy = dy_odd.contiguous()                   # row stride N: the second form
-    dw1, db1 = sg.tn(dy_odd, x, 3)
-    dw2, db2 = sg.tn(dy, x, 3)
-    ref = dy.double().t() @ x.double()
-    refb = dy.double().sum(0)
-    for dw, db in ((dw1, db1), (dw2, db2)):
-        assert _merr(dw, ref) <= 1e-6 and _merr(db, refb) <= 2e-6
-    assert _nerr(dw1, dw2) <= 1e-6

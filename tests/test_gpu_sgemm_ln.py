@@ -161,7 +161,7 @@ def test_ln_out_dropout_matches_layernorm_kernel(skip):
 
 
 @pytest.mark.parametrize("M", ROWS)
-@pytest.mark.parametrize("planes,store", [(3, "fp32"), (1, "bf16")])
+@pytest.mark.parametrize("planes,store", [(1, "fp32"), (1, "bf16")])
 @pytest.mark.parametrize("with_dres", [True, False])
 def test_ln_bwd(M, planes, store, with_dres):
     dev = _dev()
@@ -198,6 +198,6 @@ def test_ln_supported_shapes():
     _dev()
     from tagan_amd import stream_gemm as sg
     for op in ("in", "out", "bwd"):
-        assert sg.ln_supported(128, 3, False, op) and sg.ln_supported(128, 1, True, op)
-        assert sg.ln_supported(128, 1, False, op)
+        assert sg.ln_supported(128, 1, True, op) and sg.ln_supported(128, 1, False, op)
+        assert sg.ln_supported(128, 3, False, op) == (op != "bwd")   # the three-plane LN1-backward form is not built
         assert not sg.ln_supported(256, 3, False, op)

@@ -11,3 +11,14 @@ timeout -k 10 300 python tools/tn_ab.py --H 128 > $OUT/tn_ab_h128.jsonl 2>&1 || 
 cat $OUT/tn_ab_h128.jsonl
 timeout -k 10 300 python tools/tn_ab.py --H 256 --M 1600000 > $OUT/tn_ab_h256.jsonl 2>&1 || { tail -20 $OUT/tn_ab_h256.jsonl; exit 1; }
 cat $OUT/tn_ab_h256.jsonl
+# NT staging order A/B: the shipped library (stash first) against the round-3 order (make variant NAME=ntold)
+SGEMM_PROBE_OUT=$OUT/probe_new.json timeout -k 10 300 python tools/sgemm_probe.py --H 128 > $OUT/probe_new.log 2>&1 || { tail -20 $OUT/probe_new.log; exit 1; }
+TAGAN_LIB=$GRAFT_REPO_ROOT/temporal-asymmetric-graph-attention-network_amd/libtagan_hip_ntold.so SGEMM_PROBE_OUT=$OUT/probe_old.json \
+    timeout -k 10 300 python tools/sgemm_probe.py --H 128 > $OUT/probe_old.log 2>&1 || { tail -20 $OUT/probe_old.log; exit 1; }
+python - <<PY
+import json
+a = {c["case"]: c for c in json.load(open("$OUT/probe_new.json"))["cases"]}
+b = {c["case"]: c for c in json.load(open("$OUT/probe_old.json"))["cases"]}
+for k in a:
+    print("%-18s new %8.1f us  old %8.1f us" % (k, a[k]["us_kernel"], b[k]["us_kernel"]))
+PY
