@@ -93,6 +93,61 @@ static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; 
 // ---------------------------------------------------------------- device helpers
 constexpr int WAVE = 64;
 
+// ---------------------------------------------------------------- lane reductions without the LDS crossbar
+// __shfl_xor lowers to ds_bpermute_b32: an LDS-pipe round trip (~100 cycles) per butterfly step, serialised by the
+// reduction's dependency chain and waited for with s_waitcnt lgkmcnt(0) each time.  Here the steps inside a 16-lane
+// row are DPP moves (quad_perm xor 1 / xor 2; row_half_mirror pairs the same quads as xor 4, row_mirror the same
+// octets as xor 8) and the steps across rows are v_permlane16_swap / v_permlane32_swap (gfx950 VALU): the same
+// pairwise association as the xor butterfly, so every lane ends with the bitwise-same value the shuffle form gave.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+// the value of lane l ^ 16 / l ^ 32 (both results of the swap pair, own row first for the even rows)
+__device__ __forceinline__ void swap16(float x, float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap32(float x, float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+// x combined over the aligned group of G lanes (G = 1, 2, 4, ..., 64) with op (sum / max); G is a compile-time power
+// of two.  lo_steps = false skips the inside-row steps (the caller's group is the lanes l, l ^ 16, l ^ 32, l ^ 48).
+template <int G, bool LO = true, class Op>
+__device__ __forceinline__ float lane_reduce(float x, Op op) {
+    if constexpr (LO && G >= 2) x = op(x, dpp_mov<0xB1>(x));    // quad_perm [1,0,3,2]
+    if constexpr (LO && G >= 4) x = op(x, dpp_mov<0x4E>(x));    // quad_perm [2,3,0,1]
+    if constexpr (LO && G >= 8) x = op(x, dpp_mov<0x141>(x));   // row_half_mirror
+    if constexpr (LO && G >= 16) x = op(x, dpp_mov<0x140>(x));  // row_mirror
+    if constexpr (G >= 32) {
+        float a, b;
+        swap16(x, a, b);
+        x = op(a, b);
+    }
+    if constexpr (G >= 64) {
+        float a, b;
+        swap32(x, a, b);
+        x = op(a, b);
+    }
+    return x;
+}
+struct OpAdd {
+    __device__ __forceinline__ float operator()(float a, float b) const { return a + b; }
+};
+struct OpMax {
+    __device__ __forceinline__ float operator()(float a, float b) const { return fmaxf(a, b); }
+};
+template <int G>
+__device__ __forceinline__ float lane_sum(float x) { return lane_reduce<G>(x, OpAdd()); }
+template <int G>
+__device__ __forceinline__ float lane_max(float x) { return lane_reduce<G>(x, OpMax()); }
+// over the lanes l, l ^ 16, l ^ 32, l ^ 48 (same lane index inside each row): two swaps
+__device__ __forceinline__ float rows_sum(float x) { return lane_reduce<64, false>(x, OpAdd()); }
+__device__ __forceinline__ float rows_max(float x) { return lane_reduce<64, false>(x, OpMax()); }
+
 // Dropout masks: counter-based, two-level.  A 32-bit key per (seed, stream) is mixed once
 // (per lane / per row, amortised), then each element costs one lowbias32 round
 // (2 integer multiplies) on (counter ^ key).  Streams / counters per kernel are

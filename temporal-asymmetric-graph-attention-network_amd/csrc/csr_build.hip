@@ -858,6 +858,18 @@ __device__ void csr_bucket(const Geo& g, int64_t b, uint32_t* A, uint32_t* B, bo
         csr_lsd<NTH>(g, b, nv, A, B, m, off, keys, rowptr, ucnt, sh_base, sh_tot, L.wc, L.rc, sh_sm);
 }
 
+// the buckets too large for the small finish kernels (CSR: raw keys + self-loops > CAP_S; CSC: pairs > CAP_C), listed
+// before the finish so the big-bucket kernel runs on a side stream beside the small one (their buckets are disjoint;
+// the list order is irrelevant: every bucket's output depends on the bucket alone)
+template <bool CSC>
+__global__ void __launch_bounds__(BLK) k_big_list(Geo g, const int32_t* __restrict__ fill, int32_t* __restrict__ big,
+                                                  int32_t* __restrict__ nbig) {
+    for (int64_t b = blockIdx.x * (int64_t)BLK + threadIdx.x; b < g.NB; b += (int64_t)gridDim.x * BLK) {
+        const bool is_big = CSC ? fill[b] > CAP_C : fill[b] + (int)bucket_rows(b, g.SB, g.N) > CAP_S;
+        if (is_big) big[atomicAdd(nbig + (CSC ? 1 : 0), 1)] = (int32_t)b;
+    }
+}
+
 __global__ void __launch_bounds__(FNT) k_csr_finish(Geo g, const int32_t* __restrict__ bstart,
                                                     const int32_t* __restrict__ fill_src,
                                                     const int64_t* __restrict__ node_ptr, uint32_t* __restrict__ keys,
@@ -872,10 +884,7 @@ __global__ void __launch_bounds__(FNT) k_csr_finish(Geo g, const int32_t* __rest
     __shared__ int32_t sm[FNT / WAVE + 1];
     const int64_t b = blockIdx.x;
     const int c = fill_src[b];
-    if (c + (int)bucket_rows(b, g.SB, g.N) > CAP_S) {
-        if (threadIdx.x == 0) big[atomicAdd(nbig, 1)] = (int32_t)b;
-        return;
-    }
+    if (c + (int)bucket_rows(b, g.SB, g.N) > CAP_S) return;   // listed by k_big_list, finished by k_csr_finish_big
     const SegLds L{rc, ro, (uint32_t*)rk, (uint16_t*)(rk + (FNT / WAVE) * BMW), rk, rk, &flag};
     csr_bucket<FNT>(g, b, A, Bk, false, c, bstart[b], node_ptr, keys, rowptr, ucnt, L, base, tot, sm);
 }
@@ -949,10 +958,7 @@ __global__ void __launch_bounds__(FNT) k_csc_finish(Geo g, const int32_t* __rest
     __shared__ int32_t sm[FNT / WAVE + 1];
     const int64_t b = blockIdx.x;
     const int m = fill_dst[b];
-    if (m > CAP_C) {
-        if (threadIdx.x == 0) big[atomicAdd(nbig + 1, 1)] = (int32_t)b;
-        return;
-    }
+    if (m > CAP_C) return;   // listed by k_big_list, finished by k_csc_finish_big
     const int32_t ro0 = cstart[b];
     for (int i = threadIdx.x; i < m; i += FNT) { K[i] = ckey[ro0 + i]; V[i] = cval[ro0 + i]; }
     const SegLds L{rc, ro, (uint32_t*)rk, (uint16_t*)(rk + (FNT / WAVE) * BMW), rk, rk, &flag};
@@ -1166,6 +1172,30 @@ CsrWs plan(const Geo& g) {
     return w;
 }
 
+// The side stream of the big-bucket kernels (one per device, created on first use) and the fork / join events:
+// record on the caller's stream -> the side stream waits -> big kernel there -> record -> the caller waits before the
+// scan that reads both kernels' outputs.  Under HIP-graph capture the two waits make the side launch a parallel
+// branch of the captured graph.
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+SideStream* side_stream() {
+    static SideStream ss[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SideStream& x = ss[dev];
+    if (!x.s) {
+        if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) {
+            x.s = nullptr;
+            return nullptr;
+        }
+    }
+    return &x;
+}
+
 }  // namespace
 }  // namespace tagan
 
@@ -1249,11 +1279,19 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
             TAGAN_CHECK_LAUNCH("csr_build.refine");
         }
     }
+    SideStream* side = side_stream();
+    TAGAN_REQUIRE(side, TAGAN_ERR_LAUNCH, "tagan_csr_build: cannot create the side stream");
+    k_big_list<false><<<grid_for(g.NB), BLK, 0, s>>>(g, fill_src, big_src, nbig);
+    TAGAN_CHECK_LAUNCH("csr_build.big_list");
+    TAGAN_REQUIRE(hipEventRecord(side->fork, s) == hipSuccess && hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess,
+                  TAGAN_ERR_LAUNCH, "tagan_csr_build: fork");
+    k_csr_finish_big<<<BIG_WG, BNT, BIG_LDS, side->s>>>(g, cap_src, fill_src, node_ptr, keys, stage, sloc, rowptr, ucnt,
+                                                        big_src, nbig);
+    TAGAN_CHECK_LAUNCH("csr_build.csr_finish_big");
     k_csr_finish<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_src, fill_src, node_ptr, keys, rowptr, ucnt, big_src, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.csr_finish");
-    k_csr_finish_big<<<BIG_WG, BNT, BIG_LDS, s>>>(g, cap_src, fill_src, node_ptr, keys, stage, sloc, rowptr, ucnt,
-                                                  big_src, nbig);
-    TAGAN_CHECK_LAUNCH("csr_build.csr_finish_big");
+    TAGAN_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess && hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
+                  TAGAN_ERR_LAUNCH, "tagan_csr_build: join");
     scan::exclusive(ucnt, ucnt, g.NB, (int32_t)0, plus, part, true, s);           // -> CSR bucket offsets
     TAGAN_CHECK_LAUNCH("csr_build.scan_unique");
     k_csr_place<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_src, ucnt, node_ptr, keys, rowptr, col, sloc, nnz_out);
@@ -1269,12 +1307,18 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     }
     scan::exclusive(fill_dst, coff, g.NB, (int32_t)0, plus, part, true, s);       // -> CSC bucket offsets
     TAGAN_CHECK_LAUNCH("csr_build.scan_csc");
+    k_big_list<true><<<grid_for(g.NB), BLK, 0, s>>>(g, fill_dst, big_dst, nbig);
+    TAGAN_CHECK_LAUNCH("csr_build.big_list_csc");
+    TAGAN_REQUIRE(hipEventRecord(side->fork, s) == hipSuccess && hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess,
+                  TAGAN_ERR_LAUNCH, "tagan_csr_build: fork (CSC)");
+    k_csc_finish_big<<<BIG_WG, BNT, BIG_LDS, side->s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, stage,
+                                                        sval, sloc, csc_ptr, csc_row, csc_eid, csr_cpos, big_dst, nbig);
+    TAGAN_CHECK_LAUNCH("csr_build.csc_finish_big");
     k_csc_finish<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, csc_ptr,
                                                 csc_row, csc_eid, csr_cpos, big_dst, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.csc_finish");
-    k_csc_finish_big<<<BIG_WG, BNT, BIG_LDS, s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, stage,
-                                                  sval, sloc, csc_ptr, csc_row, csc_eid, csr_cpos, big_dst, nbig);
-    TAGAN_CHECK_LAUNCH("csr_build.csc_finish_big");
+    TAGAN_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess && hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
+                  TAGAN_ERR_LAUNCH, "tagan_csr_build: join (CSC)");
     return TAGAN_OK;
 }
 

@@ -55,7 +55,16 @@ __device__ __forceinline__ float grp_sum(float x, int lph) {
     if (lph > 2) x += dpp<0x4E>(x);
     if (lph > 4) x += dpp<0x141>(x);
     if (lph > 8) x += dpp<0x140>(x);
-    for (int o = 16; o < lph; o <<= 1) x += __shfl_xor(x, o, 64);
+    if (lph > 16) {   // across rows: v_permlane16_swap / v_permlane32_swap (common.cuh)
+        float a, b;
+        swap16(x, a, b);
+        x = a + b;
+    }
+    if (lph > 32) {
+        float a, b;
+        swap32(x, a, b);
+        x = a + b;
+    }
     return x;
 }
 

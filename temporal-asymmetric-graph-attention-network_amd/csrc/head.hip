@@ -145,8 +145,7 @@ __global__ void __launch_bounds__(HB) k_head_fwd(HeadArgs A) {
         if (w == 0) {   // softmax over T
             float m = -INFINITY;
             for (int t = lane; t < T; t += 64) m = fmaxf(m, L.va[t]);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+            m = lane_max<64>(m);
             float e[2], den = 0.f;
             for (int q = 0; q < 2; ++q) {
                 const int t = lane + 64 * q;

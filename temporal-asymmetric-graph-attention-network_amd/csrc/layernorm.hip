@@ -17,11 +17,7 @@ namespace {
 constexpr int BLK = 256;
 
 template <int LPR>
-__device__ __forceinline__ float row_sum(float x) {
-#pragma unroll
-    for (int o = 1; o < LPR; o <<= 1) x += __shfl_xor(x, o, 64);
-    return x;
-}
+__device__ __forceinline__ float row_sum(float x) { return lane_sum<LPR>(x); }   // DPP / permlane (common.cuh)
 
 struct LnArgs {
     int64_t M;

@@ -174,34 +174,27 @@ struct NtArgs {
     float* rstd_s;
     const float* dres;
     float* part;
-    // MODE_PLAIN split-K: B's fragments are k-blocks [kk0, kk0 + K / 32) of a panel prepared with kkt k-blocks per
-    // n-subtile (kkt = 0: K / 32), and accum = 1 adds the product to the fp32 C already there
-    int kkt, kk0, accum;
+    // split-K: B's fragments are k-blocks [kk0, kk0 + K / 32) of a panel prepared with kkt k-blocks per n-subtile
+    // (kkt = 0: K / 32); MODE_ACC adds the product to the fp32 C already there
+    int kkt, kk0;
 };
 
-enum { MODE_PLAIN = 0, MODE_LN_IN = 1, MODE_LN_OUT = 2, MODE_LN_BWD = 3 };
+// MODE_ACC: MODE_PLAIN whose epilogue adds C's old value (the second half of a split-K product; a separate
+// instantiation: a runtime "add the old C" branch beside the output stores made the plain kernels wait for every
+// outstanding load before each store)
+enum { MODE_PLAIN = 0, MODE_LN_IN = 1, MODE_LN_OUT = 2, MODE_LN_BWD = 3, MODE_ACC = 4 };
 
-// k_sgemm_nt A-tile load map (compile-time A/B switch: make variant NAME=x EXTRA=-DNT_ROWLOAD=0): 1 = whole rows
-#ifndef NT_ROWLOAD
-#define NT_ROWLOAD 1
-#endif
 
 // h = LN(x) element: one expression shared by the prologue and the weight gradient's recompute (bitwise equal)
 __device__ __forceinline__ float ln_apply(float x, float m, float rs, float g, float b) {
     return __builtin_fmaf((x - m) * rs, g, b);
 }
 
+// sums over aligned lane groups (DPP / permlane swaps, common.cuh: no LDS round trips)
 template <int G>
-__device__ __forceinline__ float xsum(float x) {
-#pragma unroll
-    for (int o = 1; o < G; o <<= 1) x += __shfl_xor(x, o, 64);
-    return x;
-}
+__device__ __forceinline__ float xsum(float x) { return lane_sum<G>(x); }
 // sum over the four 16-lane groups of a wave (lanes l, l ^ 16, l ^ 32, l ^ 48: same MFMA output row)
-__device__ __forceinline__ float gsum4(float x) {
-    x += __shfl_xor(x, 16, 64);
-    return x + __shfl_xor(x, 32, 64);
-}
+__device__ __forceinline__ float gsum4(float x) { return rows_sum(x); }
 
 // Workgroup: NW waves; wave w owns columns [16 NSUB (NW blockIdx.y + w), +16 NSUB) and keeps their B planes
 // (NSUB x K/32 x P fragments) in registers.  A tile = BM rows x K; thread chunk = 8 consecutive k of one row.
@@ -278,49 +271,26 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
     int64_t tile = blockIdx.x;
     if (tile >= ntiles) return;   // uniform over the workgroup (the host launches at most ntiles workgroups)
 
-    // ---- staging: global -> registers (pf) -> planes in LDS
-    // NT_ROWLOAD: the workgroup's loads walk whole rows -- consecutive lanes take consecutive 16-byte pieces of a row
-    // (fp32: 32 lanes per 512-B row; bf16: 16 lanes per 256-B row), so one wave instruction reads 1 KB of contiguous
-    // lines; a fp32 float4 is half a fragment chunk and goes to LDS as an 8-byte half slot.  (0: the round-3 map, a
-    // lane loads a whole 8-k chunk and the 64 lanes of an instruction spread over 16 rows at half-line granularity.)
-    constexpr bool RL = NT_ROWLOAD != 0;
-    constexpr int C4 = BM * K / 4 / NT;   // fp32 float4 pieces per thread (= 2 CPT)
+    // ---- staging: global -> registers (pf) -> planes in LDS.  A lane loads one whole 8-k chunk (32 B) per piece;
+    // the 64 lanes of an instruction spread over 16 rows.  (A whole-row map -- 1 KB of contiguous lines per
+    // instruction, fp32 float4 pieces stored as half slots -- measured slower in the step: C2 fp32 6.84 vs 6.79 ms,
+    // dC 71 vs 67 us, profiles/r4i_*; the A tile is mostly cache-resident there, written by the kernel before.)
     float pf[ABF ? 1 : CPT][8];
     uint4 pb[ABF ? CPT : 1];
-    // (row in tile, 8-k chunk q, half h) of piece i: fp32 row loads (RL) walk float4 pieces, else whole chunks
-    auto piece = [&](int i, int& r, int& q, int& h) {
-        if constexpr (RL && !ABF) {
-            const int c = i * NT + threadIdx.x, c4 = c % (K / 4);
-            r = c / (K / 4); q = c4 >> 1; h = c4 & 1;
-        } else if constexpr (RL) {
-            const int c = i * NT + threadIdx.x;
-            r = c / QK; q = c % QK; h = 0;
-        } else {
-            const int c = i * NT + threadIdx.x;
-            const int rl = MODE == MODE_LN_IN ? (c >> 4) & 15 : c & 15;
-            q = MODE == MODE_LN_IN ? c & 15 : (c >> 4) % QK;
-            r = (MODE == MODE_LN_IN ? c >> 8 : (c >> 4) / QK) * 16 + rl;
-            h = 0;
-        }
-    };
-    constexpr int NPC = (RL && !ABF) ? C4 : CPT;   // pieces per thread
-    auto pf4 = [&](int i) -> float* { return (RL && !ABF) ? &pf[i >> 1][4 * (i & 1)] : pf[i]; };
     auto load = [&](int64_t t) {
 #pragma unroll
-        for (int i = 0; i < NPC; ++i) {
-            int r, q, h;
-            piece(i, r, q, h);
+        for (int i = 0; i < CPT; ++i) {
+            const int c = i * NT + threadIdx.x;
+            const int rl = MODE == MODE_LN_IN ? (c >> 4) & 15 : c & 15;
+            const int q = MODE == MODE_LN_IN ? c & 15 : (c >> 4) % QK;
+            const int rh = MODE == MODE_LN_IN ? c >> 8 : (c >> 4) / QK;
             // rows past M reload row M - 1: they only feed output rows that are never stored, and an unconditional
             // load needs no zero-filled destination (a conditional one made the compiler drain every store of the
             // previous tile -- s_waitcnt vmcnt(0) -- before this prefetch could issue)
-            const int64_t row0 = t * BM + r;
+            const int64_t row0 = t * BM + rh * 16 + rl;
             const int64_t row = row0 < g.M ? row0 : g.M - 1;
             if constexpr (ABF) {
                 pb[i] = *reinterpret_cast<const uint4*>((const uint16_t*)g.a + row * g.lda + 8 * q);
-            } else if constexpr (RL) {
-                const float4 v = *reinterpret_cast<const float4*>((const float*)g.a + row * g.lda + 8 * q + 4 * h);
-                float* d = pf4(i);
-                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
             } else {
                 float4 v0, v1;
                 {
@@ -333,55 +303,40 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
             }
         }
     };
-    auto stash_one = [&](uint4* buf, int64_t t, int i) {
-        constexpr int W = (RL && !ABF) ? 4 : 8;   // values per piece
-        {
-            int r, q, h;
-            piece(i, r, q, h);
-            const int rh = r >> 4, rl = r & 15;
-            const int e0 = ((q >> 2) * J + rh) * 64 + 16 * (q & 3) + (rl ^ ((q & 3) + 4 * ((q >> 2) & 3)));
-            float* v = pf4(i);
-            if constexpr (MODE == MODE_LN_IN) {   // the row's pieces sit in K / W consecutive lanes
-                constexpr int G = K / W;
-                float sm = 0.f;
+    auto stash = [&](uint4* buf, int64_t t) {
 #pragma unroll
-                for (int e = 0; e < W; ++e) sm += v[e];
-                const float mean = xsum<G>(sm) / (float)K;
+        for (int i = 0; i < CPT; ++i) {
+            const int c = i * NT + threadIdx.x;
+            const int rl = MODE == MODE_LN_IN ? (c >> 4) & 15 : c & 15;
+            const int q = MODE == MODE_LN_IN ? c & 15 : (c >> 4) % QK;
+            const int rh = MODE == MODE_LN_IN ? c >> 8 : (c >> 4) / QK;
+            const int e0 = ((q >> 2) * J + rh) * 64 + 16 * (q & 3) + (rl ^ ((q & 3) + 4 * ((q >> 2) & 3)));
+            if constexpr (MODE == MODE_LN_IN) {   // the 16 lanes of a DPP row hold the whole row
+                float sm = (pf[i][0] + pf[i][1]) + (pf[i][2] + pf[i][3]) + ((pf[i][4] + pf[i][5]) + (pf[i][6] + pf[i][7]));
+                const float mean = xsum<16>(sm) / (float)K;
                 float sq = 0.f;
 #pragma unroll
-                for (int e = 0; e < W; ++e) sq += (v[e] - mean) * (v[e] - mean);
-                const float rstd = 1.f / sqrtf(xsum<G>(sq) / (float)K + g.eps);
-                const int k0 = 8 * q + 4 * h;
+                for (int e = 0; e < 8; ++e) sq += (pf[i][e] - mean) * (pf[i][e] - mean);
+                const float rstd = 1.f / sqrtf(xsum<16>(sq) / (float)K + g.eps);
 #pragma unroll
-                for (int e = 0; e < W; ++e) v[e] = ln_apply(v[e], mean, rstd, lgb[k0 + e], lgb[K + k0 + e]);
-                const int64_t row = t * BM + r;
-                if (q == 0 && h == 0 && row < g.M) {
+                for (int e = 0; e < 8; ++e) pf[i][e] = ln_apply(pf[i][e], mean, rstd, lgb[8 * q + e], lgb[K + 8 * q + e]);
+                const int64_t row = t * BM + rh * 16 + rl;
+                if (q == 0 && row < g.M) {
                     g.mean[row] = mean;
                     g.rstd[row] = rstd;
                 }
             }
             if constexpr (ABF) {
                 buf[e0] = pb[i];
-            } else if constexpr (RL) {
-                uint32_t lo[P], hi[P];
-                split2<P>(v[0], v[1], lo);
-                split2<P>(v[2], v[3], hi);
-#pragma unroll
-                for (int p = 0; p < P; ++p)
-                    reinterpret_cast<uint2*>(buf + p * KK * J * 64 + e0)[h] = make_uint2(lo[p], hi[p]);
             } else {
                 uint32_t pl[4][P];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) split2<P>(v[2 * e], v[2 * e + 1], pl[e]);
+                for (int e = 0; e < 4; ++e) split2<P>(pf[i][2 * e], pf[i][2 * e + 1], pl[e]);
 #pragma unroll
                 for (int p = 0; p < P; ++p)
                     buf[p * KK * J * 64 + e0] = make_uint4(pl[0][p], pl[1][p], pl[2][p], pl[3][p]);
             }
         }
-    };
-    auto stash = [&](uint4* buf, int64_t t) {
-#pragma unroll
-        for (int i = 0; i < NPC; ++i) stash_one(buf, t, i);
     };
 
     // fragment slot of this lane in a 64-entry block of k-block kk (the swizzle of stash)
@@ -426,16 +381,37 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
         for (int j = 0; j < J; ++j)
 #pragma unroll
             for (int s = 0; s < NSUB; ++s) acc[j][s] = bias[s];
+        if constexpr (P == 1) {
+            // one plane: a fragment feeds only NSUB MFMAs, so the fragments of k-block kk + 1 are read while kk's
+            // MFMAs run (otherwise every read's LDS latency sits in front of its 1-3 MFMAs)
+            bf16x8 af[2][J];
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
+            for (int j = 0; j < J; ++j) af[0][j] = __builtin_bit_cast(bf16x8, buf[j * 64 + rslot[0]]);
 #pragma unroll
-            for (int j = 0; j < J; ++j) {
-                bf16x8 a[P];
+            for (int kk = 0; kk < KK; ++kk) {
+                if (kk + 1 < KK) {
 #pragma unroll
-                for (int p = 0; p < P; ++p)
-                    a[p] = __builtin_bit_cast(bf16x8, buf[((p * KK + kk) * J + j) * 64 + rslot[kk & 3]]);
+                    for (int j = 0; j < J; ++j)
+                        af[(kk + 1) & 1][j] = __builtin_bit_cast(bf16x8, buf[((kk + 1) * J + j) * 64 + rslot[(kk + 1) & 3]]);
+                }
+                __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs (the scheduler sinks them)
 #pragma unroll
-                for (int s = 0; s < NSUB; ++s) acc[j][s] = mfma_planes<P>(wr[s][kk], a, acc[j][s]);
+                for (int j = 0; j < J; ++j)
+#pragma unroll
+                    for (int s = 0; s < NSUB; ++s) acc[j][s] = mfma(wr[s][kk][0], af[kk & 1][j], acc[j][s]);
+            }
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) {
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    bf16x8 a[P];
+#pragma unroll
+                    for (int p = 0; p < P; ++p)
+                        a[p] = __builtin_bit_cast(bf16x8, buf[((p * KK + kk) * J + j) * 64 + rslot[kk & 3]]);
+#pragma unroll
+                    for (int s = 0; s < NSUB; ++s) acc[j][s] = mfma_planes<P>(wr[s][kk], a, acc[j][s]);
+                }
             }
         }
         // stage the next tile first: its loads were issued before this tile's MFMAs, and waiting for them after
@@ -609,9 +585,7 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
                 for (int s = 0; s < NSUB; ++s) {
                     const int64_t off = row * g.ldc + (nsub0 + s) * 16 + 4 * (lane >> 4);
                     f32x4 v = acc[j][s];
-                    if constexpr (!CBF && MODE == MODE_PLAIN) {
-                        if (g.accum) v += *reinterpret_cast<const f32x4*>((const float*)g.c + off);
-                    }
+                    if constexpr (MODE == MODE_ACC) v += *reinterpret_cast<const f32x4*>((const float*)g.c + off);
                     if constexpr (CBF) {
                         *reinterpret_cast<uint2*>((uint16_t*)g.c + off) = make_uint2(pk_bf16(v[0], v[1]),
                                                                                      pk_bf16(v[2], v[3]));
@@ -1172,7 +1146,7 @@ constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
     nt_cfg<128, 3, 8, 32, 3, false, false>(384, 1), nt_cfg<128, 1, 8, 32, 3, false, false>(128, 2),            \
     nt_cfg<384, 1, 8, 32, 3, false, false>(128, 1),                                                            \
     nt_cfg<256, 1, 8, 32, 3, false, false>(768, 1), nt_cfg<256, 1, 8, 32, 3, false, false>(256, 1),            \
-    nt_cfg<384, 1, 8, 32, 3, false, false>(256, 1),                                                            \
+    nt_cfg<384, 1, 8, 32, 3, false, false>(256, 1), nt_cfg<384, 1, 8, 32, 3, false, false, MODE_ACC>(256, 1),   \
     nt_cfg<64, 3, 4, 32, 3, false, false>(192, 1), nt_cfg<64, 1, 4, 32, 3, false, false>(64, 2),               \
     nt_cfg<192, 1, 4, 32, 3, false, false>(64, 2)
 #define NT_SET1(ABF, CBF)                                                                                    \
@@ -1324,11 +1298,12 @@ bool lds_ok(const void* fn, size_t lds) {
     return true;
 }
 
-// split-K form of a plain fp32-output product without a kernel of its own: two K / 2 halves, the second accumulating
-// into C (K = 768 three-plane: the H = 256 QKV input gradient)
-const NtCfg* nt_find_half(int K, int N, int P, int abf, int cbf) {
+// split-K form of a plain fp32-output product without a kernel of its own: two K / 2 halves, the second (MODE_ACC)
+// accumulating into C (K = 768 three-plane: the H = 256 QKV input gradient)
+const NtCfg* nt_find_half(int K, int N, int P, int abf, int cbf, int mode = MODE_PLAIN) {
     if (cbf || K % 64 != 0 || nt_find(K, N, P, abf, cbf)) return nullptr;
-    return nt_find(K / 2, N, P, abf, cbf);
+    if (!nt_find(K / 2, N, P, abf, cbf, MODE_ACC)) return nullptr;
+    return nt_find(K / 2, N, P, abf, cbf, mode);
 }
 
 }  // namespace
@@ -1404,8 +1379,8 @@ extern "C" int tagan_sgemm_nt(int32_t a_dtype, int32_t c_dtype, int64_t M, int32
         g.a = (const char*)a + (size_t)(K / 2) * es;
         g.bias = nullptr;
         g.kk0 = K / 64;
-        g.accum = 1;
-        return nt_launch(half, g, N, stream, "tagan_sgemm_nt (second K half)");
+        return nt_launch(nt_find_half(K, N, planes, a_dtype == TAGAN_BF16, 0, MODE_ACC), g, N, stream,
+                         "tagan_sgemm_nt (second K half)");
     }
     return nt_launch(cfg, g, N, stream, "tagan_sgemm_nt");
 }

@@ -1112,8 +1112,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_F) k_tattn_fwd_v4(TArgs A, 
                     s[jt][it][e] = sc;
                     mx = fmaxf(mx, sc);
                 }
-            mx = fmaxf(mx, __shfl_xor(mx, 16, WAVE));
-            mx = fmaxf(mx, __shfl_xor(mx, 32, WAVE));
+            mx = rows_max(mx);
             float l = 0.f;
 #pragma unroll
             for (int jt = 0; jt < TT; ++jt)
@@ -1124,8 +1123,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_F) k_tattn_fwd_v4(TArgs A, 
                     l += p;
                     s[jt][it][e] = p * drop_scale(A, drk, i, jt * 16 + 4 * g + e);
                 }
-            l += __shfl_xor(l, 16, WAVE);
-            l += __shfl_xor(l, 32, WAVE);
+            l = rows_sum(l);
             inv_l[it] = (l > 0.f) ? 1.f / l : NAN;
             if (g == 0 && i < T) A.lse[(r * A.heads + h) * T + i] = mx + __logf(l);
         }
@@ -1297,8 +1295,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
                         dp[jt][it][e] = dpv;
                         dl = fmaf(p, dpv, dl);
                     }
-                dl += __shfl_xor(dl, 16, WAVE);
-                dl += __shfl_xor(dl, 32, WAVE);
+                dl = rows_sum(dl);
 #pragma unroll
                 for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
@@ -1327,8 +1324,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
                     dp[jt][it][e] *= m;
                     dl = fmaf(p, dp[jt][it][e], dl);
                 }
-            dl += __shfl_xor(dl, 16, WAVE);
-            dl += __shfl_xor(dl, 32, WAVE);
+            dl = rows_sum(dl);
 #pragma unroll
             for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
@@ -1451,10 +1447,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     float v = bsum[t3][dt][e];
-                    v += __shfl_xor(v, 1, WAVE);
-                    v += __shfl_xor(v, 2, WAVE);
-                    v += __shfl_xor(v, 4, WAVE);
-                    v += __shfl_xor(v, 8, WAVE);
+                    v = lane_sum<16>(v);
                     if (c0 == 0) prow[t3 * (int64_t)A.H + dt * 16 + 4 * g0 + e] = v;
                 }
     }
@@ -1603,8 +1596,7 @@ __global__ void __launch_bounds__(WAVE * GH, TAGAN_V6_WPE) k_tattn_fwd_v6(TArgs 
                     s[jt][it][e] = sc;
                     mx = fmaxf(mx, sc);
                 }
-            mx = fmaxf(mx, __shfl_xor(mx, 16, WAVE));
-            mx = fmaxf(mx, __shfl_xor(mx, 32, WAVE));
+            mx = rows_max(mx);
             float l = 0.f;
 #pragma unroll
             for (int jt = 0; jt < TT; ++jt)
@@ -1615,8 +1607,7 @@ __global__ void __launch_bounds__(WAVE * GH, TAGAN_V6_WPE) k_tattn_fwd_v6(TArgs 
                     l += p;
                     s[jt][it][e] = p * drop_scale(A, drk, i, jt * 16 + 4 * g + e);
                 }
-            l += __shfl_xor(l, 16, WAVE);
-            l += __shfl_xor(l, 32, WAVE);
+            l = rows_sum(l);
             inv_l[it] = (l > 0.f) ? 1.f / l : NAN;
             if (g == 0 && i < T) A.lse[(r * A.heads + h) * T + i] = mx + __logf(l);
         }
@@ -1783,8 +1774,7 @@ __global__ void __launch_bounds__(WAVE * GH, (TT == 2 && DT == 2) ? 2 : TAGAN_V6
                     dp[jt][it][e] *= m;
                     dl = fmaf(p, dp[jt][it][e], dl);
                 }
-            dl += __shfl_xor(dl, 16, WAVE);
-            dl += __shfl_xor(dl, 32, WAVE);
+            dl = rows_sum(dl);
 #pragma unroll
             for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
@@ -1902,10 +1892,7 @@ __global__ void __launch_bounds__(WAVE * GH, (TT == 2 && DT == 2) ? 2 : TAGAN_V6
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     float v = bsum[t3][dt][e];
-                    v += __shfl_xor(v, 1, WAVE);
-                    v += __shfl_xor(v, 2, WAVE);
-                    v += __shfl_xor(v, 4, WAVE);
-                    v += __shfl_xor(v, 8, WAVE);
+                    v = lane_sum<16>(v);
                     if (c0 == 0) prow[t3 * (int64_t)A.H + dt * 16 + 4 * g0 + e] = v;
                 }
     }
@@ -2066,8 +2053,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
                     s[jt][e] = sc;
                     mx = fmaxf(mx, sc);
                 }
-            mx = fmaxf(mx, __shfl_xor(mx, 16, WAVE));
-            mx = fmaxf(mx, __shfl_xor(mx, 32, WAVE));
+            mx = rows_max(mx);
             const uint32_t cb = (uint32_t)(i * T + 4 * g);   // dropout counter of element (jt, e): cb + 16 jt + e
             float l = 0.f;
             auto soft = [&](int jt) {
@@ -2098,8 +2084,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
-            l += __shfl_xor(l, 16, WAVE);
-            l += __shfl_xor(l, 32, WAVE);
+            l = rows_sum(l);
             inv_l = (MODE == 2 ? A.inv_keep : 1.f) / l;
             if (g == 0) A.lse[(r * A.heads + h) * T + i] = (mx + __log2f(l)) * LN2_F;
         } else {
@@ -2119,8 +2104,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
                 s[jt][e] = sc;
                 mx = fmaxf(mx, sc);
             }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, WAVE));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, WAVE));
+        mx = rows_max(mx);
         float l = 0.f;
 #pragma unroll
         for (int jt = 0; jt < TT; ++jt)
@@ -2131,8 +2115,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
                 l += p;
                 s[jt][e] = p * drop_scale(A, drk, i, jt * 16 + 4 * g + e);
             }
-        l += __shfl_xor(l, 16, WAVE);
-        l += __shfl_xor(l, 32, WAVE);
+        l = rows_sum(l);
         inv_l = (l > 0.f) ? 1.f / l : NAN;
         if (g == 0 && i < T) A.lse[(r * A.heads + h) * T + i] = mx + __logf(l);
 #pragma unroll
@@ -2272,8 +2255,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
                     dp[jt][e] = dpv;
                     dl = fmaf(p, dpv, dl);
                 }
-            dl += __shfl_xor(dl, 16, WAVE);
-            dl += __shfl_xor(dl, 32, WAVE);
+            dl = rows_sum(dl);
 #pragma unroll
             for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
@@ -2306,8 +2288,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
                 dp[jt][e] *= m;
                 dl = fmaf(p, dp[jt][e], dl);
             }
-        dl += __shfl_xor(dl, 16, WAVE);
-        dl += __shfl_xor(dl, 32, WAVE);
+        dl = rows_sum(dl);
 #pragma unroll
         for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
@@ -2392,10 +2373,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     float x = bsum[t3][dt][e];
-                    x += __shfl_xor(x, 1, WAVE);
-                    x += __shfl_xor(x, 2, WAVE);
-                    x += __shfl_xor(x, 4, WAVE);
-                    x += __shfl_xor(x, 8, WAVE);
+                    x = lane_sum<16>(x);
                     if (c0 == 0) red[w * 3 * DP + t3 * DP + dt * 16 + 4 * g0 + e] = x;
                 }
         __syncthreads();
