@@ -224,7 +224,10 @@ int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t head
  *        mask[r*mask_bstride + h*mask_hstride + i*T + j]; causal != 0 adds j<=i.
  *   out: element (r,t,f) at out[r*o_row + t*o_t + f];  lse: [rows, heads, T].
  *   attn (optional): [rows, heads, T, T] post-dropout weights.
- * Dropout layout: stream = r*heads + h, counter = i*T + j.
+ * Dropout layout: key = the mixed (seed, stream = r*heads + h), counter c = i*T + j; one
+ * lowbias32((c >> 1) ^ key) decides the pair {c & ~1, c | 1}: bits 0-15 the even counter, bits 16-31
+ * the odd one, kept iff that half >= ceil(p * 65536) (drop probability within 2^-16 of p), kept
+ * weights scaled by 1 / (1 - p).
  * ------------------------------------------------------------------------- */
 int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim,
                             const void* q, const void* k, const void* v, int64_t s_row, int64_t s_t,
@@ -233,6 +236,25 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
                             float p_drop, uint64_t seed,
                             void* out, int64_t o_row, int64_t o_t,
                             float* lse, float* attn, void* stream);
+
+/* Dropout keep-bit cache (the matrix-core path for T in (32, 128], T a multiple of 16, head_dim 16/32, no mask,
+ * causal or dense bias, p_drop > 0): the forward can store every element's keep decision as one bit, and the
+ * backward reads them instead of re-evaluating the counter hash (the same bits: the hash decides them once).
+ * tagan_temporal_attn_keep_bytes returns the bytes such a forward writes, 0 where no path uses the cache.
+ * tagan_temporal_attn_fwd_keep = tagan_temporal_attn_fwd + keep (device, keep_bytes) and *keep_written (host,
+ * may be NULL): 1 iff this call wrote the bits.  Pass keep to tagan_temporal_attn_bwd_keep ONLY when the
+ * matching forward reported keep_written = 1 (same shapes, strides, seed and kernel-selection environment);
+ * otherwise pass NULL, which is tagan_temporal_attn_bwd. */
+size_t tagan_temporal_attn_keep_bytes(int64_t rows, int32_t T, int32_t heads, int32_t head_dim, int causal,
+                                      int has_mask, int has_bias_dense, float p_drop);
+int tagan_temporal_attn_fwd_keep(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim,
+                                 const void* q, const void* k, const void* v, int64_t s_row, int64_t s_t,
+                                 const float* bias_table, const float* bias_dense, int64_t bias_bstride,
+                                 const uint8_t* mask, int64_t mask_bstride, int64_t mask_hstride, int causal,
+                                 float p_drop, uint64_t seed,
+                                 void* out, int64_t o_row, int64_t o_t,
+                                 float* lse, float* attn, uint32_t* keep, size_t keep_bytes, int32_t* keep_written,
+                                 void* stream);
 
 /* Backward.  dbias_table: [heads, 2T-1] (reduced over rows, deterministic) or NULL.
  * dbias_dense: [rows, heads, T, T] per-row score gradients (caller reduces a
@@ -252,6 +274,17 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
                             void* dq, void* dk, void* dv, int64_t d_row, int64_t d_t,
                             float* dbias_table, float* dbias_dense, float* dsum_qkv,
                             void* workspace, size_t workspace_bytes, void* stream);
+int tagan_temporal_attn_bwd_keep(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim,
+                                 const void* q, const void* k, const void* v, int64_t s_row, int64_t s_t,
+                                 const float* bias_table, const float* bias_dense, int64_t bias_bstride,
+                                 const uint8_t* mask, int64_t mask_bstride, int64_t mask_hstride, int causal,
+                                 float p_drop, uint64_t seed,
+                                 const void* out, int64_t o_row, int64_t o_t, const float* lse,
+                                 const void* dout, int64_t do_row, int64_t do_t,
+                                 void* dq, void* dk, void* dv, int64_t d_row, int64_t d_t,
+                                 float* dbias_table, float* dbias_dense, float* dsum_qkv,
+                                 const uint32_t* keep, size_t keep_bytes,
+                                 void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Row LayerNorm with fused residual + dropout.  Replaces the ATen chain

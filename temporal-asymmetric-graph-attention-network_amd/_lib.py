@@ -66,6 +66,14 @@ _SIGNATURES = {
     "tagan_temporal_attn_fwd": (_c.c_int, [_c.c_int, _i64, _i32, _i32, _i32, _p, _p, _p, _i64, _i64, _p, _p,
                                            _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,
                                            _p]),
+    "tagan_temporal_attn_keep_bytes": (_sz, [_i64, _i32, _i32, _i32, _c.c_int, _c.c_int, _c.c_int, _f32]),
+    "tagan_temporal_attn_fwd_keep": (_c.c_int, [_c.c_int, _i64, _i32, _i32, _i32, _p, _p, _p, _i64, _i64, _p, _p,
+                                                _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,
+                                                _p, _sz, _p, _p]),
+    "tagan_temporal_attn_bwd_keep": (_c.c_int, [_c.c_int, _i64, _i32, _i32, _i32, _p, _p, _p, _i64, _i64, _p, _p,
+                                                _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,
+                                                _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p, _p, _sz, _p, _sz,
+                                                _p]),
     "tagan_temporal_attn_bwd_workspace": (_sz, [_i64, _i32, _i32, _i32]),
     "tagan_temporal_attn_bwd": (_c.c_int, [_c.c_int, _i64, _i32, _i32, _i32, _p, _p, _p, _i64, _i64, _p, _p,
                                            _i64, _p, _i64, _i64, _c.c_int, _f32, _u64, _p, _i64, _i64, _p, _p,

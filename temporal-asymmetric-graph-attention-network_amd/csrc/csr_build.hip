@@ -859,8 +859,9 @@ __device__ void csr_bucket(const Geo& g, int64_t b, uint32_t* A, uint32_t* B, bo
 }
 
 // the buckets too large for the small finish kernels (CSR: raw keys + self-loops > CAP_S; CSC: pairs > CAP_C), listed
-// before the finish so the big-bucket kernel runs on a side stream beside the small one (their buckets are disjoint;
-// the list order is irrelevant: every bucket's output depends on the bucket alone)
+// before the finish so the big-bucket kernel's workgroups take them straight from the list (the list order is
+// irrelevant: every bucket's output depends on the bucket alone).  Running that kernel on a side stream beside the
+// small-bucket one was measured slower in the step (profiles/r4k_csr_side_ab.txt) and removed.
 template <bool CSC>
 __global__ void __launch_bounds__(BLK) k_big_list(Geo g, const int32_t* __restrict__ fill, int32_t* __restrict__ big,
                                                   int32_t* __restrict__ nbig) {
@@ -1172,29 +1173,6 @@ CsrWs plan(const Geo& g) {
     return w;
 }
 
-// The side stream of the big-bucket kernels (one per device, created on first use) and the fork / join events:
-// record on the caller's stream -> the side stream waits -> big kernel there -> record -> the caller waits before the
-// scan that reads both kernels' outputs.  Under HIP-graph capture the two waits make the side launch a parallel
-// branch of the captured graph.
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-SideStream* side_stream() {
-    static SideStream ss[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    SideStream& x = ss[dev];
-    if (!x.s) {
-        if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) {
-            x.s = nullptr;
-            return nullptr;
-        }
-    }
-    return &x;
-}
 
 }  // namespace
 }  // namespace tagan
@@ -1279,19 +1257,13 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
             TAGAN_CHECK_LAUNCH("csr_build.refine");
         }
     }
-    SideStream* side = side_stream();
-    TAGAN_REQUIRE(side, TAGAN_ERR_LAUNCH, "tagan_csr_build: cannot create the side stream");
     k_big_list<false><<<grid_for(g.NB), BLK, 0, s>>>(g, fill_src, big_src, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.big_list");
-    TAGAN_REQUIRE(hipEventRecord(side->fork, s) == hipSuccess && hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess,
-                  TAGAN_ERR_LAUNCH, "tagan_csr_build: fork");
-    k_csr_finish_big<<<BIG_WG, BNT, BIG_LDS, side->s>>>(g, cap_src, fill_src, node_ptr, keys, stage, sloc, rowptr, ucnt,
+    k_csr_finish_big<<<BIG_WG, BNT, BIG_LDS, s>>>(g, cap_src, fill_src, node_ptr, keys, stage, sloc, rowptr, ucnt,
                                                         big_src, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.csr_finish_big");
     k_csr_finish<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_src, fill_src, node_ptr, keys, rowptr, ucnt, big_src, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.csr_finish");
-    TAGAN_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess && hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
-                  TAGAN_ERR_LAUNCH, "tagan_csr_build: join");
     scan::exclusive(ucnt, ucnt, g.NB, (int32_t)0, plus, part, true, s);           // -> CSR bucket offsets
     TAGAN_CHECK_LAUNCH("csr_build.scan_unique");
     k_csr_place<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_src, ucnt, node_ptr, keys, rowptr, col, sloc, nnz_out);
@@ -1309,16 +1281,12 @@ int tagan_csr_build(const int64_t* edge_index, int64_t ld_ei, int64_t n_edges, c
     TAGAN_CHECK_LAUNCH("csr_build.scan_csc");
     k_big_list<true><<<grid_for(g.NB), BLK, 0, s>>>(g, fill_dst, big_dst, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.big_list_csc");
-    TAGAN_REQUIRE(hipEventRecord(side->fork, s) == hipSuccess && hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess,
-                  TAGAN_ERR_LAUNCH, "tagan_csr_build: fork (CSC)");
-    k_csc_finish_big<<<BIG_WG, BNT, BIG_LDS, side->s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, stage,
+    k_csc_finish_big<<<BIG_WG, BNT, BIG_LDS, s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, stage,
                                                         sval, sloc, csc_ptr, csc_row, csc_eid, csr_cpos, big_dst, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.csc_finish_big");
     k_csc_finish<<<(unsigned)g.NB, FNT, 0, s>>>(g, cap_dst, fill_dst, coff, node_ptr, keys, cval, csc_ptr,
                                                 csc_row, csc_eid, csr_cpos, big_dst, nbig);
     TAGAN_CHECK_LAUNCH("csr_build.csc_finish");
-    TAGAN_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess && hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
-                  TAGAN_ERR_LAUNCH, "tagan_csr_build: join (CSC)");
     return TAGAN_OK;
 }
 

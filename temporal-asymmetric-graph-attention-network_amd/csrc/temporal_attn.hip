@@ -60,6 +60,7 @@ struct TArgs {
     float* dbias_dense;
     float* part;   // [gridDim.x, heads, 2T-1] block partials of dbias_table
     float* qkv_part;   // v4: [row groups, 3H] partial column sums of dq | dk | dv (QKV bias gradient)
+    uint32_t* keep;    // v5 MODE 3: the dropout keep bits, one word per (row, head, wave, lane); fwd writes, bwd reads
 };
 
 __device__ __forceinline__ bool keep_ij(const TArgs& A, int64_t r, int h, int i, int j) {
@@ -79,10 +80,20 @@ __device__ __forceinline__ uint32_t tkey(const TArgs& A, int64_t r, int h) {
     return A.p_drop > 0.f ? drop_key(A.seed, (uint64_t)r * A.heads + h) : 0u;
 }
 
-// dropout stream = r*heads + h, counter = i*T + j
+// Attention dropout: stream = r*heads + h (the key), counter c = i*T + j.  One lowbias32 of (c >> 1) ^ key decides
+// the counter pair {2m, 2m + 1}: its low 16 bits the even counter, its high 16 bits the odd one; kept iff that half
+// >= tthr(p) = ceil(p 2^16) -- drop probability tthr / 2^16, within 2^-16 of p.  (A matrix-core lane's four
+// elements j = 16 jt + 4g + e are two such pairs: two hashes per four elements.)
+__host__ __device__ __forceinline__ uint32_t tthr(float p) { return (uint32_t)ceilf(p * 65536.f); }
+template <int E>   // half E & 1 of the pair word
+__device__ __forceinline__ uint32_t thalf(uint32_t w) { return (E & 1) ? (w >> 16) : (w & 0xFFFFu); }
+__device__ __forceinline__ bool tkeep(uint32_t key, uint32_t c, uint32_t thr) {
+    const uint32_t w = lowbias32((c >> 1) ^ key);
+    return ((c & 1u) ? (w >> 16) : (w & 0xFFFFu)) >= thr;
+}
 __device__ __forceinline__ float drop_scale(const TArgs& A, uint32_t key, int i, int j) {
     if (A.p_drop <= 0.f) return 1.f;
-    return drop_u(key, (uint32_t)(i * A.T + j)) >= A.p_drop ? A.inv_keep : 0.f;
+    return tkeep(key, (uint32_t)(i * A.T + j), tthr(A.p_drop)) ? A.inv_keep : 0.f;
 }
 
 template <int D>
@@ -947,25 +958,40 @@ constexpr int v4_ld(int TP) { return TP + 8; }
 size_t v4_fwd_lds(int TT, int DT) { return (size_t)(16 * DT * v4_ld(16 * TT)) * 4; }
 size_t v4_bwd_lds(int TT, int DT) { return (size_t)(16 * TT * v4_ld(16 * TT) + 3 * 16 * DT * v4_ld(16 * TT)) * 4; }
 
-// Fast path (MODE 1: no dropout, 2: dropout) for the common shape: T = TP, no causal flag, no keep-mask, no dense
-// bias (or dense-bias gradient).  Every element is then valid, so the per-element range / mask tests go; the
-// scores are kept in log2 units (log2 e folded into the 1/sqrt(d) scale and the staged bias table: one v_exp_f32
-// per element, no separate multiply); the dropout test is one integer compare of the element's hash against a
-// precomputed threshold -- the same decision as drop_u(...) >= p, bit for bit; the backward carries the keep bit
-// in the sign of the stored probability.  MODE 0 is the general path.
+// Fast path (MODE 1: no dropout, 2: dropout, 3: dropout with the keep-bit cache of v5) for the common shape:
+// T = TP, no causal flag, no keep-mask, no dense bias (or dense-bias gradient).  Every element is then valid, so the
+// per-element range / mask tests go; the scores are kept in log2 units (log2 e folded into the 1/sqrt(d) scale and
+// the staged bias table: one v_exp_f32 per element, no separate multiply); the dropout test is one integer compare
+// of the element's pair-word half against tthr(p) (two hashes per four elements) -- the same decision as
+// drop_scale, bit for bit; the backward carries the keep bit in the sign of the stored probability.  MODE 0 is the
+// general path.
 constexpr float LOG2E_F = 1.4426950408889634f;
 constexpr float LN2_F = 0.6931471805599453f;
 
-// keep an element iff lowbias32(counter ^ key) >= drop_thr(p): (h >> 8) * 2^-24 >= p  <=>  (h >> 8) >= ceil(p 2^24)
-// (exact: p 2^24 is exact in fp32).  Valid for p < 1 - 2^-24 (the host takes MODE 0 otherwise).
-__host__ __device__ __forceinline__ uint32_t drop_thr(float p) {
-    return ((uint32_t)ceilf(p * 16777216.f)) << 8;
-}
-
 bool v5_fast_shape(int T, int TT, int causal, const void* mask, const void* bias_dense, const void* dbias_dense,
                    float p_drop) {
-    return T == 16 * TT && !causal && !mask && !bias_dense && !dbias_dense &&
-           (p_drop <= 0.f || ceilf(p_drop * 16777216.f) < 16777216.f);
+    return T == 16 * TT && !causal && !mask && !bias_dense && !dbias_dense && (p_drop <= 0.f || tthr(p_drop) < 65536u);
+}
+
+// the keep decisions of the lane's four elements of key tile jt (counters cb + 16 jt + e, cb even): two pair words
+__device__ __forceinline__ void tpair(uint32_t key, uint32_t cb, int jt, uint32_t (&w)[2]) {
+    const uint32_t m = (cb + (uint32_t)(jt * 16)) >> 1;
+    w[0] = lowbias32(m ^ key);
+    w[1] = lowbias32((m + 1u) ^ key);
+}
+// all ones iff element e of the pair words is kept (half >= thr, thr1 = thr - 1 >= 0), else 0: arithmetic (no
+// lane-mask compares, whose masks the compiler otherwise keeps live in SGPRs and spills)
+template <int E>
+__device__ __forceinline__ uint32_t tkeepmask(const uint32_t (&w)[2], uint32_t thr1) {
+    const uint32_t half = (E & 1) ? (w[E >> 1] >> 16) : (w[E >> 1] & 0xFFFFu);
+    return (uint32_t)((int32_t)(thr1 - half) >> 31);
+}
+// the keep-bit cache: all ones iff bit b of the word is set
+__device__ __forceinline__ uint32_t tbitmask(uint32_t kw, int b) { return (uint32_t)((int32_t)(kw << (31 - b)) >> 31); }
+__device__ __forceinline__ float fand(float x, uint32_t m) { return __uint_as_float(__float_as_uint(x) & m); }
+// +p where kept, -p where dropped (the backward's keep bit in the sign of P)
+__device__ __forceinline__ float fsignkeep(float p, uint32_t m) {
+    return __uint_as_float(__float_as_uint(p) ^ (~m & 0x80000000u));
 }
 
 // The unit-invariant part of the score of the lane's elements (i = it*16 + c, j = jt*16 + 4g + e):
@@ -1176,7 +1202,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
     if constexpr (MODE != 0) v4_fast_bias<TT>(A, h, c0, g0, bst);
     else v4_static_bias<TT>(A, h, c0, g0, bst);
     const float msc = A.p_drop > 0.f ? A.inv_keep : 1.f;   // drop_scale of a kept element
-    const uint32_t thr = MODE == 2 ? drop_thr(A.p_drop) : 0u;
+    const uint32_t thr = MODE == 2 ? tthr(A.p_drop) : 0u;
     // Σ of dSᵀ over this wave's units, in unit order: the bias-table gradient before its diagonal
     // sums, which run once at the end (fixed order: bitwise reproducible)
     f4v gsum[TT][TT];
@@ -1280,21 +1306,28 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
                 const uint32_t cb = (uint32_t)(i * T + 4 * g);
                 float dl = 0.f;
 #pragma unroll
-                for (int jt = 0; jt < TT; ++jt)
+                for (int jt = 0; jt < TT; ++jt) {
+                    uint32_t pw[2] = {0u, 0u};
+                    if constexpr (MODE == 2) tpair(drk, cb, jt, pw);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const float p = __builtin_amdgcn_exp2f(fmaf(s[jt][it][e], sc2, bst[jt][it][e]) - lse2);
                         float dpv = dp[jt][it][e];
                         if constexpr (MODE == 2) {
-                            const bool kp = lowbias32((cb + (uint32_t)(jt * 16 + e)) ^ drk) >= thr;
-                            dpv = kp ? dpv * msc : 0.f;
-                            s[jt][it][e] = kp ? p : -p;
+                            uint32_t km;
+                            if (e == 0) km = tkeepmask<0>(pw, thr - 1u);
+                            else if (e == 1) km = tkeepmask<1>(pw, thr - 1u);
+                            else if (e == 2) km = tkeepmask<2>(pw, thr - 1u);
+                            else km = tkeepmask<3>(pw, thr - 1u);
+                            dpv = fand(dpv * msc, km);
+                            s[jt][it][e] = fsignkeep(p, km);
                         } else {
                             s[jt][it][e] = p;
                         }
                         dp[jt][it][e] = dpv;
                         dl = fmaf(p, dpv, dl);
                     }
+                }
                 dl = rows_sum(dl);
 #pragma unroll
                 for (int jt = 0; jt < TT; ++jt)
@@ -1930,6 +1963,9 @@ __global__ void __launch_bounds__(WAVE * GH, (TT == 2 && DT == 2) ? 2 : TAGAN_V6
 // dwords (m = DP/4 + 2 = 6 or 10, i.e. m = 2 mod 4) the 16-lane groups of ds_read_b128 hit distinct bank slots
 // (the same argument as v4_ld).
 constexpr int v5_lk(int DP) { return DP + 8; }
+#ifndef TAGAN_V5B_IL
+#define TAGAN_V5B_IL 1   // 0: the fast-path backward without the software pipelining of phase 1 (A/B builds)
+#endif
 size_t v5_fwd_lds(int TT, int DT) { return (size_t)(16 * TT * v5_lk(16 * DT) + 16 * DT * v4_ld(16 * TT) + 32 * TT) * 4; }
 size_t v5_bwd_lds(int TT, int DT) {
     const int TP = 16 * TT, DP = 16 * DT;
@@ -1995,7 +2031,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
     } else {
         for (int t = threadIdx.x; t < 2 * T - 1; t += WAVE * TT) Bt[t] = A.bias_table ? A.bias_table[h * (2 * T - 1) + t] : 0.f;
     }
-    const uint32_t thr = MODE == 2 ? drop_thr(A.p_drop) : 0u;
+    const uint32_t thr = MODE >= 2 ? tthr(A.p_drop) : 0u;
     f4v qv[DT], kv[DT], vv[DT];
     auto load = [&](int64_t rr) {
         const int i = w * 16 + c0;
@@ -2056,12 +2092,25 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
             mx = rows_max(mx);
             const uint32_t cb = (uint32_t)(i * T + 4 * g);   // dropout counter of element (jt, e): cb + 16 jt + e
             float l = 0.f;
+            uint32_t kw = 0;   // MODE 3: keep bit of element (jt, e) at bit 4 jt + e, for the backward
             auto soft = [&](int jt) {
+                uint32_t pw[2] = {0u, 0u};
+                if constexpr (MODE >= 2) tpair(drk, cb, jt, pw);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const float p = __builtin_amdgcn_exp2f(s[jt][e] - mx);
                     l += p;
-                    s[jt][e] = (MODE == 2 && lowbias32((cb + (uint32_t)(jt * 16 + e)) ^ drk) < thr) ? 0.f : p;
+                    if constexpr (MODE >= 2) {
+                        uint32_t km;
+                        if (e == 0) km = tkeepmask<0>(pw, thr - 1u);
+                        else if (e == 1) km = tkeepmask<1>(pw, thr - 1u);
+                        else if (e == 2) km = tkeepmask<2>(pw, thr - 1u);
+                        else km = tkeepmask<3>(pw, thr - 1u);
+                        if constexpr (MODE == 3) kw |= km & (1u << (jt * 4 + e));
+                        s[jt][e] = fand(p, km);
+                    } else {
+                        s[jt][e] = p;
+                    }
                 }
             };
             // Oᵀ = Vᵀ·P'ᵀ: the products of key tile jt issued between the softmax instructions of tile jt+1
@@ -2085,8 +2134,9 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
                 __builtin_amdgcn_sched_barrier(0);
             }
             l = rows_sum(l);
-            inv_l = (MODE == 2 ? A.inv_keep : 1.f) / l;
+            inv_l = (MODE >= 2 ? A.inv_keep : 1.f) / l;
             if (g == 0) A.lse[(r * A.heads + h) * T + i] = (mx + __log2f(l)) * LN2_F;
+            if constexpr (MODE == 3) A.keep[((r * A.heads + h) * TT + w) * WAVE + lane] = kw;
         } else {
         float mx = -INFINITY;
 #pragma unroll
@@ -2171,7 +2221,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
         // (visible to all waves after the first unit's staging barrier)
     }
     const float msc = A.p_drop > 0.f ? A.inv_keep : 1.f;
-    const uint32_t thr = MODE == 2 ? drop_thr(A.p_drop) : 0u;
+    const uint32_t thr = MODE >= 2 ? tthr(A.p_drop) : 0u;
     f4v gsum[TT];   // Σ over units of dSᵀ[jt tiles][query tile w]: the bias-table gradient before its diagonal sums
 #pragma unroll
     for (int jt = 0; jt < TT; ++jt) gsum[jt] = f4v{0.f, 0.f, 0.f, 0.f};
@@ -2182,10 +2232,12 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
         for (int dt = 0; dt < DT; ++dt) bsum[t3][dt] = f4v{0.f, 0.f, 0.f, 0.f};
     f4v qv[DT], kv[DT], vv[DT], dov[DT];
     float lsev;
+    uint32_t kwv = 0;   // MODE 3: the forward's keep bits of this lane's elements (bit 4 jt + e)
     auto load = [&](int64_t rr) {
         const int i = w * 16 + c0;
         const int64_t off = rr * A.s_row + (int64_t)h * d + (int64_t)i * A.s_t + 4 * g0;
         const int64_t offd = rr * A.do_row + (int64_t)h * d + (int64_t)i * A.do_t + 4 * g0;
+        if constexpr (MODE == 3) kwv = A.keep[((rr * A.heads + h) * TT + w) * WAVE + lane];
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
             qv[dt] = ld4v<S>(q, off + dt * 16, i < T);
@@ -2213,9 +2265,115 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
             }
         }
         const float lse_i = lsev;
+        const uint32_t kw = kwv;
         __syncthreads();
         // ---- phase 1, query tile w: Sᵀ, dPᵀ (all key tiles), P, δ, dS, P', dQ
         f4v s[TT], dp[TT];
+        if constexpr (MODE != 0 && TAGAN_V5B_IL) {
+            // fast path, software-pipelined: the softmax / dropout VALU work of key tile jt issues between the
+            // S / dP products of tile jt + 1, and dS of tile jt + 1 between the dQ products of tile jt
+            auto sdp = [&](int jt) {
+                s[jt] = f4v{0.f, 0.f, 0.f, 0.f};
+                dp[jt] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int dt = 0; dt < DT; ++dt) {
+                    const f4v ka = lds4(Kr + (jt * 16 + c) * LK + dt * 16 + 4 * g);
+                    const f4v va = lds4(Vr + (jt * 16 + c) * LK + dt * 16 + 4 * g);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        s[jt] = mfma4(ka[e], qv[dt][e], s[jt]);
+                        dp[jt] = mfma4(va[e], dov[dt][e], dp[jt]);
+                    }
+                }
+            };
+            const uint32_t drk = tkey(A, r, h);
+            const float sc2 = A.inv_sqrt_d * LOG2E_F, lse2 = lse_i * LOG2E_F;
+            const int rb = T - 1 - i + 4 * g;
+            const uint32_t cb = (uint32_t)(i * T + 4 * g);
+            float dl = 0.f;
+            auto softA = [&](int jt) {   // P, the keep decision (sign of P), masked dP, Σ P·dP
+                uint32_t pw[2] = {0u, 0u};
+                if constexpr (MODE == 2) tpair(drk, cb, jt, pw);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float b2 = BREG ? bst[jt][e] : Bt[rb + jt * 16 + e];
+                    const float p = __builtin_amdgcn_exp2f(fmaf(s[jt][e], sc2, b2) - lse2);
+                    float dpv = dp[jt][e];
+                    if constexpr (MODE >= 2) {
+                        uint32_t km;
+                        if constexpr (MODE == 3) km = tbitmask(kw, jt * 4 + e);
+                        else if (e == 0) km = tkeepmask<0>(pw, thr - 1u);
+                        else if (e == 1) km = tkeepmask<1>(pw, thr - 1u);
+                        else if (e == 2) km = tkeepmask<2>(pw, thr - 1u);
+                        else km = tkeepmask<3>(pw, thr - 1u);
+                        dpv = fand(dpv * msc, km);
+                        s[jt][e] = fsignkeep(p, km);
+                    } else {
+                        s[jt][e] = p;
+                    }
+                    dp[jt][e] = dpv;
+                    dl = fmaf(p, dpv, dl);
+                }
+            };
+            constexpr int NM = 8 * DT;                     // products per key tile
+            constexpr int VA = (MODE == 3 ? 40 : 64) / NM;  // VALU of softA per product slot
+            sdp(0);
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt) {
+                if (jt + 1 < TT) sdp(jt + 1);
+                softA(jt);
+                if (jt + 1 < TT) {
+#pragma unroll
+                    for (int k2 = 0; k2 < NM; ++k2) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, VA, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (r + G < A.rows) load(r + G);   // the next unit's rows in flight during the rest of this one
+            dl = rows_sum(dl);
+            auto softB = [&](int jt) {   // dS (to X, transposed, and kept for dQ), P' in s, the bias-table sum
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float sv = s[jt][e];
+                    const float dsv = fabsf(sv) * (dp[jt][e] - dl);
+                    dp[jt][e] = dsv;
+                    if constexpr (MODE >= 2) s[jt][e] = fmaxf(sv, 0.f) * msc;
+                    X[(jt * 16 + 4 * g + e) * LD + i] = dsv;   // dSᵀ[j][i]
+                }
+                gsum[jt] += dp[jt];   // (unused when A.part is null)
+            };
+            f4v acc[DT][2];
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) acc[dt][0] = acc[dt][1] = f4v{0.f, 0.f, 0.f, 0.f};
+            softB(0);
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt) {
+                if (jt + 1 < TT) softB(jt + 1);
+#pragma unroll
+                for (int dt = 0; dt < DT; ++dt) {   // dQᵀ += Kᵀ[dt tile][key tile jt] · dSᵀ[jt]
+                    const f4v ka = lds4(Kt + (dt * 16 + c) * LD + jt * 16 + 4 * g);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[dt][jt & 1] = mfma4(ka[e], dp[jt][e], acc[dt][jt & 1]);
+                }
+                if (jt + 1 < TT) {
+#pragma unroll
+                    for (int k2 = 0; k2 < 4 * DT; ++k2) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 6 / DT + 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                const f4v a = acc[dt][0] + acc[dt][1];
+                st4v<S>(A.dq, r * A.d_row + (int64_t)i * A.d_t + h * d + dt * 16 + 4 * g, a, A.inv_sqrt_d);
+                bsum[0][dt] += a * A.inv_sqrt_d;
+            }
+        } else {
 #pragma unroll
         for (int jt = 0; jt < TT; ++jt) {
             s[jt] = f4v{0.f, 0.f, 0.f, 0.f};
@@ -2239,22 +2397,30 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
             const uint32_t cb = (uint32_t)(i * T + 4 * g);
             float dl = 0.f;
 #pragma unroll
-            for (int jt = 0; jt < TT; ++jt)
+            for (int jt = 0; jt < TT; ++jt) {
+                uint32_t pw[2] = {0u, 0u};
+                if constexpr (MODE == 2) tpair(drk, cb, jt, pw);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const float b2 = BREG ? bst[jt][e] : Bt[rb + jt * 16 + e];
                     const float p = __builtin_amdgcn_exp2f(fmaf(s[jt][e], sc2, b2) - lse2);
                     float dpv = dp[jt][e];
-                    if constexpr (MODE == 2) {
-                        const bool kp = lowbias32((cb + (uint32_t)(jt * 16 + e)) ^ drk) >= thr;
-                        dpv = kp ? dpv * msc : 0.f;
-                        s[jt][e] = kp ? p : -p;
+                    if constexpr (MODE >= 2) {
+                        uint32_t km;
+                        if constexpr (MODE == 3) km = tbitmask(kw, jt * 4 + e);
+                        else if (e == 0) km = tkeepmask<0>(pw, thr - 1u);
+                        else if (e == 1) km = tkeepmask<1>(pw, thr - 1u);
+                        else if (e == 2) km = tkeepmask<2>(pw, thr - 1u);
+                        else km = tkeepmask<3>(pw, thr - 1u);
+                        dpv = fand(dpv * msc, km);
+                        s[jt][e] = fsignkeep(p, km);
                     } else {
                         s[jt][e] = p;
                     }
                     dp[jt][e] = dpv;
                     dl = fmaf(p, dpv, dl);
                 }
+            }
             dl = rows_sum(dl);
 #pragma unroll
             for (int jt = 0; jt < TT; ++jt)
@@ -2263,7 +2429,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
                     const float sv = s[jt][e];
                     const float dsv = fabsf(sv) * (dp[jt][e] - dl);
                     dp[jt][e] = dsv;
-                    if constexpr (MODE == 2) s[jt][e] = fmaxf(sv, 0.f) * msc;
+                    if constexpr (MODE >= 2) s[jt][e] = fmaxf(sv, 0.f) * msc;
                     X[(jt * 16 + 4 * g + e) * LD + i] = dsv;   // dSᵀ[j][i]
                 }
         } else {
@@ -2325,6 +2491,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
                 if (i < T) st4v<S>(A.dq, r * A.d_row + (int64_t)i * A.d_t + h * d + dt * 16 + 4 * g, a, A.inv_sqrt_d);
                 if (A.qkv_part) bsum[0][dt] += a * A.inv_sqrt_d;   // padded steps add exact zeros (dS = 0)
             }
+        }
         }
         __syncthreads();   // dSᵀ complete in X
         // ---- phase 2, key tile w: dKᵀ = Qᵀ·dS (B = X[16w + c][i]), then dVᵀ = dOᵀ·P' (B = X after P'ᵀ replaces dSᵀ)
@@ -2533,12 +2700,35 @@ TArgs make(int64_t rows, int T, int heads, int d, int64_t s_row, int64_t s_t, co
 
 extern "C" {
 
+size_t tagan_temporal_attn_keep_bytes(int64_t rows, int32_t T, int32_t heads, int32_t head_dim, int causal,
+                                      int has_mask, int has_bias_dense, float p_drop) {
+    using namespace tagan;
+    if (rows <= 0 || heads <= 0 || !(p_drop > 0.f) || !v5_ok(T, head_dim)) return 0;
+    const int TT = v5_tiles(T);
+    const int one = 1;   // any non-null pointer: v5_fast_shape tests presence only
+    if (!v5_fast_shape(T, TT, causal, has_mask ? &one : nullptr, has_bias_dense ? &one : nullptr, nullptr, p_drop))
+        return 0;
+    return (size_t)rows * heads * TT * WAVE * sizeof(uint32_t);
+}
+
 int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim, const void* q,
                             const void* k, const void* v, int64_t s_row, int64_t s_t, const float* bias_table,
                             const float* bias_dense, int64_t bias_bstride, const uint8_t* mask,
                             int64_t mask_bstride, int64_t mask_hstride, int causal, float p_drop, uint64_t seed,
                             void* out, int64_t o_row, int64_t o_t, float* lse, float* attn, void* stream) {
+    return tagan_temporal_attn_fwd_keep(dtype, rows, T, heads, head_dim, q, k, v, s_row, s_t, bias_table, bias_dense,
+                                        bias_bstride, mask, mask_bstride, mask_hstride, causal, p_drop, seed, out,
+                                        o_row, o_t, lse, attn, nullptr, 0, nullptr, stream);
+}
+
+int tagan_temporal_attn_fwd_keep(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim, const void* q,
+                                 const void* k, const void* v, int64_t s_row, int64_t s_t, const float* bias_table,
+                                 const float* bias_dense, int64_t bias_bstride, const uint8_t* mask,
+                                 int64_t mask_bstride, int64_t mask_hstride, int causal, float p_drop, uint64_t seed,
+                                 void* out, int64_t o_row, int64_t o_t, float* lse, float* attn, uint32_t* keep,
+                                 size_t keep_bytes, int32_t* keep_written, void* stream) {
     using namespace tagan;
+    if (keep_written) *keep_written = 0;
     int rc = check(dtype, rows, T, heads, head_dim, p_drop);
     if (rc) return rc;
     TAGAN_REQUIRE(q && k && v && out && lse, TAGAN_ERR_ARG, "temporal_attn_fwd: null pointer");
@@ -2578,16 +2768,23 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
         const int TT = v5_tiles(T);
         const dim3 g5((unsigned)(v4_groups(rows) * heads));
         const size_t lds = v5_fwd_lds(TT, head_dim / 16);
-        const int mode = v5_fast_shape(T, TT, causal, mask, bias_dense, nullptr, p_drop) ? (p_drop > 0.f ? 2 : 1) : 0;
+        int mode = v5_fast_shape(T, TT, causal, mask, bias_dense, nullptr, p_drop) ? (p_drop > 0.f ? 2 : 1) : 0;
+        // MODE 3: also store the keep bits for the backward (one word per row, head, wave and lane)
+        if (mode == 2 && keep && keep_bytes >= (size_t)rows * heads * TT * WAVE * sizeof(uint32_t)) {
+            mode = 3;
+            A.keep = keep;
+        }
 #define TAGAN_V5F_M(TTT, DDT, MM) { auto kern = bf ? k_tattn_fwd_v5<TTT, DDT, bf16s, MM> : k_tattn_fwd_v5<TTT, DDT, float, MM>; \
                               rc = lds_optin(kern, lds); if (rc) return rc; kern<<<g5, WAVE * TTT, lds, s>>>(A, qf, kf, vf); }
-#define TAGAN_V5F(TTT, DDT) { if (mode == 2) TAGAN_V5F_M(TTT, DDT, 2) else if (mode == 1) TAGAN_V5F_M(TTT, DDT, 1) else TAGAN_V5F_M(TTT, DDT, 0) }
+#define TAGAN_V5F(TTT, DDT) { if (mode == 3) TAGAN_V5F_M(TTT, DDT, 3) else if (mode == 2) TAGAN_V5F_M(TTT, DDT, 2) \
+                              else if (mode == 1) TAGAN_V5F_M(TTT, DDT, 1) else TAGAN_V5F_M(TTT, DDT, 0) }
 #define TAGAN_V5F_D(TTT) if (head_dim == 16) TAGAN_V5F(TTT, 1) else TAGAN_V5F(TTT, 2)
         if (TT == 2) TAGAN_V5F_D(2) else if (TT == 4) TAGAN_V5F_D(4) else TAGAN_V5F_D(8)
 #undef TAGAN_V5F_D
 #undef TAGAN_V5F
 #undef TAGAN_V5F_M
         TAGAN_CHECK_LAUNCH("temporal_attn_fwd_v5");
+        if (keep_written) *keep_written = mode == 3;
         return TAGAN_OK;
     }
     if (al4 && !attn && v4_ok(T, head_dim)) {
@@ -2656,6 +2853,21 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
                             int64_t do_row, int64_t do_t, void* dq, void* dk, void* dv, int64_t d_row, int64_t d_t,
                             float* dbias_table, float* dbias_dense, float* dsum_qkv, void* workspace,
                             size_t workspace_bytes, void* stream) {
+    return tagan_temporal_attn_bwd_keep(dtype, rows, T, heads, head_dim, q, k, v, s_row, s_t, bias_table, bias_dense,
+                                        bias_bstride, mask, mask_bstride, mask_hstride, causal, p_drop, seed, out,
+                                        o_row, o_t, lse, dout, do_row, do_t, dq, dk, dv, d_row, d_t, dbias_table,
+                                        dbias_dense, dsum_qkv, nullptr, 0, workspace, workspace_bytes, stream);
+}
+
+int tagan_temporal_attn_bwd_keep(int dtype, int64_t rows, int32_t T, int32_t heads, int32_t head_dim, const void* q,
+                                 const void* k, const void* v, int64_t s_row, int64_t s_t, const float* bias_table,
+                                 const float* bias_dense, int64_t bias_bstride, const uint8_t* mask,
+                                 int64_t mask_bstride, int64_t mask_hstride, int causal, float p_drop, uint64_t seed,
+                                 const void* out, int64_t o_row, int64_t o_t, const float* lse, const void* dout,
+                                 int64_t do_row, int64_t do_t, void* dq, void* dk, void* dv, int64_t d_row,
+                                 int64_t d_t, float* dbias_table, float* dbias_dense, float* dsum_qkv,
+                                 const uint32_t* keep, size_t keep_bytes, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
     using namespace tagan;
     int rc = check(dtype, rows, T, heads, head_dim, p_drop);
     if (rc) return rc;
@@ -2738,10 +2950,16 @@ int tagan_temporal_attn_bwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
         const int64_t G5 = v4_groups(rows);   // <= nblk: the workspace rows
         const dim3 g5((unsigned)(G5 * heads));
         const size_t lds = v5_bwd_lds(TT, head_dim / 16);
-        const int mode = v5_fast_shape(T, TT, causal, mask, bias_dense, dbias_dense, p_drop) ? (p_drop > 0.f ? 2 : 1) : 0;
+        int mode = v5_fast_shape(T, TT, causal, mask, bias_dense, dbias_dense, p_drop) ? (p_drop > 0.f ? 2 : 1) : 0;
+        // MODE 3: the forward's keep bits (tagan_temporal_attn_fwd_keep reported them written) instead of the hash
+        if (mode == 2 && keep && keep_bytes >= (size_t)rows * heads * TT * WAVE * sizeof(uint32_t)) {
+            mode = 3;
+            A.keep = const_cast<uint32_t*>(keep);
+        }
 #define TAGAN_V5B_M(TTT, DDT, MM) { auto kern = bf ? k_tattn_bwd_v5<TTT, DDT, bf16s, MM> : k_tattn_bwd_v5<TTT, DDT, float, MM>; \
                               rc = lds_optin(kern, lds); if (rc) return rc; kern<<<g5, WAVE * TTT, lds, s>>>(A, qf, kf, vf, df, lse); }
-#define TAGAN_V5B(TTT, DDT) { if (mode == 2) TAGAN_V5B_M(TTT, DDT, 2) else if (mode == 1) TAGAN_V5B_M(TTT, DDT, 1) else TAGAN_V5B_M(TTT, DDT, 0) }
+#define TAGAN_V5B(TTT, DDT) { if (mode == 3) TAGAN_V5B_M(TTT, DDT, 3) else if (mode == 2) TAGAN_V5B_M(TTT, DDT, 2) \
+                              else if (mode == 1) TAGAN_V5B_M(TTT, DDT, 1) else TAGAN_V5B_M(TTT, DDT, 0) }
 #define TAGAN_V5B_D(TTT) if (head_dim == 16) TAGAN_V5B(TTT, 1) else TAGAN_V5B(TTT, 2)
         if (TT == 2) TAGAN_V5B_D(2) else if (TT == 4) TAGAN_V5B_D(4) else TAGAN_V5B_D(8)
 #undef TAGAN_V5B_D

@@ -15,6 +15,7 @@ autograd nodes of host overhead per layer.  Here the backward is written out onc
 
 Cores: ``GeoCore`` (tagan_geo_attn_*) and ``TemporalCore`` (tagan_temporal_attn_*).
 """
+import ctypes
 import os
 from typing import Optional
 
@@ -24,7 +25,7 @@ import torch.nn.functional as F
 from . import _lib
 from ._lib import check, lib, ptr, require_hip, stream_of
 from . import stream_gemm as sg
-from .kernels import TemporalMask, _geo_fwd, colsum, split_rows, weight_grad
+from .kernels import TemporalMask, _geo_fwd, _keep_cache, colsum, split_rows, weight_grad
 
 
 # ----------------------------------------------------------------------------- raw LayerNorm calls
@@ -169,16 +170,18 @@ class TemporalCore:
         bd_stride = (0 if bd.shape[0] == 1 else heads * T * T) if bd is not None else 0
         m = self.mask
         b, es = qkv2.data_ptr(), qkv2.element_size()
-        check(lib().tagan_temporal_attn_fwd(_lib.dtype_code(qkv2), R, T, heads, d, b, b + H * es, b + 2 * H * es, s_row,
-                                            s_t, ptr(bt), ptr(bd), bd_stride, ptr(m.keep), m.bstride, m.hstride,
-                                            int(m.causal), float(self.p_drop), self.seed, ptr(out), o_row, o_t,
-                                            ptr(lse), None, stream_of(qkv2)), "tagan_temporal_attn_fwd")
-        return out, (lse, bt, bd, bd_stride)
+        keep, kb, written = _keep_cache(R, T, heads, d, m, bd, self.p_drop, qkv2.device)
+        check(lib().tagan_temporal_attn_fwd_keep(_lib.dtype_code(qkv2), R, T, heads, d, b, b + H * es,
+                                                 b + 2 * H * es, s_row, s_t, ptr(bt), ptr(bd), bd_stride, ptr(m.keep),
+                                                 m.bstride, m.hstride, int(m.causal), float(self.p_drop), self.seed,
+                                                 ptr(out), o_row, o_t, ptr(lse), None, ptr(keep), kb,
+                                                 ctypes.byref(written), stream_of(qkv2)), "tagan_temporal_attn_fwd_keep")
+        return out, (lse, bt, bd, bd_stride, keep if written.value else None)
 
     def bwd(self, qkv2, out, saved, dctx, want_p1, want_p2, want_bias_sum=False):
         """``want_bias_sum``: also return the column sums of dq|dk|dv (the QKV bias gradient) when the
         matrix-core kernel can sum them in place (else None: the caller reduces dqkv itself)."""
-        lse, bt, bd, bd_stride = saved
+        lse, bt, bd, bd_stride, keep = saved
         T, R, heads = self.T, self.R, self.heads
         H = qkv2.shape[1] // 3
         d = H // heads
@@ -194,11 +197,14 @@ class TemporalCore:
         dsum = torch.empty(3 * H, device=dev) if want_bias_sum else None
         b, db, es = qkv2.data_ptr(), dqkv.data_ptr(), qkv2.element_size()
         def call(ds):
-            return L.tagan_temporal_attn_bwd(_lib.dtype_code(qkv2), R, T, heads, d, b, b + H * es, b + 2 * H * es,
-                                             s_row, s_t, ptr(bt), ptr(bd), bd_stride, ptr(m.keep), m.bstride,
-                                             m.hstride, int(m.causal), float(self.p_drop), self.seed, ptr(out), o_row,
-                                             o_t, ptr(lse), ptr(dctx), o_row, o_t, db, db + H * es, db + 2 * H * es,
-                                             s_row, s_t, ptr(dbt), ptr(dbd), ptr(ds), ptr(ws), wsb, stream_of(qkv2))
+            return L.tagan_temporal_attn_bwd_keep(_lib.dtype_code(qkv2), R, T, heads, d, b, b + H * es,
+                                                  b + 2 * H * es, s_row, s_t, ptr(bt), ptr(bd), bd_stride,
+                                                  ptr(m.keep), m.bstride, m.hstride, int(m.causal),
+                                                  float(self.p_drop), self.seed, ptr(out), o_row, o_t, ptr(lse),
+                                                  ptr(dctx), o_row, o_t, db, db + H * es, db + 2 * H * es, s_row, s_t,
+                                                  ptr(dbt), ptr(dbd), ptr(ds), ptr(keep),
+                                                  keep.numel() * 4 if keep is not None else 0, ptr(ws), wsb,
+                                                  stream_of(qkv2))
         rc = call(dsum)
         if rc == _lib.TAGAN_ERR_UNSUPPORTED and dsum is not None:   # rejected before any launch: not this path
             dsum = None

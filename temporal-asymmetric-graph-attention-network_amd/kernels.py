@@ -366,6 +366,19 @@ class TemporalMask:
     hstride: int = 0
 
 
+def _keep_cache(R, T, heads, d, mask, bias_dense, p_drop, device):
+    """(buffer, bytes, c_int32 flag) for the forward's dropout keep bits (tagan_temporal_attn_keep_bytes: the
+    matrix-core path for T in (32, 128] stores them so the backward skips the counter hash); (None, 0, flag) where no
+    path uses them.  The flag tells whether the forward wrote the bits: only then does the backward get them."""
+    written = ctypes.c_int32(0)
+    kb = int(lib().tagan_temporal_attn_keep_bytes(R, T, heads, d, int(mask.causal) if mask is not None else 0,
+                                                  int(mask is not None and mask.keep is not None),
+                                                  int(bias_dense is not None), float(p_drop)))
+    if kb == 0:
+        return None, 0, written
+    return torch.empty(kb // 4, dtype=torch.int32, device=device), kb, written
+
+
 class TemporalAttnFn(torch.autograd.Function):
     """Per-row attention over T steps.  ``qkv`` is [R, T, 3H] (row-major) or [T, R, 3H] (time_major)."""
 
@@ -387,11 +400,14 @@ class TemporalAttnFn(torch.autograd.Function):
         bd = bias_dense.detach().contiguous() if bias_dense is not None else None
         bd_stride = (0 if bd.shape[0] == 1 else heads * T * T) if bd is not None else 0
         base, es = qkv.data_ptr(), qkv.element_size()
-        check(lib().tagan_temporal_attn_fwd(_lib.TAGAN_F32, R, T, heads, d, base, base + H * es,
-                                            base + 2 * H * es, s_row, s_t, ptr(bt), ptr(bd), bd_stride,
-                                            ptr(mask.keep), mask.bstride, mask.hstride, int(mask.causal),
-                                            float(p_drop), seed, ptr(out), o_row, o_t, ptr(lse), ptr(attn),
-                                            stream_of(qkv)), "tagan_temporal_attn_fwd")
+        keep, kb, written = _keep_cache(R, T, heads, d, mask, bd, p_drop, qkv.device)
+        check(lib().tagan_temporal_attn_fwd_keep(_lib.TAGAN_F32, R, T, heads, d, base, base + H * es,
+                                                 base + 2 * H * es, s_row, s_t, ptr(bt), ptr(bd), bd_stride,
+                                                 ptr(mask.keep), mask.bstride, mask.hstride, int(mask.causal),
+                                                 float(p_drop), seed, ptr(out), o_row, o_t, ptr(lse), ptr(attn),
+                                                 ptr(keep), kb, ctypes.byref(written), stream_of(qkv)),
+              "tagan_temporal_attn_fwd_keep")
+        ctx.keep = keep if written.value else None
         ctx.save_for_backward(qkv, out, lse, bt, bd)
         ctx.cfg = (time_major, heads, mask, p_drop, seed, bd_stride)
         ctx.need_bt = bias_table is not None
@@ -419,12 +435,16 @@ class TemporalAttnFn(torch.autograd.Function):
         ws = torch.empty(int(ws_bytes), dtype=torch.uint8, device=qkv.device)
         base, es = qkv.data_ptr(), qkv.element_size()
         dbase = dqkv.data_ptr()
-        check(L.tagan_temporal_attn_bwd(_lib.TAGAN_F32, R, T, heads, d, base, base + H * es, base + 2 * H * es,
-                                        s_row, s_t, ptr(bt), ptr(bd), bd_stride, ptr(mask.keep), mask.bstride,
-                                        mask.hstride, int(mask.causal), float(p_drop), seed, ptr(out), o_row, o_t,
-                                        ptr(lse), ptr(dout), o_row, o_t, dbase, dbase + H * es, dbase + 2 * H * es,
-                                        s_row, s_t, ptr(dbt), ptr(dbd), None, ptr(ws), ws_bytes, stream_of(qkv)),
-              "tagan_temporal_attn_bwd")
+        keep = ctx.keep
+        ctx.keep = None
+        check(L.tagan_temporal_attn_bwd_keep(_lib.TAGAN_F32, R, T, heads, d, base, base + H * es,
+                                             base + 2 * H * es, s_row, s_t, ptr(bt), ptr(bd), bd_stride,
+                                             ptr(mask.keep), mask.bstride, mask.hstride, int(mask.causal),
+                                             float(p_drop), seed, ptr(out), o_row, o_t, ptr(lse), ptr(dout), o_row,
+                                             o_t, dbase, dbase + H * es, dbase + 2 * H * es, s_row, s_t, ptr(dbt),
+                                             ptr(dbd), None, ptr(keep), keep.numel() * 4 if keep is not None else 0,
+                                             ptr(ws), ws_bytes, stream_of(qkv)),
+              "tagan_temporal_attn_bwd_keep")
         if dbd is not None and bd is not None and bd.shape[0] == 1:
             dbd = dbd.sum(0, keepdim=True)
         return dqkv, dbt, dbd, None, None, None, None, None, None

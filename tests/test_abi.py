@@ -43,6 +43,38 @@ def _drop_uniform(seed, stream, counter):
     return u.astype(np.float64) / 16777216.0
 
 
+def _drop_key(seed, stream):
+    seed = int(seed)
+    stream = np.asarray(stream, dtype=np.uint64)
+    k = _lowbias32(np.uint32(seed & 0xFFFFFFFF) ^ np.uint32(0x9E3779B9))
+    k = _lowbias32(k ^ np.uint32(seed >> 32))
+    k = _lowbias32(k ^ (stream & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+    return _lowbias32(k ^ (stream >> np.uint64(32)).astype(np.uint32))
+
+
+def _temporal_keep(seed, stream, counter, p):
+    """numpy restatement of the temporal attention dropout (temporal_attn.hip tkeep / include/tagan_hip.h): one
+    lowbias32((c >> 1) ^ key) per counter pair, low half for the even counter, high half for the odd one, kept iff
+    half >= ceil(p 2^16).  stream and counter broadcast against each other."""
+    c = np.asarray(counter, dtype=np.uint32)
+    w = _lowbias32((c >> np.uint32(1)) ^ _drop_key(seed, stream))
+    half = np.where((c & np.uint32(1)) != 0, w >> np.uint32(16), w & np.uint32(0xFFFF))
+    return half >= np.uint32(np.ceil(np.float32(p) * np.float32(65536.0)))
+
+
+def test_temporal_dropout_statistics():
+    """Keep rate of the pair-word temporal dropout at p = 0.1 / 0.5, and no correlation between the two halves of one
+    word (even / odd counters) or between neighbouring pairs."""
+    for p in (0.1, 0.5):
+        k = _temporal_keep(7, np.arange(256, dtype=np.uint64)[:, None], np.arange(4096, dtype=np.uint32)[None, :], p)
+        rate = k.mean()
+        assert abs(rate - (1 - p)) < 4 * np.sqrt(p * (1 - p) / k.size), rate
+        x = k.astype(np.float64)
+        for a, b in ((x[:, 0::2], x[:, 1::2]), (x[:, 0:-2:2], x[:, 2::2])):
+            r = np.corrcoef(a.ravel(), b.ravel())[0, 1]
+            assert abs(r) < 4 / np.sqrt(a.size), r
+
+
 def test_uniform_matches_numpy_restatement():
     L = _lib.lib()
     for seed in (0, 1, 123456789, 2 ** 62 - 1, 2 ** 64 - 1):

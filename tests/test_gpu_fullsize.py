@@ -155,33 +155,37 @@ def test_c2_full_model_vs_oracle(dev):
 
 # bf16 mode (BASELINE's C2 dtype; fused.py "bf16": activations stored in bf16 between kernels, fp32 math and
 # accumulation inside every kernel, bf16 GEMM operands) against the same fp64 oracle.  Tolerance per tensor t,
-# derived from the bf16 roundings on t's dependency path:
-#     bound_t = KAPPA * U_RMS * sqrt(n_t)
-#   U_RMS = 2^-8 / sqrt(3): RMS relative error of one round-to-nearest store to bf16 (8 significant bits, error
-#           uniform within half an ulp);
-#   n_t   = the bf16 stores whose errors reach t: every attention block stores h = LN1(x), Q|K|V and the
-#           attention output and rounds its two weight operands (5 per block, 3 blocks = 15 before the logits);
-#           its backward stores d(out-proj output), d(context) and dQ|dK|dV and re-uses the two rounded weights
-#           (5 more per block the gradient flows back through): head 15, temporal block 20, geometric layer 1 25,
-#           geometric layer 0 / skip LayerNorm / node embedding / d(node features) 30;
-#   KAPPA = 4: the amplification of independent relative perturbations through LayerNorm, softmax and the
-#           BCE head (their Jacobians are O(1) in norm; 4 leaves 2x margin over the largest measured ratio).
+# derived from the bf16 roundings on its dependency path:
+#     bound_t = SAFETY * U_RMS * max(kappa_t, 1)
+#   U_RMS   = 2^-8 / sqrt(3): RMS relative error of one round-to-nearest store to bf16 (8 significant bits, error
+#             uniform within half an ulp);
+#   kappa_t = sqrt(sum_s kappa_{t,s}^2) over the 24 store sites s of the mode (per attention block: h = LN1(x),
+#             Q|K|V, the attention output, the rounded W_qkv and W_o, d(out-projection output), d(context),
+#             dQ|dK|dV), kappa_{t,s} = t's relative condition number for elementwise relative perturbations at s:
+#             measured on this workload by tools/bf16_conditioning.py with the fp64 oracle (16 draws of every site
+#             perturbed at once, tests/golden/bf16_conditioning.json "kappa_rss"); to first order the normwise
+#             error of t has RMS U_RMS * kappa_t;
+#   SAFETY  = 4: a 4-sigma tail of that error;
+#   max(., 1): the head's scalar-like gradients (classifier biases, the loss) measure up to 4.5 U_RMS * kappa_t on
+#             the GPU, more than the first-order model predicts for them (profiles/r4j_parity_errors.json): their
+#             kappa is floored at one rounding's worth.
 # Written exceptions: the analytically zero gradients (golden_io.ANALYTIC_ZERO: noise on both sides, checked to be
 # zero) and the ill-conditioned attention-pool bias (COND_GRADS: its fp32 oracle already carries a 1.7e-4
 # normwise error, i.e. a ~2900x amplification of fp32 rounding -- at bf16 precision that tensor has no correct
 # digits in ANY bf16 implementation; it is held to the element-wise bound only).
 U_RMS = 2.0 ** -8 / 3 ** 0.5
-KAPPA = 4.0
+SAFETY = 4.0
 
 
-def _bf16_stores(name):
-    if name.startswith(("classification_head.", "loss_fn.")):
-        return 15
-    if name.startswith("temporal_attention."):
-        return 20
-    if name.startswith("geometric_attention_layers.1."):
-        return 25
-    return 30      # geometric layer 0, skip LayerNorm, node embedding, d(node features)
+def _kappa():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bf16_conditioning.json")) as f:
+        return json.load(f)["kappa_rss"]
+
+
+def _bf16_bound(kappa, key):
+    return SAFETY * U_RMS * max(kappa[key], 1.0)
 
 
 @pytest.mark.timeout(900)
@@ -189,9 +193,10 @@ def test_c2_bf16_vs_oracle(dev):
     cfg, model, seq, labels, out = _c2_run(dev, "bf16")
     # the oracle runs on the fp32 master weights (the same initialisation as the fp32 test)
     ref, pgrad, xgrad = _c2_oracle(model, seq, labels, cfg)
-    bound_out = KAPPA * U_RMS * 15 ** 0.5
+    kappa = _kappa()
     for key, got, want in (("logits", out["logits"], ref["logits"]),
                            ("loss", out["loss"].reshape(1), ref["loss"].reshape(1))):
+        bound_out = _bf16_bound(kappa, key)
         nr = G.normwise_rel(got, want)
         G.ERRORS.setdefault("test_c2_bf16_vs_oracle", {})[key] = [nr, bound_out]
         assert nr <= bound_out, "%s: bf16 normwise %.3e > %.3e" % (key, nr, bound_out)
@@ -207,13 +212,13 @@ def test_c2_bf16_vs_oracle(dev):
         if any(name.endswith(k) for k in COND_GRADS):
             G.assert_close("grad " + name, p.grad, pgrad[name], GRAD_ATOL, GRAD_RTOL, norm_rtol=float("inf"))
             continue
-        bound = KAPPA * U_RMS * _bf16_stores(name) ** 0.5
+        bound = _bf16_bound(kappa, "grad " + name)
         nr = G.normwise_rel(p.grad, pgrad[name])
         G.ERRORS.setdefault("test_c2_bf16_vs_oracle", {})["grad " + name] = [nr, bound]
         worst = max(worst, (nr / bound, name))
         assert nr <= bound, "grad %s: bf16 normwise %.3e > %.3e" % (name, nr, bound)
     assert n_checked >= 30
-    bound_x = KAPPA * U_RMS * 30 ** 0.5
+    bound_x = _bf16_bound(kappa, "grad x")
     for t, ((x, _, _, _), g64) in enumerate(zip(seq, xgrad)):
         nr = G.normwise_rel(x.grad, g64)
         G.ERRORS.setdefault("test_c2_bf16_vs_oracle", {})["grad x.%d" % t] = [nr, bound_x]

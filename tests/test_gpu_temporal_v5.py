@@ -109,3 +109,56 @@ def test_v5_deterministic_and_qkv_bias_sum(dev, monkeypatch):
     ref = dqkv.double().sum(0)
     err = (dsum.double() - ref).abs().max().item()
     assert err <= 1e-4 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("T,H,heads,dtype", [(64, 256, 8, torch.float32), (128, 256, 16, torch.float32),
+                                             (128, 256, 16, torch.bfloat16), (48, 128, 8, torch.float32)])
+def test_v5_keep_bits_match_counter_hash(dev, monkeypatch, T, H, heads, dtype):
+    """The keep-bit cache (the forward stores each element's dropout decision, the backward reads it instead of
+    re-evaluating the counter hash) gives bitwise the results of the hash path, and is used exactly on the fast
+    shapes: written at p > 0 on the v5 path, not at p = 0, not with a causal mask (tagan_temporal_attn_keep_bytes)."""
+    import ctypes
+    from tagan_amd import _lib, fused, kernels
+    from tagan_amd.kernels import TemporalMask
+    monkeypatch.setenv("TAGAN_TATTN_V5", "1")
+    R = 45
+    qkv, dctx, bt, _, mask = _inputs(dev, T, H, heads, True, False, False, False, dtype, R)
+    a = _run(dev, qkv, T, R, True, heads, mask, 0.1, 4242, bt, None, dctx, monkeypatch, "1", "1")
+    core = fused.TemporalCore(T, R, True, heads, mask, 0.1, 4242)
+    out, saved = core.fwd(qkv, bt, None)
+    fast = T in (64, 128)   # T = 16 x tiles (T = 48 pads its tiles: the general path, no cache)
+    assert (saved[-1] is not None) == fast, "the fast shape at p > 0 stores keep bits"
+    monkeypatch.setattr(fused, "_keep_cache", lambda *args: (None, 0, ctypes.c_int32(0)))
+    b = _run(dev, qkv, T, R, True, heads, mask, 0.1, 4242, bt, None, dctx, monkeypatch, "1", "1")
+    for name, x, y in zip(["out", "lse", "dqkv", "dbias_table"], a, b):
+        assert torch.equal(x, y), name
+    L = _lib.lib()
+    d = H // heads
+    assert L.tagan_temporal_attn_keep_bytes(R, T, heads, d, 0, 0, 0, 0.1) == (R * heads * (T // 16) * 64 * 4
+                                                                             if fast else 0)
+    assert L.tagan_temporal_attn_keep_bytes(R, T, heads, d, 0, 0, 0, 0.0) == 0
+    assert L.tagan_temporal_attn_keep_bytes(R, T, heads, d, 1, 0, 0, 0.1) == 0
+    assert L.tagan_temporal_attn_keep_bytes(R, T, heads, d, 0, 1, 0, 0.1) == 0
+    assert L.tagan_temporal_attn_keep_bytes(R, 32, heads, d, 0, 0, 0, 0.1) == 0   # v4 / v6 range
+    assert kernels._keep_cache(R, T, heads, d, TemporalMask(causal=True), None, 0.1, dev)[0] is None
+
+
+def test_temporal_dropout_mask_matches_restatement(dev):
+    """The post-dropout attention weights of the general kernel are zero exactly where the numpy restatement of the
+    pair-word mask (tests/test_abi.py::_temporal_keep) drops; every other kernel generation is held to the general
+    one by the comparisons above, so this pins the mask of them all."""
+    import numpy as np
+    from test_abi import _temporal_keep
+    from tagan_amd.kernels import TemporalAttnFn, TemporalMask
+    T, H, heads, R, p, seed = 24, 64, 4, 7, 0.3, 987654321
+    g = torch.Generator(device=dev).manual_seed(1)
+    qkv = torch.randn(R, T, 3 * H, device=dev, generator=g)
+    _, attn = TemporalAttnFn.apply(qkv, None, None, False, heads, TemporalMask(), p, seed, True)
+    torch.cuda.synchronize()
+    stream = (np.arange(R, dtype=np.uint64)[:, None] * heads + np.arange(heads, dtype=np.uint64)[None, :])
+    ctr = (np.arange(T, dtype=np.uint32)[:, None] * T + np.arange(T, dtype=np.uint32)[None, :])
+    keep = _temporal_keep(seed, stream[:, :, None, None], ctr[None, None], p)
+    got = (attn != 0).cpu().numpy()
+    assert got.shape == keep.shape
+    assert (got == keep).all(), "%d of %d decisions differ" % ((got != keep).sum(), keep.size)
+    assert 0.6 < keep.mean() < 0.8

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--p", type=float, default=0.1)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--causal", type=int, default=0)
+    ap.add_argument("--keep", type=int, default=1, help="dropout keep-bit cache between fwd and bwd (as the model)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     N, _E, T, H, heads = synthetic.CONFIGS[a.config][:5]
@@ -49,17 +50,24 @@ def main():
     b, db, es = qkv.data_ptr(), dqkv.data_ptr(), 4
     sr, st = 3 * H, N * 3 * H
 
+    kb = int(L.tagan_temporal_attn_keep_bytes(N, T, heads, d, a.causal, 0, 0, a.p)) if a.keep else 0
+    keep = torch.empty(max(kb // 4, 1), dtype=torch.int32, device=dev)
+    written = ctypes.c_int32(0)
+
     def fwd():
-        _lib.check(L.tagan_temporal_attn_fwd(0, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, st,
-                                             _lib.ptr(table), None, 0, None, 0, 0, a.causal, a.p, 99,
-                                             _lib.ptr(out), H, N * H, _lib.ptr(lse), None, sp), "fwd")
+        _lib.check(L.tagan_temporal_attn_fwd_keep(0, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, st,
+                                                  _lib.ptr(table), None, 0, None, 0, 0, a.causal, a.p, 99,
+                                                  _lib.ptr(out), H, N * H, _lib.ptr(lse), None,
+                                                  _lib.ptr(keep) if kb else None, kb, ctypes.byref(written), sp),
+                   "fwd")
 
     def bwd():
-        _lib.check(L.tagan_temporal_attn_bwd(0, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, st,
-                                             _lib.ptr(table), None, 0, None, 0, 0, a.causal, a.p, 99,
-                                             _lib.ptr(out), H, N * H, _lib.ptr(lse), _lib.ptr(dout), H, N * H,
-                                             db, db + H * es, db + 2 * H * es, sr, st, _lib.ptr(dtable), None, None,
-                                             _lib.ptr(ws), wsb, sp), "bwd")
+        kp = _lib.ptr(keep) if written.value else None
+        _lib.check(L.tagan_temporal_attn_bwd_keep(0, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, st,
+                                                  _lib.ptr(table), None, 0, None, 0, 0, a.causal, a.p, 99,
+                                                  _lib.ptr(out), H, N * H, _lib.ptr(lse), _lib.ptr(dout), H, N * H,
+                                                  db, db + H * es, db + 2 * H * es, sr, st, _lib.ptr(dtable), None,
+                                                  None, kp, kb if written.value else 0, _lib.ptr(ws), wsb, sp), "bwd")
 
     for _ in range(3):
         fwd()
@@ -85,7 +93,7 @@ def main():
     mm = 2.0 * T * T * d * N * heads   # flops of one T x T x d product over all units
     chk = [float(out.double().abs().sum()), float(dqkv.double().abs().sum()), float(dtable.double().abs().sum())]
     print(json.dumps({"lib": os.environ.get("TAGAN_LIB", "default"), "config": a.config, "rows": N, "T": T,
-                      "heads": heads, "d": d, "p": a.p, "ms_fwd": round(tf, 4), "ms_bwd": round(tb, 4),
+                      "heads": heads, "d": d, "p": a.p, "keep_bits": bool(written.value), "ms_fwd": round(tf, 4), "ms_bwd": round(tb, 4),
                       "gbs_fwd": round(bf / tf / 1e6, 1), "gbs_bwd": round(bb / tb / 1e6, 1),
                       "frac_hbm": round((bf + bb) / (tf + tb) / 1e6 / bench.HBM_PEAK_GBS, 4),
                       "tflops_fwd": round(2 * mm / tf / 1e9, 1), "tflops_bwd": round(5 * mm / tb / 1e9, 1),
