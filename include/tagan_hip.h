@@ -237,8 +237,8 @@ int tagan_temporal_attn_fwd(int dtype, int64_t rows, int32_t T, int32_t heads, i
                             void* out, int64_t o_row, int64_t o_t,
                             float* lse, float* attn, void* stream);
 
-/* Dropout keep-bit cache (the matrix-core path for T in (32, 128], T a multiple of 16, head_dim 16/32, no mask,
- * causal or dense bias, p_drop > 0): the forward can store every element's keep decision as one bit, and the
+/* Dropout keep-bit cache (the matrix-core path at T = 128, head_dim 16/32, no mask, causal or dense bias,
+ * p_drop > 0; at smaller T it measured no gain): the forward can store every element's keep decision as one bit, and the
  * backward reads them instead of re-evaluating the counter hash (the same bits: the hash decides them once).
  * tagan_temporal_attn_keep_bytes returns the bytes such a forward writes, 0 where no path uses the cache.
  * tagan_temporal_attn_fwd_keep = tagan_temporal_attn_fwd + keep (device, keep_bytes) and *keep_written (host,

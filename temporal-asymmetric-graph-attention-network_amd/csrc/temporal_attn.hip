@@ -2612,6 +2612,10 @@ bool v6_bwd_ok(int T, int d) {
     return d == 32 || v4_tiles(T) == 1;
 }
 
+// the keep-bit cache where it wins: at TT = 8 (C5: fwd + bwd 80.2 -> 76.7 ms); at TT = 4 (C3) the forward's bit
+// stores cost more than the backward saves (21.8 -> 22.0 ms; profiles/r4m_tattn.txt)
+bool v5_keep_tiles(int TT) { return TT >= 8; }
+
 // > 64 KB of dynamic LDS needs the per-kernel opt-in (once per instantiation)
 template <typename K>
 int lds_optin(K* kern, size_t bytes) {
@@ -2705,6 +2709,7 @@ size_t tagan_temporal_attn_keep_bytes(int64_t rows, int32_t T, int32_t heads, in
     using namespace tagan;
     if (rows <= 0 || heads <= 0 || !(p_drop > 0.f) || !v5_ok(T, head_dim)) return 0;
     const int TT = v5_tiles(T);
+    if (!v5_keep_tiles(TT)) return 0;
     const int one = 1;   // any non-null pointer: v5_fast_shape tests presence only
     if (!v5_fast_shape(T, TT, causal, has_mask ? &one : nullptr, has_bias_dense ? &one : nullptr, nullptr, p_drop))
         return 0;
@@ -2770,7 +2775,7 @@ int tagan_temporal_attn_fwd_keep(int dtype, int64_t rows, int32_t T, int32_t hea
         const size_t lds = v5_fwd_lds(TT, head_dim / 16);
         int mode = v5_fast_shape(T, TT, causal, mask, bias_dense, nullptr, p_drop) ? (p_drop > 0.f ? 2 : 1) : 0;
         // MODE 3: also store the keep bits for the backward (one word per row, head, wave and lane)
-        if (mode == 2 && keep && keep_bytes >= (size_t)rows * heads * TT * WAVE * sizeof(uint32_t)) {
+        if (mode == 2 && v5_keep_tiles(TT) && keep && keep_bytes >= (size_t)rows * heads * TT * WAVE * sizeof(uint32_t)) {
             mode = 3;
             A.keep = keep;
         }
@@ -2952,7 +2957,7 @@ int tagan_temporal_attn_bwd_keep(int dtype, int64_t rows, int32_t T, int32_t hea
         const size_t lds = v5_bwd_lds(TT, head_dim / 16);
         int mode = v5_fast_shape(T, TT, causal, mask, bias_dense, dbias_dense, p_drop) ? (p_drop > 0.f ? 2 : 1) : 0;
         // MODE 3: the forward's keep bits (tagan_temporal_attn_fwd_keep reported them written) instead of the hash
-        if (mode == 2 && keep && keep_bytes >= (size_t)rows * heads * TT * WAVE * sizeof(uint32_t)) {
+        if (mode == 2 && v5_keep_tiles(TT) && keep && keep_bytes >= (size_t)rows * heads * TT * WAVE * sizeof(uint32_t)) {
             mode = 3;
             A.keep = const_cast<uint32_t*>(keep);
         }
