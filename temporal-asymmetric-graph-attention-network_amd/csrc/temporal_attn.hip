@@ -984,10 +984,17 @@ __device__ __forceinline__ void tpair(uint32_t key, uint32_t cb, int jt, uint32_
 template <int E>
 __device__ __forceinline__ uint32_t tkeepmask(const uint32_t (&w)[2], uint32_t thr1) {
     const uint32_t half = (E & 1) ? (w[E >> 1] >> 16) : (w[E >> 1] & 0xFFFFu);
-    return (uint32_t)((int32_t)(thr1 - half) >> 31);
+    uint32_t m = (uint32_t)((int32_t)(thr1 - half) >> 31);
+    asm("" : "+v"(m));   // see tbitmask
+    return m;
 }
-// the keep-bit cache: all ones iff bit b of the word is set
-__device__ __forceinline__ uint32_t tbitmask(uint32_t kw, int b) { return (uint32_t)((int32_t)(kw << (31 - b)) >> 31); }
+// the keep-bit cache: all ones iff bit b of the word is set (opaque VGPR value: otherwise the compiler turns the
+// masking into lane-mask compares + selects, whose masks it keeps in SGPRs and spills)
+__device__ __forceinline__ uint32_t tbitmask(uint32_t kw, int b) {
+    uint32_t m = (uint32_t)((int32_t)(kw << (31 - b)) >> 31);
+    asm("" : "+v"(m));
+    return m;
+}
 __device__ __forceinline__ float fand(float x, uint32_t m) { return __uint_as_float(__float_as_uint(x) & m); }
 // +p where kept, -p where dropped (the backward's keep bit in the sign of P)
 __device__ __forceinline__ float fsignkeep(float p, uint32_t m) {
@@ -2221,6 +2228,9 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
         // (visible to all waves after the first unit's staging barrier)
     }
     const float msc = A.p_drop > 0.f ? A.inv_keep : 1.f;
+    // the pipelined MODE 3 path carries dS and P' without the 1 / (1 - p) factor and applies it to dQ, dK, dV and the
+    // bias-table sums instead (one multiply per output instead of two per element)
+    const float fsc = (MODE == 3 && TAGAN_V5B_IL) ? msc : 1.f;
     const uint32_t thr = MODE >= 2 ? tthr(A.p_drop) : 0u;
     f4v gsum[TT];   // Σ over units of dSᵀ[jt tiles][query tile w]: the bias-table gradient before its diagonal sums
 #pragma unroll
@@ -2299,10 +2309,12 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
                     const float b2 = BREG ? bst[jt][e] : Bt[rb + jt * 16 + e];
                     const float p = __builtin_amdgcn_exp2f(fmaf(s[jt][e], sc2, b2) - lse2);
                     float dpv = dp[jt][e];
-                    if constexpr (MODE >= 2) {
+                    if constexpr (MODE == 3) {   // keep bits at hand: no sign trick; 1 / (1 - p) folded into the outputs
+                        dpv = fand(dpv, tbitmask(kw, jt * 4 + e));
+                        s[jt][e] = p;
+                    } else if constexpr (MODE == 2) {
                         uint32_t km;
-                        if constexpr (MODE == 3) km = tbitmask(kw, jt * 4 + e);
-                        else if (e == 0) km = tkeepmask<0>(pw, thr - 1u);
+                        if (e == 0) km = tkeepmask<0>(pw, thr - 1u);
                         else if (e == 1) km = tkeepmask<1>(pw, thr - 1u);
                         else if (e == 2) km = tkeepmask<2>(pw, thr - 1u);
                         else km = tkeepmask<3>(pw, thr - 1u);
@@ -2337,9 +2349,10 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const float sv = s[jt][e];
-                    const float dsv = fabsf(sv) * (dp[jt][e] - dl);
+                    const float dsv = (MODE == 3 ? sv : fabsf(sv)) * (dp[jt][e] - dl);   // (MODE 3: dS (1 - p))
                     dp[jt][e] = dsv;
-                    if constexpr (MODE >= 2) s[jt][e] = fmaxf(sv, 0.f) * msc;
+                    if constexpr (MODE == 3) s[jt][e] = fand(sv, tbitmask(kw, jt * 4 + e));   // P' (1 - p)
+                    else if constexpr (MODE == 2) s[jt][e] = fmaxf(sv, 0.f) * msc;
                     X[(jt * 16 + 4 * g + e) * LD + i] = dsv;   // dSᵀ[j][i]
                 }
                 gsum[jt] += dp[jt];   // (unused when A.part is null)
@@ -2370,8 +2383,8 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
                 const f4v a = acc[dt][0] + acc[dt][1];
-                st4v<S>(A.dq, r * A.d_row + (int64_t)i * A.d_t + h * d + dt * 16 + 4 * g, a, A.inv_sqrt_d);
-                bsum[0][dt] += a * A.inv_sqrt_d;
+                st4v<S>(A.dq, r * A.d_row + (int64_t)i * A.d_t + h * d + dt * 16 + 4 * g, a, A.inv_sqrt_d * fsc);
+                bsum[0][dt] += a * (A.inv_sqrt_d * fsc);
             }
         } else {
 #pragma unroll
@@ -2520,7 +2533,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
                 }
             }
             float* dst = pass == 0 ? A.dk : A.dv;
-            const float sc = pass == 0 ? A.inv_sqrt_d : 1.f;
+            const float sc = (pass == 0 ? A.inv_sqrt_d : 1.f) * fsc;
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
                 const f4v a = acc[dt][0] + acc[dt][1];
@@ -2556,7 +2569,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
 #pragma unroll
         for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g0 + e) * LD + w * 16 + c0] = gsum[jt][e];
+            for (int e = 0; e < 4; ++e) X[(jt * 16 + 4 * g0 + e) * LD + w * 16 + c0] = gsum[jt][e] * fsc;
         __syncthreads();
         float* prow = A.part + rg * A.heads * NB + (int64_t)h * NB;
         for (int t = threadIdx.x; t < NB; t += WAVE * TT) {

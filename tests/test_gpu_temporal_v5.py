@@ -115,8 +115,9 @@ def test_v5_deterministic_and_qkv_bias_sum(dev, monkeypatch):
                                              (128, 256, 16, torch.bfloat16), (48, 128, 8, torch.float32)])
 def test_v5_keep_bits_match_counter_hash(dev, monkeypatch, T, H, heads, dtype):
     """The keep-bit cache (the forward stores each element's dropout decision, the backward reads it instead of
-    re-evaluating the counter hash) gives bitwise the results of the hash path, and is used exactly on the fast
-    shapes: written at p > 0 on the v5 path, not at p = 0, not with a causal mask (tagan_temporal_attn_keep_bytes)."""
+    re-evaluating the counter hash) gives the results of the hash path (the forward bitwise, the backward to fp32
+    rounding), and is used exactly where it is meant to be: written at p > 0 on the v5 path at T = 128, not at p = 0,
+    not with a causal mask or an explicit mask (tagan_temporal_attn_keep_bytes)."""
     import ctypes
     from tagan_amd import _lib, fused, kernels
     from tagan_amd.kernels import TemporalMask
@@ -131,7 +132,12 @@ def test_v5_keep_bits_match_counter_hash(dev, monkeypatch, T, H, heads, dtype):
     monkeypatch.setattr(fused, "_keep_cache", lambda *args: (None, 0, ctypes.c_int32(0)))
     b = _run(dev, qkv, T, R, True, heads, mask, 0.1, 4242, bt, None, dctx, monkeypatch, "1", "1")
     for name, x, y in zip(["out", "lse", "dqkv", "dbias_table"], a, b):
-        assert torch.equal(x, y), name
+        if name in ("out", "lse"):   # the forward is the same arithmetic with or without storing the bits
+            assert torch.equal(x, y), name
+        else:   # the cached backward applies 1 / (1 - p) to its outputs instead of per element: fp32 rounding apart
+            x, y = x.float(), y.float()
+            tol = (2e-6 if dtype == torch.float32 else 8e-3) * max(1.0, y.abs().max().item())
+            assert (x - y).abs().max().item() <= tol, name
     L = _lib.lib()
     d = H // heads
     assert L.tagan_temporal_attn_keep_bytes(R, T, heads, d, 0, 0, 0, 0.1) == (R * heads * (T // 16) * 64 * 4
