@@ -292,9 +292,16 @@ SGEMM = os.environ.get("TAGAN_SGEMM", "1") != "0"
 _SG_OK = {}
 
 
+# bf16 operands at H = 256 stay on the library GEMMs: the C5 bf16 step measured 678 ms on the one-plane stream GEMMs
+# against 643 ms on hipBLASLt (same box, profiles/r4p_c345.txt); fp32 (three planes) at H = 256 wins on the stream GEMMs
+# (C3 604 -> 540-566 ms), as does bf16 at H = 128 (C2)
+SG_BF16_MAX_H = 128
+
+
 def _sg_use(H: int, bf: bool, act: bool) -> bool:
-    """The block's six projection products all have a stream_gemm kernel at this H / precision."""
-    if not SGEMM:
+    """The block's six projection products all have a stream_gemm kernel at this H / precision, and it is the faster
+    path there."""
+    if not SGEMM or (bf and H > SG_BF16_MAX_H):
         return False
     key = (H, bf, act)
     ok = _SG_OK.get(key)
