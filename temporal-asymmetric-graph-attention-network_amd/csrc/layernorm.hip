@@ -325,10 +325,16 @@ bool geometry(int H, int& lpr, int& nv) {
 
 // Backward grid (persistent blocks, one [3H] partial row each): 1024 blocks (4 waves / SIMD); 1280 / 2048 / 4096 were
 // 3 / 10 / 27 % slower on the full backward (profiles/r1_ln_bwd_blocks_ab.txt).
-int ln_bwd_blocks() { return 1024; }
+#ifndef TAGAN_LN_BWD_BLOCKS
+#define TAGAN_LN_BWD_BLOCKS 1024
+#endif
+int ln_bwd_blocks() { return TAGAN_LN_BWD_BLOCKS; }
 
 // Row groups per wave (U): 2, the best of 1 / 2 / 4 at C2 (tools/ln_probe.py, profiles/r1_ln_rows_ab.txt).
-int ln_rows(int /*nv*/) { return 2; }
+#ifndef TAGAN_LN_ROWS
+#define TAGAN_LN_ROWS 2
+#endif
+int ln_rows(int /*nv*/) { return TAGAN_LN_ROWS; }
 
 // the fused LN2 + skip-LN backward (H = 128: LPR 32, NV 1; any U)
 template <typename S>

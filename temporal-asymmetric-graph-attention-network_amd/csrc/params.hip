@@ -13,49 +13,38 @@ namespace {
 
 constexpr int BLK = 256;
 
-// one thread per element of the packed [3H, ld] matrix (bias column / zero pad included)
+// one workgroup per packed row r < 3H (blockIdx.x), its threads over the row's ld columns (bias column / zero pad
+// included): no index divisions (the 64-bit divides of a flat index had made this 200-KB copy a 15-us kernel)
 __global__ void __launch_bounds__(BLK) k_qkv_pack(int64_t H, const float* __restrict__ wq, const float* __restrict__ wk,
                                                   const float* __restrict__ wv, const float* __restrict__ bq,
                                                   const float* __restrict__ bk, const float* __restrict__ bv,
                                                   float* __restrict__ w, int64_t ld, int bias_col,
                                                   float* __restrict__ b) {
-    const int64_t n = 3 * H * ld;
-    for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK) {
-        const int64_t r = t / ld, c = t - r * ld;
-        const int64_t part = r / H, rr = r - part * H;
-        const float* src = part == 0 ? wq : part == 1 ? wk : wv;
-        const float* bs = part == 0 ? bq : part == 1 ? bk : bv;
+    const int r = blockIdx.x, part = r / (int)H, rr = r - part * (int)H;
+    const float* src = part == 0 ? wq : part == 1 ? wk : wv;
+    const float* bs = part == 0 ? bq : part == 1 ? bk : bv;
+    for (int c = threadIdx.x; c < (int)ld; c += BLK) {
         float val = 0.f;
-        if (c < H) val = src[rr * H + c];
+        if (c < H) val = src[(int64_t)rr * H + c];
         else if (c == H && bias_col) val = bs[rr];
-        if (c < H || bias_col) w[t] = val;
-        if (b && c == 0) b[r] = bs[rr];
+        if (c < H || bias_col) w[(int64_t)r * ld + c] = val;
     }
+    if (b && threadIdx.x == 0) b[r] = bs[rr];
 }
 
-// dW rows r < 3H (row stride ld_dw) -> dwq | dwk | dwv [H, H]; db[r * db_stride] -> dbq | dbk | dbv [H]
+// dW rows r < 3H (row stride ld_dw) -> dwq | dwk | dwv [H, H]; db[r * db_stride] -> dbq | dbk | dbv [H]; one
+// workgroup per row
 __global__ void __launch_bounds__(BLK) k_qkv_unpack(int64_t H, const float* __restrict__ dw, int64_t ld_dw,
                                                     const float* __restrict__ db, int64_t db_stride,
                                                     float* __restrict__ dwq, float* __restrict__ dwk,
                                                     float* __restrict__ dwv, float* __restrict__ dbq,
                                                     float* __restrict__ dbk, float* __restrict__ dbv) {
-    const int64_t n = 3 * H * (H + 1);
-    for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK) {
-        const int64_t r = t / (H + 1), c = t - r * (H + 1);
-        const int64_t part = r / H, rr = r - part * H;
-        if (c < H) {
-            float* dst = part == 0 ? dwq : part == 1 ? dwk : dwv;
-            if (dw && dst) dst[rr * H + c] = dw[r * ld_dw + c];
-        } else {
-            float* dst = part == 0 ? dbq : part == 1 ? dbk : dbv;
-            if (db && dst) dst[rr] = db[r * db_stride];
-        }
-    }
-}
-
-int grid_for(int64_t n) {
-    const int64_t g = (n + BLK - 1) / BLK;
-    return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 2048);
+    const int r = blockIdx.x, part = r / (int)H, rr = r - part * (int)H;
+    float* dst = part == 0 ? dwq : part == 1 ? dwk : dwv;
+    if (dw && dst)
+        for (int c = threadIdx.x; c < (int)H; c += BLK) dst[(int64_t)rr * H + c] = dw[(int64_t)r * ld_dw + c];
+    float* dstb = part == 0 ? dbq : part == 1 ? dbk : dbv;
+    if (db && dstb && threadIdx.x == 0) dstb[rr] = db[(int64_t)r * db_stride];
 }
 
 }  // namespace
@@ -69,7 +58,8 @@ int tagan_qkv_pack(int64_t H, const float* wq, const float* wk, const float* wv,
     TAGAN_REQUIRE(H > 0 && wq && wk && wv && w && ld_w >= H + (bias_col ? 1 : 0), TAGAN_ERR_ARG,
                   "qkv_pack: bad argument (H=%lld ld=%lld)", (long long)H, (long long)ld_w);
     TAGAN_REQUIRE(!(bias_col || b) || (bq && bk && bv), TAGAN_ERR_ARG, "qkv_pack: null bias");
-    k_qkv_pack<<<grid_for(3 * H * ld_w), BLK, 0, as_stream(stream)>>>(H, wq, wk, wv, bq, bk, bv, w, ld_w, bias_col, b);
+    TAGAN_REQUIRE(3 * H <= (1 << 30) && ld_w <= (1 << 30), TAGAN_ERR_ARG, "qkv_pack: H=%lld too large", (long long)H);
+    k_qkv_pack<<<(unsigned)(3 * H), BLK, 0, as_stream(stream)>>>(H, wq, wk, wv, bq, bk, bv, w, ld_w, bias_col, b);
     TAGAN_CHECK_LAUNCH("qkv_pack");
     return TAGAN_OK;
 }
@@ -78,8 +68,9 @@ int tagan_qkv_unpack(int64_t H, const float* dw, int64_t ld_dw, const float* db,
                      float* dwk, float* dwv, float* dbq, float* dbk, float* dbv, void* stream) {
     using namespace tagan;
     TAGAN_REQUIRE(H > 0 && (!dw || ld_dw >= H) && (!db || db_stride >= 1), TAGAN_ERR_ARG, "qkv_unpack: bad argument");
-    k_qkv_unpack<<<grid_for(3 * H * (H + 1)), BLK, 0, as_stream(stream)>>>(H, dw, ld_dw, db, db_stride, dwq, dwk, dwv,
-                                                                          dbq, dbk, dbv);
+    TAGAN_REQUIRE(3 * H <= (1 << 30), TAGAN_ERR_ARG, "qkv_unpack: H=%lld too large", (long long)H);
+    k_qkv_unpack<<<(unsigned)(3 * H), BLK, 0, as_stream(stream)>>>(H, dw, ld_dw, db, db_stride, dwq, dwk, dwv, dbq, dbk,
+                                                                 dbv);
     TAGAN_CHECK_LAUNCH("qkv_unpack");
     return TAGAN_OK;
 }
