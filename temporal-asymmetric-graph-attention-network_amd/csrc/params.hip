@@ -14,7 +14,7 @@ namespace {
 constexpr int BLK = 256;
 
 // one workgroup per packed row r < 3H (blockIdx.x), its threads over the row's ld columns (bias column / zero pad
-// included): no index divisions (the 64-bit divides of a flat index had made this 200-KB copy a 15-us kernel)
+// included): no per-element index divisions
 __global__ void __launch_bounds__(BLK) k_qkv_pack(int64_t H, const float* __restrict__ wq, const float* __restrict__ wk,
                                                   const float* __restrict__ wv, const float* __restrict__ bq,
                                                   const float* __restrict__ bk, const float* __restrict__ bv,
