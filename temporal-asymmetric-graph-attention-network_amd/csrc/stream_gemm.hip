@@ -1134,8 +1134,7 @@ constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
 
 // (K, N) of the attention blocks at H = 128: QKV forward (128, 384), out-projection forward and its input
 // gradient (128, 128), QKV input gradient (384, 128).
-// Several configurations per key: the first is the default, TAGAN_SGEMM_VARIANT=v (probe knob, read once) picks
-// the v-th where one exists.
+// One configuration per key (compile-time alternatives are A/B'd as variant libraries: make variant NAME=.. EXTRA=..).
 // fp32 (three planes): MFMA-bound, tiles sized by the registers the weight fragments leave; one plane: HBM-bound,
 // taller tiles so that more bytes are in flight per workgroup.
 // H = 256 (C3, C5): a K = 256 three-plane panel is 96 VGPRs per 16 columns, so one n-subtile per wave and the

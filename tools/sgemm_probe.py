@@ -2,7 +2,7 @@
 
 Per shape: kernel time (HIP events, median of 20 after 5 warm-ups), the same product through torch (with the bench's
 TunableOp table), and the error of both against fp64 (max-abs / max|ref| and normwise) on the same inputs.
-Usage: python tools/sgemm_probe.py [--M 320000] [--bf16] ; TAGAN_SGEMM_VARIANT picks a kernel configuration.
+Usage: python tools/sgemm_probe.py [--M 320000] [--bf16] ; TAGAN_LIB=<variant library> times another build.
 """
 import argparse
 import json
@@ -50,7 +50,7 @@ def main():
     torch.manual_seed(0)
     M, H = args.M, args.H
     R = min(M, args.check_rows)
-    out = {"variant": os.environ.get("TAGAN_SGEMM_VARIANT", "0"), "M": M, "H": H, "cases": []}
+    out = {"variant": os.path.basename(os.environ.get("TAGAN_LIB", "libtagan_hip.so")), "M": M, "H": H, "cases": []}
 
     def rec(name, bytes_, flops, t_k, t_t, e_k, e_t, extra=None):
         r = {"case": name, "us_kernel": round(t_k, 1), "us_torch": round(t_t, 1),
