@@ -45,8 +45,14 @@ constexpr int FNT = 256;           // small-bucket finish workgroups (4 waves)
 #endif
 constexpr int CAP_S = TAGAN_CSR_TARGET * 5 / 4;   // keys per small CSR finish (LDS)
 constexpr int CAP_C = TAGAN_CSR_TARGET;           // (key, CSR position) pairs per small CSC finish
-constexpr int BNT = 512;           // big-bucket finish workgroups (8 waves)
-constexpr int BIG_LDS = 140 * 1024;   // dynamic LDS of the big-bucket kernels (2 key buffers / 2 + 2 pair buffers)
+#ifndef TAGAN_CSR_BNT
+#define TAGAN_CSR_BNT 512
+#endif
+constexpr int BNT = TAGAN_CSR_BNT;   // big-bucket finish workgroups (8 waves)
+#ifndef TAGAN_CSR_BIG_LDS_KB
+#define TAGAN_CSR_BIG_LDS_KB 140
+#endif
+constexpr int BIG_LDS = TAGAN_CSR_BIG_LDS_KB * 1024;   // dynamic LDS of the big-bucket kernels (2 key buffers / 2 + 2 pair buffers)
 constexpr int BIG_WG = 256;        // persistent workgroups of the big-bucket kernels (one per CU)
 constexpr int RB = 8;              // radix digit bits
 constexpr int RBINS = 1 << RB;
