@@ -15,13 +15,13 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _setup(dev, dropout, seed=3):
+def _setup(dev, dropout, seed=3, config="c2", snapshots=6, nodes=400, edges=3000):
     from tagan_amd import TAGAN, synthetic
-    cfg = synthetic.config_for("c2", dropout=dropout)
+    cfg = synthetic.config_for(config, dropout=dropout)
     torch.manual_seed(seed)
     model = TAGAN(cfg).to(dev).train()
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=True)
-    seq = synthetic.make_sequence("c2", dev, seed=7, snapshots=6, nodes=400, edges=3000)
+    seq = synthetic.make_sequence(config, dev, seed=7, snapshots=snapshots, nodes=nodes, edges=edges)
     labels = torch.tensor([1.0], device=dev)
 
     def step():
@@ -163,3 +163,40 @@ def test_graphed_step_has_no_split_form(dev):
     m, o, s = _setup(dev, 0.0)
     with pytest.raises(TypeError):
         GraphedStep(m, s, optimizer=o, warmup=1, between=lambda: None, post=lambda: None)
+
+
+def test_graph_keep_cache_matches_hash_path_at_t128(dev, monkeypatch):
+    """C5's temporal shape (T = 128, 16 heads, H = 256) with attention dropout, captured: the replays with the
+    keep-bit cache (the forward stores its dropout decisions, the backward reads them) against the same replays with
+    the backward re-hashing the counters -- the same masks, so the same trajectory to fp32 rounding (the cached
+    backward applies 1 / (1 - p) per output instead of per element)."""
+    import ctypes
+    from tagan_amd import fused
+    from tagan_amd.graph_step import GraphedStep
+
+    def run():
+        model, opt, step = _setup(dev, 0.1, config="c5", snapshots=128, nodes=200, edges=1200)
+        g = GraphedStep(model, step, optimizer=opt, warmup=2)
+        try:
+            losses = [float(g()) for _ in range(3)]
+        finally:
+            g.close()
+        torch.cuda.synchronize()
+        return losses, [p.detach().clone() for p in model.parameters()]
+
+    written = []
+    real = fused._keep_cache
+
+    def spy(*args):
+        out = real(*args)
+        written.append(out[0] is not None)
+        return out
+    monkeypatch.setattr(fused, "_keep_cache", spy)
+    la, pa = run()
+    assert any(written), "the T = 128 temporal forward allocates the keep-bit cache"
+    monkeypatch.setattr(fused, "_keep_cache", lambda *args: (None, 0, ctypes.c_int32(0)))
+    lb, pb = run()
+    for a, b in zip(la, lb):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (la, lb)
+    for x, y in zip(pa, pb):
+        torch.testing.assert_close(x, y, atol=1e-5, rtol=1e-4)
