@@ -285,10 +285,10 @@ template <typename S, int F>
 __device__ __forceinline__ void stf(void* p, int64_t i, const float (&r)[F]) {
     if constexpr (IsBf16<S>::v && F == 8) {
         uint4 u;
-        u.x = f2bf_bits(r[0]) | (f2bf_bits(r[1]) << 16);
-        u.y = f2bf_bits(r[2]) | (f2bf_bits(r[3]) << 16);
-        u.z = f2bf_bits(r[4]) | (f2bf_bits(r[5]) << 16);
-        u.w = f2bf_bits(r[6]) | (f2bf_bits(r[7]) << 16);
+        u.x = f2bf2(r[0], r[1]);
+        u.y = f2bf2(r[2], r[3]);
+        u.z = f2bf2(r[4], r[5]);
+        u.w = f2bf2(r[6], r[7]);
         *(uint4*)((uint16_t*)p + i) = u;
     } else {
 #pragma unroll
