@@ -20,7 +20,8 @@ namespace {
 constexpr int HB = 1024;     // threads: NG = HB / H groups of H feature threads
 constexpr int HU = 8;        // steps per thread in the [T, H] products (ceil(T / NG); T·H <= 8192)
 constexpr int HC = 16;       // max classes
-constexpr int KC = 32;       // weight rows / columns staged per LDS chunk (H > 128; the whole matrix at H <= 128)
+constexpr int KC = 64;       // weight rows / columns staged per LDS chunk (H > 128; the whole matrix at H <= 128):
+                             // 64 (H + 1) floats next to both [T, H] tiles stay under 141 KB at T·H = 8192
 // staging width: at H <= 128 the whole H x H weight fits the LDS next to the [T, H] tiles, so a product stages it in
 // ONE pass (one global-load latency instead of H / KC dependent rounds)
 __host__ __device__ inline int kstep(int H) { return H <= 128 ? H : KC; }
@@ -89,12 +90,19 @@ __device__ __forceinline__ void xw_t(const float* __restrict__ W, const float* x
         }
         __syncthreads();
         if (act) {
-            for (int kk = 0; kk < kn; ++kk) {
-                const float w = wt[kk * (H + 1) + j];
+            for (int kk = 0; kk < kn; kk += 4) {
+                const float w0 = wt[kk * (H + 1) + j], w1 = wt[(kk + 1) * (H + 1) + j];
+                const float w2 = wt[(kk + 2) * (H + 1) + j], w3 = wt[(kk + 3) * (H + 1) + j];
 #pragma unroll
                 for (int u = 0; u < HU; ++u) {
                     const int t = grp + NG * u;
-                    if (t < T) acc[u] = fmaf(w, xs[t * H + kc + kk], acc[u]);
+                    if (t < T) {
+                        const float4 x = *reinterpret_cast<const float4*>(xs + t * H + kc + kk);
+                        acc[u] = fmaf(w0, x.x, acc[u]);
+                        acc[u] = fmaf(w1, x.y, acc[u]);
+                        acc[u] = fmaf(w2, x.z, acc[u]);
+                        acc[u] = fmaf(w3, x.w, acc[u]);
+                    }
                 }
             }
         }
@@ -316,7 +324,7 @@ __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
         // dpooled[k] = Σ_j du_j Wc1[j][k]: thread (grp, k) over j = grp, grp + NG, ..., then the groups in order
         if (act) {
             float g = 0.f;
-#pragma unroll 8
+#pragma unroll 32
             for (int jj = grp; jj < H; jj += NG) g += vq[jj] * A.Wc1[(int64_t)jj * H + j];
             L.part[grp * H + j] = g;
         }
@@ -358,12 +366,32 @@ __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
         }
         __syncthreads();
         if (first) {   // rows >= 1 have x = 0: no dW1 and no dx
-            // dW1[j][k] = Σ_t dpre_tj x_tk (coalesced over the flat index)
-            for (int o = tid; o < H * H; o += HB) {
-                const int jj = o / H, k = o % H;
-                float acc = 0.f;
-                for (int t = 0; t < T; ++t) acc = fmaf(L.zs[t * H + jj], L.xs[t * H + k], acc);
-                A.dW1[o] = acc;
+            // dW1[j][k] = Σ_t dpre_tj x_tk, t ascending: one 4 x 4 block of (j, k) per thread and pass (two float4
+            // LDS reads per 16 FMAs instead of two scalar reads per FMA); the stores stay scalar (dW1 is a caller
+            // pointer, 4-byte alignment only), consecutive lanes on consecutive k quads
+            const int H4 = H / 4;
+            for (int o = tid; o < H4 * H4; o += HB) {
+                const int j4 = (o / H4) * 4, k4 = (o % H4) * 4;
+                float4 acc[4];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) acc[a] = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int t = 0; t < T; ++t) {
+                    const float4 zv = *reinterpret_cast<const float4*>(L.zs + t * H + j4);
+                    const float4 xv = *reinterpret_cast<const float4*>(L.xs + t * H + k4);
+                    const float zz[4] = {zv.x, zv.y, zv.z, zv.w};
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) {
+                        acc[a].x = fmaf(zz[a], xv.x, acc[a].x);
+                        acc[a].y = fmaf(zz[a], xv.y, acc[a].y);
+                        acc[a].z = fmaf(zz[a], xv.z, acc[a].z);
+                        acc[a].w = fmaf(zz[a], xv.w, acc[a].w);
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    float* o4 = A.dW1 + (int64_t)(j4 + a) * H + k4;
+                    o4[0] = acc[a].x; o4[1] = acc[a].y; o4[2] = acc[a].z; o4[3] = acc[a].w;
+                }
             }
             // dx_t[k] = a_t dpooled_k + Σ_jj dpre_t,jj W1[jj][k]: W1 rows staged through LDS in chunks of KC
             float acc[HU];
@@ -376,12 +404,19 @@ __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
                 for (int e = tid; e < jn * H; e += HB) L.wt[(e / H) * (H + 1) + e % H] = A.W1[(int64_t)jc * H + e];
                 __syncthreads();
                 if (act) {
-                    for (int kk = 0; kk < jn; ++kk) {
-                        const float wv = L.wt[kk * (H + 1) + j];
+                    for (int kk = 0; kk < jn; kk += 4) {   // four rows per float4 read of dpre (jc, jn, H % 4 == 0)
+                        const float w0 = L.wt[kk * (H + 1) + j], w1 = L.wt[(kk + 1) * (H + 1) + j];
+                        const float w2 = L.wt[(kk + 2) * (H + 1) + j], w3 = L.wt[(kk + 3) * (H + 1) + j];
 #pragma unroll
                         for (int u = 0; u < HU; ++u) {
                             const int t = grp + NG * u;
-                            if (t < T) acc[u] = fmaf(L.zs[t * H + jc + kk], wv, acc[u]);
+                            if (t < T) {
+                                const float4 z = *reinterpret_cast<const float4*>(L.zs + t * H + jc + kk);
+                                acc[u] = fmaf(z.x, w0, acc[u]);
+                                acc[u] = fmaf(z.y, w1, acc[u]);
+                                acc[u] = fmaf(z.z, w2, acc[u]);
+                                acc[u] = fmaf(z.w, w3, acc[u]);
+                            }
                         }
                     }
                 }

@@ -1,14 +1,35 @@
 #!/bin/bash
-# C3 / C4 / C5 bench lines (tools/runs/c3c4c5_bench.sh) + rocprofv3 kernel stats of 3 C3 steps (which GEMM kernels
-# the H = 256 attention blocks run).   bash tools/runs/r4h.sh <tag>
+# Head kernels: the register-blocked dW1 product, float4 step reads in the chunked products and KC = 64 (shipped
+# library) against the same without the float4 dx reads (libtagan_hip_hj.so) and the previous head
+# (libtagan_hip_oldhead.so): head GPU tests, then per library a kernel-trace profile of the C2 bench and two
+# interleaved bench runs.
+#   bash tools/runs/r4h.sh <tag>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${1:-r4h}
 mkdir -p $OUT
-bash tools/runs/c3c4c5_bench.sh ${1:-r4h} || exit 1
+L=$GRAFT_REPO_ROOT/temporal-asymmetric-graph-attention-network_amd
+timeout -k 10 300 python -u -m pytest tests/test_gpu_head.py -x -q --timeout 120 --timeout-method thread \
+    > $OUT/test_head.log 2>&1 || { tail -30 $OUT/test_head.log; exit 1; }
+tail -2 $OUT/test_head.log
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_c3 -o run -- \
-    python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-roofline --no-alt-precision --no-c1 \
-    --launch eager > $OUT/stats_c3.log 2>&1 || { tail -20 $OUT/stats_c3.log; exit 1; }
-find $OUT/stats_c3 -name "*kernel_trace*" -delete
-python tools/kstats.py $(find $OUT/stats_c3 -name "*kernel_stats.csv" | head -1) | sed -n 1,24p
+for lib in libtagan_hip.so libtagan_hip_hj.so libtagan_hip_oldhead.so; do
+  TAGAN_LIB=$L/$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$lib -o run \
+      -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --no-c1 \
+      > $OUT/prof_$lib.log 2>&1 || { tail -20 $OUT/prof_$lib.log; exit 1; }
+  find $OUT/prof_$lib -name "*kernel_trace*" -delete
+  python - $OUT/prof_$lib <<'EOF'
+import csv, glob, sys
+for f in glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "k_head" in r["Name"]:
+            print(sys.argv[1].split("prof_")[-1], r["Name"][:60], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us")
+EOF
+done
+for rep in 1 2; do
+  for lib in libtagan_hip.so libtagan_hip_hj.so libtagan_hip_oldhead.so; do
+    TAGAN_LIB=$L/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --no-c1 \
+        > $OUT/bench_${lib}_$rep.json 2> $OUT/bench_${lib}_$rep.err || { tail -20 $OUT/bench_${lib}_$rep.err; exit 1; }
+    python -c "import json;d=json.load(open('$OUT/bench_${lib}_$rep.json'));print('$lib', d['ms_per_step'], d['alt_precision']['ms_per_step'])"
+  done
+done
