@@ -18,7 +18,7 @@ namespace tagan {
 namespace {
 
 constexpr int HB = 1024;     // threads: NG = HB / H groups of H feature threads
-constexpr int HU = 8;        // steps per thread in the [T, H] products (ceil(T / NG); T·H <= 8192)
+constexpr int HU = 8;        // max steps per thread in the [T, H] products (ceil(T / NG); T·H <= 8192)
 constexpr int HC = 16;       // max classes
 constexpr int KC = 64;       // weight rows / columns staged per LDS chunk (H > 128; the whole matrix at H <= 128):
                              // 64 (H + 1) floats next to both [T, H] tiles stay under 141 KB at T·H = 8192
@@ -73,39 +73,95 @@ struct HeadLds {
     }
 };
 
-// Z[t][j] = Σ_k X[t][k] W[j][k] for the thread's steps t = grp + NG·u (thread (grp, j)); W (nn.Linear [H, H]) is
-// staged through LDS in chunks of KC columns, transposed (row stride H + 1: conflict-free both ways), so every
-// global read is a coalesced run and the H·H weight reads of one workgroup are all in flight together
-__device__ __forceinline__ void xw_t(const float* __restrict__ W, const float* xs, float* wt, int T, int H, int NG,
-                                     bool act, int grp, int j, float (&acc)[HU]) {
+// Global -> LDS copies move float4 quads and issue LB of them per thread before the first store (one latency per
+// batch: a runtime-bounded copy loop otherwise waits on every load before the next); the loads of the last batch
+// are clamped into range (always valid addresses), only the stores are guarded.  n, H and kn are multiples of 4.
+constexpr int LB = 4;
+
+// dst[i] = src ? src[i] : 0 for i < n (dst 16-byte aligned; src float4 runs when it is 16-byte aligned too)
+__device__ __forceinline__ void copy_in(float* dst, const float* __restrict__ src, int n) {
+    if (!src) {
+        for (int e = threadIdx.x * 4; e < n; e += HB * 4)
+            *reinterpret_cast<float4*>(dst + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+        const int n4 = n / 4;
+        for (int e0 = threadIdx.x; e0 < n4; e0 += LB * HB) {
+            float4 r[LB];
 #pragma unroll
-    for (int u = 0; u < HU; ++u) acc[u] = 0.f;
+            for (int q = 0; q < LB; ++q) r[q] = reinterpret_cast<const float4*>(src)[min(e0 + q * HB, n4 - 1)];
+#pragma unroll
+            for (int q = 0; q < LB; ++q)
+                if (e0 + q * HB < n4) reinterpret_cast<float4*>(dst)[e0 + q * HB] = r[q];
+        }
+    } else {   // a saved row b >= 1 (saved_floats is not a multiple of 4)
+        for (int e = threadIdx.x; e < n; e += HB) dst[e] = src[e];
+    }
+}
+
+// weight chunk kc of W (nn.Linear [H, H], 16-byte aligned: tagan_head_fwd / _bwd check) -> wt[kk][jj] (row stride
+// H + 1: conflict-free both ways), kk < kn: W[jj][kc + kk] (COLS: columns kc..kc+kn of every row) or W[kc + kk][jj]
+// (rows kc..kc+kn); one float4 of a row per load, coalesced runs along the row
+template <bool COLS>
+__device__ __forceinline__ void stage_chunk(const float* __restrict__ W, float* wt, int H, int kc, int kn) {
+    const int nq = H * kn / 4, kq = kn / 4, hq = H / 4;
+    for (int e0 = threadIdx.x; e0 < nq; e0 += LB * HB) {
+        float4 r[LB];
+#pragma unroll
+        for (int q = 0; q < LB; ++q) {
+            const int e = min(e0 + q * HB, nq - 1);
+            r[q] = COLS ? *reinterpret_cast<const float4*>(W + (int64_t)(e / kq) * H + kc + 4 * (e % kq))
+                        : *reinterpret_cast<const float4*>(W + (int64_t)kc * H + 4 * e);
+        }
+#pragma unroll
+        for (int q = 0; q < LB; ++q) {
+            const int e = e0 + q * HB;
+            if (e < nq) {
+                // COLS: row jj = e / kq, columns 4 (e % kq) + i; else row e / hq of the chunk, columns 4 (e % hq) + i
+                float* o = COLS ? wt + 4 * (e % kq) * (H + 1) + e / kq : wt + (e / hq) * (H + 1) + 4 * (e % hq);
+                const int st = COLS ? H + 1 : 1;
+                o[0] = r[q].x; o[st] = r[q].y; o[2 * st] = r[q].z; o[3 * st] = r[q].w;
+            }
+        }
+    }
+}
+
+// acc[u] += Σ_{kk < kn} wt[kk][j] · V[t][kc + kk] for the thread's steps t = grp + NG·u, kk ascending (bitwise the
+// sums of the scalar loop), four kk per float4 read of V (kc, kn, H are multiples of 4).  Steps past T read row
+// T - 1 (their sums are never stored), so the NU reads of a kk quad carry no branch and go out together.
+template <int NU>
+__device__ __forceinline__ void chunk_fma(const float* wt, const float* V, int T, int H, int NG, int grp, int j,
+                                          int kc, int kn, float (&acc)[NU]) {
+    int row[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) row[u] = min(grp + NG * u, T - 1) * H + kc;
+    for (int kk = 0; kk < kn; kk += 4) {
+        const float w0 = wt[kk * (H + 1) + j], w1 = wt[(kk + 1) * (H + 1) + j];
+        const float w2 = wt[(kk + 2) * (H + 1) + j], w3 = wt[(kk + 3) * (H + 1) + j];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const float4 x = *reinterpret_cast<const float4*>(V + row[u] + kk);
+            acc[u] = fmaf(w0, x.x, acc[u]);
+            acc[u] = fmaf(w1, x.y, acc[u]);
+            acc[u] = fmaf(w2, x.z, acc[u]);
+            acc[u] = fmaf(w3, x.w, acc[u]);
+        }
+    }
+}
+
+// acc[u] = Σ_k V[t][k] Wc[k][j] over the weight chunks, Wc = Wᵀ (COLS: Z = V Wᵀ, the nn.Linear forward) or W
+// (Z = V W, its input gradient), for the thread's steps t = grp + NG·u (thread (grp, j))
+template <bool COLS, int NU>
+__device__ __forceinline__ void xw_chunks(const float* __restrict__ W, const float* V, float* wt, int T, int H,
+                                          int NG, bool act, int grp, int j, float (&acc)[NU]) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) acc[u] = 0.f;
     const int KS = kstep(H);
     for (int kc = 0; kc < H; kc += KS) {
         const int kn = min(KS, H - kc);
-        __syncthreads();   // the previous chunk's reads are done
-        for (int e = threadIdx.x; e < H * kn; e += HB) {
-            const int jj = e / kn, kk = e % kn;
-            wt[kk * (H + 1) + jj] = W[(int64_t)jj * H + kc + kk];
-        }
+        __syncthreads();   // the previous chunk's reads of wt (and the writes of V) are done
+        stage_chunk<COLS>(W, wt, H, kc, kn);
         __syncthreads();
-        if (act) {
-            for (int kk = 0; kk < kn; kk += 4) {
-                const float w0 = wt[kk * (H + 1) + j], w1 = wt[(kk + 1) * (H + 1) + j];
-                const float w2 = wt[(kk + 2) * (H + 1) + j], w3 = wt[(kk + 3) * (H + 1) + j];
-#pragma unroll
-                for (int u = 0; u < HU; ++u) {
-                    const int t = grp + NG * u;
-                    if (t < T) {
-                        const float4 x = *reinterpret_cast<const float4*>(xs + t * H + kc + kk);
-                        acc[u] = fmaf(w0, x.x, acc[u]);
-                        acc[u] = fmaf(w1, x.y, acc[u]);
-                        acc[u] = fmaf(w2, x.z, acc[u]);
-                        acc[u] = fmaf(w3, x.w, acc[u]);
-                    }
-                }
-            }
-        }
+        if (act) chunk_fma<NU>(wt, V, T, H, NG, grp, j, kc, kn, acc);
     }
 }
 
@@ -119,6 +175,7 @@ __device__ __forceinline__ int ce_count(const HeadArgs& A) {
     return n;
 }
 
+template <int NU>
 __global__ void __launch_bounds__(HB) k_head_fwd(HeadArgs A) {
     TAGAN_LIVE_SEED(A);
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -129,14 +186,14 @@ __global__ void __launch_bounds__(HB) k_head_fwd(HeadArgs A) {
     float lsum = 0.f;
     for (int b = 0; b < A.B; ++b) {
         float* sv = A.saved + (int64_t)b * saved_floats(T, H);
-        for (int i = tid; i < T * H; i += HB) L.xs[i] = b == 0 ? A.x0[i] : 0.f;
+        copy_in(L.xs, b == 0 ? A.x0 : nullptr, T * H);
         // z_t = tanh(W1 x_t + b1)
-        float acc[HU];
-        xw_t(A.W1, L.xs, L.wt, T, H, NG, act, grp, j, acc);
+        float acc[NU];
+        xw_chunks<true, NU>(A.W1, L.xs, L.wt, T, H, NG, act, grp, j, acc);
         if (act) {
             const float bj = A.b1[j];
 #pragma unroll
-            for (int u = 0; u < HU; ++u) {
+            for (int u = 0; u < NU; ++u) {
                 const int t = grp + NG * u;
                 if (t < T) L.zs[t * H + j] = tanhf(acc[u] + bj);
             }
@@ -253,6 +310,7 @@ __global__ void __launch_bounds__(HB) k_head_fwd(HeadArgs A) {
         A.loss[0] = A.loss_kind == 1 ? lsum / (float)(A.B * C) : lsum / (float)ce_count(A);
 }
 
+template <int NU>
 __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
     TAGAN_LIVE_SEED(A);
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -265,7 +323,8 @@ __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
     for (int b = 0; b < A.B; ++b) {
         const bool first = b == 0;
         const float* sv = A.saved + (int64_t)b * saved_floats(T, H);
-        for (int i = tid; i < T * H; i += HB) { L.xs[i] = first ? A.x0[i] : 0.f; L.zs[i] = sv[i]; }
+        copy_in(L.xs, first ? A.x0 : nullptr, T * H);
+        copy_in(L.zs, sv, T * H);
         for (int t = tid; t < T; t += HB) L.va[t] = sv[T * H + t];
         if (tid < H) L.vp[tid] = sv[T * H + T + tid];
         if (tid == 0) {   // dlogits of this row
@@ -394,36 +453,11 @@ __global__ void __launch_bounds__(HB) k_head_bwd(HeadArgs A) {
                 }
             }
             // dx_t[k] = a_t dpooled_k + Σ_jj dpre_t,jj W1[jj][k]: W1 rows staged through LDS in chunks of KC
-            float acc[HU];
-#pragma unroll
-            for (int u = 0; u < HU; ++u) acc[u] = 0.f;
-            const int KS = kstep(H);
-            for (int jc = 0; jc < H; jc += KS) {
-                const int jn = min(KS, H - jc);
-                __syncthreads();
-                for (int e = tid; e < jn * H; e += HB) L.wt[(e / H) * (H + 1) + e % H] = A.W1[(int64_t)jc * H + e];
-                __syncthreads();
-                if (act) {
-                    for (int kk = 0; kk < jn; kk += 4) {   // four rows per float4 read of dpre (jc, jn, H % 4 == 0)
-                        const float w0 = L.wt[kk * (H + 1) + j], w1 = L.wt[(kk + 1) * (H + 1) + j];
-                        const float w2 = L.wt[(kk + 2) * (H + 1) + j], w3 = L.wt[(kk + 3) * (H + 1) + j];
-#pragma unroll
-                        for (int u = 0; u < HU; ++u) {
-                            const int t = grp + NG * u;
-                            if (t < T) {
-                                const float4 z = *reinterpret_cast<const float4*>(L.zs + t * H + jc + kk);
-                                acc[u] = fmaf(z.x, w0, acc[u]);
-                                acc[u] = fmaf(z.y, w1, acc[u]);
-                                acc[u] = fmaf(z.z, w2, acc[u]);
-                                acc[u] = fmaf(z.w, w3, acc[u]);
-                            }
-                        }
-                    }
-                }
-            }
+            float acc[NU];
+            xw_chunks<false, NU>(A.W1, L.zs, L.wt, T, H, NG, act, grp, j, acc);
             if (act) {
 #pragma unroll
-                for (int u = 0; u < HU; ++u) {
+                for (int u = 0; u < NU; ++u) {
                     const int t = grp + NG * u;
                     if (t < T) A.dx0[(int64_t)t * H + j] = L.va[t] * L.vg[j] + acc[u];
                 }
@@ -437,17 +471,39 @@ size_t head_lds(int T, int H) {
     return (size_t)(2 * T * H + kstep(H) * (H + 1) + HB + 2 * 128 + 4 * 256 + 16 + 32) * sizeof(float);
 }
 
-int head_lds_optin(size_t bytes) {
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// steps per thread in the [T, H] products (ceil(T / NG)) rounded up to the kernels' template argument 1, 2, 4 or 8
+int head_nu(int T, int H) {
+    const int ng = HB / H, n = (T + ng - 1) / ng;
+    return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : 8;
+}
+
+template <int NU>
+int head_optin_nu() {
     static bool done = false;
-    if (done || bytes <= 64 * 1024) return TAGAN_OK;
-    hipError_t e1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_head_fwd),
+    if (done) return TAGAN_OK;
+    hipError_t e1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_head_fwd<NU>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_head_bwd),
+    hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_head_bwd<NU>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     TAGAN_REQUIRE(e1 == hipSuccess && e2 == hipSuccess, TAGAN_ERR_LAUNCH, "head: LDS opt-in failed");
     done = true;
     return TAGAN_OK;
 }
+
+int head_lds_optin(size_t bytes, int nu) {
+    if (bytes <= 64 * 1024) return TAGAN_OK;
+    return nu == 1 ? head_optin_nu<1>() : nu == 2 ? head_optin_nu<2>() : nu == 4 ? head_optin_nu<4>() : head_optin_nu<8>();
+}
+
+#define TAGAN_HEAD_LAUNCH(KERN, NU, LDS, STREAM, ARGS)                                       \
+    do {                                                                                  \
+        if ((NU) == 1) KERN<1><<<1, HB, LDS, STREAM>>>(ARGS);                             \
+        else if ((NU) == 2) KERN<2><<<1, HB, LDS, STREAM>>>(ARGS);                        \
+        else if ((NU) == 4) KERN<4><<<1, HB, LDS, STREAM>>>(ARGS);                        \
+        else KERN<8><<<1, HB, LDS, STREAM>>>(ARGS);                                       \
+    } while (0)
 
 }  // namespace
 }  // namespace tagan
@@ -474,13 +530,16 @@ int tagan_head_fwd(int32_t B, int32_t T, int32_t H, int32_t C, const float* x0, 
     TAGAN_REQUIRE(loss_kind >= 0 && loss_kind <= 2 && (loss_kind == 0 || (labels && loss)), TAGAN_ERR_ARG,
                   "head_fwd: loss_kind %d", loss_kind);
     TAGAN_REQUIRE(p_drop >= 0.f && p_drop < 1.f, TAGAN_ERR_ARG, "head_fwd: p_drop");
+    TAGAN_REQUIRE(aligned16(W1) && aligned16(Wc1) && aligned16(x0), TAGAN_ERR_ARG,
+                  "head_fwd: W1, Wc1 and x0 must be 16-byte aligned");
     HeadArgs A{};
     A.B = B; A.T = T; A.H = H; A.C = C; A.x0 = x0; A.W1 = W1; A.b1 = b1; A.w2 = w2; A.Wc1 = Wc1; A.bc1 = bc1;
     A.lng = ln_w; A.lnb = ln_b; A.eps = eps; A.Wc2 = Wc2; A.bc2 = bc2; A.p_drop = p_drop;
     A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed; A.seed_ctr = seed_counter(); A.labels = labels; A.loss_kind = loss_kind;
     A.logits = logits; A.preds = preds; A.loss = loss; A.saved = saved;
-    if (int rc = head_lds_optin(head_lds(T, H))) return rc;
-    k_head_fwd<<<1, HB, head_lds(T, H), as_stream(stream)>>>(A);
+    const int nu = head_nu(T, H);
+    if (int rc = head_lds_optin(head_lds(T, H), nu)) return rc;
+    TAGAN_HEAD_LAUNCH(k_head_fwd, nu, head_lds(T, H), as_stream(stream), A);
     TAGAN_CHECK_LAUNCH("head_fwd");
     return TAGAN_OK;
 }
@@ -497,14 +556,17 @@ int tagan_head_bwd(int32_t B, int32_t T, int32_t H, int32_t C, const float* x0, 
                   db1 && dw2 && dWc1 && dbc1 && dln_w && dln_b && dWc2 && dbc2, TAGAN_ERR_ARG, "head_bwd: bad args");
     TAGAN_REQUIRE(loss_kind >= 0 && loss_kind <= 2 && (loss_kind == 0 || labels), TAGAN_ERR_ARG,
                   "head_bwd: loss_kind %d", loss_kind);
+    TAGAN_REQUIRE(aligned16(W1) && aligned16(Wc1) && aligned16(x0), TAGAN_ERR_ARG,
+                  "head_bwd: W1, Wc1 and x0 must be 16-byte aligned");
     HeadArgs A{};
     A.B = B; A.T = T; A.H = H; A.C = C; A.x0 = x0; A.W1 = W1; A.w2 = w2; A.Wc1 = Wc1; A.lng = ln_w; A.lnb = ln_b;
     A.Wc2 = Wc2; A.p_drop = p_drop; A.inv_keep = 1.f / (1.f - p_drop); A.seed = seed; A.seed_ctr = seed_counter(); A.labels = labels;
     A.loss_kind = loss_kind; A.logits = (float*)logits; A.preds = (float*)preds; A.saved = (float*)saved;
     A.g_loss = g_loss; A.g_logits = g_logits; A.g_preds = g_preds; A.dx0 = dx0; A.dW1 = dW1; A.db1 = db1;
     A.dw2 = dw2; A.dWc1 = dWc1; A.dbc1 = dbc1; A.dlng = dln_w; A.dlnb = dln_b; A.dWc2 = dWc2; A.dbc2 = dbc2;
-    if (int rc = head_lds_optin(head_lds(T, H))) return rc;
-    k_head_bwd<<<1, HB, head_lds(T, H), as_stream(stream)>>>(A);
+    const int nu = head_nu(T, H);
+    if (int rc = head_lds_optin(head_lds(T, H), nu)) return rc;
+    TAGAN_HEAD_LAUNCH(k_head_bwd, nu, head_lds(T, H), as_stream(stream), A);
     TAGAN_CHECK_LAUNCH("head_bwd");
     return TAGAN_OK;
 }
