@@ -414,6 +414,7 @@ int tagan_sgemm_nt_ln_bwd(int32_t a_dtype, int64_t M, int32_t H, int32_t K, cons
  * kept for the backward.  One workgroup per call.  Backward: any of g_loss [1] / g_logits [B, C] /
  * g_preds [B, C] (the incoming gradients) may be NULL; writes dx0 [T, H] and every parameter gradient.
  * Supported: tagan_head_supported(T, H, C) (H <= 256, H % 4 == 0, T <= 128, C <= 16, T·H <= 8192).
+ * x0, W1 and Wc1 must be 16-byte aligned (read as float4 runs; TAGAN_ERR_ARG before any launch otherwise).
  * ------------------------------------------------------------------------- */
 int tagan_head_supported(int32_t T, int32_t H, int32_t C);
 size_t tagan_head_saved_floats(int32_t B, int32_t T, int32_t H);

@@ -129,6 +129,12 @@ def test_argument_validation_reports_errors():
     rc = L.tagan_geo_attn_fwd(0, 0, ctypes.byref(g), 4, 16, None, None, None, 64, None, 1.5, 0, None, None, None,
                               None, 0, None)
     assert rc == -1 and b"p_drop" in L.tagan_last_error()
+    # the head kernels read x0, W1 and Wc1 as float4 runs: a pointer off 16 bytes is refused before any launch
+    a, odd = 0x10000, 0x10004
+    for W1 in (odd, a):
+        x0 = a if W1 == odd else odd
+        rc = L.tagan_head_fwd(1, 32, 128, 1, x0, W1, a, a, a, a, a, a, 1e-5, a, a, 0.0, 0, None, 0, a, a, None, a, None)
+        assert rc == -1 and b"16-byte aligned" in L.tagan_last_error()
 
 
 def test_no_cpu_path():
