@@ -212,7 +212,10 @@ class FusedHeadFn(torch.autograd.Function):
         preds = torch.empty(B, C, device=dev)
         loss = torch.empty(1, device=dev) if loss_kind else None
         saved = torch.empty(int(L.tagan_head_saved_floats(B, T, H)), device=dev)
+        # x0, W1, Wc1 go to the kernel as float4 runs (tagan_head_fwd refuses pointers off 16 bytes): a view at an
+        # odd offset is copied
         ps = [t.detach().contiguous() for t in (x0, W1, b1, w2, Wc1, bc1, lnw, lnb, Wc2, bc2)]
+        ps = [t.clone() if i in (0, 1, 4) and t.data_ptr() % 16 else t for i, t in enumerate(ps)]
         check(L.tagan_head_fwd(B, T, H, C, *[ptr(t) for t in ps[:8]], float(eps), ptr(ps[8]), ptr(ps[9]),
                                float(p_drop), seed, ptr(labels), int(loss_kind), ptr(logits), ptr(preds), ptr(loss),
                                ptr(saved), stream_of(x0)), "tagan_head_fwd")

@@ -147,3 +147,26 @@ def test_fused_head_in_model_matches_module_path(dev):
         torch.testing.assert_close(a, b, atol=ATOL, rtol=RTOL)
     for k in res[True][4]:
         torch.testing.assert_close(res[True][4][k], res[False][4][k], atol=ATOL, rtol=RTOL, msg=k)
+
+
+def test_fused_head_misaligned_pooled_view(dev):
+    """A pooled [T, H] view 4 bytes into its storage (the kernels read x0 as float4 runs): the wrapper copies it, and
+    the results equal the aligned call's bit for bit."""
+    from tagan_amd.layers.classification import fused_head
+    T, H = 32, 128
+    m = _module(H, 1, 0.0, seed=3).to(dev).train()
+    g = torch.Generator().manual_seed(9)
+    base = (torch.randn(T * H + 1, generator=g) * 0.5).to(dev)
+    odd = base[1:].view(T, H).detach().requires_grad_()
+    assert odd.data_ptr() % 16 != 0
+    even = odd.detach().clone().requires_grad_()
+    labels = torch.ones(1, device=dev)
+    outs = []
+    for x in (odd, even):
+        m.zero_grad()
+        logits, preds, loss = fused_head(m, x, 1, labels, 1, seed=1)
+        loss.backward()
+        outs.append((logits.detach().clone(), loss.detach().clone(), x.grad.clone(),
+                     m.classification_head.attention[0].weight.grad.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
