@@ -906,13 +906,13 @@ __global__ void __launch_bounds__(V3_BLK * WPH) k_tattn_bwd_v3(TArgs A, const fl
 // in LDS once.  MFMA work per unit: 8·TT²·DT instructions forward, 20·TT²·DT backward.
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-// Build-time knobs (A/B builds, tools/runs/build_v4_variants.sh + v4_variants.sh).  Measured at C2 / C4
-// (fwd, bwd ms): register prefetch of the next row (PREFETCH=1, 2 waves/SIMD in the backward) vs
-// loads at the row's start with the backward held to 3 waves/SIMD (PREFETCH=0, WPE_B=3) are within
-// run-to-run noise (+-3 %); the default is the lighter one.  NOHOIST re-derives the lane indices per
+// Build-time knobs (A/B builds: make variant, tools/runs/r4tv.sh / r4tv2.sh).  Register prefetch of the next
+// row (PREFETCH=1): the C2 backward 0.337 -> 0.308 ms in bf16 storage and 0.352 -> 0.344 ms in fp32
+// (profiles/r4tv_c2_tattn_v4_knobs.txt; round 2 had measured the fp32 kernels within noise), so it is the
+// default; 2 or 4 waves / EU instead of 3 (WPE_B) are within noise.  NOHOIST re-derives the lane indices per
 // row (no hoisted per-element constants); SPLIT prefetches only Q, K, LSE in the backward.
 #ifndef TAGAN_V4_PREFETCH
-#define TAGAN_V4_PREFETCH 0
+#define TAGAN_V4_PREFETCH 1
 #endif
 #ifndef TAGAN_V4_WPE_F
 #define TAGAN_V4_WPE_F 1

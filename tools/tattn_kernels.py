@@ -31,14 +31,16 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--causal", type=int, default=0)
     ap.add_argument("--keep", type=int, default=1, help="dropout keep-bit cache between fwd and bwd (as the model)")
+    ap.add_argument("--bf16", action="store_true", help="bf16 storage of q, k, v, out, dout, dq, dk, dv (the bf16 step)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     N, _E, T, H, heads = synthetic.CONFIGS[a.config][:5]
     d = H // heads
     g = torch.Generator(device=dev).manual_seed(3)
-    qkv = torch.randn(T, N, 3 * H, device=dev, generator=g)
-    out = torch.empty(T, N, H, device=dev)
-    dout = torch.randn(T, N, H, device=dev, generator=g)
+    dt = torch.bfloat16 if a.bf16 else torch.float32
+    qkv = torch.randn(T, N, 3 * H, device=dev, generator=g).to(dt)
+    out = torch.empty(T, N, H, device=dev, dtype=dt)
+    dout = torch.randn(T, N, H, device=dev, generator=g).to(dt)
     dqkv = torch.empty_like(qkv)
     lse = torch.empty(N, heads, T, device=dev)
     table = torch.randn(heads, 2 * T - 1, device=dev, generator=g) * 0.1
@@ -47,7 +49,8 @@ def main():
     wsb = L.tagan_temporal_attn_bwd_workspace(N, T, heads, d)
     ws = torch.empty(max(int(wsb), 1), dtype=torch.uint8, device=dev)
     sp = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    b, db, es = qkv.data_ptr(), dqkv.data_ptr(), 4
+    b, db, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
+    code = 1 if a.bf16 else 0
     sr, st = 3 * H, N * 3 * H
 
     kb = int(L.tagan_temporal_attn_keep_bytes(N, T, heads, d, a.causal, 0, 0, a.p)) if a.keep else 0
@@ -55,7 +58,7 @@ def main():
     written = ctypes.c_int32(0)
 
     def fwd():
-        _lib.check(L.tagan_temporal_attn_fwd_keep(0, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, st,
+        _lib.check(L.tagan_temporal_attn_fwd_keep(code, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, st,
                                                   _lib.ptr(table), None, 0, None, 0, 0, a.causal, a.p, 99,
                                                   _lib.ptr(out), H, N * H, _lib.ptr(lse), None,
                                                   _lib.ptr(keep) if kb else None, kb, ctypes.byref(written), sp),
@@ -63,7 +66,7 @@ def main():
 
     def bwd():
         kp = _lib.ptr(keep) if written.value else None
-        _lib.check(L.tagan_temporal_attn_bwd_keep(0, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, st,
+        _lib.check(L.tagan_temporal_attn_bwd_keep(code, N, T, heads, d, b, b + H * es, b + 2 * H * es, sr, st,
                                                   _lib.ptr(table), None, 0, None, 0, 0, a.causal, a.p, 99,
                                                   _lib.ptr(out), H, N * H, _lib.ptr(lse), _lib.ptr(dout), H, N * H,
                                                   db, db + H * es, db + 2 * H * es, sr, st, _lib.ptr(dtable), None,
@@ -85,14 +88,14 @@ def main():
         tf += ev[0].elapsed_time(ev[1])
         tb += ev[1].elapsed_time(ev[2])
     tf, tb = tf / a.reps, tb / a.reps
-    unit = N * T * H * 4
+    unit = N * T * H * es
     bf = 4 * unit + N * heads * T * 4
     v4 = os.environ.get("TAGAN_TATTN_V4", "1") != "0" and T <= 32 and d in (16, 32)
     v5 = os.environ.get("TAGAN_TATTN_V5", "1") != "0" and 16 < T <= 128 and d in (16, 32)
     bb = (7 if (v4 or v5) else 8) * unit + N * heads * T * 4   # v4/v5 take delta from P·dP and never read O
     mm = 2.0 * T * T * d * N * heads   # flops of one T x T x d product over all units
     chk = [float(out.double().abs().sum()), float(dqkv.double().abs().sum()), float(dtable.double().abs().sum())]
-    print(json.dumps({"lib": os.environ.get("TAGAN_LIB", "default"), "config": a.config, "rows": N, "T": T,
+    print(json.dumps({"lib": os.environ.get("TAGAN_LIB", "default"), "config": a.config, "dtype": "bf16" if a.bf16 else "f32", "rows": N, "T": T,
                       "heads": heads, "d": d, "p": a.p, "keep_bits": bool(written.value), "ms_fwd": round(tf, 4), "ms_bwd": round(tb, 4),
                       "gbs_fwd": round(bf / tf / 1e6, 1), "gbs_bwd": round(bb / tb / 1e6, 1),
                       "frac_hbm": round((bf + bb) / (tf + tb) / 1e6 / bench.HBM_PEAK_GBS, 4),
