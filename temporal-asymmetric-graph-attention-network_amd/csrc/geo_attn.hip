@@ -1011,13 +1011,18 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_generic(GeoArgs A) {
 // Fast path: H in {32, 64, 128, 256}, d = 4*LPH with LPH a power of two.  A lane owns FPL
 // features: FPL = 8 (LPR = H/8 lanes per chunk group) where d % 8 == 0 and H >= 64 for the
 // passes TAGAN_GEO_FPL_* select, else 4.  Measured at C2/C4 (tools/geo_kernels.py):
-// the forward gains from 8 (more chunks per wave in flight); the backward passes, whose
-// register footprint at FPL = 8 halves the occupancy, do not at C2.
+// the forward gains from 8 (more chunks per wave in flight); the fp32 backward passes, whose
+// register footprint at FPL = 8 halves the occupancy, do not (C2 0.74 vs 0.755 ms); in bf16 storage
+// they do: 16-B instead of 8-B loads per lane, C2 bwd 0.63 -> 0.53 ms, C4 83.5 -> 76.1 ms
+// (profiles/r4g8_geo_fpl_bwd_ab.txt).
 #ifndef TAGAN_GEO_FPL_FWD
 #define TAGAN_GEO_FPL_FWD 8
 #endif
 #ifndef TAGAN_GEO_FPL_BWD
 #define TAGAN_GEO_FPL_BWD 4
+#endif
+#ifndef TAGAN_GEO_FPL_BWD_BF16
+#define TAGAN_GEO_FPL_BWD_BF16 8
 #endif
 
 enum Pass { P_FWD, P_BWD_ROW, P_BWD_COL, P_ALPHA, P_BWD_DELTA, P_BWD_ROW_DS };
@@ -1030,8 +1035,8 @@ int pick_lpr(int H, int d) {   // nonzero = fast path
     return 0;
 }
 
-int pick_fpl(int H, int d, Pass pass) {
-    const int want = pass == P_FWD ? TAGAN_GEO_FPL_FWD : TAGAN_GEO_FPL_BWD;
+int pick_fpl(int H, int d, Pass pass, bool bf16) {
+    const int want = pass == P_FWD ? TAGAN_GEO_FPL_FWD : bf16 ? TAGAN_GEO_FPL_BWD_BF16 : TAGAN_GEO_FPL_BWD;
     if (want == 8 && d % 8 == 0 && ((d / 8) & (d / 8 - 1)) == 0 && (H == 64 || H == 128 || H == 256)) return 8;
     return 4;
 }
@@ -1067,7 +1072,7 @@ int launch_metric(Pass pass, int lpr, const GeoArgs& A, hipStream_t s, float* al
         k_geo_alpha<METRIC><<<gg, BLK, 0, s>>>(A, alpha);
         return TAGAN_OK;
     }
-    const int fpl = lpr ? pick_fpl(A.H, A.d, pass) : 0;
+    const int fpl = lpr ? pick_fpl(A.H, A.d, pass, A.bf16 != 0) : 0;
     lpr = lpr ? A.H / fpl : 0;
     if (fpl == 8) {
         switch (lpr) {
@@ -1189,7 +1194,9 @@ BwdWs bwd_ws(const tagan_graph* g, int heads, int d) {
     if (lpr) {
         GeoArgs tmp{};
         tmp.g = *g;
-        nprm = std::max<int64_t>(nprm, chunk_blocks(tmp, H / pick_fpl(H, d, P_BWD_ROW)));
+        // the row pass's partial rows under either storage type (the workspace query does not know it)
+        nprm = std::max<int64_t>(nprm, chunk_blocks(tmp, H / pick_fpl(H, d, P_BWD_ROW, false)));
+        nprm = std::max<int64_t>(nprm, chunk_blocks(tmp, H / pick_fpl(H, d, P_BWD_ROW, true)));
     }
     w.prm = take((size_t)nprm * heads * 4);
     w.pv = take(lpr ? (size_t)g->part_cap * H * 4 : 0);
@@ -1342,7 +1349,7 @@ int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t head
     }
     if (dmetric_param) {
         if (want_prm) {
-            const int64_t nparts = lpr ? chunk_blocks(A, H / pick_fpl(H, head_dim, P_BWD_ROW)) : g->n_nodes;
+            const int64_t nparts = lpr ? chunk_blocks(A, H / pick_fpl(H, head_dim, P_BWD_ROW, A.bf16 != 0)) : g->n_nodes;
             k_reduce_partials<<<heads, BLK, 0, s>>>(A.prm_partial, nparts, heads, dmetric_param);
             TAGAN_CHECK_LAUNCH("geo_attn_bwd_reduce");
         } else {
