@@ -18,18 +18,34 @@ import torch
 import torch.distributed as dist
 
 
-# ProcessGroupNCCL's per-device CUDA-event cache (on by default in this torch) hands a retired collective's end event
-# to the next collective.  With the step's all-reduce captured into a HIP graph, such an event can end up recorded in
-# the capturing stream while the watchdog thread still polls it through an earlier Work: the poll then fails with
-# hipErrorCapturedEvent and the watchdog aborts the process (seen once in five round-3 suites).  With the cache off
-# every Work owns its event, so an event the watchdog polls is never recorded by a capture.  The flag is read when a
-# process group is constructed: it must be set before init_process_group / new_group.
+# Capturing a collective while a process group is live.  ProcessGroupNCCL's watchdog thread polls the
+# end event of every eager collective's Work (``hipEventQuery``) until it has seen it complete and dropped the Work
+# from its list -- up to one poll period (100 ms) after the device finished it.  A collective issued with
+# async_op=False runs on, and records its end event on, the CALLER's current stream; GraphedStep warms up on the very
+# stream it then captures.  HIP answers a query of an event whose recording stream is capturing with
+# hipErrorCapturedEvent -- even when the record itself was eager (tools/captured_event_probe.py shows it without any
+# process group) -- and the watchdog treats that as fatal.  So an eager Work still on the watchdog's list when the
+# capture starts aborts the process whenever a poll lands inside the capture: a timing race (once in ~5 suites).
+# ``retire_pending_works`` removes it: it returns only when every RCCL group's watchdog list is empty
+# (ProcessGroupNCCL::waitForPendingWorks), so no event the watchdog can poll was recorded on the capturing stream.
+#
+# The event cache is switched off too (independent of the race): with it on, a retired Work's end event is handed to
+# the next collective -- the captured one -- so one event object would be shared between a graph node and later
+# eager Works.  The flag is read when a process group is constructed: it must be set before init_process_group.
 EVENT_CACHE_ENV = "TORCH_NCCL_CUDA_EVENT_CACHE"
+_graph_safe_groups = False   # set by init_process_group: the groups of this process were built with the cache off
 
 
 def graph_safe_env() -> None:
     """Switch ProcessGroupNCCL's event recycling off for the process groups created from here on."""
+    global _graph_safe_groups
     os.environ[EVENT_CACHE_ENV] = "0"
+    _graph_safe_groups = True
+
+
+def graph_safe_groups() -> bool:
+    """True when this process's groups were created after ``graph_safe_env()`` (with the event cache off)."""
+    return _graph_safe_groups
 
 
 def init_process_group(backend: str, **kw) -> None:
@@ -37,6 +53,34 @@ def init_process_group(backend: str, **kw) -> None:
     group created with ``new_group`` reads the same flag)."""
     graph_safe_env()
     dist.init_process_group(backend, **kw)
+
+
+def nccl_groups() -> list:
+    """Every live process group whose backend is RCCL ("nccl")."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return []
+    out = []
+    for pg in list(dist.distributed_c10d._world.pg_map.keys()):
+        try:
+            if "nccl" in str(dist.get_backend(pg)).lower():
+                out.append(pg)
+        except Exception:
+            continue
+    return out
+
+
+def retire_pending_works(device=None) -> int:
+    """Drain the device, then block until every RCCL group's watchdog has retired all of its eager Works
+    (``ProcessGroup._wait_for_pending_works``: returns once the watchdog's work list is empty; the watchdog holds
+    the list's mutex while it polls, so after the return it polls no earlier event).  Returns the number of groups
+    waited on.  Call it right before capturing a graph on a stream that eager collectives have used."""
+    groups = nccl_groups()
+    if not groups:
+        return 0
+    torch.cuda.synchronize(device)
+    for pg in groups:
+        pg._wait_for_pending_works()
+    return len(groups)
 
 
 def _staged(t: torch.Tensor, group) -> bool:

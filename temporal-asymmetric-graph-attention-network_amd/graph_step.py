@@ -23,7 +23,6 @@ There is deliberately no split form (an eager segment between two captured ones)
 that form faulted and why the collective lives inside the one graph instead.
 """
 import ctypes
-import os
 from typing import Callable
 
 import torch
@@ -33,13 +32,8 @@ from ._lib import check, lib, ptr
 
 def _nccl_live() -> bool:
     """A process group with an RCCL ("nccl") backend is initialised (its watchdog thread polls work events)."""
-    import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()):
-        return False
-    try:
-        return "nccl" in str(dist.get_backend()).lower()
-    except Exception:
-        return False
+    from .distributed import nccl_groups
+    return bool(nccl_groups())
 
 
 class GraphedStep:
@@ -69,16 +63,16 @@ class GraphedStep:
         if optimizer is not None:
             optimizer.zero_grad(set_to_none=True)
         if _nccl_live():
-            # the RCCL group's watchdog polls the end events of the warm-up steps' collectives; with ProcessGroupNCCL's
-            # event cache on, a retired Work's event can be handed to the captured all-reduce and recorded in the
-            # capture while an earlier Work of the watchdog still references it (hipErrorCapturedEvent, an abort).
-            # distributed.init_process_group switches the cache off before the group exists; refuse to capture a
-            # collective without that guarantee instead of racing.
-            from .distributed import EVENT_CACHE_ENV
-            if os.environ.get(EVENT_CACHE_ENV) != "0":
-                raise RuntimeError("GraphedStep with a live RCCL process group needs %s=0 set before the group is "
-                                   "created (tagan_amd.distributed.init_process_group does it)" % EVENT_CACHE_ENV)
-            torch.cuda.synchronize(dev)
+            # the warm-up steps' collectives ran on `side` and recorded their end events there; the RCCL watchdog
+            # polls those events until it retires their Works, and a poll of an event whose recording stream is
+            # capturing fails (hipErrorCapturedEvent) and aborts the process.  Wait until the watchdog's lists are
+            # empty before `side` starts capturing (distributed.py).
+            from .distributed import EVENT_CACHE_ENV, graph_safe_groups, retire_pending_works
+            if not graph_safe_groups():
+                raise RuntimeError("GraphedStep with a live RCCL process group needs the group created through "
+                                   "tagan_amd.distributed.init_process_group (%s=0 before the group exists)"
+                                   % EVENT_CACHE_ENV)
+            retire_pending_works(dev)
         self.graph = torch.cuda.CUDAGraph()
         # captured on the warm-up stream: autograd nodes that outlive a warm-up step (a loss the caller kept,
         # AccumulateGrad nodes) then belong to the capture stream, so the backward adds no cross-stream join.

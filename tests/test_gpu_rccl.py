@@ -10,8 +10,9 @@ Each case runs in a child process (``python tests/test_gpu_rccl.py <case>``).  T
 step (``GraphedStep.close``: graph reset first) and then destroy the process group and exit normally -- the order whose
 absence aborted a round-3 suite run after a graph had captured the group's collective.  The
 graph cases create the group through ``tagan_amd.distributed.init_process_group`` (ProcessGroupNCCL's event cache
-off, the deterministic fix of the watchdog's hipErrorCapturedEvent abort).  The parent test asserts the child's exit
-status and its completion marker.
+off) and ``GraphedStep`` waits for the watchdog to retire every eager Work before it captures -- the fix of the
+watchdog's hipErrorCapturedEvent abort, which ``capture_after_eager_collective`` forces open.  The parent test
+asserts the child's exit status and its completion marker.
 """
 import os
 import subprocess
@@ -163,8 +164,49 @@ def _case_graph_step_c2():
     dist.destroy_process_group()
 
 
+def _capture_after_eager_collective():
+    """The watchdog race made deterministic: the warm-up steps' eager all-reduces record their end events on the
+    stream that is captured next, and the capture (only the capture) holds the host for 0.45 s (several 100-ms watchdog polls).  Without
+    ``retire_pending_works`` a Work still on the watchdog's list is polled during the capture and the watchdog aborts
+    the process (hipErrorCapturedEvent); with it, the capture and the replays are clean."""
+    import time
+    import tagan_amd  # noqa: F401
+    from tagan_amd.graph_step import GraphedStep
+    dev = torch.device("cuda:0")
+    _init_nccl(dev, "race")
+    lin = torch.nn.Linear(4, 4).to(dev)
+    x = torch.ones(1 << 14, device=dev)
+    out = torch.empty_like(x)
+
+    def step():
+        out.copy_(x * 2)
+        dist.all_reduce(out)           # eager in the warm-up, captured afterwards
+        if torch.cuda.is_current_stream_capturing():
+            time.sleep(0.45)           # host time inside the capture only: the warm-up's Works stay un-retired
+        return out.sum()
+
+    try:
+        g = GraphedStep(lin, step, warmup=3)
+        try:
+            vals = [float(g()) for _ in range(3)]
+        finally:
+            g.close()
+        assert vals == [2.0 * x.numel()] * 3, vals
+    finally:
+        dist.destroy_process_group()
+
+
+def _case_capture_race_unfixed():
+    """NOT a test: the same case with ``retire_pending_works`` reduced to a device sync (the round-4 state), used by
+    ``tools/runs/r5_watchdog.sh`` to show the abort the fix removes.  Expected: rc -6 / 134, the watchdog message."""
+    import tagan_amd.distributed as D
+    D.retire_pending_works = lambda device=None: torch.cuda.synchronize(device) or 0
+    _capture_after_eager_collective()
+
+
 CASES = {"shard_and_buckets": _case_shard_and_buckets, "graph_step_small": _case_graph_step_small,
-         "graph_step_c2": _case_graph_step_c2}
+         "graph_step_c2": _case_graph_step_c2, "capture_after_eager_collective": _capture_after_eager_collective,
+         "capture_race_unfixed": _case_capture_race_unfixed}
 OK = "RCCL_CASE_OK"
 
 
@@ -188,6 +230,13 @@ def test_rccl_world1_graph_step_c2():
     """The graph-step case at the full C2 workload (10k nodes, 100k Zipf edges per snapshot, 32 snapshots): the size
     at which the round-2 split capture (an eager all-reduce between two captured segments) faulted on replay."""
     _run_case("graph_step_c2", timeout=280)
+
+
+def test_rccl_capture_after_eager_collective():
+    """The capture-time watchdog race forced open: eager collectives on the capture stream right
+    before a capture that holds the host across several watchdog polls.  Passes only because GraphedStep waits for the
+    watchdog to retire every eager Work first."""
+    _run_case("capture_after_eager_collective", timeout=120)
 
 
 if __name__ == "__main__":
