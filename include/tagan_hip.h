@@ -403,6 +403,24 @@ int tagan_sgemm_nt_ln_bwd(int32_t a_dtype, int64_t M, int32_t H, int32_t K, cons
                           const float* gamma, const float* dres, float* dx, float* dgamma, float* dbeta,
                           void* workspace, size_t workspace_bytes, void* stream);
 
+/* tagan_ln2_bwd_out: the start of an attention block's backward in one pass over the rows (H = 128):
+ *   LN2 backward of y = LN(s) [+ LN_s(xs)]:  ds = rstd (g dy - mean(g dy x̂) x̂ - mean(g dy)) [+ LN_s's input gradient]
+ *     -> dres [M, H] fp32; do = dropout(ds) with the forward's mask (p_drop, seed; stream = row, counter = column);
+ *     dgamma, dbeta [, dgamma_s, dbeta_s] = column sums;
+ *   the out projection's gradients from do without storing it: dc = do·W_o [M, H] (c's storage dtype), dw_o = doᵀ·c
+ *     [H, H] and db_o = Σ do [H] (fp32);
+ *   wp_km = tagan_sgemm_wprep(w_o, kmajor = 1, planes); act_dtype = storage of c and dc (TAGAN_BF16 needs planes = 1);
+ *   xs == NULL: no skip LayerNorm.  Fixed-order partial sums (bitwise reproducible); workspace
+ *   tagan_ln2_bwd_out_workspace bytes; M > 0.  Replaces tagan_layernorm_bwd + tagan_sgemm_nt + tagan_sgemm_tn of
+ *   geometric_attention.py:586-596 / temporal_attention.py:1190-1200 (backward). */
+int tagan_ln2_bwd_out_supported(int32_t H, int32_t planes, int32_t act_dtype);
+size_t tagan_ln2_bwd_out_workspace(int64_t M, int32_t H, int32_t skip);
+int tagan_ln2_bwd_out(int32_t act_dtype, int32_t planes, int64_t M, int32_t H, const float* dy, const float* s,
+                      const float* mean, const float* rstd, const float* gamma, float p_drop, uint64_t seed,
+                      const float* xs, const float* mean_s, const float* rstd_s, const float* gamma_s, const void* c,
+                      const void* wp_km, float* dres, void* dc, float* dw_o, float* db_o, float* dgamma, float* dbeta,
+                      float* dgamma_s, float* dbeta_s, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Fused classification head + loss (csrc/head.hip).  Replaces model.py:377-459 after the pooling:
  * graph_features [B, T, H] (row 0 = x0 [T, H], rows 1..B-1 zero, model.py:382-394) ->

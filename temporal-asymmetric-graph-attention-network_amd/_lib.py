@@ -105,6 +105,10 @@ _SIGNATURES = {
     "tagan_sgemm_nt_ln_bwd_workspace": (_sz, [_i64, _i32, _i32]),
     "tagan_sgemm_nt_ln_bwd": (_c.c_int, [_i32, _i64, _i32, _i32, _p, _i64, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _p,
                                          _p, _sz, _p]),
+    "tagan_ln2_bwd_out_supported": (_c.c_int, [_i32, _i32, _i32]),
+    "tagan_ln2_bwd_out_workspace": (_sz, [_i64, _i32, _i32]),
+    "tagan_ln2_bwd_out": (_c.c_int, [_i32, _i32, _i64, _i32, _p, _p, _p, _p, _p, _f32, _u64, _p, _p, _p, _p, _p, _p,
+                                     _p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
     "tagan_head_supported": (_c.c_int, [_i32, _i32, _i32]),
     "tagan_head_saved_floats": (_sz, [_i32, _i32, _i32]),
     "tagan_head_fwd": (_c.c_int, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _f32, _p, _p, _f32, _u64,

@@ -1098,6 +1098,295 @@ __global__ void __launch_bounds__(TNR_COLS * TNR_SLICES) k_sgemm_tn_reduce(const
     }
 }
 
+// ------------------------------------------------------------------------------------------- LN2 backward + out-projection
+// The first three steps of an attention block's backward (geometric_attention.py:586-596, temporal_attention.py:
+// 1190-1200 reversed) in ONE pass over the rows, H = 128:
+//   LN2 backward   ds = rstd (g dy - mean(g dy x̂) x̂ - mean(g dy)) [+ the skip LayerNorm's input gradient] -> dres,
+//                  do = dropout(ds) (the forward's mask: stream = row, counter = column), dγ, dβ [, dγ_s, dβ_s]
+//   dC = do · W_o  (the out-projection input gradient)                                     -> dc
+//   dW_o = doᵀ · c, db_o = Σ do  (its weight and bias gradients)                           -> per-workgroup partials
+// Separately these were a LayerNorm pass (s, dy in; dres, do out), an NT GEMM (do in; dc out) and a TN GEMM (do, c
+// in): 8 row-sized HBM passes.  Here do never reaches HBM: 5 passes (dy, s, c in; dres, dc out).
+// Workgroup: 8 waves over contiguous 32-row tiles (fixed ranges: the partials are summed in workgroup order, bitwise
+// reproducible).  Thread c owns row c >> 4 of the tile and columns 8 (c & 15) + [0, 8) for the row math (the 16 lanes
+// of a DPP row hold a whole row: row sums by butterflies); do and c go to LDS as row-major bf16 planes ([32][H + 16]);
+// wave w then runs the dW_o rows 16 w.. (k_sgemm_tn's transposed reads, the db_o sum against a ones fragment) and the
+// dc columns 16 w.. (B = W_oᵀ fragments in registers, A = do rows straight from the planes).
+struct L2Args {
+    int64_t M;
+    int64_t tiles_per_wg;
+    const float* dy;          // [M, H] gradient of the block output
+    const float* s;           // [M, H] LN2 input (saved by the forward)
+    const float* mean;
+    const float* rstd;
+    const float* gamma;
+    float p_drop, inv_keep;
+    uint64_t seed;
+    const uint64_t* seed_ctr;
+    const float* xs;          // skip branch: LN_s input [M, H], statistics, gamma (null: no skip LayerNorm)
+    const float* mean_s;
+    const float* rstd_s;
+    const float* gamma_s;
+    const void* c;            // [M, H] out-projection input (fp32, or bf16 with ABF)
+    const uint4* wp;          // W_oᵀ fragment planes (tagan_sgemm_wprep(w_o, kmajor = 1))
+    float* dres;              // [M, H] gradient of the block input through the residual (+ skip) path
+    void* dc;                 // [M, H] (fp32, or bf16 with ABF)
+    float* part_w;            // [G][H * H + H]: dW_o | db_o partials (k_sgemm_tn_reduce layout)
+    float* part_ln;           // [G][NPL * H]: dγ | dβ [| dγ_s | dβ_s]
+};
+
+template <int P, bool ABF, bool SK>
+__global__ void __launch_bounds__(512, 1) k_ln2_bwd_out(L2Args g) {
+    constexpr int H = 128, BM = 32, NW = 8, KK = H / 32, KS = H / 16, S = H + 16, PL = BM * S;
+    static_assert(!ABF || P == 1, "bf16 operands have one plane");
+    extern __shared__ uint4 sg_lds[];
+    uint16_t* ldo = reinterpret_cast<uint16_t*>(sg_lds);   // P planes of do [BM][S]
+    uint16_t* lcp = ldo + P * PL;                          // P planes of c
+    float* red = reinterpret_cast<float*>(lcp + P * PL);   // [NW][NPL * H] wave partials of the LN sums (end)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int grp = lane >> 4, li = lane & 15;
+    const int rr = threadIdx.x >> 4, q = threadIdx.x & 15;   // row-math chunk: tile row, 8-column group
+    TAGAN_LIVE_SEED(g);
+
+    // this thread's 8 columns of gamma (and gamma_s)
+    float gm[8], gms[SK ? 8 : 1];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        gm[e] = g.gamma[8 * q + e];
+        if constexpr (SK) gms[e] = g.gamma_s[8 * q + e];
+    }
+    // dc columns 16 w..: B fragments of W_oᵀ
+    bf16x8 wr[KK][P];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+        for (int p = 0; p < P; ++p) wr[kk][p] = __builtin_bit_cast(bf16x8, g.wp[((int64_t)(w * KK + kk) * P + p) * 64 + lane]);
+    bf16x8 ones;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+
+    float dg[8], db[8], dgs[SK ? 8 : 1], dbs[SK ? 8 : 1];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        dg[e] = db[e] = 0.f;
+        if constexpr (SK) dgs[e] = dbs[e] = 0.f;
+    }
+    f32x4 accw[KS], accb = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KS; ++k) accw[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int64_t t0 = (int64_t)blockIdx.x * g.tiles_per_wg;
+    const int64_t t1 = min(t0 + g.tiles_per_wg, (g.M + BM - 1) / BM);
+
+    // the tile's operands of this thread (row rr, columns 8 q..)
+    float4 vdy[2], vs[2], vx[SK ? 2 : 1];
+    float4 vc[ABF ? 1 : 2];
+    uint4 vcb;
+    float mrow = 0.f, rrow = 0.f, mrs = 0.f, rrs = 0.f;
+    auto load = [&](int64_t t) {
+        const int64_t row0 = t * BM + rr;
+        const int64_t r = row0 < g.M ? row0 : g.M - 1;
+        const float* pdy = g.dy + r * H + 8 * q;
+        const float* ps = g.s + r * H + 8 * q;
+        vdy[0] = *reinterpret_cast<const float4*>(pdy);
+        vdy[1] = *reinterpret_cast<const float4*>(pdy + 4);
+        vs[0] = *reinterpret_cast<const float4*>(ps);
+        vs[1] = *reinterpret_cast<const float4*>(ps + 4);
+        if constexpr (ABF) {
+            vcb = *reinterpret_cast<const uint4*>((const uint16_t*)g.c + r * H + 8 * q);
+        } else {
+            const float* pc = (const float*)g.c + r * H + 8 * q;
+            vc[0] = *reinterpret_cast<const float4*>(pc);
+            vc[1] = *reinterpret_cast<const float4*>(pc + 4);
+        }
+        mrow = g.mean[r];
+        rrow = g.rstd[r];
+        if constexpr (SK) {
+            const float* px = g.xs + r * H + 8 * q;
+            vx[0] = *reinterpret_cast<const float4*>(px);
+            vx[1] = *reinterpret_cast<const float4*>(px + 4);
+            mrs = g.mean_s[r];
+            rrs = g.rstd_s[r];
+        }
+    };
+    // transposed fragment of columns [c0, c0 + 16) of a plane (k_sgemm_tn's frag)
+    auto frag = [&](const uint16_t* plane, int c0) {
+        const int qq = li >> 2, p4 = li & 3;
+        const uint16_t* a0 = plane + (4 * grp + qq) * S + c0 + 4 * p4;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 16 * S));
+        const short __attribute__((ext_vector_type(8))) v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, v);
+    };
+
+    if (t0 < t1) load(t0);
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t row = t * BM + rr;
+        const bool live = row < g.M;
+        // ---- LN2 backward of this thread's 8 columns
+        const float d[8] = {vdy[0].x, vdy[0].y, vdy[0].z, vdy[0].w, vdy[1].x, vdy[1].y, vdy[1].z, vdy[1].w};
+        const float sv[8] = {vs[0].x, vs[0].y, vs[0].z, vs[0].w, vs[1].x, vs[1].y, vs[1].z, vs[1].w};
+        float xh[8], gd[8];
+        float c1 = 0.f, c2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            xh[e] = (sv[e] - mrow) * rrow;
+            gd[e] = d[e] * gm[e];
+        }
+        // the LayerNorm kernel's association: (x0 + x1) + (x2 + x3) per float4, then the float4 halves
+        c1 = ((gd[0] * xh[0] + gd[1] * xh[1]) + (gd[2] * xh[2] + gd[3] * xh[3])) +
+             ((gd[4] * xh[4] + gd[5] * xh[5]) + (gd[6] * xh[6] + gd[7] * xh[7]));
+        c2 = ((gd[0] + gd[1]) + (gd[2] + gd[3])) + ((gd[4] + gd[5]) + (gd[6] + gd[7]));
+        c1 = xsum<16>(c1) / (float)H;
+        c2 = xsum<16>(c2) / (float)H;
+        float xsk[SK ? 8 : 1], gsk[SK ? 8 : 1], c1s = 0.f, c2s = 0.f;
+        if constexpr (SK) {
+            const float xv[8] = {vx[0].x, vx[0].y, vx[0].z, vx[0].w, vx[1].x, vx[1].y, vx[1].z, vx[1].w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                xsk[e] = (xv[e] - mrs) * rrs;
+                gsk[e] = d[e] * gms[e];
+            }
+            c1s = ((gsk[0] * xsk[0] + gsk[1] * xsk[1]) + (gsk[2] * xsk[2] + gsk[3] * xsk[3])) +
+                  ((gsk[4] * xsk[4] + gsk[5] * xsk[5]) + (gsk[6] * xsk[6] + gsk[7] * xsk[7]));
+            c2s = ((gsk[0] + gsk[1]) + (gsk[2] + gsk[3])) + ((gsk[4] + gsk[5]) + (gsk[6] + gsk[7]));
+            c1s = xsum<16>(c1s) / (float)H;
+            c2s = xsum<16>(c2s) / (float)H;
+        }
+        const uint32_t key = drop_key(g.seed, (uint64_t)row);
+        float dov[8], dsv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float o = rrow * (gd[e] - c1 * xh[e] - c2);
+            float a = o;
+            if (g.p_drop > 0.f) a = drop_u(key, (uint32_t)(8 * q + e)) >= g.p_drop ? o * g.inv_keep : 0.f;
+            dov[e] = live ? a : 0.f;    // dead rows add nothing to dW_o / db_o
+            float sres = o;
+            if constexpr (SK) sres += rrs * (gsk[e] - c1s * xsk[e] - c2s);
+            dsv[e] = sres;
+            const float dl = live ? d[e] : 0.f;   // dead rows add exact zeros (their operands are row M - 1's)
+            dg[e] += dl * xh[e];
+            db[e] += dl;
+            if constexpr (SK) {
+                dgs[e] += dl * xsk[e];
+                dbs[e] += dl;
+            }
+        }
+        if (live) {
+            float* pr = g.dres + row * H + 8 * q;
+            *reinterpret_cast<float4*>(pr) = make_float4(dsv[0], dsv[1], dsv[2], dsv[3]);
+            *reinterpret_cast<float4*>(pr + 4) = make_float4(dsv[4], dsv[5], dsv[6], dsv[7]);
+        }
+        // The next tile's loads go out here, right after this tile's row math, into the same variables (c is copied
+        // first).  Issued after the plane-writing barriers instead (where the matrix work would cover them better),
+        // the kernel's LN column sums came out nondeterministic at multi-tile workgroups (column 8q + 4 of dgamma,
+        // bf16 planes + skip LayerNorm; tools/ln2_debug_probe.py, profiles/r5d_ln2_probe.txt): the compiler had sunk
+        // the sums' arithmetic below those loads.
+        float4 vc_cur[ABF ? 1 : 2];
+        const uint4 vcb_cur = vcb;
+        if constexpr (!ABF) { vc_cur[0] = vc[0]; vc_cur[1] = vc[1]; }
+        if (t + 1 < t1) load(t + 1);
+        // ---- do and c -> row-major bf16 planes
+        lds_barrier();   // the previous tile's fragments are read
+        {
+            uint32_t pd[4][P], pc[4][P];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) split2<P>(dov[2 * e], dov[2 * e + 1], pd[e]);
+            const uint4 cb = vcb_cur;
+            const float4* cv = vc_cur;
+            if constexpr (ABF) {
+                pc[0][0] = cb.x; pc[1][0] = cb.y; pc[2][0] = cb.z; pc[3][0] = cb.w;
+            } else {
+                split2<P>(cv[0].x, cv[0].y, pc[0]);
+                split2<P>(cv[0].z, cv[0].w, pc[1]);
+                split2<P>(cv[1].x, cv[1].y, pc[2]);
+                split2<P>(cv[1].z, cv[1].w, pc[3]);
+            }
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                *reinterpret_cast<uint4*>(ldo + p * PL + rr * S + 8 * q) = make_uint4(pd[0][p], pd[1][p], pd[2][p], pd[3][p]);
+                *reinterpret_cast<uint4*>(lcp + p * PL + rr * S + 8 * q) = make_uint4(pc[0][p], pc[1][p], pc[2][p], pc[3][p]);
+            }
+        }
+        lds_barrier();
+        // ---- dW_o rows 16 w.., db_o
+        {
+            bf16x8 ya[P];
+#pragma unroll
+            for (int p = 0; p < P; ++p) ya[p] = frag(ldo + p * PL, 16 * w);
+#pragma unroll
+            for (int p = 0; p < P; ++p) accb = mfma(ya[p], ones, accb);
+#pragma unroll
+            for (int k = 0; k < KS; ++k) {
+                bf16x8 xb[P];
+#pragma unroll
+                for (int p = 0; p < P; ++p) xb[p] = frag(lcp + p * PL, 16 * k);
+                accw[k] = mfma_planes<P>(ya, xb, accw[k]);
+            }
+        }
+        // ---- dc columns 16 w.. for the tile's two 16-row halves
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) {
+                bf16x8 a[P];
+#pragma unroll
+                for (int p = 0; p < P; ++p)
+                    a[p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+                                                          ldo + p * PL + (16 * j + li) * S + 32 * kk + 8 * grp));
+                acc = mfma_planes<P>(wr[kk], a, acc);
+            }
+            const int64_t orow = t * BM + 16 * j + li;
+            if (orow < g.M) {
+                const int64_t off = orow * H + 16 * w + 4 * grp;
+                if constexpr (ABF) {
+                    *reinterpret_cast<uint2*>((uint16_t*)g.dc + off) = make_uint2(pk_bf16(acc[0], acc[1]),
+                                                                                  pk_bf16(acc[2], acc[3]));
+                } else {
+                    *reinterpret_cast<f32x4*>((float*)g.dc + off) = acc;
+                }
+            }
+        }
+    }
+    // ---- partials: dW_o | db_o (k_sgemm_tn layout: lane holds rows n = 16 w + 4 grp + r, column k = 16 k + li)
+    float* pw = g.part_w + (int64_t)blockIdx.x * (H * H + H);
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pw[(int64_t)(16 * w + 4 * grp + r) * H + 16 * k + li] = accw[k][r];
+    if (li == 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pw[H * H + 16 * w + 4 * grp + r] = accb[r];
+    // LN sums: lanes l, l ^ 16, l ^ 32, l ^ 48 share columns; then the 8 waves in order through LDS
+    constexpr int NPL = SK ? 4 : 2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float a0 = gsum4(dg[e]), a1 = gsum4(db[e]);
+        float a2 = 0.f, a3 = 0.f;
+        if constexpr (SK) {
+            a2 = gsum4(dgs[e]);
+            a3 = gsum4(dbs[e]);
+        }
+        if (grp == 0) {
+            float* rw = red + w * NPL * H + 8 * q + e;
+            rw[0] = a0;
+            rw[H] = a1;
+            if constexpr (SK) {
+                rw[2 * H] = a2;
+                rw[3 * H] = a3;
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NPL * H; i += NW * 64) {
+        float a = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) a += red[ww * NPL * H + i];
+        g.part_ln[(int64_t)blockIdx.x * NPL * H + i] = a;
+    }
+}
+
 // ------------------------------------------------------------------------------------------- dispatch
 int g_num_cu = 0;
 int num_cu() {
@@ -1174,6 +1463,7 @@ const NtCfg NT_TABLE[] = {
 #undef NT_SETLN
 #undef NT_SET3
 #undef NT_SET1
+
 
 const NtCfg* nt_find(int K, int N, int P, int abf, int cbf, int mode = MODE_PLAIN) {
     for (const NtCfg& c : NT_TABLE)
@@ -1534,5 +1824,77 @@ static int tn_run(int32_t dtype, int64_t M, int32_t N, int32_t K, const void* dy
     k_sgemm_tn_reduce<<<(L + TNR_COLS - 1) / TNR_COLS, TNR_COLS * TNR_SLICES, 0, as_stream(stream)>>>(
         (const float*)ws, (int)G, N, K, dw, lddw, db);
     TAGAN_CHECK_LAUNCH("tagan_sgemm_tn_reduce");
+    return TAGAN_OK;
+}
+
+// ------------------------------------------------------------------------------------------- LN2 backward + out-proj
+namespace tagan {
+namespace {
+typedef void (*l2_fn)(L2Args);
+l2_fn l2_pick(int planes, int abf, int skip) {
+    if (planes == 3 && !abf) return skip ? k_ln2_bwd_out<3, false, true> : k_ln2_bwd_out<3, false, false>;
+    if (planes == 1 && abf) return skip ? k_ln2_bwd_out<1, true, true> : k_ln2_bwd_out<1, true, false>;
+    if (planes == 1 && !abf) return skip ? k_ln2_bwd_out<1, false, true> : k_ln2_bwd_out<1, false, false>;
+    return nullptr;
+}
+size_t l2_lds(int planes, int skip) { return (size_t)2 * planes * 32 * (128 + 16) * 2 + (size_t)8 * (skip ? 4 : 2) * 128 * 4; }
+int64_t l2_groups(int64_t M) {
+    const int64_t tiles = (M + 31) / 32;
+    const int64_t g = num_cu();
+    return tiles < g ? (tiles > 0 ? tiles : 1) : g;
+}
+}  // namespace
+}  // namespace tagan
+
+extern "C" int tagan_ln2_bwd_out_supported(int32_t H, int32_t planes, int32_t act_dtype) {
+    return H == 128 && l2_pick(planes, act_dtype == TAGAN_BF16, 0) != nullptr;
+}
+
+extern "C" size_t tagan_ln2_bwd_out_workspace(int64_t M, int32_t H, int32_t skip) {
+    const int64_t G = l2_groups(M);
+    return (size_t)G * ((size_t)H * H + H + (size_t)(skip ? 4 : 2) * H) * sizeof(float);
+}
+
+extern "C" int tagan_ln2_bwd_out(int32_t act_dtype, int32_t planes, int64_t M, int32_t H, const float* dy,
+                                 const float* s, const float* mean, const float* rstd, const float* gamma, float p_drop,
+                                 uint64_t seed, const float* xs, const float* mean_s, const float* rstd_s,
+                                 const float* gamma_s, const void* c, const void* wp_km, float* dres, void* dc,
+                                 float* dw_o, float* db_o, float* dgamma, float* dbeta, float* dgamma_s,
+                                 float* dbeta_s, void* ws, size_t ws_bytes, void* stream) {
+    const int abf = act_dtype == TAGAN_BF16, skip = xs != nullptr;
+    const l2_fn fn = H == 128 ? l2_pick(planes, abf, skip) : nullptr;
+    TAGAN_REQUIRE(fn, TAGAN_ERR_UNSUPPORTED, "tagan_ln2_bwd_out: no kernel for H=%d planes=%d act dtype %d", H, planes,
+                  act_dtype);
+    TAGAN_REQUIRE(M > 0 && dy && s && mean && rstd && gamma && c && wp_km && dres && dc && dgamma && dbeta &&
+                      p_drop >= 0.f && p_drop < 1.f,
+                  TAGAN_ERR_ARG, "tagan_ln2_bwd_out: bad arguments");
+    TAGAN_REQUIRE(!skip || (mean_s && rstd_s && gamma_s && dgamma_s && dbeta_s), TAGAN_ERR_ARG,
+                  "tagan_ln2_bwd_out: the skip LayerNorm needs its statistics, gamma and gradient outputs");
+    TAGAN_REQUIRE((uintptr_t)dy % 16 == 0 && (uintptr_t)s % 16 == 0 && (uintptr_t)c % 16 == 0 &&
+                      (uintptr_t)dres % 16 == 0 && (uintptr_t)dc % 16 == 0 && (!skip || (uintptr_t)xs % 16 == 0),
+                  TAGAN_ERR_ARG, "tagan_ln2_bwd_out: operands must be 16-byte aligned (dense [M, H] rows)");
+    const size_t need = tagan_ln2_bwd_out_workspace(M, H, skip);
+    TAGAN_REQUIRE(ws && ws_bytes >= need, TAGAN_ERR_ARG, "tagan_ln2_bwd_out: workspace %zu < %zu", ws_bytes, need);
+    const size_t lds = l2_lds(planes, skip);
+    TAGAN_REQUIRE(lds_ok((const void*)fn, lds), TAGAN_ERR_LAUNCH, "tagan_ln2_bwd_out: LDS attribute");
+    const int64_t G = l2_groups(M), tiles = (M + 31) / 32;
+    L2Args g{};
+    g.M = M; g.tiles_per_wg = (tiles + G - 1) / G;
+    g.dy = dy; g.s = s; g.mean = mean; g.rstd = rstd; g.gamma = gamma;
+    g.p_drop = p_drop; g.inv_keep = 1.f / (1.f - p_drop); g.seed = seed; g.seed_ctr = seed_counter();
+    g.xs = xs; g.mean_s = mean_s; g.rstd_s = rstd_s; g.gamma_s = gamma_s;
+    g.c = c; g.wp = (const uint4*)wp_km; g.dres = dres; g.dc = dc;
+    g.part_w = (float*)ws;
+    g.part_ln = (float*)ws + (size_t)G * (H * H + H);
+    hipLaunchKernelGGL(fn, dim3((unsigned)G), dim3(512), lds, as_stream(stream), g);
+    TAGAN_CHECK_LAUNCH("tagan_ln2_bwd_out");
+    const int L = H * H + H;
+    k_sgemm_tn_reduce<<<(L + TNR_COLS - 1) / TNR_COLS, TNR_COLS * TNR_SLICES, 0, as_stream(stream)>>>(
+        g.part_w, (int)G, H, H, dw_o, H, db_o);
+    TAGAN_CHECK_LAUNCH("tagan_ln2_bwd_out (dW_o reduce)");
+    const int npl = skip ? 4 : 2;
+    launch_colsum(g.part_ln, (int)G, 2 * H, dgamma, dbeta, H, as_stream(stream), 1.f, npl * H);
+    if (skip) launch_colsum(g.part_ln + 2 * H, (int)G, 2 * H, dgamma_s, dbeta_s, H, as_stream(stream), 1.f, npl * H);
+    TAGAN_CHECK_LAUNCH("tagan_ln2_bwd_out (LayerNorm sums)");
     return TAGAN_OK;
 }

@@ -322,7 +322,9 @@ def _sg_use(H: int, bf: bool, act: bool) -> bool:
 #   fp32  none 6.99  in 6.82  in+out 6.75  all 6.99   (fp32 "bwd" runs on k_sgemm_nt: its K = 384 three-plane weight
 #                                                      fragments do not fit a row-owner kernel's LDS, 288 KB)
 #   bf16  none 5.62  in 5.50  in+out 5.41  all 5.26
-SG_LN_OPS = {False: frozenset({"in", "out"}), True: frozenset({"in", "out", "bwd"})}
+# "ln2bwd" (round 5): LN2's backward and the out-projection's input / weight / bias gradients in one pass over the
+# rows (tagan_ln2_bwd_out: do never reaches HBM).
+SG_LN_OPS = {False: frozenset({"in", "out", "ln2bwd"}), True: frozenset({"in", "out", "bwd", "ln2bwd"})}
 _SG_LN_OK = {}
 
 
@@ -332,7 +334,10 @@ def _sg_ln_use(H: int, bf: bool, act: bool, op: str) -> bool:
     key = (H, bf, act, op)
     ok = _SG_LN_OK.get(key)
     if ok is None:
-        ok = _SG_LN_OK[key] = sg.ln_supported(H, 1 if bf else 3, act, op)
+        if op == "ln2bwd":
+            ok = _SG_LN_OK[key] = sg.ln2_bwd_out_supported(H, 1 if bf else 3, act)
+        else:
+            ok = _SG_LN_OK[key] = sg.ln_supported(H, 1 if bf else 3, act, op)
     return ok
 
 
@@ -447,12 +452,19 @@ class AttnBlockFn(torch.autograd.Function):
         P = 1 if bf else 3
         adt = torch.bfloat16 if act else torch.float32
         dy2 = dy.reshape(-1, H).contiguous()
-        dres, do, dg2, db2, dbo, dgs, dbs = _ln2_bwd(s2, mean2, rstd2, ln2_w, dy2, skip, x2, lns_w, p_out, seed_out,
-                                                     adt)
-        dc = sg.nt(do, wo_km, H, P, out_dtype=adt)
-        dw_o = sg.tn(do, c, P, want_db=False)[0] if ng[7] else None
+        if _sg_ln_use(H, bf, act, "ln2bwd") and dy2.shape[0] > 0 and c.is_contiguous():
+            # LN2 backward + dC + dW_o + db_o in one pass (do stays on chip)
+            skip_args = (x2, skip[0], skip[1], lns_w) if skip is not None else None
+            dres, dc, dw_o, dbo, dg2, db2, dgs, dbs = sg.ln2_bwd_out(dy2, s2, mean2, rstd2, ln2_w, p_out, seed_out, c,
+                                                                     wo_km, P, skip=skip_args, want_dw=bool(ng[7]))
+        else:
+            dres, do, dg2, db2, dbo, dgs, dbs = _ln2_bwd(s2, mean2, rstd2, ln2_w, dy2, skip, x2, lns_w, p_out,
+                                                         seed_out, adt)
+            dc = sg.nt(do, wo_km, H, P, out_dtype=adt)
+            dw_o = sg.tn(do, c, P, want_db=False)[0] if ng[7] else None
+            del do
         dqkv, dp1, dp2, db_core = core.bwd(qkv, c, saved, dc, ng[1], ng[2], want_bias_sum=bool(ng[6]))
-        del dc, do
+        del dc
         dw_qkv = db_qkv = None
         if ng[5] or (ng[6] and db_core is None):
             if lnf:

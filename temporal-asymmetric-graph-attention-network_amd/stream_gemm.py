@@ -161,3 +161,37 @@ def nt_ln_bwd(a, wp, planes: int, x, mean, rstd, gamma, dres=None):
                                   ptr(rstd), ptr(gamma), ptr(dres), ptr(dx), ptr(dgb[0]), ptr(dgb[1]), ptr(ws), wsb,
                                   stream_of(a)), "tagan_sgemm_nt_ln_bwd")
     return dx, dgb[0], dgb[1]
+
+
+def ln2_bwd_out_supported(H: int, planes: int, act_bf16: bool) -> bool:
+    """tagan_ln2_bwd_out exists for (H, planes, activation storage)."""
+    return bool(lib().tagan_ln2_bwd_out_supported(H, planes, TAGAN_BF16 if act_bf16 else 0))
+
+
+def ln2_bwd_out(dy, s, mean, rstd, gamma, p_drop: float, seed: int, c, wp_km, planes: int, skip=None,
+                want_dw: bool = True):
+    """The LN2 backward + out-projection gradients of an attention block in one pass (tagan_ln2_bwd_out):
+    returns dres [M, H] fp32, dc [M, H] (c's dtype), dw_o [H, H] (None unless ``want_dw``), db_o, dgamma, dbeta,
+    dgamma_s, dbeta_s (the last two None without ``skip`` = (xs, mean_s, rstd_s, gamma_s))."""
+    M, H = dy.shape
+    dev = dy.device
+    for t in (dy, s, c):
+        assert t.is_contiguous() and t.shape == (M, H)
+    dres = torch.empty(M, H, device=dev)
+    dc = torch.empty(M, H, device=dev, dtype=c.dtype)
+    out = torch.empty(5 if skip is not None else 3, H, device=dev)   # db_o, dgamma, dbeta [, dgamma_s, dbeta_s]
+    dw = torch.empty(H, H, device=dev) if want_dw else None
+    xs, ms, rs, gs = skip if skip is not None else (None, None, None, None)
+    if xs is not None:
+        assert xs.is_contiguous() and xs.shape == (M, H)
+    L = lib()
+    wsb = int(L.tagan_ln2_bwd_out_workspace(M, H, int(skip is not None)))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    check(L.tagan_ln2_bwd_out(dtype_code(c), planes, M, H, ptr(dy), ptr(s), ptr(mean), ptr(rstd), ptr(gamma),
+                              float(p_drop), seed, ptr(xs), ptr(ms), ptr(rs), ptr(gs), ptr(c), ptr(wp_km), ptr(dres),
+                              ptr(dc), ptr(dw), ptr(out[0]), ptr(out[1]), ptr(out[2]),
+                              ptr(out[3]) if skip is not None else None, ptr(out[4]) if skip is not None else None,
+                              ptr(ws), wsb, stream_of(dy)), "tagan_ln2_bwd_out")
+    dgs = out[3] if skip is not None else None
+    dbs = out[4] if skip is not None else None
+    return dres, dc, dw, out[0], out[1], out[2], dgs, dbs

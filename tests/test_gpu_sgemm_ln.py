@@ -194,6 +194,132 @@ def test_ln_bwd(M, planes, store, with_dres):
     assert torch.equal(dx, dx2) and torch.equal(dg, dg2) and torch.equal(db, db2)
 
 
+def _ln2_ref(dy, s, ln_w, c, w_o, skip):
+    """fp64 LN2 backward (p_drop = 0) + the out-projection gradients: dres, dc, dw_o, db_o, dg, db, dgs, dbs."""
+    _, m64, rs64 = _ln64(s, ln_w, ln_w, 1e-5)
+    d = dy.double()
+    xh = (s.double() - m64[:, None]) * rs64[:, None]
+    gd = d * ln_w.double()
+    o = rs64[:, None] * (gd - (gd * xh).mean(1, keepdim=True) * xh - gd.mean(1, keepdim=True))
+    dres = o.clone()
+    dgs = dbs = None
+    if skip is not None:
+        xs, gs = skip
+        _, ms, rss = _ln64(xs, gs, gs, 1e-5)
+        xsh = (xs.double() - ms[:, None]) * rss[:, None]
+        gsd = d * gs.double()
+        dres = dres + rss[:, None] * (gsd - (gsd * xsh).mean(1, keepdim=True) * xsh - gsd.mean(1, keepdim=True))
+        dgs, dbs = (d * xsh).sum(0), d.sum(0)
+    cd = c.double()
+    return dres, o @ w_o.double(), o.t() @ cd, o.sum(0), (d * xh).sum(0), d.sum(0), dgs, dbs
+
+
+@pytest.mark.parametrize("M", ROWS)
+@pytest.mark.parametrize("planes,store", [(3, "fp32"), (1, "bf16"), (1, "fp32")])
+@pytest.mark.parametrize("skip", [False, True])
+def test_ln2_bwd_out(M, planes, store, skip):
+    """tagan_ln2_bwd_out (LN2 backward + dC + dW_o + db_o in one pass) against fp64 (no dropout)."""
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    if not sg.ln2_bwd_out_supported(H, planes, store == "bf16"):
+        pytest.skip("no kernel")
+    g, ln_w, _ = _params(dev, 500 + M + planes)
+    dt = torch.bfloat16 if store == "bf16" else torch.float32
+    s = 0.2 + torch.randn(M, H, device=dev, generator=g)
+    dy = torch.randn(M, H, device=dev, generator=g)
+    c = torch.randn(M, H, device=dev, generator=g).to(dt)
+    w_o = torch.randn(H, H, device=dev, generator=g) / H ** 0.5
+    _, m64, rs64 = _ln64(s, ln_w, ln_w, 1e-5)
+    sk = ref_sk = None
+    if skip:
+        xs = torch.randn(M, H, device=dev, generator=g)
+        gs = 1.0 + 0.1 * torch.randn(H, device=dev, generator=g)
+        _, ms, rss = _ln64(xs, gs, gs, 1e-5)
+        sk, ref_sk = (xs, ms.float(), rss.float(), gs), (xs, gs)
+    out = sg.ln2_bwd_out(dy, s, m64.float(), rs64.float(), ln_w, 0.0, 0, c, sg.wprep(w_o, True, planes), planes,
+                         skip=sk)
+    ref = _ln2_ref(dy, s, ln_w, c, w_o, ref_sk)
+    names = ["dres", "dc", "dw_o", "db_o", "dgamma", "dbeta", "dgamma_s", "dbeta_s"]
+    for name, got, want in zip(names, out, ref):
+        if want is None:
+            assert got is None, name
+            continue
+        if planes == 3 or name in ("dres", "dgamma", "dbeta", "dgamma_s", "dbeta_s"):
+            assert _merr(got, want) <= 2e-5 and _nerr(got, want) <= 1e-5, (name, _merr(got, want), _nerr(got, want))
+        else:   # one bf16 plane of do (and c) in the products
+            assert _nerr(got, want) < 1e-2, (name, _nerr(got, want))
+    again = sg.ln2_bwd_out(dy, s, m64.float(), rs64.float(), ln_w, 0.0, 0, c, sg.wprep(w_o, True, planes), planes,
+                           skip=sk)
+    for name, a, b in zip(names, out, again):
+        assert (a is None and b is None) or torch.equal(a, b), name   # fixed-order sums: bitwise reproducible
+
+
+@pytest.mark.parametrize("planes,store", [(3, "fp32"), (1, "bf16")])
+def test_ln2_bwd_out_reproducible_at_c2_rows(planes, store):
+    """320,000 rows (many tiles per workgroup, where a first form's LN sums came out nondeterministic,
+    profiles/r5d_ln2_probe.txt): five calls bitwise equal, dgamma within fp32 accuracy of fp64."""
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    g, ln_w, _ = _params(dev, 31)
+    M = 320000
+    dt = torch.bfloat16 if store == "bf16" else torch.float32
+    s = 0.2 + torch.randn(M, H, device=dev, generator=g)
+    dy = torch.randn(M, H, device=dev, generator=g)
+    c = torch.randn(M, H, device=dev, generator=g).to(dt)
+    w_o = torch.randn(H, H, device=dev, generator=g) / H ** 0.5
+    xs = torch.randn(M, H, device=dev, generator=g)
+    gs = 1.0 + 0.1 * torch.randn(H, device=dev, generator=g)
+    _, m64, rs64 = _ln64(s, ln_w, ln_w, 1e-5)
+    _, ms, rss = _ln64(xs, gs, gs, 1e-5)
+    wp = sg.wprep(w_o, True, planes)
+    runs = [sg.ln2_bwd_out(dy, s, m64.float(), rs64.float(), ln_w, 0.1, 99, c, wp, planes,
+                           skip=(xs, ms.float(), rss.float(), gs)) for _ in range(5)]
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
+    xh = (s.double() - m64[:, None]) * rs64[:, None]
+    assert _merr(runs[0][4], (dy.double() * xh).sum(0)) <= 2e-5
+
+
+@pytest.mark.parametrize("skip", [False, True])
+def test_ln2_bwd_out_matches_unfused_chain_with_dropout(skip):
+    """Same dropout decisions as the standalone LayerNorm backward (stream = row, counter = column), so the fused
+    pass equals tagan_layernorm_bwd [+ skip] -> tagan_sgemm_nt -> tagan_sgemm_tn on the same inputs."""
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    from tagan_amd.fused import ln_bwd, ln_skip_bwd
+    g, ln_w, _ = _params(dev, 91)
+    M = 5003
+    s = torch.randn(M, H, device=dev, generator=g)
+    dy = torch.randn(M, H, device=dev, generator=g)
+    c = torch.randn(M, H, device=dev, generator=g)
+    w_o = torch.randn(H, H, device=dev, generator=g) / H ** 0.5
+    _, m64, rs64 = _ln64(s, ln_w, ln_w, 1e-5)
+    mean, rstd = m64.float(), rs64.float()
+    wp = sg.wprep(w_o, True, 3)
+    if skip:
+        xs = torch.randn(M, H, device=dev, generator=g)
+        gs = 1.0 + 0.1 * torch.randn(H, device=dev, generator=g)
+        _, ms, rss = _ln64(xs, gs, gs, 1e-5)
+        ms, rss = ms.float(), rss.float()
+        dres0, do0, dg0, db0, dbo0, dgs0, dbs0 = ln_skip_bwd(s, mean, rstd, ln_w, xs, ms, rss, gs, dy, 0.1, 4321)
+        got = sg.ln2_bwd_out(dy, s, mean, rstd, ln_w, 0.1, 4321, c, wp, 3, skip=(xs, ms, rss, gs))
+    else:
+        dres0, do0, dg0, db0, dbo0 = ln_bwd(s, mean, rstd, ln_w, dy, None, 0.1, 4321, True, True, True)
+        dgs0 = dbs0 = None
+        got = sg.ln2_bwd_out(dy, s, mean, rstd, ln_w, 0.1, 4321, c, wp, 3)
+    dc0 = sg.nt(do0, wp, H, 3)
+    dw0 = sg.tn(do0, c, 3, want_db=False)[0]
+    want = [dres0, dc0, dw0, dbo0, dg0, db0, dgs0, dbs0]
+    dropped = float((do0 == 0).float().mean())
+    assert 0.05 < dropped < 0.15
+    for name, a, b in zip(["dres", "dc", "dw_o", "db_o", "dgamma", "dbeta", "dgamma_s", "dbeta_s"], got, want):
+        if b is None:
+            assert a is None
+            continue
+        assert _merr(a, b.double()) <= 2e-5, (name, _merr(a, b.double()))
+
+
 def test_ln_supported_shapes():
     _dev()
     from tagan_amd import stream_gemm as sg

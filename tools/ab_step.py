@@ -48,7 +48,7 @@ def main():
         # capture: none, all, default, or a "+"-list of in / out / bwd
         bf = args.precision != "fp32"
         default = DEFAULT_OPS[bf]
-        fused.SG_LN_OPS[bf] = (frozenset() if v == "none" else frozenset({"in", "out", "bwd"}) if v == "all" else
+        fused.SG_LN_OPS[bf] = (frozenset() if v == "none" else frozenset({"in", "out", "bwd", "ln2bwd"}) if v == "all" else
                                default if v == "default" else frozenset(v.replace("+", ",").split(",")))
         fused._SG_LN_OK.clear()
         graphs[v] = bench.graphed(model, opt, cfg, fwd)
