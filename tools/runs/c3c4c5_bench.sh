@@ -1,3 +1,4 @@
+#!/bin/bash
 # C3 (fp32), C4 (fp32) and C5 (bf16 activations, one GPU) bench lines on the current tree: >= 3 warm-ups, >= 5 steps
 set -o pipefail
 cd $GRAFT_REPO_ROOT

@@ -1,3 +1,5 @@
+#!/bin/bash
+# graph-replay checks: the GPU graph tests and repeated replays of the captured C2 step (capture / destroy / re-capture)
 # graph-step robustness: graph tests (warnings shown), the default bench, then a long-replay bench (auto trial)
 set -o pipefail
 cd $GRAFT_REPO_ROOT

@@ -1,3 +1,5 @@
+#!/bin/bash
+# Round 5 (d): dgamma determinism probe (tools/ln2_debug_probe.py) of three k_ln2_bwd_out builds -> profiles/r5d_ln2_probe.txt
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 L=$GRAFT_REPO_ROOT/temporal-asymmetric-graph-attention-network_amd
