@@ -215,7 +215,9 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
     constexpr int CPT = BM * QK / NT;
     static_assert(BM * QK % NT == 0, "tile chunks must divide over the workgroup");
     static_assert(!ABF || P == 1, "bf16 operands have one plane");
-    static_assert(MODE != MODE_LN_IN || (QK == 16 && !ABF), "LN prologue: K = 128 fp32 rows");
+    static_assert(MODE != MODE_LN_IN || ((QK == 16 || QK == 32) && !ABF), "LN prologue: K = 128 or 256 fp32 rows");
+    // LN_IN chunk map: QK consecutive lanes (one or two DPP rows) hold one whole row of x
+    constexpr int LQ = MODE == MODE_LN_IN ? QK : 16;
     constexpr bool EPI = MODE == MODE_LN_OUT || MODE == MODE_LN_BWD;
     constexpr int BUF = P * KK * J * 64;
     extern __shared__ uint4 sg_lds[];
@@ -281,9 +283,9 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
             const int c = i * NT + threadIdx.x;
-            const int rl = MODE == MODE_LN_IN ? (c >> 4) & 15 : c & 15;
-            const int q = MODE == MODE_LN_IN ? c & 15 : (c >> 4) % QK;
-            const int rh = MODE == MODE_LN_IN ? c >> 8 : (c >> 4) / QK;
+            const int rl = MODE == MODE_LN_IN ? (c / LQ) & 15 : c & 15;
+            const int q = MODE == MODE_LN_IN ? c % LQ : (c >> 4) % QK;
+            const int rh = MODE == MODE_LN_IN ? c / (16 * LQ) : (c >> 4) / QK;
             // rows past M reload row M - 1: they only feed output rows that are never stored, and an unconditional
             // load needs no zero-filled destination (a conditional one made the compiler drain every store of the
             // previous tile -- s_waitcnt vmcnt(0) -- before this prefetch could issue)
@@ -307,17 +309,17 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
             const int c = i * NT + threadIdx.x;
-            const int rl = MODE == MODE_LN_IN ? (c >> 4) & 15 : c & 15;
-            const int q = MODE == MODE_LN_IN ? c & 15 : (c >> 4) % QK;
-            const int rh = MODE == MODE_LN_IN ? c >> 8 : (c >> 4) / QK;
+            const int rl = MODE == MODE_LN_IN ? (c / LQ) & 15 : c & 15;
+            const int q = MODE == MODE_LN_IN ? c % LQ : (c >> 4) % QK;
+            const int rh = MODE == MODE_LN_IN ? c / (16 * LQ) : (c >> 4) / QK;
             const int e0 = ((q >> 2) * J + rh) * 64 + 16 * (q & 3) + (rl ^ ((q & 3) + 4 * ((q >> 2) & 3)));
-            if constexpr (MODE == MODE_LN_IN) {   // the 16 lanes of a DPP row hold the whole row
+            if constexpr (MODE == MODE_LN_IN) {   // the LQ lanes of one or two DPP rows hold the whole row
                 float sm = (pf[i][0] + pf[i][1]) + (pf[i][2] + pf[i][3]) + ((pf[i][4] + pf[i][5]) + (pf[i][6] + pf[i][7]));
-                const float mean = xsum<16>(sm) / (float)K;
+                const float mean = xsum<LQ>(sm) / (float)K;
                 float sq = 0.f;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) sq += (pf[i][e] - mean) * (pf[i][e] - mean);
-                const float rstd = 1.f / sqrtf(xsum<16>(sq) / (float)K + g.eps);
+                const float rstd = 1.f / sqrtf(xsum<LQ>(sq) / (float)K + g.eps);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) pf[i][e] = ln_apply(pf[i][e], mean, rstd, lgb[8 * q + e], lgb[K + 8 * q + e]);
                 const int64_t row = t * BM + rh * 16 + rl;
@@ -633,7 +635,8 @@ template <int K, int P, bool ABF, bool CBF, int MODE, int W, int NN = 128>
 __global__ void __launch_bounds__(W * 64) k_rowgemm(NtArgs g) {
     constexpr int N = NN, NS = N / 16, KK = K / 32;
     static_assert(MODE != MODE_LN_IN || (!ABF && K == 128), "LN prologue: fp32 rows of K = 128");
-    static_assert(MODE == MODE_LN_IN || N == 128, "row-wide epilogues: N = 128");
+    static_assert(MODE == MODE_LN_IN || N == 128 || (MODE == MODE_LN_OUT && N == 256 && P == 1),
+                  "row-wide epilogues: N = 128 (LN2 epilogue: also N = 256 with one plane)");
     constexpr int NB = NS * KK * P * 64;             // B fragments (uint4) in LDS
     static_assert(!ABF || P == 1, "bf16 operands have one plane");
     extern __shared__ uint4 sg_lds[];
@@ -1446,13 +1449,28 @@ constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
     nt_cfg<192, 1, 4, 64, 1, ABF, CBF>(64, 2)
 // The LayerNorm-fused forms (H = 128): LN1 prologue of the QKV projection (x fp32 in; qkv fp32, or bf16 in the
 // bf16 activation mode), dropout + residual + LN2 [+ skip LN] epilogue of the out-projection (y fp32), LN1 backward
-// epilogue of the QKV input gradient (dx fp32).
+// epilogue of the QKV input gradient (dx fp32).  At H = 256 (C3, C5) the LN1 prologue (32 lanes per row) and its
+// LN-recomputing weight gradient; LN2 and LN1's backward stay standalone there.
 // (The LN2 epilogue and the one-plane LN1-backward epilogue run on the row-owner kernels, RG_TABLE; the three-plane
 // LN1-backward epilogue lost its A/B -- fp32 step 6.99 vs 6.75 ms, profiles/r3d_ab_step.txt -- and is not built.)
+#ifndef TAGAN_SG_LN256
+#define TAGAN_SG_LN256 1
+#endif
+#if TAGAN_SG_LN256
+// (one plane only: the three-plane C3 form lost its A/B -- C3 fp32 547 vs 540 ms, its LN-recomputing weight gradient
+// re-reads the fp32 x six times, profiles/r5i_h256_ln_ab.txt)
+#define NT_LN256                                                                                             \
+    , nt_cfg<256, 2, 8, 64, 1, false, true, MODE_LN_IN>(768, 1),                                                \
+    nt_cfg<256, 2, 8, 64, 1, false, false, MODE_LN_IN>(768, 1)
+#define TN_LN256 tn_cfg<768, 256, 2, 8, 3, 1, true, true>(1), tn_cfg<768, 256, 2, 8, 3, 1, false, true>(1),
+#else
+#define NT_LN256
+#define TN_LN256
+#endif
 #define NT_SETLN                                                                                             \
     nt_cfg<128, 3, 8, 32, 3, false, false, MODE_LN_IN>(384, 1),                                                 \
     nt_cfg<128, 3, 8, 64, 1, false, true, MODE_LN_IN>(384, 1),                                                  \
-    nt_cfg<128, 3, 8, 64, 1, false, false, MODE_LN_IN>(384, 1)
+    nt_cfg<128, 3, 8, 64, 1, false, false, MODE_LN_IN>(384, 1) NT_LN256
 const NtCfg NT_TABLE[] = {
     NT_SET3,
     NT_SET1(false, false),
@@ -1489,14 +1507,17 @@ constexpr TnCfg tn_cfg(int wg_per_cu) {
 // H = 64: 4-wave workgroups over the whole N.
 #define TN_SETP(P, ABF)                                                                                      \
     tn_cfg<384, 128, 3, 8, 1, P, ABF>(1), tn_cfg<128, 128, 1, 8, 1, P, ABF>(2),                               \
-    tn_cfg<768, 256, 1, 8, 6, P, ABF>(1), tn_cfg<256, 256, 1, 8, 2, P, ABF>(1),                               \
+    tn_cfg<768, 256, (P == 1 ? 2 : 1), 8, (P == 1 ? 3 : 6), P, ABF>(1), tn_cfg<256, 256, 1, 8, 2, P, ABF>(1),   \
     tn_cfg<192, 64, 3, 4, 1, P, ABF>(2), tn_cfg<64, 64, 1, 4, 1, P, ABF>(2)
 const TnCfg TN_TABLE[] = {
     TN_SETP(3, false), TN_SETP(1, false), TN_SETP(1, true),
     tn_cfg<384, 128, 3, 8, 1, 3, false, true>(1),
     tn_cfg<384, 128, 3, 8, 1, 1, true, true>(1),
     tn_cfg<384, 128, 3, 8, 1, 1, false, true>(1),
+    TN_LN256
 };
+#undef NT_LN256
+#undef TN_LN256
 #undef TN_SETP
 const TnCfg* tn_find(int N, int K, int P, int abf, int lnx = 0) {
     for (const TnCfg& c : TN_TABLE)
@@ -1528,6 +1549,10 @@ const RgCfg RG_TABLE[] = {
     rg_cfg<128, 3, false, false, MODE_LN_OUT>(), rg_cfg<128, 1, true, false, MODE_LN_OUT>(),
     rg_cfg<128, 1, false, false, MODE_LN_OUT>(),
     rg_cfg<384, 1, true, false, MODE_LN_BWD, 8>(), rg_cfg<384, 1, false, false, MODE_LN_BWD, 8>(),
+#if TAGAN_SG_LN256
+    // H = 256, one plane (bf16 operands): W_o's planes are 128 KB of LDS, 8 waves per CU
+    rg_cfg<256, 1, true, false, MODE_LN_OUT, 8, 256>(), rg_cfg<256, 1, false, false, MODE_LN_OUT, 8, 256>(),
+#endif
 };
 
 // Row-owner kernels take the LayerNorm-fused N = 128 products only.  The plain products measured faster on the

@@ -292,10 +292,11 @@ SGEMM = os.environ.get("TAGAN_SGEMM", "1") != "0"
 _SG_OK = {}
 
 
-# bf16 operands at H = 256 stay on the library GEMMs: the C5 bf16 step measured 678 ms on the one-plane stream GEMMs
-# against 643 ms on hipBLASLt (same box, profiles/r4p_c345.txt); fp32 (three planes) at H = 256 wins on the stream GEMMs
-# (C3 604 -> 540-566 ms), as does bf16 at H = 128 (C2)
-SG_BF16_MAX_H = 128
+# bf16 operands at H = 256 (C5): since round 5 on the stream GEMMs too -- with LN1 in the QKV projection's prologue, the
+# LN2 epilogue on a one-plane N = 256 row-owner kernel and the 768 x 256 weight gradients over three column groups, the
+# C5 bf16 step measured 608-610 ms against 618 ms on hipBLASLt (profiles/r5k_c5_bf16_ab.txt; round 4's stream path
+# without those lost, 678 vs 643 ms)
+SG_BF16_MAX_H = int(os.environ.get("TAGAN_SG_BF16_MAX_H", "256"))   # A/B knob: 128 puts C5 bf16 on hipBLASLt
 
 
 def _sg_use(H: int, bf: bool, act: bool) -> bool:

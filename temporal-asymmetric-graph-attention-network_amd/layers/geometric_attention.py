@@ -10,10 +10,11 @@ same initial weights.  The forward runs:
   (metric score, edge-softmax, attn-dropout, A·V over the mask's CSR; HIP)
   -> out-projection GEMM with dropout + residual + LN2 in its epilogue (HIP)
 
-(the fp32 path has a stream-GEMM kernel at every width BASELINE names, 64 / 128 / 256; at
-H = 64 / 256 the LayerNorms run as their own kernels beside the stream GEMMs.  bf16 operands
-at H = 256 (C5 in the bf16 activation mode) take hipBLASLt plus the standalone LayerNorm
-kernels -- ``fused.SG_BF16_MAX_H`` -- as do widths with no stream-GEMM kernel at all).
+(every width BASELINE names, 64 / 128 / 256, has stream-GEMM kernels in both precisions.  The
+LayerNorm fusions: all of them at H = 128; at H = 256 in the bf16 activation mode (C5) LN1 in
+the QKV prologue and LN2 in the out-projection epilogue, LN2's and LN1's backward standalone;
+fp32 at H = 64 / 256 runs the LayerNorms as their own kernels beside the stream GEMMs.  Widths
+with no stream-GEMM kernel take hipBLASLt plus the standalone LayerNorm kernels).
 
 Dense masks become CSR (``graph_from_dense_mask``); TAGANGraphAttention hands in
 a prebuilt snapshot CSR through ``forward_graph``.  There is no CPU path.

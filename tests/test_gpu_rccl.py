@@ -166,7 +166,8 @@ def _case_graph_step_c2():
 
 def _capture_after_eager_collective():
     """The watchdog race made deterministic: the warm-up steps' eager all-reduces record their end events on the
-    stream that is captured next, and the capture (only the capture) holds the host for 0.45 s (several 100-ms watchdog polls).  Without
+    stream that is captured next, and the capture (only the capture) holds the host for 0.45 s (several 100-ms
+    watchdog polls).  Without
     ``retire_pending_works`` a Work still on the watchdog's list is polled during the capture and the watchdog aborts
     the process (hipErrorCapturedEvent); with it, the capture and the replays are clean."""
     import time
@@ -198,7 +199,7 @@ def _capture_after_eager_collective():
 
 def _case_capture_race_unfixed():
     """NOT a test: the same case with ``retire_pending_works`` reduced to a device sync (the round-4 state), used by
-    ``tools/runs/r5_watchdog.sh`` to show the abort the fix removes.  Expected: rc -6 / 134, the watchdog message."""
+    ``tools/runs/r5b.sh`` to show the abort the fix removes.  Expected: rc -6 / 134, the watchdog message."""
     import tagan_amd.distributed as D
     D.retire_pending_works = lambda device=None: torch.cuda.synchronize(device) or 0
     _capture_after_eager_collective()

@@ -50,11 +50,19 @@ def _params(dev, seed):
 
 
 @pytest.mark.parametrize("M", ROWS)
-@pytest.mark.parametrize("planes,store", [(3, "fp32"), (1, "bf16")])
-def test_ln_in_qkv(M, planes, store):
+@pytest.mark.parametrize("planes,store", [(3, "fp32"), (1, "bf16"), (1, "fp32")])
+@pytest.mark.parametrize("Hw", [128, 256])
+def test_ln_in_qkv(M, planes, store, Hw):
+    """LN1 in the QKV projection's prologue (16 lanes per row at H = 128, 32 at H = 256) and the LN-recomputing
+    weight gradient."""
     dev = _dev()
     from tagan_amd import stream_gemm as sg
-    g, ln_w, ln_b = _params(dev, M + planes)
+    H = Hw
+    if not sg.ln_supported(H, planes, store == "bf16", "in"):
+        pytest.skip("no LN1-prologue kernel at this width / precision")
+    g = torch.Generator(device=dev).manual_seed(M + planes + H)
+    ln_w = 1.0 + 0.1 * torch.randn(H, device=dev, generator=g)
+    ln_b = 0.1 * torch.randn(H, device=dev, generator=g)
     x = 0.5 + 2.0 * torch.randn(M, H, device=dev, generator=g)
     w = torch.randn(3 * H, H, device=dev, generator=g) / H ** 0.5
     bias = torch.randn(3 * H, device=dev, generator=g)
@@ -77,7 +85,8 @@ def test_ln_in_qkv(M, planes, store):
         assert _merr(dw, refw) <= 2e-5, _merr(dw, refw)
     else:
         assert _nerr(dw, refw) < 1e-2
-    assert _merr(db, dq.double().sum(0)) <= (2e-6 if planes == 3 else 1e-3)
+    # db: Σ dq through dq's planes (one bf16 plane of an fp32 dq rounds it: bf16-gemm mode)
+    assert _merr(db, dq.double().sum(0)) <= (2e-6 if planes == 3 else 1e-3 if store == "bf16" else 1e-2)
     dw2, db2 = sg.tn_ln(dq, x, ln_w, ln_b, mean, rstd, planes)
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
 
@@ -102,12 +111,16 @@ def test_ln_in_recompute_matches_stored_h():
 
 
 @pytest.mark.parametrize("M", ROWS)
-@pytest.mark.parametrize("planes,store", [(3, "fp32"), (1, "bf16")])
+@pytest.mark.parametrize("planes,store,Hw", [(3, "fp32", 128), (1, "bf16", 128), (1, "bf16", 256), (1, "fp32", 256)])
 @pytest.mark.parametrize("skip", [False, True])
-def test_ln_out(M, planes, store, skip):
+def test_ln_out(M, planes, store, Hw, skip):
+    """Out-projection + dropout + residual + LN2 (+ skip LN) epilogue; H = 256 on the one-plane row-owner kernel."""
     dev = _dev()
     from tagan_amd import stream_gemm as sg
-    g, ln_w, ln_b = _params(dev, 100 + M + planes)
+    H = Hw
+    g = torch.Generator(device=dev).manual_seed(100 + M + planes + H)
+    ln_w = 1.0 + 0.1 * torch.randn(H, device=dev, generator=g)
+    ln_b = 0.1 * torch.randn(H, device=dev, generator=g)
     dt = torch.bfloat16 if store == "bf16" else torch.float32
     a = torch.randn(M, H, device=dev, generator=g).to(dt)
     res = torch.randn(M, H, device=dev, generator=g)
@@ -128,7 +141,10 @@ def test_ln_out(M, planes, store, skip):
     tol = (2e-5, 1e-5) if planes == 3 else (5e-2, 1e-2)
     assert _merr(s, s64) <= tol[0] and _nerr(s, s64) <= tol[1], (_merr(s, s64), _nerr(s, s64))
     assert _merr(y, y64) <= tol[0] and _nerr(y, y64) <= tol[1], (_merr(y, y64), _nerr(y, y64))
-    assert _merr(mean, m64) <= (1e-5 if planes == 3 else 1e-2) and _merr(rstd, rs64) <= (1e-5 if planes == 3 else 1e-2)
+    # the mean against the row's scale (a near-zero mean of a single row has no relative accuracy to speak of)
+    mtol = 1e-5 if planes == 3 else 1e-2
+    assert float((mean.double() - m64).abs().max()) <= mtol * max(1.0, float(m64.abs().max()))
+    assert _merr(rstd, rs64) <= mtol
 
 
 @pytest.mark.parametrize("skip", [False, True])
@@ -326,4 +342,7 @@ def test_ln_supported_shapes():
     for op in ("in", "out", "bwd"):
         assert sg.ln_supported(128, 1, True, op) and sg.ln_supported(128, 1, False, op)
         assert sg.ln_supported(128, 3, False, op) == (op != "bwd")   # the three-plane LN1-backward form is not built
+        # H = 256: the LN1 prologue only (LN2 and LN1's backward stay standalone there)
+        # (the three-plane H = 256 LN1 prologue lost its A/B and is not built)
         assert not sg.ln_supported(256, 3, False, op)
+        assert sg.ln_supported(256, 1, True, op) == (op in ("in", "out"))
