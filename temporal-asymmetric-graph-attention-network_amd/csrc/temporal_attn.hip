@@ -23,6 +23,7 @@
 #include "common.cuh"
 
 #include <mutex>
+#include <type_traits>
 #include <unordered_set>
 
 namespace tagan {
@@ -931,6 +932,28 @@ __device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// bf16 storage: the score products Sᵀ = K·Qᵀ and dPᵀ = V·dOᵀ multiply STORED bf16 values only, so one
+// v_mfma_f32_16x16x16_bf16 per 16 features gives the same products (a bf16 x bf16 product is exact in fp32) and
+// fp32 accumulation in another summation order -- against four v_mfma_f32_16x16x4_f32 (32 cycles each).  Its operand
+// layout is the f32 instruction's with the k index widened to 4 per lane: lane (c, g) holds row c, k = 4g + [0, 4)
+// -- exactly the f4v a lane already holds (features 16dt + 4g + e).  The products with the softmax-derived
+// operands (P', dS) stay on the f32 instruction.  TAGAN_TATTN_BFMM=0 keeps every product f32 (A/B builds).
+#ifndef TAGAN_TATTN_BFMM
+#define TAGAN_TATTN_BFMM 1
+#endif
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+// four fp32 registers holding exact bf16 values -> the packed bf16 operand (the high halves; no rounding)
+__device__ __forceinline__ s16x4 pk4bf(const f4v& x) {
+    const uint32_t lo = __builtin_amdgcn_perm(__float_as_uint(x[1]), __float_as_uint(x[0]), 0x07060302u);
+    const uint32_t hi = __builtin_amdgcn_perm(__float_as_uint(x[3]), __float_as_uint(x[2]), 0x07060302u);
+    return __builtin_bit_cast(s16x4, make_uint2(lo, hi));
+}
+__device__ __forceinline__ f4v mfma16bf(const s16x4& a, const s16x4& b, f4v c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+template <typename S>
+constexpr bool bf_scores() { return TAGAN_TATTN_BFMM && std::is_same<S, bf16s>::value; }
+
 template <typename S>
 __device__ __forceinline__ f4v ld4v(const void* p, int64_t i, bool ok) {
     if (!ok) return f4v{0.f, 0.f, 0.f, 0.f};
@@ -1075,6 +1098,36 @@ __device__ __forceinline__ void v4_wave_map(int heads, int& h, int64_t& rg) {
     }
 }
 
+// Sᵀ[jt][it] += A[jt]·B[it]ᵀ over the head's features, the row tiles of both operands in registers (lane (c, g):
+// row 16t + c, features 16dt + 4g + e): Sᵀ = K·Qᵀ and dPᵀ = V·dOᵀ; BF: stored bf16 operands on the bf16 instruction
+template <int TT, int DT, bool BF>
+__device__ __forceinline__ void v4_scores(const f4v (&a)[TT][DT], const f4v (&b)[TT][DT], f4v (&acc)[TT][TT]) {
+    if constexpr (BF) {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+            s16x4 pa[TT], pb[TT];
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                pa[t] = pk4bf(a[t][dt]);
+                pb[t] = pk4bf(b[t][dt]);
+            }
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int it = 0; it < TT; ++it) acc[jt][it] = mfma16bf(pa[jt], pb[it], acc[jt][it]);
+        }
+    } else {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                    for (int it = 0; it < TT; ++it) acc[jt][it] = mfma4(a[jt][dt][e], b[it][dt][e], acc[jt][it]);
+    }
+}
+
 template <int TT, int DT, typename S>
 __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_F) k_tattn_fwd_v4(TArgs A, const float* __restrict__ q,
                                                        const float* __restrict__ k,
@@ -1119,14 +1172,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_F) k_tattn_fwd_v4(TArgs A, 
         for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
             for (int it = 0; it < TT; ++it) s[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int jt = 0; jt < TT; ++jt)
-#pragma unroll
-                    for (int it = 0; it < TT; ++it) s[jt][it] = mfma4(kv[jt][dt][e], qv[it][dt][e], s[jt][it]);
+        v4_scores<TT, DT, bf_scores<S>()>(kv, qv, s);
         wave_sync();   // the previous unit's reads of Vt are done
         v4_stage_t<TT, DT, LT>(Vt, vv, c, g);
         if (TAGAN_V4_PREFETCH && r + G < A.rows) load(r + G, c, g);   // next unit's rows in flight during this one
@@ -1278,22 +1324,8 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
                 s[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
                 dp[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
             }
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int jt = 0; jt < TT; ++jt)
-#pragma unroll
-                    for (int it = 0; it < TT; ++it) s[jt][it] = mfma4(kv[jt][dt][e], qv[it][dt][e], s[jt][it]);
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int jt = 0; jt < TT; ++jt)
-#pragma unroll
-                    for (int it = 0; it < TT; ++it) dp[jt][it] = mfma4(vv[jt][dt][e], dov[it][dt][e], dp[jt][it]);
+        v4_scores<TT, DT, bf_scores<S>()>(kv, qv, s);
+        v4_scores<TT, DT, bf_scores<S>()>(vv, dov, dp);
         wave_sync();   // the previous unit's reads of Kt / Qt / Ot / X are done
         v4_stage_t<TT, DT, LD>(Kt, kv, c, g);
         v4_stage_t<TT, DT, LD>(Qt, qv, c, g);
@@ -1574,6 +1606,30 @@ struct V6Slab {
     }
 };
 
+// v4_scores for one feature tile whose operands were read from the slab
+template <int TT, bool BF>
+__device__ __forceinline__ void v6_scores(const f4v (&a)[TT], const f4v (&b)[TT], f4v (&acc)[TT][TT]) {
+    if constexpr (BF) {
+        s16x4 pa[TT], pb[TT];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            pa[t] = pk4bf(a[t]);
+            pb[t] = pk4bf(b[t]);
+        }
+#pragma unroll
+        for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+            for (int it = 0; it < TT; ++it) acc[jt][it] = mfma16bf(pa[jt], pb[it], acc[jt][it]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int jt = 0; jt < TT; ++jt)
+#pragma unroll
+                for (int it = 0; it < TT; ++it) acc[jt][it] = mfma4(a[jt][e], b[it][e], acc[jt][it]);
+    }
+}
+
 template <int TT, int DT, int GH, typename S>
 __global__ void __launch_bounds__(WAVE * GH, TAGAN_V6_WPE) k_tattn_fwd_v6(TArgs A, const float* __restrict__ q,
                                                             const float* __restrict__ k,
@@ -1615,12 +1671,7 @@ __global__ void __launch_bounds__(WAVE * GH, TAGAN_V6_WPE) k_tattn_fwd_v6(TArgs 
                 qv[t] = lds4(sq + (t * 16 + c) * SP + dt * 16 + 4 * g);
                 kv[t] = lds4(sk + (t * 16 + c) * SP + dt * 16 + 4 * g);
             }
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int jt = 0; jt < TT; ++jt)
-#pragma unroll
-                    for (int it = 0; it < TT; ++it) s[jt][it] = mfma4(kv[jt][e], qv[it][e], s[jt][it]);
+            v6_scores<TT, bf_scores<S>()>(kv, qv, s);
         }
         const uint32_t drk = tkey(A, r, h);
         float inv_l[TT];
@@ -1771,23 +1822,13 @@ __global__ void __launch_bounds__(WAVE * GH, (TT == 2 && DT == 2) ? 2 : TAGAN_V6
                 xa[t] = lds4(sk + (t * 16 + c) * SP + dt * 16 + 4 * g);
                 xb[t] = lds4(sq + (t * 16 + c) * SP + dt * 16 + 4 * g);
             }
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int jt = 0; jt < TT; ++jt)
-#pragma unroll
-                    for (int it = 0; it < TT; ++it) s[jt][it] = mfma4(xa[jt][e], xb[it][e], s[jt][it]);
+            v6_scores<TT, bf_scores<S>()>(xa, xb, s);
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
                 xa[t] = lds4(sv + (t * 16 + c) * SP + dt * 16 + 4 * g);
                 xb[t] = lds4(so + (t * 16 + c) * SP + dt * 16 + 4 * g);
             }
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int jt = 0; jt < TT; ++jt)
-#pragma unroll
-                    for (int it = 0; it < TT; ++it) dp[jt][it] = mfma4(xa[jt][e], xb[it][e], dp[jt][it]);
+            v6_scores<TT, bf_scores<S>()>(xa, xb, dp);
         }
         uint32_t keep = 0;
 #pragma unroll
@@ -2062,9 +2103,14 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
 #pragma unroll
             for (int e = 0; e < 4; ++e) Vt[(dt * 16 + 4 * g + e) * LT + i] = vv[dt][e];
         }
-        f4v qc[DT];
+        constexpr bool BFS = bf_scores<S>();
+        f4v qc[BFS ? 1 : DT];
+        s16x4 qb[BFS ? DT : 1];
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) qc[dt] = qv[dt];
+        for (int dt = 0; dt < DT; ++dt) {
+            if constexpr (BFS) qb[dt] = pk4bf(qv[dt]);
+            else qc[dt] = qv[dt];
+        }
         __syncthreads();
         if (r + G < A.rows) load(r + G);   // the next unit's rows in flight during this one
         f4v s[TT];   // Sᵀ tiles [jt] of query tile w
@@ -2074,8 +2120,12 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
                 const f4v ka = lds4(Kr + (jt * 16 + c) * LK + dt * 16 + 4 * g);   // K[16jt + c][16dt + 4g + e]
+                if constexpr (BFS) {
+                    s[jt] = mfma16bf(pk4bf(ka), qb[dt], s[jt]);
+                } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) s[jt] = mfma4(ka[e], qc[dt][e], s[jt]);
+                    for (int e = 0; e < 4; ++e) s[jt] = mfma4(ka[e], qc[dt][e], s[jt]);
+                }
             }
         }
         const uint32_t drk = tkey(A, r, h);
@@ -2276,26 +2326,42 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
         }
         const float lse_i = lsev;
         const uint32_t kw = kwv;
+        constexpr bool BFS = bf_scores<S>();
+        s16x4 qb[BFS ? DT : 1], db[BFS ? DT : 1];   // the query tile's Q and dO as packed bf16 operands
+        if constexpr (BFS) {
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                qb[dt] = pk4bf(qv[dt]);
+                db[dt] = pk4bf(dov[dt]);
+            }
+        }
+        // Sᵀ and dPᵀ of key tile jt (A = K | V rows of the key tile from LDS, B = this lane's query row)
+        auto sdp0 = [&](int jt, f4v& sj, f4v& dpj) {
+            sj = f4v{0.f, 0.f, 0.f, 0.f};
+            dpj = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+                const f4v ka = lds4(Kr + (jt * 16 + c) * LK + dt * 16 + 4 * g);
+                const f4v va = lds4(Vr + (jt * 16 + c) * LK + dt * 16 + 4 * g);
+                if constexpr (BFS) {
+                    sj = mfma16bf(pk4bf(ka), qb[dt], sj);
+                    dpj = mfma16bf(pk4bf(va), db[dt], dpj);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        sj = mfma4(ka[e], qv[dt][e], sj);
+                        dpj = mfma4(va[e], dov[dt][e], dpj);
+                    }
+                }
+            }
+        };
         __syncthreads();
         // ---- phase 1, query tile w: Sᵀ, dPᵀ (all key tiles), P, δ, dS, P', dQ
         f4v s[TT], dp[TT];
         if constexpr (MODE != 0 && TAGAN_V5B_IL) {
             // fast path, software-pipelined: the softmax / dropout VALU work of key tile jt issues between the
             // S / dP products of tile jt + 1, and dS of tile jt + 1 between the dQ products of tile jt
-            auto sdp = [&](int jt) {
-                s[jt] = f4v{0.f, 0.f, 0.f, 0.f};
-                dp[jt] = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int dt = 0; dt < DT; ++dt) {
-                    const f4v ka = lds4(Kr + (jt * 16 + c) * LK + dt * 16 + 4 * g);
-                    const f4v va = lds4(Vr + (jt * 16 + c) * LK + dt * 16 + 4 * g);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        s[jt] = mfma4(ka[e], qv[dt][e], s[jt]);
-                        dp[jt] = mfma4(va[e], dov[dt][e], dp[jt]);
-                    }
-                }
-            };
+            auto sdp = [&](int jt) { sdp0(jt, s[jt], dp[jt]); };
             const uint32_t drk = tkey(A, r, h);
             const float sc2 = A.inv_sqrt_d * LOG2E_F, lse2 = lse_i * LOG2E_F;
             const int rb = T - 1 - i + 4 * g;
@@ -2327,7 +2393,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
                     dl = fmaf(p, dpv, dl);
                 }
             };
-            constexpr int NM = 8 * DT;                     // products per key tile
+            constexpr int NM = (BFS ? 2 : 8) * DT;         // products per key tile
             constexpr int VA = (MODE == 3 ? 40 : 64) / NM;  // VALU of softA per product slot
             sdp(0);
 #pragma unroll
@@ -2388,20 +2454,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
             }
         } else {
 #pragma unroll
-        for (int jt = 0; jt < TT; ++jt) {
-            s[jt] = f4v{0.f, 0.f, 0.f, 0.f};
-            dp[jt] = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int dt = 0; dt < DT; ++dt) {
-                const f4v ka = lds4(Kr + (jt * 16 + c) * LK + dt * 16 + 4 * g);
-                const f4v va = lds4(Vr + (jt * 16 + c) * LK + dt * 16 + 4 * g);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    s[jt] = mfma4(ka[e], qv[dt][e], s[jt]);
-                    dp[jt] = mfma4(va[e], dov[dt][e], dp[jt]);
-                }
-            }
-        }
+        for (int jt = 0; jt < TT; ++jt) sdp0(jt, s[jt], dp[jt]);
         if (r + G < A.rows) load(r + G);   // the next unit's rows in flight during the rest of this one
         const uint32_t drk = tkey(A, r, h);
         if constexpr (MODE != 0) {   // fast path (see v5_fast_shape): log2 units, keep bit in the sign of P
