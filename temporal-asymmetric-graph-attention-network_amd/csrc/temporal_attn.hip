@@ -961,6 +961,39 @@ __device__ __forceinline__ f4v ld4v(const void* p, int64_t i, bool ok) {
     return f4v{t.x, t.y, t.z, t.w};
 }
 
+// A prefetched 4-element chunk kept in its STORED form until use: in bf16 storage a conversion right at the load
+// would make the prefetch wait for its data there (the v5 / v6 backwards spent twice the fp32 kernels' cycles in
+// s_waitcnt: profiles/r5q_tattn_bf16_pmc.txt); f() converts where the values are consumed, pk() hands the four bf16
+// straight to the bf16 matrix instruction.
+template <typename S>
+struct Raw4 {
+    f4v v;
+    __device__ __forceinline__ f4v f() const { return v; }
+};
+template <>
+struct Raw4<bf16s> {
+    uint2 u;
+    __device__ __forceinline__ f4v f() const {
+        return f4v{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                   __uint_as_float(u.y & 0xffff0000u)};
+    }
+};
+template <typename S>
+__device__ __forceinline__ Raw4<S> ldr4(const void* p, int64_t i, bool ok) {
+    if constexpr (std::is_same<S, bf16s>::value) {
+        Raw4<bf16s> r{make_uint2(0u, 0u)};
+        if (ok) r.u = *(const uint2*)((const uint16_t*)p + i);
+        return r;
+    } else {
+        return Raw4<S>{ld4v<S>(p, i, ok)};
+    }
+}
+template <typename S>
+__device__ __forceinline__ s16x4 pk4(const Raw4<S>& r) {
+    if constexpr (std::is_same<S, bf16s>::value) return __builtin_bit_cast(s16x4, r.u);
+    else return pk4bf(r.v);
+}
+
 template <typename S>
 __device__ __forceinline__ float ld1v(const void* p, int64_t i, bool ok) {
     return ok ? Io<S>::ld1(p, i) : 0.f;
@@ -1069,14 +1102,16 @@ __device__ __forceinline__ float v4_score(const TArgs& A, float bst, int64_t r, 
 // Transposed staging of a row tile held as lane (c, g): X[row = t*16 + c][dt*16 + 4g .. +3]
 // into Xt[feature][row] (row stride LT), so a lane can read Xt[dt*16 + c][t*16 + 4g .. +3] -- the
 // A operand of a product that sums over rows -- as one 16-B LDS read.
-template <int TT, int DT, int LT>
-__device__ __forceinline__ void v4_stage_t(float* Xt, const f4v (&x)[TT][DT], int c, int g) {
+template <int TT, int DT, int LT, typename S>
+__device__ __forceinline__ void v4_stage_t(float* Xt, const Raw4<S> (&x)[TT][DT], int c, int g) {
 #pragma unroll
     for (int t = 0; t < TT; ++t)
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
+        for (int dt = 0; dt < DT; ++dt) {
+            const f4v xf = x[t][dt].f();
 #pragma unroll
-            for (int e = 0; e < 4; ++e) Xt[(dt * 16 + 4 * g + e) * LT + t * 16 + c] = x[t][dt][e];
+            for (int e = 0; e < 4; ++e) Xt[(dt * 16 + 4 * g + e) * LT + t * 16 + c] = xf[e];
+        }
 }
 
 __device__ __forceinline__ f4v lds4(const float* p) { return *(const f4v*)p; }
@@ -1100,16 +1135,16 @@ __device__ __forceinline__ void v4_wave_map(int heads, int& h, int64_t& rg) {
 
 // Sᵀ[jt][it] += A[jt]·B[it]ᵀ over the head's features, the row tiles of both operands in registers (lane (c, g):
 // row 16t + c, features 16dt + 4g + e): Sᵀ = K·Qᵀ and dPᵀ = V·dOᵀ; BF: stored bf16 operands on the bf16 instruction
-template <int TT, int DT, bool BF>
-__device__ __forceinline__ void v4_scores(const f4v (&a)[TT][DT], const f4v (&b)[TT][DT], f4v (&acc)[TT][TT]) {
+template <int TT, int DT, bool BF, typename S>
+__device__ __forceinline__ void v4_scores(const Raw4<S> (&a)[TT][DT], const Raw4<S> (&b)[TT][DT], f4v (&acc)[TT][TT]) {
     if constexpr (BF) {
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
             s16x4 pa[TT], pb[TT];
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
-                pa[t] = pk4bf(a[t][dt]);
-                pb[t] = pk4bf(b[t][dt]);
+                pa[t] = pk4(a[t][dt]);
+                pb[t] = pk4(b[t][dt]);
             }
 #pragma unroll
             for (int jt = 0; jt < TT; ++jt)
@@ -1118,13 +1153,20 @@ __device__ __forceinline__ void v4_scores(const f4v (&a)[TT][DT], const f4v (&b)
         }
     } else {
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
+        for (int dt = 0; dt < DT; ++dt) {
+            f4v af[TT], bf[TT];
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                af[t] = a[t][dt].f();
+                bf[t] = b[t][dt].f();
+            }
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
                 for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
-                    for (int it = 0; it < TT; ++it) acc[jt][it] = mfma4(a[jt][dt][e], b[it][dt][e], acc[jt][it]);
+                    for (int it = 0; it < TT; ++it) acc[jt][it] = mfma4(af[jt][e], bf[it][e], acc[jt][it]);
+        }
     }
 }
 
@@ -1144,7 +1186,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_F) k_tattn_fwd_v4(TArgs A, 
     float* Vt = sm;    // [16*DT][LT]
     float bst[TT][TT][4];
     v4_static_bias<TT>(A, h, c0, g0, bst);
-    f4v qv[TT][DT], kv[TT][DT], vv[TT][DT];
+    Raw4<S> qv[TT][DT], kv[TT][DT], vv[TT][DT];
     auto load = [&](int64_t rr, int c, int g) {
         const int64_t hb = rr * A.s_row + (int64_t)h * d;
 #pragma unroll
@@ -1153,9 +1195,9 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_F) k_tattn_fwd_v4(TArgs A, 
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
                 const int64_t off = hb + (int64_t)i * A.s_t + dt * 16 + 4 * g;
-                qv[t][dt] = ld4v<S>(q, off, i < T);
-                kv[t][dt] = ld4v<S>(k, off, i < T);
-                vv[t][dt] = ld4v<S>(v, off, i < T);
+                qv[t][dt] = ldr4<S>(q, off, i < T);
+                kv[t][dt] = ldr4<S>(k, off, i < T);
+                vv[t][dt] = ldr4<S>(v, off, i < T);
             }
         }
     };
@@ -1172,7 +1214,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_F) k_tattn_fwd_v4(TArgs A, 
         for (int jt = 0; jt < TT; ++jt)
 #pragma unroll
             for (int it = 0; it < TT; ++it) s[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
-        v4_scores<TT, DT, bf_scores<S>()>(kv, qv, s);
+        v4_scores<TT, DT, bf_scores<S>(), S>(kv, qv, s);
         wave_sync();   // the previous unit's reads of Vt are done
         v4_stage_t<TT, DT, LT>(Vt, vv, c, g);
         if (TAGAN_V4_PREFETCH && r + G < A.rows) load(r + G, c, g);   // next unit's rows in flight during this one
@@ -1270,7 +1312,7 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
     for (int t3 = 0; t3 < 3; ++t3)
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) bsum[t3][dt] = f4v{0.f, 0.f, 0.f, 0.f};
-    f4v qv[TT][DT], kv[TT][DT], vv[TT][DT], dov[TT][DT];
+    Raw4<S> qv[TT][DT], kv[TT][DT], vv[TT][DT], dov[TT][DT];
     float lsev[TT];
     // The next row's Q, K, LSE (and, unless TAGAN_V4_SPLIT, V and dO) are prefetched during this one.
     auto load_qk = [&](int64_t rr, int c, int g) {
@@ -1281,8 +1323,8 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
                 const int64_t off = hb + (int64_t)i * A.s_t + dt * 16 + 4 * g;
-                qv[t][dt] = ld4v<S>(q, off, i < T);
-                kv[t][dt] = ld4v<S>(k, off, i < T);
+                qv[t][dt] = ldr4<S>(q, off, i < T);
+                kv[t][dt] = ldr4<S>(k, off, i < T);
             }
             lsev[t] = (i < T) ? lse[(rr * A.heads + h) * T + i] : 0.f;
         }
@@ -1294,8 +1336,8 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
             const int i = t * 16 + c;
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
-                vv[t][dt] = ld4v<S>(v, hb + (int64_t)i * A.s_t + dt * 16 + 4 * g, i < T);
-                dov[t][dt] = ld4v<S>(dout, rr * A.do_row + (int64_t)h * d + (int64_t)i * A.do_t + dt * 16 + 4 * g,
+                vv[t][dt] = ldr4<S>(v, hb + (int64_t)i * A.s_t + dt * 16 + 4 * g, i < T);
+                dov[t][dt] = ldr4<S>(dout, rr * A.do_row + (int64_t)h * d + (int64_t)i * A.do_t + dt * 16 + 4 * g,
                                      i < T);
             }
         }
@@ -1324,8 +1366,8 @@ __global__ void __launch_bounds__(WAVE, TAGAN_V4_WPE_B) k_tattn_bwd_v4(TArgs A, 
                 s[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
                 dp[jt][it] = f4v{0.f, 0.f, 0.f, 0.f};
             }
-        v4_scores<TT, DT, bf_scores<S>()>(kv, qv, s);
-        v4_scores<TT, DT, bf_scores<S>()>(vv, dov, dp);
+        v4_scores<TT, DT, bf_scores<S>(), S>(kv, qv, s);
+        v4_scores<TT, DT, bf_scores<S>(), S>(vv, dov, dp);
         wave_sync();   // the previous unit's reads of Kt / Qt / Ot / X are done
         v4_stage_t<TT, DT, LD>(Kt, kv, c, g);
         v4_stage_t<TT, DT, LD>(Qt, qv, c, g);
@@ -1580,7 +1622,7 @@ template <int TT, int DT, int GH, int NT, typename S>
 struct V6Slab {
     static constexpr int TP = 16 * TT, DP = 16 * DT, C4 = NT * GH * DP / 4, NPF = TP * C4 / (WAVE * GH);
     static constexpr int SP = v6_pitch<NT, GH, DP>();
-    f4v pf[NPF];
+    Raw4<S> pf[NPF];
     // tensor x of the slab: 0..2 = Q, K, V (row stride s_row, step stride s_t), 3 = dO
     __device__ __forceinline__ void load(const TArgs& A, const void* q, const void* k, const void* v, const void* dout,
                                          int64_t r, int hg) {
@@ -1591,9 +1633,9 @@ struct V6Slab {
             const bool ok = t < A.T;
             if (x < 3) {
                 const void* src = x == 0 ? q : x == 1 ? k : v;
-                pf[n] = ld4v<S>(src, r * A.s_row + (int64_t)t * A.s_t + hg * GH * DP + cc, ok);
+                pf[n] = ldr4<S>(src, r * A.s_row + (int64_t)t * A.s_t + hg * GH * DP + cc, ok);
             } else {
-                pf[n] = ld4v<S>(dout, r * A.do_row + (int64_t)t * A.do_t + hg * GH * DP + cc, ok);
+                pf[n] = ldr4<S>(dout, r * A.do_row + (int64_t)t * A.do_t + hg * GH * DP + cc, ok);
             }
         }
     }
@@ -1601,7 +1643,7 @@ struct V6Slab {
 #pragma unroll
         for (int n = 0; n < NPF; ++n) {
             const int e = threadIdx.x + n * WAVE * GH;
-            *(f4v*)(slab + (e / C4) * SP + 4 * (e % C4)) = pf[n];
+            *(f4v*)(slab + (e / C4) * SP + 4 * (e % C4)) = pf[n].f();
         }
     }
 };
@@ -2080,15 +2122,15 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
         for (int t = threadIdx.x; t < 2 * T - 1; t += WAVE * TT) Bt[t] = A.bias_table ? A.bias_table[h * (2 * T - 1) + t] : 0.f;
     }
     const uint32_t thr = MODE >= 2 ? tthr(A.p_drop) : 0u;
-    f4v qv[DT], kv[DT], vv[DT];
+    Raw4<S> qv[DT], kv[DT], vv[DT];
     auto load = [&](int64_t rr) {
         const int i = w * 16 + c0;
         const int64_t off = rr * A.s_row + (int64_t)h * d + (int64_t)i * A.s_t + 4 * g0;
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-            qv[dt] = ld4v<S>(q, off + dt * 16, i < T);
-            kv[dt] = ld4v<S>(k, off + dt * 16, i < T);
-            vv[dt] = ld4v<S>(v, off + dt * 16, i < T);
+            qv[dt] = ldr4<S>(q, off + dt * 16, i < T);
+            kv[dt] = ldr4<S>(k, off + dt * 16, i < T);
+            vv[dt] = ldr4<S>(v, off + dt * 16, i < T);
         }
     };
     if (rg < A.rows) load(rg);
@@ -2099,17 +2141,18 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_fwd_v5(TArgs A, const float
         __syncthreads();   // the previous unit's reads of Kr / Vt are done
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-            *(f4v*)(Kr + i * LK + dt * 16 + 4 * g) = kv[dt];
+            *(f4v*)(Kr + i * LK + dt * 16 + 4 * g) = kv[dt].f();
+            const f4v vf = vv[dt].f();
 #pragma unroll
-            for (int e = 0; e < 4; ++e) Vt[(dt * 16 + 4 * g + e) * LT + i] = vv[dt][e];
+            for (int e = 0; e < 4; ++e) Vt[(dt * 16 + 4 * g + e) * LT + i] = vf[e];
         }
         constexpr bool BFS = bf_scores<S>();
         f4v qc[BFS ? 1 : DT];
         s16x4 qb[BFS ? DT : 1];
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-            if constexpr (BFS) qb[dt] = pk4bf(qv[dt]);
-            else qc[dt] = qv[dt];
+            if constexpr (BFS) qb[dt] = pk4(qv[dt]);
+            else qc[dt] = qv[dt].f();
         }
         __syncthreads();
         if (r + G < A.rows) load(r + G);   // the next unit's rows in flight during this one
@@ -2290,7 +2333,7 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
     for (int t3 = 0; t3 < 3; ++t3)
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) bsum[t3][dt] = f4v{0.f, 0.f, 0.f, 0.f};
-    f4v qv[DT], kv[DT], vv[DT], dov[DT];
+    Raw4<S> qv[DT], kv[DT], vv[DT], dov[DT];
     float lsev;
     uint32_t kwv = 0;   // MODE 3: the forward's keep bits of this lane's elements (bit 4 jt + e)
     auto load = [&](int64_t rr) {
@@ -2300,10 +2343,10 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
         if constexpr (MODE == 3) kwv = A.keep[((rr * A.heads + h) * TT + w) * WAVE + lane];
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-            qv[dt] = ld4v<S>(q, off + dt * 16, i < T);
-            kv[dt] = ld4v<S>(k, off + dt * 16, i < T);
-            vv[dt] = ld4v<S>(v, off + dt * 16, i < T);
-            dov[dt] = ld4v<S>(dout, offd + dt * 16, i < T);
+            qv[dt] = ldr4<S>(q, off + dt * 16, i < T);
+            kv[dt] = ldr4<S>(k, off + dt * 16, i < T);
+            vv[dt] = ldr4<S>(v, off + dt * 16, i < T);
+            dov[dt] = ldr4<S>(dout, offd + dt * 16, i < T);
         }
         lsev = (i < T) ? lse[(rr * A.heads + h) * T + i] : 0.f;
     };
@@ -2313,15 +2356,19 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
         asm volatile("" : "+v"(c), "+v"(g));   // see k_tattn_fwd_v4
         const int i = w * 16 + c;   // this lane's query step (phase 1) and key step (phase 2)
         __syncthreads();   // the previous unit's reads of every LDS tile are done
+        f4v qf[DT], df[DT];   // this unit's Q and dO rows as fp32 (the f32-instruction score products read them)
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-            *(f4v*)(Kr + i * LK + dt * 16 + 4 * g) = kv[dt];
-            *(f4v*)(Vr + i * LK + dt * 16 + 4 * g) = vv[dt];
+            const f4v kf = kv[dt].f();
+            qf[dt] = qv[dt].f();
+            df[dt] = dov[dt].f();
+            *(f4v*)(Kr + i * LK + dt * 16 + 4 * g) = kf;
+            *(f4v*)(Vr + i * LK + dt * 16 + 4 * g) = vv[dt].f();
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                Kt[(dt * 16 + 4 * g + e) * LD + i] = kv[dt][e];
-                Qt[(dt * 16 + 4 * g + e) * LD + i] = qv[dt][e];
-                Ot[(dt * 16 + 4 * g + e) * LD + i] = dov[dt][e];
+                Kt[(dt * 16 + 4 * g + e) * LD + i] = kf[e];
+                Qt[(dt * 16 + 4 * g + e) * LD + i] = qf[dt][e];
+                Ot[(dt * 16 + 4 * g + e) * LD + i] = df[dt][e];
             }
         }
         const float lse_i = lsev;
@@ -2331,8 +2378,8 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
         if constexpr (BFS) {
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
-                qb[dt] = pk4bf(qv[dt]);
-                db[dt] = pk4bf(dov[dt]);
+                qb[dt] = pk4(qv[dt]);
+                db[dt] = pk4(dov[dt]);
             }
         }
         // Sᵀ and dPᵀ of key tile jt (A = K | V rows of the key tile from LDS, B = this lane's query row)
@@ -2349,8 +2396,8 @@ __global__ void __launch_bounds__(WAVE * TT) k_tattn_bwd_v5(TArgs A, const float
                 } else {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        sj = mfma4(ka[e], qv[dt][e], sj);
-                        dpj = mfma4(va[e], dov[dt][e], dpj);
+                        sj = mfma4(ka[e], qf[dt][e], sj);
+                        dpj = mfma4(va[e], df[dt][e], dpj);
                     }
                 }
             }
