@@ -213,6 +213,8 @@ struct GeoArgs {
     float* part_v2;     // [part_cap, 2H] (bwd col: dk | dv)
     float inv_sqrt_d;
     int bf16;           // activation storage: 0 fp32, 1 bf16 (fast path only)
+    int xcd;            // chunk-kernel block order (geo_xcd_mode): 0 launch order, 1 XCD-contiguous over the grid,
+                        // 2 XCD-contiguous over the blocks that hold valid chunks
 };
 
 #ifndef TAGAN_GEO_UNROLL
@@ -238,17 +240,29 @@ __device__ __forceinline__ void partial4(const float4& q, const float4& k, float
 
 // =================================================================== fast path: chunked kernels
 // Lane geometry shared by the chunk kernels.
+// The grid is sized for the chunk CAPACITY (rows + entries / chunk: a static shape for graph capture), and the
+// valid chunks (a device-side count) fill only its front -- 75 % of it for the uniform C3 / C4 / C5 graphs.  Mode 1
+// (the round-2..4 map) gives each XCD a contiguous eighth of the whole grid, so the XCDs whose eighths lie past the
+// valid count had nothing to do; mode 2 spreads the VALID blocks over the XCDs the same way; mode 0 keeps the launch
+// order (consecutive blocks round-robin over the XCDs: every XCD works on the same region of the graph at a time).
 template <int LPR>
 struct Lanes {
     static constexpr int RPW = WAVE / LPR;   // chunks per wave
     int lane, sub, sl, base;                  // base = first lane of this chunk's group
     int64_t chunk;                            // global chunk id of this group
-    __device__ __forceinline__ Lanes() {
+    __device__ __forceinline__ Lanes(int64_t nvalid, int mode) {
         lane = threadIdx.x & (WAVE - 1);
         sub = lane / LPR;
         sl = lane % LPR;
         base = sub * LPR;
-        const int64_t wave = xcd_remap(blockIdx.x, gridDim.x) * (BLK / WAVE) + (threadIdx.x >> 6);
+        int64_t b = blockIdx.x;
+        if (mode == 1) {
+            b = xcd_remap(b, gridDim.x);
+        } else if (mode == 2) {
+            const int64_t nv = (nvalid + RPW * (BLK / WAVE) - 1) / (RPW * (BLK / WAVE));
+            if (b < nv) b = xcd_remap(b, nv);
+        }
+        const int64_t wave = b * (BLK / WAVE) + (threadIdx.x >> 6);
         chunk = wave * RPW + sub;
     }
 };
@@ -309,8 +323,8 @@ template <int METRIC, int LPR, int FPL, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
     TAGAN_LIVE_SEED(A);
     constexpr int UN = Unroll<FPL>::v;
-    Lanes<LPR> L;
     const int nchunks = A.g.row_counts[0];
+    Lanes<LPR> L(nchunks, A.xcd);
     const bool valid = L.chunk < nchunks;
     if (valid && A.g.row_chunk_order) L.chunk = A.g.row_chunk_order[L.chunk];   // length-sorted order
     int row = 0, e0 = 0, cnt = 0;
@@ -481,8 +495,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
     TAGAN_LIVE_SEED(A);
     constexpr int UN = Unroll<FPL>::v;
     __shared__ float red[BLK];
-    Lanes<LPR> L;
     const int nchunks = A.g.row_counts[0];
+    Lanes<LPR> L(nchunks, A.xcd);
     const bool valid = L.chunk < nchunks;
     if (valid && A.g.row_chunk_order) L.chunk = A.g.row_chunk_order[L.chunk];   // length-sorted order
     int row = 0, e0 = 0, cnt = 0;
@@ -616,8 +630,8 @@ template <int METRIC, int LPR, int FPL, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
     TAGAN_LIVE_SEED(A);
     constexpr int UN = Unroll<FPL>::v;
-    Lanes<LPR> L;
     const int nchunks = A.g.col_counts[0];
+    Lanes<LPR> L(nchunks, A.xcd);
     const bool valid = L.chunk < nchunks;
     if (valid && A.g.col_chunk_order) L.chunk = A.g.col_chunk_order[L.chunk];   // length-sorted order
     int colj = 0, e0 = 0, cnt = 0;
@@ -720,7 +734,7 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_col_chunk(GeoArgs A) {
 template <int LPR, int FPL, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_bwd_delta(GeoArgs A) {
     TAGAN_LIVE_SEED(A);
-    Lanes<LPR> L;
+    Lanes<LPR> L(A.N, A.xcd != 0 ? 1 : 0);   // grid sized by N: every block valid (modes 1 and 2 agree)
     const bool valid = L.chunk < A.N;
     if (!__any(valid)) return;
     const int64_t row = valid ? L.chunk : 0;
@@ -742,8 +756,8 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_ds(GeoArgs A) {
     TAGAN_LIVE_SEED(A);
     constexpr int UN = Unroll<FPL>::v;
     __shared__ float red[BLK];
-    Lanes<LPR> L;
     const int nchunks = A.g.row_counts[0];
+    Lanes<LPR> L(nchunks, A.xcd);
     const bool valid = L.chunk < nchunks;
     if (valid && A.g.row_chunk_order) L.chunk = A.g.row_chunk_order[L.chunk];   // length-sorted order
     int row = 0, e0 = 0, cnt = 0;
@@ -1137,6 +1151,20 @@ int check_common(int dtype, int metric, const tagan_graph* g, int heads, int d, 
     return TAGAN_OK;
 }
 
+// Block order of the chunk kernels (Lanes).  Launch order (0) when the gathered K | V rows of the whole batch exceed
+// what the 256 MB Infinity Cache can hold: every XCD then works on the same stretch of rows -- one snapshot's
+// neighbourhoods at a time -- and the gathers share that cache; with XCD-contiguous eighths each XCD streams its own
+// region and the eight regions' K | V evict one another.  XCD-contiguous over the valid blocks (2) when the whole
+// batch fits (C2).  Edge kernels alone, fwd / bwd ms, shipped map (1) -> chosen order (profiles/r5u_geo_xcd_ab.txt):
+// C2 0.296 / 0.745 -> 0.281 / 0.706, C3 50.1 / 86.8 -> 38.7 / 66.5, C4 68.2 / 128.4 -> 57.3 / 105.9, C5 bf16
+// 48.3 / 97.4 -> 38.0 / 75.4.  TAGAN_GEO_XCD=0|1|2 forces one (read per call: A/B runs, tests).
+int geo_xcd_mode(int64_t n, int H, bool bf16) {
+    const char* e = getenv("TAGAN_GEO_XCD");
+    if (e && e[0] >= '0' && e[0] <= '2' && !e[1]) return e[0] - '0';
+    const int64_t kv_bytes = 2 * n * (int64_t)H * (bf16 ? 2 : 4);
+    return kv_bytes <= ((int64_t)512 << 20) ? 2 : 0;
+}
+
 GeoArgs make_args(const tagan_graph* g, int heads, int d, const void* q, const void* k, const void* v, int64_t ld,
                   const float* mparam, float p_drop, uint64_t seed) {
     GeoArgs A{};
@@ -1231,6 +1259,7 @@ int tagan_geo_attn_fwd(int dtype, int metric, const tagan_graph* g, int32_t head
     TAGAN_REQUIRE(!(dtype == TAGAN_BF16 && edge_alpha), TAGAN_ERR_UNSUPPORTED, "geo_attn_fwd: edge_alpha needs fp32");
     GeoArgs A = make_args(g, heads, head_dim, q, k, v, ld_qkv, metric_param, p_drop, seed);
     A.bf16 = dtype == TAGAN_BF16;
+    A.xcd = geo_xcd_mode(A.N, A.H, A.bf16 != 0);
     A.out = (float*)out;
     A.lse = lse;
     if (need) {
@@ -1290,6 +1319,7 @@ int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t head
     }
     GeoArgs A = make_args(g, heads, head_dim, q, k, v, ld_qkv, metric_param, p_drop, seed);
     A.bf16 = dtype == TAGAN_BF16;
+    A.xcd = geo_xcd_mode(A.N, A.H, A.bf16 != 0);
     A.o = (const float*)out;
     A.lse_in = lse;
     A.dout = (const float*)dout;
