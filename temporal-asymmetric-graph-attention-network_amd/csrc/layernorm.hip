@@ -330,11 +330,14 @@ bool geometry(int H, int& lpr, int& nv) {
 #endif
 int ln_bwd_blocks() { return TAGAN_LN_BWD_BLOCKS; }
 
-// Row groups per wave (U): 2, the best of 1 / 2 / 4 at C2 (tools/ln_probe.py, profiles/r1_ln_rows_ab.txt).
+// Row groups per wave (U): 4.  Round 1 measured 2 best at C2 (profiles/r1_ln_rows_ab.txt); round 5 re-measured the
+// backward at 4: C2 shape 162-163 vs 166 us, H = 256 (3.2M rows) 3.24 vs 3.41-3.48 ms, the C2 step within noise
+// (profiles/r5w_ln_bwd_ab.txt; a register prefetch of the next iteration's rows measured no gain and is not built).
+// NV = 2 (H = 512) is instantiated for U <= 2 only.
 #ifndef TAGAN_LN_ROWS
-#define TAGAN_LN_ROWS 2
+#define TAGAN_LN_ROWS 4
 #endif
-int ln_rows(int /*nv*/) { return TAGAN_LN_ROWS; }
+int ln_rows(int nv) { return nv == 2 && TAGAN_LN_ROWS > 2 ? 2 : TAGAN_LN_ROWS; }
 
 // the fused LN2 + skip-LN backward (H = 128: LPR 32, NV 1; any U)
 template <typename S>

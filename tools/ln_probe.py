@@ -1,8 +1,9 @@
-"""LayerNorm kernels at C2's shape (M = 320k rows, H = 128), each variant the model launches:
-HIP-event time per launch and algorithmic GB/s.  The row-groups-per-wave factor is read once
-per process from TAGAN_LN_ROWS (1|2|4), so A/B it across processes:
+"""LayerNorm kernels at C2's shape (M = 320k rows, H = 128; LN_PROBE_M / LN_PROBE_H override), each variant the model launches:
+HIP-event time per launch and algorithmic GB/s.  Compile-time variants (the row groups per wave, TAGAN_LN_ROWS) are
+A/B'd as variant libraries:
 
-    for u in 1 2 4; do TAGAN_LN_ROWS=$u python tools/ln_probe.py; done
+    make -C temporal-asymmetric-graph-attention-network_amd/csrc variant NAME=lnu2 EXTRA=-DTAGAN_LN_ROWS=2
+    TAGAN_LIB=$PWD/temporal-asymmetric-graph-attention-network_amd/libtagan_hip_lnu2.so python tools/ln_probe.py
 """
 import os
 import sys
@@ -16,7 +17,8 @@ import tagan_amd  # noqa: E402,F401
 from tagan_amd.fused import ln_bwd, ln_fwd  # noqa: E402
 
 dev = torch.device("cuda")
-M, H = 320_000, 128
+M = int(os.environ.get("LN_PROBE_M", 320_000))
+H = int(os.environ.get("LN_PROBE_H", 128))
 g = torch.Generator(device=dev).manual_seed(0)
 a = torch.randn(M, H, device=dev, generator=g)
 b = torch.randn(M, H, device=dev, generator=g)
@@ -40,7 +42,7 @@ def bench(name, f, nbytes, reps=50):
     e1.record(s)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
-    print("U=%s %-40s %8.1f us  %7.1f GB/s" % (os.environ.get("TAGAN_LN_ROWS", "default"), name, us,
+    print("%s M=%d H=%d %-40s %8.1f us  %7.1f GB/s" % (os.path.basename(os.environ.get("TAGAN_LIB", "default")), M, H, name, us,
                                               nbytes / us / 1e3), flush=True)
 
 
