@@ -14,6 +14,7 @@ FAMILIES = [
     ("geo", r"k_geo_"),
     ("temporal", r"k_tattn"),
     ("layernorm", r"k_ln_"),
+    ("LN2 bwd + out-proj grads (fused)", r"k_ln2_bwd_out"),
     ("proj (fused MFMA)", r"k_proj"),
     ("csr", r"rocprim|k_scatter|k_fill_tail|k_keys|k_chunk|k_tri|csr|k_count"),
     ("colsum/pool", r"k_colsum|k_pool"),
