@@ -135,6 +135,49 @@ __device__ __forceinline__ int64_t bucket_rows(int64_t b, int sb, int64_t N) {
     return min(N, r0 + ((int64_t)1 << sb)) - r0;
 }
 
+// Global -> LDS copy of n items with PER loads in flight per thread (a plain strided loop waits for each load before
+// its LDS store, so a bucket's ~8 loads per thread ran back to back: the finish kernels' serial latency chain)
+template <int NTH, int PER, typename T>
+__device__ __forceinline__ void gload_lds(T* dst, const T* __restrict__ src, int n) {
+    for (int base = 0; base < n; base += NTH * PER) {
+        T r[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = base + u * NTH + (int)threadIdx.x;
+            if (i < n) r[u] = src[i];
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = base + u * NTH + (int)threadIdx.x;
+            if (i < n) dst[i] = r[u];
+        }
+    }
+}
+template <int NTH, int PER>
+__device__ __forceinline__ void gload_lds2(uint32_t* dk, const uint32_t* __restrict__ sk, int32_t* dv,
+                                           const int32_t* __restrict__ sv, int n) {
+    for (int base = 0; base < n; base += NTH * PER) {
+        uint32_t rk[PER];
+        int32_t rv[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = base + u * NTH + (int)threadIdx.x;
+            if (i < n) {
+                rk[u] = sk[i];
+                rv[u] = sv[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = base + u * NTH + (int)threadIdx.x;
+            if (i < n) {
+                dk[i] = rk[u];
+                dv[i] = rv[u];
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------- LDS radix sort
 // Stable LSD radix sort of n 32-bit keys over bits [0, nbits) (+ int32 values), NTH threads, ping-pong between
 // (ka, va) and (kb, vb) -- LDS or global (the big-bucket fallback).  Per pass and per round of NTH*IPT keys
@@ -849,8 +892,7 @@ __device__ void csr_bucket(const Geo& g, int64_t b, uint32_t* A, uint32_t* B, bo
     const int tid = threadIdx.x;
     const int64_t r0 = b << g.SB;
     const int nv = (int)bucket_rows(b, g.SB, g.N);
-    if (!global_bufs)
-        for (int i = tid; i < c; i += NTH) A[i] = keys[off + i];
+    if (!global_bufs) gload_lds<NTH, NTH >= BNT ? 4 : 8>(A, keys + off, c);
     const BucketBase nbase(node_ptr, g.G, r0);
     for (int j = tid; j < nv; j += NTH) {     // the bucket's self-loops ("+ eye")
         const int64_t v = r0 + j;
@@ -967,7 +1009,7 @@ __global__ void __launch_bounds__(FNT) k_csc_finish(Geo g, const int32_t* __rest
     const int m = fill_dst[b];
     if (m > CAP_C) return;   // listed by k_big_list, finished by k_csc_finish_big
     const int32_t ro0 = cstart[b];
-    for (int i = threadIdx.x; i < m; i += FNT) { K[i] = ckey[ro0 + i]; V[i] = cval[ro0 + i]; }
+    gload_lds2<FNT, 8>(K, ckey + ro0, V, cval + ro0, m);
     const SegLds L{rc, ro, (uint32_t*)rk, (uint16_t*)(rk + (FNT / WAVE) * BMW), rk, rk, &flag};
     csc_bucket<FNT>(g, b, K, K2, V, V2, m, coff[b], node_ptr, csc_ptr, csc_row, csc_eid, cpos, L, cb, base,
                     tot, sm);
@@ -1004,7 +1046,7 @@ __global__ void __launch_bounds__(BNT) k_csc_finish_big(Geo g, const int32_t* __
             uint32_t* K2 = dyn + CAP;
             int32_t* V = (int32_t*)(dyn + 2 * CAP);
             int32_t* V2 = (int32_t*)(dyn + 3 * CAP);
-            for (int i = threadIdx.x; i < m; i += BNT) { K[i] = ckey[ro0 + i]; V[i] = cval[ro0 + i]; }
+            gload_lds2<BNT, 4>(K, ckey + ro0, V, cval + ro0, m);
             csc_bucket<BNT>(g, b, K, K2, V, V2, m, coff[b], node_ptr, csc_ptr, csc_row, csc_eid, cpos, L,
                             cb, base, tot, sm);
         } else {
@@ -1035,13 +1077,25 @@ __global__ void __launch_bounds__(FNT) k_csr_place(Geo g, const int32_t* __restr
     }
     __syncthreads();
     const uint32_t lmask = (uint32_t)(((uint64_t)1 << g.LB) - 1);
-    for (int i = threadIdx.x; i < cnt; i += FNT) {
-        const uint32_t k = keys[off + i];
-        const int j = (int)(k >> g.LB);
-        if (TAGAN_DBAD(j < nv && u + i < g.E + g.N, j, u + i)) continue;   // row of the bucket, CSR capacity
-        if (TAGAN_DBAD(rb[j] + (int64_t)(k & lmask) < g.N, rb[j], k & lmask)) continue;   // column id
-        col[u + i] = rb[j] + (int32_t)(k & lmask);
-        sloc[u + i] = (int32_t)(r0 + j) - rb[j];
+    constexpr int PER = 8;   // loads in flight per thread (see gload_lds)
+    for (int base = 0; base < cnt; base += FNT * PER) {
+        uint32_t kr[PER];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int i = base + q * FNT + (int)threadIdx.x;
+            if (i < cnt) kr[q] = keys[off + i];
+        }
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int i = base + q * FNT + (int)threadIdx.x;
+            if (i >= cnt) continue;
+            const uint32_t k = kr[q];
+            const int j = (int)(k >> g.LB);
+            if (TAGAN_DBAD(j < nv && u + i < g.E + g.N, j, u + i)) continue;   // row of the bucket, CSR capacity
+            if (TAGAN_DBAD(rb[j] + (int64_t)(k & lmask) < g.N, rb[j], k & lmask)) continue;   // column id
+            col[u + i] = rb[j] + (int32_t)(k & lmask);
+            sloc[u + i] = (int32_t)(r0 + j) - rb[j];
+        }
     }
     if (b == g.NB - 1 && threadIdx.x == 0) {
         rowptr[g.N] = uoff[g.NB];
