@@ -1433,10 +1433,23 @@ constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
 // columns spread over grid.y (N / 128 workgroup columns; each re-reads A, mostly from L2); K = 768 three-plane (the
 // QKV input gradient, 288 VGPRs per 16 columns) runs as two K = 384 halves, the second accumulating into C
 // (tagan_sgemm_nt splits it).  H = 64 (C1): 4-wave workgroups cover N = 192 / 64 in one grid column.
+// H = 256 three-plane NT: two n-subtiles per wave over 16-row tiles (248 VGPRs).  With one n-subtile over 32-row
+// tiles (TAGAN_SG_H256N2=0, the round-4 form) each A fragment read from LDS fed 6 MFMAs -- as many LDS cycles as
+// matrix cycles per tile -- and six workgroup columns re-read A for N = 768; now 12 MFMAs per read, three columns:
+// QKV forward 3.11 -> 2.78 ms, out-projection / dC 1.12 -> 1.04 ms at 1.6M rows, C3 step 467 -> 462 ms
+// (profiles/r5za_h256_nt_ab.txt)
+#ifndef TAGAN_SG_H256N2
+#define TAGAN_SG_H256N2 1
+#endif
+#if TAGAN_SG_H256N2
+#define NT_H256_F32 nt_cfg<256, 2, 8, 16, 3, false, false>(768, 1), nt_cfg<256, 2, 8, 16, 3, false, false>(256, 1),
+#else
+#define NT_H256_F32 nt_cfg<256, 1, 8, 32, 3, false, false>(768, 1), nt_cfg<256, 1, 8, 32, 3, false, false>(256, 1),
+#endif
 #define NT_SET3                                                                                              \
     nt_cfg<128, 3, 8, 32, 3, false, false>(384, 1), nt_cfg<128, 1, 8, 32, 3, false, false>(128, 2),            \
     nt_cfg<384, 1, 8, 32, 3, false, false>(128, 1),                                                            \
-    nt_cfg<256, 1, 8, 32, 3, false, false>(768, 1), nt_cfg<256, 1, 8, 32, 3, false, false>(256, 1),            \
+    NT_H256_F32                                                                                              \
     nt_cfg<384, 1, 8, 32, 3, false, false>(256, 1), nt_cfg<384, 1, 8, 32, 3, false, false, MODE_ACC>(256, 1),   \
     nt_cfg<64, 3, 4, 32, 3, false, false>(192, 1), nt_cfg<64, 1, 4, 32, 3, false, false>(64, 2),               \
     nt_cfg<192, 1, 4, 32, 3, false, false>(64, 2)
