@@ -1518,9 +1518,16 @@ constexpr TnCfg tn_cfg(int wg_per_cu) {
 // abf = dY stored bf16 (and X too, unless lnx: X = LN(x) from the fp32 LayerNorm input)
 // H = 256: one n-subtile per wave (the K = 256 accumulator row is 64 VGPRs), grid.y = N / 128 column groups.
 // H = 64: 4-wave workgroups over the whole N.
+// H = 256 three-plane weight gradients with two n-subtiles per wave (as TAGAN_SG_H256N2 for the NT): 12 MFMAs per
+// X fragment read instead of 6 and half the column groups re-reading X -- dW_qkv 3.74 -> 3.19 ms, dW_o 1.30 -> 1.16
+// ms at 1.6M rows, C3 463 -> 453 ms (profiles/r5zb_h256_tn_ab.txt); =0 restores one n-subtile
+#ifndef TAGAN_SG_TN256N2
+#define TAGAN_SG_TN256N2 1
+#endif
 #define TN_SETP(P, ABF)                                                                                      \
     tn_cfg<384, 128, 3, 8, 1, P, ABF>(1), tn_cfg<128, 128, 1, 8, 1, P, ABF>(2),                               \
-    tn_cfg<768, 256, (P == 1 ? 2 : 1), 8, (P == 1 ? 3 : 6), P, ABF>(1), tn_cfg<256, 256, 1, 8, 2, P, ABF>(1),   \
+    tn_cfg<768, 256, (P == 1 || TAGAN_SG_TN256N2 ? 2 : 1), 8, (P == 1 || TAGAN_SG_TN256N2 ? 3 : 6), P, ABF>(1),   \
+    tn_cfg<256, 256, (P == 3 && TAGAN_SG_TN256N2 ? 2 : 1), 8, (P == 3 && TAGAN_SG_TN256N2 ? 1 : 2), P, ABF>(1),   \
     tn_cfg<192, 64, 3, 4, 1, P, ABF>(2), tn_cfg<64, 64, 1, 4, 1, P, ABF>(2)
 const TnCfg TN_TABLE[] = {
     TN_SETP(3, false), TN_SETP(1, false), TN_SETP(1, true),
