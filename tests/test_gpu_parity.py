@@ -432,3 +432,33 @@ def test_geo_backward_orders_are_bitwise_identical(dev, metric, chunk, dtype):
     assert torch.equal(res[0][1], res[1][1])
     if param is not None:
         assert torch.equal(res[0][2], res[1][2])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_geo_block_order_does_not_change_results(dev, dtype, monkeypatch):
+    """The edge chunk kernels' block order (geo_attn.hip geo_xcd_mode: 0 launch order, 1 XCD eighths of the
+    capacity-sized grid, 2 XCD eighths of the valid blocks; chosen by working set) only decides WHICH workgroup runs a
+    chunk: every chunk's output / partial slot is fixed by its index, so outputs and gradients are bitwise identical
+    in all three orders, with hub rows over many chunks, dropout and both storage types."""
+    from tagan_amd import _lib
+    from tagan_amd.fused import GeoCore
+    from tagan_amd.kernels import build_graph
+    counts = [300, 257, 190]
+    eis = [_hub_graph(n, 31 + i) for i, n in enumerate(counts)]
+    N, H, heads = sum(counts), 128, 8
+    g = torch.Generator().manual_seed(5)
+    qkv = (torch.randn(N, 3 * H, generator=g) * 0.5).to(dev, dtype)
+    gout = torch.randn(N, H, generator=g).to(dev, dtype)
+    graph = build_graph([e.to(dev) for e in eis], counts, chunk=16)
+    core = GeoCore(graph, _lib.METRIC_IDS["euclidean"], heads, 0.1, 4321)
+    res = []
+    for mode in ("0", "1", "2"):
+        monkeypatch.setenv("TAGAN_GEO_XCD", mode)
+        out, saved = core.fwd(qkv, None, None)
+        dqkv, _, _ = core.bwd(qkv, out, saved, gout, False, False)
+        torch.cuda.synchronize()
+        res.append((out, dqkv))
+    assert torch.isfinite(res[0][1].float()).all()
+    for out, dqkv in res[1:]:
+        assert torch.equal(out, res[0][0])
+        assert torch.equal(dqkv, res[0][1])
