@@ -1472,9 +1472,21 @@ constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
 #if TAGAN_SG_LN256
 // (one plane only: the three-plane C3 form lost its A/B -- C3 fp32 547 vs 540 ms, its LN-recomputing weight gradient
 // re-reads the fp32 x six times, profiles/r5i_h256_ln_ab.txt)
+// two column groups of three n-subtiles per wave: the fp32 x (and its LN1 statistics) is read by two workgroup
+// columns instead of three -- 3.2M rows 3.07 -> 2.55 ms, C5 bf16 504-508 -> 500 ms (profiles/r5zd_ln256_wide_ab.txt);
+// six n-subtiles in one column group spill.  =0: three groups of two.
+#ifndef TAGAN_SG_LN256_WIDE
+#define TAGAN_SG_LN256_WIDE 1
+#endif
+#if TAGAN_SG_LN256_WIDE
+#define NT_LN256                                                                                             \
+    , nt_cfg<256, 3, 8, 32, 1, false, true, MODE_LN_IN>(768, 1),                                                \
+    nt_cfg<256, 3, 8, 32, 1, false, false, MODE_LN_IN>(768, 1)
+#else
 #define NT_LN256                                                                                             \
     , nt_cfg<256, 2, 8, 64, 1, false, true, MODE_LN_IN>(768, 1),                                                \
     nt_cfg<256, 2, 8, 64, 1, false, false, MODE_LN_IN>(768, 1)
+#endif
 #define TN_LN256 tn_cfg<768, 256, 2, 8, 3, 1, true, true>(1), tn_cfg<768, 256, 2, 8, 3, 1, false, true>(1),
 #else
 #define NT_LN256
