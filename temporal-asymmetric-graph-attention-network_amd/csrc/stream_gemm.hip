@@ -1453,11 +1453,22 @@ constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
     nt_cfg<384, 1, 8, 32, 3, false, false>(256, 1), nt_cfg<384, 1, 8, 32, 3, false, false, MODE_ACC>(256, 1),   \
     nt_cfg<64, 3, 4, 32, 3, false, false>(192, 1), nt_cfg<64, 1, 4, 32, 3, false, false>(64, 2),               \
     nt_cfg<192, 1, 4, 32, 3, false, false>(64, 2)
+// the one-plane H = 256 QKV input gradient (K = 768, N = 256) with bf16 dqkv: all 256 columns in one workgroup
+// column (two n-subtiles per wave, 16-row tiles), so dqkv is read once instead of by two column groups -- C5 bf16
+// 504.5 / 504.9 -> 496.6 / 496.0 ms (profiles/r5ze_dh256_wide_ab.txt); =0: two columns of one n-subtile
+#ifndef TAGAN_SG_DH256_WIDE
+#define TAGAN_SG_DH256_WIDE 1
+#endif
+#if TAGAN_SG_DH256_WIDE
+#define NT_DH256(ABF, CBF) nt_cfg<768, (ABF ? 2 : 1), 8, (ABF ? 16 : 32), 1, ABF, CBF>(256, 1),   // (fp32 A spills)
+#else
+#define NT_DH256(ABF, CBF) nt_cfg<768, 1, 8, 32, 1, ABF, CBF>(256, 1),
+#endif
 #define NT_SET1(ABF, CBF)                                                                                    \
     nt_cfg<128, 3, 8, 64, 1, ABF, CBF>(384, 1), nt_cfg<128, 1, 8, 128, 1, ABF, CBF>(128, 2),                  \
     nt_cfg<384, 1, 8, 64, 1, ABF, CBF>(128, 1),                                                                \
     nt_cfg<256, 2, 8, 64, 1, ABF, CBF>(768, 1), nt_cfg<256, 2, 8, 64, 1, ABF, CBF>(256, 1),                   \
-    nt_cfg<768, 1, 8, 32, 1, ABF, CBF>(256, 1),                                                                \
+    NT_DH256(ABF, CBF)                                                                                       \
     nt_cfg<64, 3, 4, 64, 1, ABF, CBF>(192, 1), nt_cfg<64, 1, 4, 64, 1, ABF, CBF>(64, 2),                      \
     nt_cfg<192, 1, 4, 64, 1, ABF, CBF>(64, 2)
 // The LayerNorm-fused forms (H = 128): LN1 prologue of the QKV projection (x fp32 in; qkv fp32, or bf16 in the

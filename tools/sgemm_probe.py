@@ -2,7 +2,7 @@
 
 Per shape: kernel time (HIP events, median of 20 after 5 warm-ups), the same product through torch (with the bench's
 TunableOp table), and the error of both against fp64 (max-abs / max|ref| and normwise) on the same inputs.
-Usage: python tools/sgemm_probe.py [--M 320000] [--bf16] ; TAGAN_LIB=<variant library> times another build.
+Usage: python tools/sgemm_probe.py [--M 320000] [--H 128] [--planes 3,1] [--cases ...] ; TAGAN_LIB=<variant library> times another build.
 """
 import argparse
 import json
