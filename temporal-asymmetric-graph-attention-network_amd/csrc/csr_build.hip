@@ -310,10 +310,20 @@ constexpr int UNR = 4;   // loads in flight per lane in the streaming passes
 // the full key.  The loader fetches item i's raw values one tile ahead (issued before this tile's scan and write-out,
 // so the loads overlap them) and decodes them into (bin, key, value).
 // LDS: tcnt, tstart, gpos: NB ints each (tcnt zero on entry and exit); stk / stv / stp: NTH * IPT each; sm: NTH/64+1.
-template <int NTH, int IPT, int NB, bool VAL, typename Loader>
+// GRES: no per-block bases -- each tile reserves its run of every non-empty bin with one global atomic
+// (res.start[(res.b0 + bin) << res.sc] + atomicAdd(&res.fill[res.b0 + bin], count)), so the caller needs no histogram
+// pre-pass over its chunk (a second read of the raw input).
+struct TileRes {
+    const int32_t* start;
+    int32_t* fill;
+    int64_t b0;
+    int sc;
+};
+
+template <int NTH, int IPT, int NB, bool VAL, bool GRES = false, typename Loader>
 __device__ void tile_partition(int64_t a, int64_t z, const Loader& ld, int* sh_base, int* tcnt, int* tstart, int* gpos,
                                uint32_t* stk, int32_t* stv, int* stp, int32_t* sm, uint32_t* __restrict__ out_k,
-                               int32_t* __restrict__ out_v) {
+                               int32_t* __restrict__ out_v, TileRes res = TileRes{}) {
     using Raw = typename Loader::Raw;
     constexpr int TILE = NTH * IPT;
     const int tid = threadIdx.x;
@@ -337,8 +347,12 @@ __device__ void tile_partition(int64_t a, int64_t z, const Loader& ld, int* sh_b
         const int32_t ex = scan::block_excl<NTH>((int32_t)c, (int32_t)0, scan::Plus(), sm, &tot);
         if (tid < NB) {
             tstart[tid] = ex;
-            gpos[tid] = sh_base[tid];
-            sh_base[tid] += c;
+            if (GRES) {
+                gpos[tid] = c ? res.start[(res.b0 + tid) << res.sc] + atomicAdd(&res.fill[res.b0 + tid], c) : 0;
+            } else {
+                gpos[tid] = sh_base[tid];
+                sh_base[tid] += c;
+            }
             tcnt[tid] = 0;
         }
         __syncthreads();
@@ -364,6 +378,9 @@ __device__ void tile_partition(int64_t a, int64_t z, const Loader& ld, int* sh_b
 constexpr int PNB = 256;   // bins of the staged partition passes (coarse bins per snapshot, buckets per coarse bin)
 constexpr int PIPT = 4;    // items per thread per tile in the partition passes
 constexpr int PTILE = PNT * PIPT;
+#ifndef TAGAN_CSR_TILE_RES
+#define TAGAN_CSR_TILE_RES 1   // staged partition passes reserve per tile (one read of the input, no block pre-pass)
+#endif
 
 // bins of shift `sh` spanned by the nodes [v0, v1) of one snapshot
 struct Span {
@@ -512,7 +529,8 @@ __global__ void __launch_bounds__(PNT) k_part_edges(Geo g, const int64_t* __rest
         const int64_t base = node_ptr[gg], n = node_ptr[gg + 1] - base;
         const int64_t a = max(e0, edge_ptr[gg]), z = min(e1, edge_ptr[gg + 1]);
         const Span sp = span_of(base, base + n, shc, PART_BINS);
-        if (sp.lds) {
+        const bool staged = sp.lds && sp.nb <= PNB;
+        if (sp.lds && !(TAGAN_CSR_TILE_RES && staged)) {
             for (int i = threadIdx.x; i < sp.nb; i += PNT) h[i] = 0;
             __syncthreads();
             for (int64_t e4 = a + threadIdx.x; e4 < z; e4 += UNR * PNT) {
@@ -538,9 +556,11 @@ __global__ void __launch_bounds__(PNT) k_part_edges(Geo g, const int64_t* __rest
             }
             __syncthreads();
         }
-        if (sp.lds && sp.nb <= PNB) {   // LDS-staged scatter
+        if (staged) {   // LDS-staged scatter
             const EdgeLoader ld{ei, ld_, base, n, sp.b0, shc, g.SB, g.LB, rmask, fmask};
-            tile_partition<PNT, PIPT, PNB, false>(a, z, ld, h, tcnt, tstart, gpos, stk, nullptr, stp, sm, out, nullptr);
+            tile_partition<PNT, PIPT, PNB, false, TAGAN_CSR_TILE_RES>(a, z, ld, h, tcnt, tstart, gpos, stk, nullptr, stp,
+                                                                      sm, out, nullptr,
+                                                                      TileRes{bstart, fill, sp.b0, g.SC});
         } else {
             for (int64_t e4 = a + threadIdx.x; e4 < z; e4 += UNR * PNT) {
                 int64_t sv[UNR], dv[UNR];
@@ -1139,7 +1159,8 @@ __global__ void __launch_bounds__(PNT) k_part_csr(Geo g, const int32_t* __restri
         const int64_t v0 = node_ptr[gg], v1 = node_ptr[gg + 1];
         const int64_t a = max(e0, (int64_t)rowptr[v0]), z = min(e1, (int64_t)rowptr[v1]);
         const Span sp = span_of(v0, v1, shc, PART_BINS);
-        if (sp.lds) {
+        const bool staged = sp.lds && sp.nb <= PNB;
+        if (sp.lds && !(TAGAN_CSR_TILE_RES && staged)) {
             for (int i = threadIdx.x; i < sp.nb; i += PNT) h[i] = 0;
             __syncthreads();
             for (int64_t e4 = a + threadIdx.x; e4 < z; e4 += UNR * PNT) {
@@ -1158,9 +1179,10 @@ __global__ void __launch_bounds__(PNT) k_part_csr(Geo g, const int32_t* __restri
             }
             __syncthreads();
         }
-        if (sp.lds && sp.nb <= PNB) {   // LDS-staged scatter
+        if (staged) {   // LDS-staged scatter
             const CsrEntryLoader ld{col, sloc, sp.b0, shc, g.SB, g.LB, cmask, fmask};
-            tile_partition<PNT, PIPT, PNB, true>(a, z, ld, h, tcnt, tstart, gpos, stk, stv, stp, sm, okey, oval);
+            tile_partition<PNT, PIPT, PNB, true, TAGAN_CSR_TILE_RES>(a, z, ld, h, tcnt, tstart, gpos, stk, stv, stp, sm,
+                                                                     okey, oval, TileRes{cstart, fill, sp.b0, g.SC});
         } else {
             for (int64_t e4 = a + threadIdx.x; e4 < z; e4 += UNR * PNT) {
                 int32_t dd[UNR], sl[UNR];
