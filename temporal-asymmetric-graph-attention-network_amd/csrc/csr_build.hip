@@ -39,7 +39,10 @@ constexpr int PNT = 1024;          // partition (count / part) blocks
 constexpr int LDS_BINS = 16384;    // LDS histogram bins per count block and direction
 constexpr int PART_BINS = 2048;    // LDS bins of the partition passes (more: global atomics)
 constexpr int RNT = 1024;          // refine blocks (one per coarse bin)
-constexpr int FNT = 256;           // small-bucket finish workgroups (4 waves)
+#ifndef TAGAN_CSR_FNT
+#define TAGAN_CSR_FNT 256
+#endif
+constexpr int FNT = TAGAN_CSR_FNT;  // small-bucket finish workgroups (4 waves)
 #ifndef TAGAN_CSR_TARGET
 #define TAGAN_CSR_TARGET 2048
 #endif
@@ -724,8 +727,8 @@ __device__ bool seg_sort(const Geo& g, int nrows, uint32_t* K, uint32_t* K2, int
         const int j = (int)(x >> g.LB), n = L.rc[j];
         if (n > SHORT_ROW) continue;
         const int s = L.ro[j];
-        const uint64_t me = ((uint64_t)x << 32) | (uint32_t)i;
         int p = 0;
+        const uint64_t me = ((uint64_t)x << 32) | (uint32_t)i;
         for (int t = s; t < s + n; ++t) p += (((uint64_t)K2[t] << 32) | (uint32_t)t) < me ? 1 : 0;
         K[s + p] = x;
         if (VAL) V[s + p] = V2[i];

@@ -16,7 +16,7 @@ FAMILIES = [
     ("layernorm", r"k_ln_"),
     ("LN2 bwd + out-proj grads (fused)", r"k_ln2_bwd_out"),
     ("proj (fused MFMA)", r"k_proj"),
-    ("csr", r"rocprim|k_scatter|k_fill_tail|k_keys|k_chunk|k_tri|csr|k_count"),
+    ("csr", r"rocprim|k_scatter|k_fill_tail|k_keys|k_chunk|k_tri|csr|csc|k_count|k_part_|k_refine|k_big_list|k_init\(|scan::k_|Tri"),
     ("colsum/pool", r"k_colsum|k_pool"),
     ("torch elementwise", r"elementwise|CatArray|index|gather|scatter"),
     ("torch reduce", r"reduce_kernel"),
