@@ -883,6 +883,9 @@ __global__ void __launch_bounds__(W * 64) k_rowgemm(NtArgs g) {
 }
 
 // ------------------------------------------------------------------------------------------- TN: dW = dYᵀ·X
+#ifndef TAGAN_SG_TN_ILOAD
+#define TAGAN_SG_TN_ILOAD 1
+#endif
 struct TnArgs {
     int64_t M;
     const void* dy;          // [M, N] rows, row stride ldy
@@ -951,9 +954,8 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_tn(TnArgs g) {
     float4 pf[(ABF && !LNX) ? 1 : CPT];
     uint2 pb[ABF ? CPT : 1];
     float pm[CX], pr[CX];
-    auto load = [&](int64_t t) {
-#pragma unroll
-        for (int i = 0; i < CPT; ++i) {
+    auto load1 = [&](int64_t t, const int i) {
+        {
             const int c = i * NT + threadIdx.x;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             uint2 u = make_uint2(0, 0);
@@ -985,9 +987,12 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_tn(TnArgs g) {
             if constexpr (!ABF || LNX) pf[i] = v;
         }
     };
-    auto stash = [&]() {
+    auto load = [&](int64_t t) {
 #pragma unroll
-        for (int i = 0; i < CPT; ++i) {
+        for (int i = 0; i < CPT; ++i) load1(t, i);
+    };
+    auto stash1 = [&](const int i) {
+        {
             const int c = i * NT + threadIdx.x;
             if (c < Q4) {
                 const bool isy = LNX ? i < CY : c < 32 * NL / 4;
@@ -1016,6 +1021,15 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_tn(TnArgs g) {
             }
         }
     };
+    // TAGAN_SG_TN_ILOAD: chunk i of the next tile is loaded as soon as chunk i of this one is stashed (the next
+    // tile's loads start during the stash instead of after it; no extra registers)
+    auto stash_reload = [&](int64_t tn, bool more) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            stash1(i);
+            if (TAGAN_SG_TN_ILOAD && more) load1(tn, i);
+        }
+    };
     // transposed fragment of columns [c0, c0 + 16) of a plane with row stride S: rows 4 grp + q and 16 + 4 grp + q
     auto frag = [&](const uint16_t* plane, int S, int c0) {
         const int q = li >> 2, p4 = li & 3;
@@ -1029,9 +1043,9 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_tn(TnArgs g) {
     if (t0 < t1) load(t0);
     for (int64_t t = t0; t < t1; ++t) {
         lds_barrier();                   // the previous tile's fragments are read
-        stash();
+        stash_reload(t + 1, t + 1 < t1);
         lds_barrier();
-        if (t + 1 < t1) load(t + 1);
+        if (!TAGAN_SG_TN_ILOAD && t + 1 < t1) load(t + 1);
         bf16x8 ya[NSN][P];
 #pragma unroll
         for (int s = 0; s < NSN; ++s)
