@@ -1158,6 +1158,11 @@ int check_common(int dtype, int metric, const tagan_graph* g, int heads, int d, 
 // batch fits (C2).  Edge kernels alone, fwd / bwd ms, shipped map (1) -> chosen order (profiles/r5u_geo_xcd_ab.txt):
 // C2 0.296 / 0.745 -> 0.281 / 0.706, C3 50.1 / 86.8 -> 38.7 / 66.5, C4 68.2 / 128.4 -> 57.3 / 105.9, C5 bf16
 // 48.3 / 97.4 -> 38.0 / 75.4.  TAGAN_GEO_XCD=0|1|2 forces one (read per call: A/B runs, tests).
+// The test is on the batch's K and V NODE rows (2·N·H·bytes, the distinct rows the gathers can touch), not on the
+// gathered bytes, against 512 MB (twice the cache): a separator between the measured cases, not the cache size.  C2's
+// node rows are 328 MB -- more than the cache -- yet XCD-contiguous order wins there, because each XCD's eighth of
+// the blocks touches only its own ~41 MB of K | V, which its share of the cache holds; C3-C5 (6.5-13 GB) gain from
+// launch order.  A batch between 256 and 512 MB has not been measured.
 int geo_xcd_mode(int64_t n, int H, bool bf16) {
     const char* e = getenv("TAGAN_GEO_XCD");
     if (e && e[0] >= '0' && e[0] <= '2' && !e[1]) return e[0] - '0';

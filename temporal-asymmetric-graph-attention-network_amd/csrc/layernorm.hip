@@ -337,33 +337,40 @@ int ln_bwd_blocks() { return TAGAN_LN_BWD_BLOCKS; }
 #ifndef TAGAN_LN_ROWS
 #define TAGAN_LN_ROWS 4
 #endif
+static_assert(TAGAN_LN_ROWS == 1 || TAGAN_LN_ROWS == 2 || TAGAN_LN_ROWS == 4, "TAGAN_LN_ROWS: 1, 2 or 4 (instantiated)");
 int ln_rows(int nv) { return nv == 2 && TAGAN_LN_ROWS > 2 ? 2 : TAGAN_LN_ROWS; }
 
 // the fused LN2 + skip-LN backward (H = 128: LPR 32, NV 1; any U)
+// Both launchers run exactly the U the caller sized the grid for, or launch nothing and return false.
 template <typename S>
-void launch_ln_skip_bwd(int u, dim3 g, hipStream_t s, const LnArgs& A) {
+bool launch_ln_skip_bwd(int u, dim3 g, hipStream_t s, const LnArgs& A) {
     if (u == 1) k_ln_bwd<32, 1, 1, S, true><<<g, BLK, 0, s>>>(A);
     else if (u == 2) k_ln_bwd<32, 1, 2, S, true><<<g, BLK, 0, s>>>(A);
-    else k_ln_bwd<32, 1, 4, S, true><<<g, BLK, 0, s>>>(A);
+    else if (u == 4) k_ln_bwd<32, 1, 4, S, true><<<g, BLK, 0, s>>>(A);
+    else return false;
+    return true;
 }
 
 template <typename S, bool FWD>
-void launch_ln(int lpr, int nv, int u, dim3 g, hipStream_t s, const LnArgs& A) {
+bool launch_ln(int lpr, int nv, int u, dim3 g, hipStream_t s, const LnArgs& A) {
 #define TAGAN_LN_K(L, N, U) (FWD ? k_ln_fwd<L, N, U, S> : k_ln_bwd<L, N, U, S>)<<<g, BLK, 0, s>>>(A)
 #define TAGAN_LN_U(L, N)                          \
     do {                                          \
         if (u == 1) TAGAN_LN_K(L, N, 1);          \
         else if (u == 2) TAGAN_LN_K(L, N, 2);     \
-        else TAGAN_LN_K(L, N, 4);                 \
+        else if (u == 4) TAGAN_LN_K(L, N, 4);     \
+        else return false;                        \
     } while (0)
     if (lpr == 8) TAGAN_LN_U(8, 1);
     else if (lpr == 16) TAGAN_LN_U(16, 1);
     else if (lpr == 32) TAGAN_LN_U(32, 1);
     else if (nv == 1) TAGAN_LN_U(64, 1);
     else if (u == 1) TAGAN_LN_K(64, 2, 1);
-    else TAGAN_LN_K(64, 2, 2);
+    else if (u == 2) TAGAN_LN_K(64, 2, 2);
+    else return false;
 #undef TAGAN_LN_U
 #undef TAGAN_LN_K
+    return true;
 }
 
 }  // namespace
@@ -396,8 +403,9 @@ int tagan_add_layernorm_fwd(int dtype, int64_t M, int32_t H, const float* a, con
     const int64_t rpw = (WAVE / lpr) * u;
     const dim3 g((unsigned)(((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE)));
     hipStream_t s = as_stream(stream);
-    if (dtype == TAGAN_BF16) launch_ln<bf16s, true>(lpr, nv, u, g, s, A);
-    else launch_ln<float, true>(lpr, nv, u, g, s, A);
+    const bool ok = dtype == TAGAN_BF16 ? launch_ln<bf16s, true>(lpr, nv, u, g, s, A)
+                                        : launch_ln<float, true>(lpr, nv, u, g, s, A);
+    TAGAN_REQUIRE(ok, TAGAN_ERR_UNSUPPORTED, "layernorm_fwd: no kernel for H=%d with %d row groups per wave", H, u);
     TAGAN_CHECK_LAUNCH("layernorm_fwd");
     return TAGAN_OK;
 }
@@ -421,7 +429,8 @@ int tagan_add_layernorm_skip_fwd(int64_t M, int32_t H, const float* a, const flo
     const int u = ln_rows(nv);
     const int64_t rpw = (WAVE / lpr) * u;
     const dim3 g((unsigned)(((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE)));
-    launch_ln<float, true>(lpr, nv, u, g, as_stream(stream), A);
+    TAGAN_REQUIRE((launch_ln<float, true>(lpr, nv, u, g, as_stream(stream), A)), TAGAN_ERR_UNSUPPORTED,
+                  "layernorm_skip_fwd: no kernel for H=%d with %d row groups per wave", H, u);
     TAGAN_CHECK_LAUNCH("layernorm_skip_fwd");
     return TAGAN_OK;
 }
@@ -453,8 +462,9 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s_in, cons
     const int64_t need = ((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE);
     const int nblk = (int)std::min<int64_t>(need, ln_bwd_blocks());
     hipStream_t s = as_stream(stream);
-    if (dtype == TAGAN_BF16) launch_ln<bf16s, false>(lpr, nv, u, dim3(nblk), s, A);
-    else launch_ln<float, false>(lpr, nv, u, dim3(nblk), s, A);
+    const bool ok = dtype == TAGAN_BF16 ? launch_ln<bf16s, false>(lpr, nv, u, dim3(nblk), s, A)
+                                        : launch_ln<float, false>(lpr, nv, u, dim3(nblk), s, A);
+    TAGAN_REQUIRE(ok, TAGAN_ERR_UNSUPPORTED, "layernorm_bwd: no kernel for H=%d with %d row groups per wave", H, u);
     TAGAN_CHECK_LAUNCH("layernorm_bwd");
     if (dgamma || dbeta) {
         launch_colsum(A.part, nblk, 2 * H, dgamma, dbeta, H, s, 1.f, 3 * H);
@@ -497,8 +507,9 @@ int tagan_layernorm_skip_bwd(int dtype, int64_t M, int32_t H, const float* s_in,
     const int64_t need = ((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE);
     const int nblk = (int)std::min<int64_t>(need, ln_bwd_blocks());
     hipStream_t s = as_stream(stream);
-    if (dtype == TAGAN_BF16) launch_ln_skip_bwd<bf16s>(u, dim3(nblk), s, A);
-    else launch_ln_skip_bwd<float>(u, dim3(nblk), s, A);
+    const bool ok = dtype == TAGAN_BF16 ? launch_ln_skip_bwd<bf16s>(u, dim3(nblk), s, A)
+                                        : launch_ln_skip_bwd<float>(u, dim3(nblk), s, A);
+    TAGAN_REQUIRE(ok, TAGAN_ERR_UNSUPPORTED, "layernorm_skip_bwd: no kernel with %d row groups per wave", u);
     TAGAN_CHECK_LAUNCH("layernorm_skip_bwd");
     launch_colsum(A.part, nblk, 2 * H, dgamma, dbeta, H, s, 1.f, 5 * H);
     TAGAN_CHECK_LAUNCH("layernorm_skip_bwd_sum");

@@ -1152,6 +1152,11 @@ struct L2Args {
     float* part_ln;           // [G][NPL * H]: dγ | dβ [| dγ_s | dβ_s]
 };
 
+// TAGAN_LN2_FORM (A/B builds only): 0 shipped; 1 the next tile's loads after the plane-writing barriers; 2 as 1 with
+// dead rows branched around in the LN sums (the round-5 first form, profiles/r5d_ln2_probe.txt).
+#ifndef TAGAN_LN2_FORM
+#define TAGAN_LN2_FORM 0
+#endif
 template <int P, bool ABF, bool SK>
 __global__ void __launch_bounds__(512, 1) k_ln2_bwd_out(L2Args g) {
     constexpr int H = 128, BM = 32, NW = 8, KK = H / 32, KS = H / 16, S = H + 16, PL = BM * S;
@@ -1281,12 +1286,23 @@ __global__ void __launch_bounds__(512, 1) k_ln2_bwd_out(L2Args g) {
             float sres = o;
             if constexpr (SK) sres += rrs * (gsk[e] - c1s * xsk[e] - c2s);
             dsv[e] = sres;
+            if (TAGAN_LN2_FORM == 2) {   // round-5 first form: dead rows branched around (A/B only)
+                if (live) {
+                    dg[e] += d[e] * xh[e];
+                    db[e] += d[e];
+                    if constexpr (SK) {
+                        dgs[e] += d[e] * xsk[e];
+                        dbs[e] += d[e];
+                    }
+                }
+            } else {
             const float dl = live ? d[e] : 0.f;   // dead rows add exact zeros (their operands are row M - 1's)
             dg[e] += dl * xh[e];
             db[e] += dl;
             if constexpr (SK) {
                 dgs[e] += dl * xsk[e];
                 dbs[e] += dl;
+            }
             }
         }
         if (live) {
@@ -1295,14 +1311,14 @@ __global__ void __launch_bounds__(512, 1) k_ln2_bwd_out(L2Args g) {
             *reinterpret_cast<float4*>(pr + 4) = make_float4(dsv[4], dsv[5], dsv[6], dsv[7]);
         }
         // The next tile's loads go out here, right after this tile's row math, into the same variables (c is copied
-        // first).  Issued after the plane-writing barriers instead (where the matrix work would cover them better),
-        // the kernel's LN column sums came out nondeterministic at multi-tile workgroups (column 8q + 4 of dgamma,
-        // bf16 planes + skip LayerNorm; tools/ln2_debug_probe.py, profiles/r5d_ln2_probe.txt): the compiler had sunk
-        // the sums' arithmetic below those loads.
+        // first).  Round 5's first form (loads after the plane-writing barriers, dead rows branched around in the LN
+        // sums: TAGAN_LN2_FORM=2) gave nondeterministic dgamma columns 8q + 4 / 8q + 6: not a load hazard, but the
+        // compiler encoding those two products as v_pk_mul_f32 with src1's high register in the low lane, a form that
+        // drops low-lane results on gfx950 (tools/isa_audit.py now rejects it at every build).
         float4 vc_cur[ABF ? 1 : 2];
         const uint4 vcb_cur = vcb;
         if constexpr (!ABF) { vc_cur[0] = vc[0]; vc_cur[1] = vc[1]; }
-        if (t + 1 < t1) load(t + 1);
+        if (TAGAN_LN2_FORM == 0 && t + 1 < t1) load(t + 1);
         // ---- do and c -> row-major bf16 planes
         lds_barrier();   // the previous tile's fragments are read
         {
@@ -1326,6 +1342,7 @@ __global__ void __launch_bounds__(512, 1) k_ln2_bwd_out(L2Args g) {
             }
         }
         lds_barrier();
+        if (TAGAN_LN2_FORM != 0 && t + 1 < t1) load(t + 1);   // round-5 first form (A/B only)
         // ---- dW_o rows 16 w.., db_o
         {
             bf16x8 ya[P];
@@ -1487,8 +1504,9 @@ constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
     nt_cfg<192, 1, 4, 64, 1, ABF, CBF>(64, 2)
 // The LayerNorm-fused forms (H = 128): LN1 prologue of the QKV projection (x fp32 in; qkv fp32, or bf16 in the
 // bf16 activation mode), dropout + residual + LN2 [+ skip LN] epilogue of the out-projection (y fp32), LN1 backward
-// epilogue of the QKV input gradient (dx fp32).  At H = 256 (C3, C5) the LN1 prologue (32 lanes per row) and its
-// LN-recomputing weight gradient; LN2 and LN1's backward stay standalone there.
+// epilogue of the QKV input gradient (dx fp32).  At H = 256 (C3, C5) the LN1 prologue (32 lanes per row) with its
+// LN-recomputing weight gradient, and in the one-plane (bf16 activation) mode the LN2 epilogue of the out-projection
+// (MODE_LN_OUT row-owner kernels with N = 256); LN1's and LN2's backward stay standalone there.
 // (The LN2 epilogue and the one-plane LN1-backward epilogue run on the row-owner kernels, RG_TABLE; the three-plane
 // LN1-backward epilogue lost its A/B -- fp32 step 6.99 vs 6.75 ms, profiles/r3d_ab_step.txt -- and is not built.)
 #ifndef TAGAN_SG_LN256

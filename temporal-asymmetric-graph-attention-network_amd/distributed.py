@@ -33,19 +33,26 @@ import torch.distributed as dist
 # the next collective -- the captured one -- so one event object would be shared between a graph node and later
 # eager Works.  The flag is read when a process group is constructed: it must be set before init_process_group.
 EVENT_CACHE_ENV = "TORCH_NCCL_CUDA_EVENT_CACHE"
-_graph_safe_groups = False   # set by init_process_group: the groups of this process were built with the cache off
+_graph_safe_groups = False   # graph_safe_env() ran (init_process_group calls it before creating the group)
+_cache_on_group = False      # graph_safe_env() ran while a group built with the cache ON already existed
 
 
 def graph_safe_env() -> None:
-    """Switch ProcessGroupNCCL's event recycling off for the process groups created from here on."""
-    global _graph_safe_groups
+    """Switch ProcessGroupNCCL's event recycling off for the process groups created from here on.  Called while a
+    process group built with the cache on already exists, it records that: that group stays unsafe to capture."""
+    global _graph_safe_groups, _cache_on_group
+    if dist.is_available() and dist.is_initialized() and os.environ.get(EVENT_CACHE_ENV) != "0":
+        _cache_on_group = True
     os.environ[EVENT_CACHE_ENV] = "0"
     _graph_safe_groups = True
 
 
 def graph_safe_groups() -> bool:
-    """True when this process's groups were created after ``graph_safe_env()`` (with the event cache off)."""
-    return _graph_safe_groups
+    """True when this process's groups were built with the event cache off: created after ``graph_safe_env()``, or
+    with ``TORCH_NCCL_CUDA_EVENT_CACHE=0`` exported by the caller before ``dist.init_process_group``."""
+    if _cache_on_group:
+        return False
+    return _graph_safe_groups or os.environ.get(EVENT_CACHE_ENV) == "0"
 
 
 def init_process_group(backend: str, **kw) -> None:
@@ -77,6 +84,11 @@ def retire_pending_works(device=None) -> int:
     groups = nccl_groups()
     if not groups:
         return 0
+    missing = [pg for pg in groups if not callable(getattr(pg, "_wait_for_pending_works", None))]
+    if missing:
+        raise RuntimeError("retire_pending_works: this torch (%s) has no ProcessGroup._wait_for_pending_works, so the "
+                           "RCCL watchdog's eager Works cannot be retired before a capture; capturing now could abort "
+                           "the process (DESIGN.md section 6) -- run the step eagerly (GraphedStep off)" % torch.__version__)
     torch.cuda.synchronize(device)
     for pg in groups:
         pg._wait_for_pending_works()

@@ -69,9 +69,9 @@ class GraphedStep:
             # empty before `side` starts capturing (distributed.py).
             from .distributed import EVENT_CACHE_ENV, graph_safe_groups, retire_pending_works
             if not graph_safe_groups():
-                raise RuntimeError("GraphedStep with a live RCCL process group needs the group created through "
-                                   "tagan_amd.distributed.init_process_group (%s=0 before the group exists)"
-                                   % EVENT_CACHE_ENV)
+                raise RuntimeError("GraphedStep with a live RCCL process group needs the group built with the event "
+                                   "cache off: create it through tagan_amd.distributed.init_process_group, or export "
+                                   "%s=0 before dist.init_process_group" % EVENT_CACHE_ENV)
             retire_pending_works(dev)
         self.graph = torch.cuda.CUDAGraph()
         # captured on the warm-up stream: autograd nodes that outlive a warm-up step (a loss the caller kept,

@@ -95,3 +95,39 @@ def test_grad_bucket_grad_on_one_rank_only():
     assert torch.allclose(res["b_avg0"], res["b0"] / 2) and torch.equal(res["b_avg0"], res["b_avg1"])
     assert torch.equal(res["a_avg0"], res["a_avg1"])
     assert res["seed0"] != res["seed1"]
+
+
+def _guard_worker(rank, world, port, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.pop("TORCH_NCCL_CUDA_EVENT_CACHE", None)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import tagan_amd.distributed as D
+    dist.init_process_group("gloo", rank=rank, world_size=world)   # built by the caller, cache env not set
+    results["before%d" % rank] = D.graph_safe_groups()
+    D.graph_safe_env()                                             # too late for the group that exists
+    results["late%d" % rank] = D.graph_safe_groups()
+    dist.destroy_process_group()
+
+
+def test_graph_safe_guard_states(monkeypatch):
+    """the capture guard accepts a caller-exported TORCH_NCCL_CUDA_EVENT_CACHE=0 and refuses a group that
+    existed before graph_safe_env() set it; retire_pending_works names a torch without _wait_for_pending_works."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import tagan_amd.distributed as D
+    monkeypatch.setattr(D, "_graph_safe_groups", False)
+    monkeypatch.setattr(D, "_cache_on_group", False)
+    monkeypatch.setenv(D.EVENT_CACHE_ENV, "0")
+    assert D.graph_safe_groups()                 # exported by the caller, no graph_safe_env() call
+    monkeypatch.delenv(D.EVENT_CACHE_ENV)
+    assert not D.graph_safe_groups()
+    monkeypatch.setattr(D, "nccl_groups", lambda: [object()])
+    with pytest.raises(RuntimeError, match="_wait_for_pending_works"):
+        D.retire_pending_works()
+    results = mp.Manager().dict()
+    mp.spawn(_guard_worker, args=(2, _free_port(), results), nprocs=2, join=True)
+    for r in range(2):
+        assert results["before%d" % r] is False
+        assert results["late%d" % r] is False

@@ -271,11 +271,11 @@ FULL = {
 }
 
 
-def _model(name, dev, dropout=0.0):
+def _model(name, dev, dropout=0.0, precision="fp32"):
     from tagan_amd import TAGAN, synthetic
     cfg = synthetic.config_for(name, dropout=dropout)
     torch.manual_seed(0)
-    model = TAGAN(cfg).to(dev).train()
+    model = TAGAN(cfg, precision=precision).to(dev).train()
     with torch.no_grad():   # non-trivial LayerNorm affine parameters (init is 1 / 0)
         g = torch.Generator(device=dev).manual_seed(3)
         for n, p in model.named_parameters():
@@ -412,14 +412,15 @@ def test_fullsize_temporal_rows(dev, name):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("name", ["c3", "c4", "c5"])
-def test_fullsize_model_finite_and_reproducible(dev, name):
+@pytest.mark.parametrize("name,precision", [("c3", "fp32"), ("c4", "fp32"), ("c5", "fp32"), ("c5", "bf16")])
+def test_fullsize_model_finite_and_reproducible(dev, name, precision):
     """Whole TAGAN forward + backward at full size (C5: one rank's 16-snapshot share), training mode with
     the config's dropout 0.1: finite loss and gradients, and a second run with the same seeds is bitwise
-    identical (atomic-free, fixed-order reductions; counter-based dropout)."""
+    identical (atomic-free, fixed-order reductions; counter-based dropout).  C5 also in the bf16 activation mode
+    (BASELINE's C5 dtype), whose one-plane stream GEMMs and weight gradients the fp32 run does not reach."""
     from tagan_amd import synthetic
     N = synthetic.CONFIGS[name][0]
-    cfg, model = _model(name, dev, dropout=0.1)
+    cfg, model = _model(name, dev, dropout=0.1, precision=precision)
     seq = synthetic.make_sequence(name, dev, seed=1000, snapshots=FULL[name])
     labels = torch.tensor([1.0], device=dev)
     runs = []

@@ -174,3 +174,46 @@ def test_wprep_block_equals_single_preps(planes, H):
             sg.wprep(wq, True, planes))
     for a, b in zip(got, want):
         assert torch.equal(a, b)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("M", [320_000, 3_200_000])
+@pytest.mark.parametrize("H", [128, 256])
+@pytest.mark.parametrize("form", ["plain", "lnx"])
+def test_one_plane_tn_reproducible_at_scale(form, H, M):
+    """The one-plane weight gradients of the bf16 activation mode (C5) at C2 / C5-share row counts, where the
+    next tile's loads are issued chunk by chunk during the stash (TAGAN_SG_TN_ILOAD) and each workgroup runs many
+    tiles: three calls bitwise equal, and within 1e-2 normwise of fp64.  "lnx": the LN-recomputing form (x fp32)."""
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    g = torch.Generator(device=dev).manual_seed(M % 9973 + H)
+    dq = torch.randn(M, 3 * H, device=dev, generator=g).to(torch.bfloat16)
+    if form == "plain":
+        x = torch.randn(M, H, device=dev, generator=g).to(torch.bfloat16)
+        runs = [sg.tn(dq, x, 1) for _ in range(3)]
+        xr = x
+    else:
+        if not sg.ln_supported(H, 1, True, "in"):
+            pytest.skip("no LN1-prologue kernels at H=%d" % H)
+        x = 0.3 + torch.randn(M, H, device=dev, generator=g)
+        ln_w = 1.0 + 0.1 * torch.randn(H, device=dev, generator=g)
+        ln_b = 0.1 * torch.randn(H, device=dev, generator=g)
+        x64 = x.double()
+        mean = x64.mean(1)
+        rstd = 1.0 / torch.sqrt(((x64 - mean[:, None]) ** 2).mean(1) + 1e-5)
+        runs = [sg.tn_ln(dq, x, ln_w, ln_b, mean.float(), rstd.float(), 1) for _ in range(3)]
+        xr = None
+        del x64
+    for dw, db in runs[1:]:
+        assert torch.equal(dw, runs[0][0]) and torch.equal(db, runs[0][1])
+    ref = torch.zeros(3 * H, H, device=dev, dtype=torch.float64)
+    for r0 in range(0, M, 400_000):
+        d = dq[r0:r0 + 400_000].double()
+        if xr is not None:
+            xx = xr[r0:r0 + 400_000].double()
+        else:
+            xc = x[r0:r0 + 400_000].double()
+            xx = (xc - mean[r0:r0 + 400_000, None]) * rstd[r0:r0 + 400_000, None] * ln_w.double() + ln_b.double()
+        ref += d.t() @ xx
+    assert _nerr(runs[0][0], ref) < 1e-2
+    assert _nerr(runs[0][1], dq.double().sum(0)) < 1e-2

@@ -342,7 +342,7 @@ def test_ln_supported_shapes():
     for op in ("in", "out", "bwd"):
         assert sg.ln_supported(128, 1, True, op) and sg.ln_supported(128, 1, False, op)
         assert sg.ln_supported(128, 3, False, op) == (op != "bwd")   # the three-plane LN1-backward form is not built
-        # H = 256: the LN1 prologue only (LN2 and LN1's backward stay standalone there)
+        # H = 256: the LN1 prologue and, one-plane, the LN2 epilogue ("out"); LN1's backward stays standalone there
         # (the three-plane H = 256 LN1 prologue lost its A/B and is not built)
         assert not sg.ln_supported(256, 3, False, op)
         assert sg.ln_supported(256, 1, True, op) == (op in ("in", "out"))
