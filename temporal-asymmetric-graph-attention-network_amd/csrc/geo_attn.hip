@@ -1049,8 +1049,24 @@ int pick_lpr(int H, int d) {   // nonzero = fast path
     return 0;
 }
 
-int pick_fpl(int H, int d, Pass pass, bool bf16) {
-    const int want = pass == P_FWD ? TAGAN_GEO_FPL_FWD : bf16 ? TAGAN_GEO_FPL_BWD_BF16 : TAGAN_GEO_FPL_BWD;
+// A batch is cache-cold when its K and V node rows exceed 512 MB (kv_cold, also geo_xcd_mode's default rule).  The
+// forward then takes 4 features per lane: twice the lanes per chunk keep more gathers in flight against HBM (fp32
+// C4 3.65-3.69 -> 3.51 ms, neutral at C2: profiles/r5zp_geo_fpl_ab.txt; bf16 C5 38.6 -> 38.1 ms,
+// profiles/r6h_cold_fpl.txt).  Keyed on the batch, not on the block order, so forcing an order (TAGAN_GEO_XCD) never
+// changes the lane reduction.  TAGAN_GEO_FPL_FWD_COLD=4|8 overrides the cold choice (read per call: A/B runs);
+// TAGAN_GEO_COLD=0|1 forces the classification (tests: the cold forward on small graphs).
+bool kv_cold(int64_t n, int H, bool bf16) {
+    const char* e = getenv("TAGAN_GEO_COLD");
+    if (e && (e[0] == '0' || e[0] == '1') && !e[1]) return e[0] == '1';
+    return 2 * n * (int64_t)H * (bf16 ? 2 : 4) > ((int64_t)512 << 20);
+}
+
+int pick_fpl(int H, int d, Pass pass, bool bf16, bool cold = false) {
+    int want = pass == P_FWD ? TAGAN_GEO_FPL_FWD : bf16 ? TAGAN_GEO_FPL_BWD_BF16 : TAGAN_GEO_FPL_BWD;
+    if (pass == P_FWD && cold) {
+        const char* e = getenv("TAGAN_GEO_FPL_FWD_COLD");
+        want = (e && (e[0] == '4' || e[0] == '8') && !e[1]) ? e[0] - '0' : 4;
+    }
     if (want == 8 && d % 8 == 0 && ((d / 8) & (d / 8 - 1)) == 0 && (H == 64 || H == 128 || H == 256)) return 8;
     return 4;
 }
@@ -1086,7 +1102,7 @@ int launch_metric(Pass pass, int lpr, const GeoArgs& A, hipStream_t s, float* al
         k_geo_alpha<METRIC><<<gg, BLK, 0, s>>>(A, alpha);
         return TAGAN_OK;
     }
-    const int fpl = lpr ? pick_fpl(A.H, A.d, pass, A.bf16 != 0) : 0;
+    const int fpl = lpr ? pick_fpl(A.H, A.d, pass, A.bf16 != 0, kv_cold(A.N, A.H, A.bf16 != 0)) : 0;
     lpr = lpr ? A.H / fpl : 0;
     if (fpl == 8) {
         switch (lpr) {
@@ -1166,8 +1182,7 @@ int check_common(int dtype, int metric, const tagan_graph* g, int heads, int d, 
 int geo_xcd_mode(int64_t n, int H, bool bf16) {
     const char* e = getenv("TAGAN_GEO_XCD");
     if (e && e[0] >= '0' && e[0] <= '2' && !e[1]) return e[0] - '0';
-    const int64_t kv_bytes = 2 * n * (int64_t)H * (bf16 ? 2 : 4);
-    return kv_bytes <= ((int64_t)512 << 20) ? 2 : 0;
+    return kv_cold(n, H, bf16) ? 0 : 2;
 }
 
 GeoArgs make_args(const tagan_graph* g, int heads, int d, const void* q, const void* k, const void* v, int64_t ld,

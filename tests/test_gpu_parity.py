@@ -279,10 +279,14 @@ def _hub_graph(n, seed):
     return torch.cat([ei, hub, hub.flip(0)], 1)
 
 
+@pytest.mark.parametrize("cold", [False, True])
 @pytest.mark.parametrize("metric", list(oracle.METRICS))
 @pytest.mark.parametrize("chunk", [4, 16, 128])
-def test_geo_kernel_chunked_vs_oracle(dev, metric, chunk):
-    """Multi-chunk rows/columns (merge passes) against the float64 oracle edge-softmax."""
+def test_geo_kernel_chunked_vs_oracle(dev, metric, chunk, cold, monkeypatch):
+    """Multi-chunk rows/columns (merge passes) against the float64 oracle edge-softmax.  ``cold``: the batch
+    classified cache-cold (TAGAN_GEO_COLD=1; C3-C5 are): launch block order and the fp32 forward with 4 features
+    per lane instead of 8."""
+    monkeypatch.setenv("TAGAN_GEO_COLD", "1" if cold else "0")
     from tagan_amd import _lib
     from tagan_amd.kernels import GeoAttnFn, build_graph
     counts = [300, 257]
