@@ -38,6 +38,8 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -614,6 +616,258 @@ __global__ void __launch_bounds__(NW * 64, MINB) k_sgemm_nt(NtArgs g) {
                     g.part[(int64_t)blockIdx.x * 2 * NW * NSUB * 16 * gridDim.y + NW * NSUB * 16 * gridDim.y + col] = b;
                 }
             }
+    }
+}
+
+// ------------------------------------------------------------------------------------------- ping-pong NT
+#ifndef TAGAN_SG_PF
+#define TAGAN_SG_PF 0
+#endif
+// k_sgemm_nt's plain / split-K / LN-prologue forms with the two waves of each SIMD half a period apart (round 6).  In
+// k_sgemm_nt all eight waves run the MFMAs of a tile together and then all stage the next one together, so each
+// SIMD's matrix pipe idles through every staging phase (PMC: 3-4 % of MFMA-busy cycles co-executing VALU, round 5).
+// Here waves 0-3 (group 0) and 4-7 (group 1; wave w runs on SIMD w % 4, so each SIMD holds one of each) alternate:
+//   phase X: group 0 runs tile t's MFMAs; group 1 stages its half (rows 16 J/2 ..) of tile t + 1 into the other
+//            buffer from the registers its loads filled a period ago, issues the loads of its half of tile t + 2 and
+//            stores its outputs of tile t - 1;
+//   phase Y: the same with the groups swapped (group 0 stores tile t's outputs).
+// One barrier between the phases and one per period; a buffer is read in X and Y of its period and rewritten only in
+// the next period, so two buffers suffice.  Each wave still owns 16 NSUB output columns (weights in registers) and
+// stages half a tile per period, i.e. as many chunks per thread as in k_sgemm_nt: no extra registers.
+template <int K, int NSUB, int BM, int P, bool ABF, bool CBF, int MODE>
+__global__ void __launch_bounds__(512, 1) k_sgemm_nt_pp(NtArgs g) {
+    constexpr int NW = 8, KK = K / 32, J = BM / 16, JH = J / 2, QK = K / 8, GT = 256;
+    constexpr int CPT = (BM / 2) * QK / GT;
+    static_assert(J % 2 == 0 && (BM / 2) * QK % GT == 0, "each group stages whole 16-row blocks");
+    static_assert(MODE == MODE_PLAIN || MODE == MODE_ACC || MODE == MODE_LN_IN, "no row-wide epilogues here");
+    static_assert(!ABF || P == 1, "bf16 operands have one plane");
+    static_assert(MODE != MODE_LN_IN || ((QK == 16 || QK == 32) && !ABF), "LN prologue: K = 128 or 256 fp32 rows");
+    constexpr int LQ = MODE == MODE_LN_IN ? QK : 16;
+    constexpr int BUF = P * KK * J * 64;
+    extern __shared__ uint4 sg_lds[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, grp = w >> 2, gtid = threadIdx.x & (GT - 1);
+    const int nsub0 = (blockIdx.y * NW + w) * NSUB;
+    float* lgb = reinterpret_cast<float*>(sg_lds + 2 * BUF);
+    if constexpr (MODE == MODE_LN_IN)
+        for (int i = threadIdx.x; i < 2 * K; i += NW * 64) lgb[i] = i < K ? g.ln_g[i] : g.ln_b[i - K];
+    bf16x8 wr[NSUB][KK][P];
+#pragma unroll
+    for (int s = 0; s < NSUB; ++s)
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+                wr[s][kk][p] = __builtin_bit_cast(
+                    bf16x8, g.wp[((int64_t)((nsub0 + s) * (g.kkt ? g.kkt : KK) + g.kk0 + kk) * P + p) * 64 + lane]);
+    if constexpr (MODE == MODE_LN_IN) __syncthreads();
+    f32x4 bias[NSUB];
+#pragma unroll
+    for (int s = 0; s < NSUB; ++s) {
+        bias[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (g.bias) bias[s] = *reinterpret_cast<const f32x4*>(g.bias + (nsub0 + s) * 16 + 4 * (lane >> 4));
+    }
+    const int64_t ntiles = (g.M + BM - 1) / BM;
+    int64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;   // uniform over the workgroup
+
+    // this thread's staging chunks: rows of its group's half of the tile (k_sgemm_nt's maps within the half)
+    auto chunk = [&](int i, int& rl, int& q, int& rh) {
+        const int c = i * GT + gtid;
+        rl = MODE == MODE_LN_IN ? (c / LQ) & 15 : c & 15;
+        q = MODE == MODE_LN_IN ? c % LQ : (c >> 4) % QK;
+        rh = grp * JH + (MODE == MODE_LN_IN ? c / (16 * LQ) : (c >> 4) / QK);
+    };
+    float pf[ABF ? 1 : CPT][8];
+    uint4 pb[ABF ? CPT : 1];
+    auto load = [&](int64_t t) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            int rl, q, rh;
+            chunk(i, rl, q, rh);
+            const int64_t row0 = t * BM + rh * 16 + rl;
+            const int64_t row = row0 < g.M ? row0 : g.M - 1;   // rows past M reload row M - 1 (never stored)
+            if constexpr (ABF) {
+                pb[i] = *reinterpret_cast<const uint4*>((const uint16_t*)g.a + row * g.lda + 8 * q);
+            } else {
+                const float* src = (const float*)g.a + row * g.lda + 8 * q;
+                const float4 v0 = *reinterpret_cast<const float4*>(src);
+                const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+                pf[i][0] = v0.x; pf[i][1] = v0.y; pf[i][2] = v0.z; pf[i][3] = v0.w;
+                pf[i][4] = v1.x; pf[i][5] = v1.y; pf[i][6] = v1.z; pf[i][7] = v1.w;
+            }
+        }
+    };
+    auto stash = [&](uint4* buf, int64_t t) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            int rl, q, rh;
+            chunk(i, rl, q, rh);
+            const int e0 = ((q >> 2) * J + rh) * 64 + 16 * (q & 3) + (rl ^ ((q & 3) + 4 * ((q >> 2) & 3)));
+            if constexpr (MODE == MODE_LN_IN) {
+                const float sm = (pf[i][0] + pf[i][1]) + (pf[i][2] + pf[i][3]) + ((pf[i][4] + pf[i][5]) + (pf[i][6] + pf[i][7]));
+                const float mean = xsum<LQ>(sm) / (float)K;
+                float sq = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sq += (pf[i][e] - mean) * (pf[i][e] - mean);
+                const float rstd = 1.f / sqrtf(xsum<LQ>(sq) / (float)K + g.eps);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) pf[i][e] = ln_apply(pf[i][e], mean, rstd, lgb[8 * q + e], lgb[K + 8 * q + e]);
+                const int64_t row = t * BM + rh * 16 + rl;
+                if (q == 0 && row < g.M) {
+                    g.mean[row] = mean;
+                    g.rstd[row] = rstd;
+                }
+            }
+            if constexpr (ABF) {
+                buf[e0] = pb[i];
+            } else {
+                uint32_t pl[4][P];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) split2<P>(pf[i][2 * e], pf[i][2 * e + 1], pl[e]);
+#pragma unroll
+                for (int p = 0; p < P; ++p)
+                    buf[p * KK * J * 64 + e0] = make_uint4(pl[0][p], pl[1][p], pl[2][p], pl[3][p]);
+            }
+        }
+    };
+    int rslot[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rslot[u] = 16 * (lane >> 4) + ((lane & 15) ^ ((lane >> 4) + 4 * u));
+    f32x4 acc[J][NSUB];
+    auto compute = [&](const uint4* buf) {
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int s = 0; s < NSUB; ++s) acc[j][s] = bias[s];
+        if constexpr (P == 1) {
+            bf16x8 af[2][J];
+#pragma unroll
+            for (int j = 0; j < J; ++j) af[0][j] = __builtin_bit_cast(bf16x8, buf[j * 64 + rslot[0]]);
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) {
+                if (kk + 1 < KK) {
+#pragma unroll
+                    for (int j = 0; j < J; ++j)
+                        af[(kk + 1) & 1][j] = __builtin_bit_cast(bf16x8, buf[((kk + 1) * J + j) * 64 + rslot[(kk + 1) & 3]]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < J; ++j)
+#pragma unroll
+                    for (int s = 0; s < NSUB; ++s) acc[j][s] = mfma(wr[s][kk][0], af[kk & 1][j], acc[j][s]);
+            }
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) {
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    bf16x8 a[P];
+#pragma unroll
+                    for (int p = 0; p < P; ++p)
+                        a[p] = __builtin_bit_cast(bf16x8, buf[((p * KK + kk) * J + j) * 64 + rslot[kk & 3]]);
+#pragma unroll
+                    for (int s = 0; s < NSUB; ++s) acc[j][s] = mfma_planes<P>(wr[s][kk], a, acc[j][s]);
+                }
+            }
+        }
+    };
+    // outputs through a buffer resource over the tile's valid rows: rows past M are dropped by the range check, so
+    // the stores are unconditional instructions and the staging phase's wait for its loads counts them exactly (a
+    // row < M branch made the compiler wait for every store too: s_waitcnt vmcnt(0)).  store(-1) issues the same
+    // instructions over an empty range: the prologue and group 1's first period end with it, so every path into a
+    // staging phase has the same number of stores behind its loads (else the merged count is vmcnt(0) again).
+    auto store = [&](int64_t t) {
+        constexpr int ES = CBF ? 2 : 4;
+        const int64_t r0 = t < 0 ? 0 : t * BM;
+        const int64_t nv = t < 0 ? 0 : g.M - r0 < BM ? g.M - r0 : BM;   // t < 0: a phantom batch (all dropped)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (char*)g.c + r0 * g.ldc * ES, (short)0, (int)(nv * g.ldc * ES), 0x00020000);
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int s = 0; s < NSUB; ++s) {
+                const int off = (int)(((j * 16 + (lane & 15)) * g.ldc + (nsub0 + s) * 16 + 4 * (lane >> 4)) * ES);
+                f32x4 v = acc[j][s];
+                if constexpr (MODE == MODE_ACC)
+                    v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+                if constexpr (CBF) {
+                    const uint2 pk = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), rs, off, 0, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, off, 0, 0);
+                }
+            }
+    };
+    // TAGAN_SG_PF: also pull tile nx2 + 1 (this group's half) into L2 one period early: one dword per 128-B line
+    // into a sink register consumed a period later, so the loads of the next period hit L2
+    float sink = 0.f;
+    auto stage = [&](uint4* buf, int64_t nx, int64_t nx2, int64_t nx3) {
+        __builtin_amdgcn_sched_barrier(0);
+        stash(buf, nx);
+        load(nx2);
+        if constexpr (TAGAN_SG_PF) {
+            asm volatile("" ::"v"(sink));
+            constexpr int LPR = K * (ABF ? 2 : 4) / 128;          // 128-B lines per row
+            constexpr int LINES = (BM / 2) * LPR;                 // lines of the group's half tile
+            if (gtid < LINES) {
+                const int64_t row0 = nx3 * BM + grp * (BM / 2) + gtid / LPR;
+                const int64_t row = row0 < g.M ? row0 : g.M - 1;
+                sink = *(reinterpret_cast<const volatile float*>(
+                    (const char*)g.a + (row * g.lda) * (ABF ? 2 : 4) + (gtid % LPR) * 128));
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    load(tile);
+    stash(sg_lds, tile);
+    {
+        const int64_t n1 = tile + gridDim.x;
+        load(n1 < ntiles ? n1 : tile);
+        store(-1);
+    }
+    __syncthreads();
+    // Each group runs its own copy of the period loop (straight-line phases, the same barriers in the same order): in
+    // one loop with the phases in grp branches the compiler merged the staging registers at every join and drained
+    // the fresh loads (s_waitcnt vmcnt(0)) at the end of each staging phase.
+    // phase boundaries: the MFMAs must not drift across a barrier (they touch no memory, so the asm's clobber does
+    // not hold them)
+    auto pp_barrier = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        lds_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    if (grp == 0) {
+        for (int it = 0;; ++it) {
+            const int64_t next = tile + gridDim.x, next2 = next + gridDim.x, next3 = next2 + gridDim.x;
+            const int64_t sx = next < ntiles ? next : tile;   // unconditional staging (see k_sgemm_nt)
+            const int64_t lx = next2 < ntiles ? next2 : sx;
+            const int64_t px = next3 < ntiles ? next3 : lx;
+            compute(sg_lds + (it & 1) * BUF);                 // phase X
+            pp_barrier();
+            stage(sg_lds + ((it + 1) & 1) * BUF, sx, lx, px);  // phase Y
+            store(tile);
+            if (next >= ntiles) break;
+            pp_barrier();
+            tile = next;
+        }
+    } else {
+        int64_t prev = -1;   // the tile whose outputs this group still holds
+        for (int it = 0;; ++it) {
+            const int64_t next = tile + gridDim.x, next2 = next + gridDim.x, next3 = next2 + gridDim.x;
+            const int64_t sx = next < ntiles ? next : tile;
+            const int64_t lx = next2 < ntiles ? next2 : sx;
+            const int64_t px = next3 < ntiles ? next3 : lx;
+            stage(sg_lds + ((it + 1) & 1) * BUF, sx, lx, px);  // phase X
+            store(prev);
+            pp_barrier();
+            compute(sg_lds + (it & 1) * BUF);                 // phase Y
+            prev = tile;
+            if (next >= ntiles) break;
+            pp_barrier();
+            tile = next;
+        }
+        store(prev);
     }
 }
 
@@ -1446,12 +1700,24 @@ struct NtCfg {
 
 // MINB: waves per SIMD the register allocation must allow (4 = two 8-wave workgroups per CU: the LN epilogues
 // serialise each workgroup's memory and matrix phases, a second workgroup per CU overlaps them)
+// TAGAN_SG_PP: the three-plane 8-wave forms without a row-wide epilogue run on the ping-pong kernel (k_sgemm_nt_pp)
+#ifndef TAGAN_SG_PP
+#define TAGAN_SG_PP 0
+#endif
+template <int K, int NSUB, int NW, int BM, int P, bool ABF, bool CBF, int MODE, int MINB>
+constexpr nt_fn nt_kernel() {
+    if constexpr (TAGAN_SG_PP && P == 3 && NW == 8 && MINB == 1 && (BM / 16) % 2 == 0 &&
+                  (MODE == MODE_PLAIN || MODE == MODE_ACC || MODE == MODE_LN_IN))
+        return k_sgemm_nt_pp<K, NSUB, BM, P, ABF, CBF, MODE>;
+    else
+        return k_sgemm_nt<K, NSUB, NW, BM, P, ABF, CBF, MODE, MINB>;
+}
 template <int K, int NSUB, int NW, int BM, int P, bool ABF, bool CBF, int MODE = MODE_PLAIN, int MINB = 1>
 constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
-    return NtCfg{K, N, P, ABF, CBF, MODE, k_sgemm_nt<K, NSUB, NW, BM, P, ABF, CBF, MODE, MINB>, NW, NSUB, BM,
+    return NtCfg{K, N, P, ABF, CBF, MODE, nt_kernel<K, NSUB, NW, BM, P, ABF, CBF, MODE, MINB>(), NW, NSUB, BM,
                  (size_t)2 * P * (K / 32) * (BM / 16) * 64 * 16 +
                      ((MODE == MODE_LN_OUT || MODE == MODE_LN_BWD) ? (size_t)(BM * NW * 4 + 4 * N) * 4 : 0) +
-                     (MODE == MODE_LN_IN ? (size_t)2 * K * 4 : 0),
+                     (MODE == MODE_LN_IN ? (size_t)2 * K * 4 : 0) + (size_t)NW * NSUB * 16 * 4,
                  wg_per_cu};
 }
 

@@ -21,9 +21,14 @@ HBM_PEAK_GBS = 8000.0
 def parse(name):
     m = re.search(r"k_sgemm_nt<(\d+), (\d+), (\d+), (\d+), (\d+), (true|false), (true|false), (\d+)(?:, (\d+))?>", name)
     if m:
-        K, _nsub, _nw, _bm, P = (int(m.group(i)) for i in range(1, 6))
+        K, nsub, nw, _bm, P = (int(m.group(i)) for i in range(1, 6))
         return {"kind": "nt", "K": K, "P": P, "abf": m.group(6) == "true", "cbf": m.group(7) == "true",
-                "mode": int(m.group(8))}
+                "mode": int(m.group(8)), "nsub": nsub, "nw": nw}
+    # ping-pong form (round 6): k_sgemm_nt_pp<K, NSUB, BM, P, ABF, CBF, MODE>, 8 waves
+    m = re.search(r"k_sgemm_nt_pp<(\d+), (\d+), (\d+), (\d+), (true|false), (true|false), (\d+)>", name)
+    if m:
+        return {"kind": "nt", "K": int(m.group(1)), "P": int(m.group(4)), "abf": m.group(5) == "true",
+                "cbf": m.group(6) == "true", "mode": int(m.group(7)), "nsub": int(m.group(2)), "nw": 8}
     m = re.search(r"k_sgemm_tn<(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (true|false), (\d+), (true|false)>", name)
     if m:
         return {"kind": "tn", "N": int(m.group(1)), "K": int(m.group(2)), "P": int(m.group(6)),
@@ -43,8 +48,7 @@ def main():
         calls = int(r["Calls"])
         avg_us = float(r["TotalDurationNs"]) / calls / 1e3
         if d["kind"] == "nt":
-            nsub = int(re.search(r"k_sgemm_nt<\d+, (\d+), (\d+)", r["Name"]).group(1))
-            nw = int(re.search(r"k_sgemm_nt<\d+, (\d+), (\d+)", r["Name"]).group(2))
+            nsub, nw = d["nsub"], d["nw"]
             N = 16 * nsub * nw
             K = d["K"]
             ea = 2 if d["abf"] else 4
