@@ -66,11 +66,13 @@ def parse():
     ap.add_argument("--no-c1", action="store_true", help="skip the GPU C1 line beside the C1 CPU baselines")
     ap.add_argument("--launch", default="auto", choices=("auto", "graph", "eager"),
                     help="graph: replay the step as a HIP graph (graph_step.py); eager: launch every kernel from "
-                         "Python; auto (default): time a short trial of both and keep the faster; --shard always launches eagerly")
+                         "Python; auto (default): time a short trial of both and keep the faster")
     ap.add_argument("--no-graph", action="store_true", help="same as --launch eager")
     ap.add_argument("--sub-records", default="auto",
                     help="BASELINE multi-GPU workloads measured beside the headline: auto (c3_dp at N = 2, 4; "
                          "c5_shard at N = 8), none, or a comma list of c3_dp, c5_shard")
+    ap.add_argument("--c5-shard-size", default=None,
+                    help="NODES,EDGES per snapshot for the c5_shard sub-record (a reduced rehearsal; default C5's)")
     ap.add_argument("--shard", action="store_true",
                     help="one sequence sharded by snapshot over all ranks (strong scaling; C5 mode) instead of "
                          "one sequence per rank (data parallel, weak scaling)")
@@ -577,9 +579,13 @@ def c3_dp_record(dev, rank, world, ctl, backend, steps=5, warmup=3):
 def c5_shard_record(dev, rank, world, ctl, backend, steps=5, warmup=3, nodes=None, edges=None):
     """BASELINE configs[4] over N ranks: ONE sequence of 128 snapshots (100k nodes / 2M edges each, hidden 256,
     16 heads, fp32) sharded by snapshot (sharded.py): the geometric stage on each rank's 128/N snapshots, one
-    all-to-all to node rows, the temporal stage on the rank's rows, one pooling all-reduce, one flagged gradient
-    all-reduce; eager launches.  ``nodes`` / ``edges`` shrink the snapshots (same T, H, heads) for a rehearsal of
-    several ranks on one GPU (tests/test_gpu_sharded.py)."""
+    all-to-all to node rows, the temporal stage on the rank's rows, one pooling all-reduce, one gradient
+    all-reduce.  ``nodes`` / ``edges`` shrink the snapshots (same T, H, heads) for a rehearsal of several ranks on
+    one GPU (tests/test_gpu_sharded.py, ``--c5-shard-size``).  Launch: the whole sharded step captured as one HIP
+    graph (the all-to-all, the pooling all-reduce and the static gradient sync inside it,
+    tests/test_gpu_rccl.py::test_rccl_world1_graph_step_sharded) when the data plane can be captured (RCCL, or one
+    rank) and the eager step's peak memory leaves room for the graph's own pool (under 45 % of the device: the full
+    C5 share at N = 8 is ~240 GB and runs eagerly); a short trial of both then keeps the faster."""
     from tagan_amd import TAGAN, synthetic
     from tagan_amd.distributed import broadcast_parameters
     from tagan_amd.sharded import ShardGradSync, SnapshotShardedTAGAN, blocks
@@ -589,7 +595,9 @@ def c5_shard_record(dev, rank, world, ctl, backend, steps=5, warmup=3, nodes=Non
     torch.manual_seed(0)
     model = TAGAN(cfg).to(dev).train()
     broadcast_parameters(model)
-    opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay, fused=True)
+    can_graph = world == 1 or backend == "nccl"   # the data plane can be captured (see the docstring)
+    opt = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay,
+                           capturable=can_graph, fused=True)
     t0, t1 = blocks(T, world)[rank]
     full = synthetic.make_sequence("c5", dev, seed=5000, nodes=N, edges=E)   # the same sequence on every rank
     seq = synthetic.take(full, t0, t1)
@@ -603,12 +611,48 @@ def c5_shard_record(dev, rank, world, ctl, backend, steps=5, warmup=3, nodes=Non
         out["loss"].backward()
         sync.sync()
     step = make_step(model, opt, cfg, lambda: sharded(seq, counts_all, labels), bwd)
+    launch, trial_ms, gstep = "eager", None, None
+    if can_graph:
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize(dev)
+        peak = torch.cuda.max_memory_allocated(dev)
+        fits = torch.tensor([1.0 if peak < 0.45 * torch.cuda.get_device_properties(dev).total_memory else 0.0])
+        if world > 1:
+            dist.all_reduce(fits, dist.ReduceOp.MIN, group=ctl)
+        if float(fits) > 0:
+            def t(fn, n=3):
+                fn()
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                for _ in range(n):
+                    fn()
+                torch.cuda.synchronize(dev)
+                x = torch.tensor([(time.perf_counter() - t0) / n], dtype=torch.float64)
+                if world > 1:
+                    dist.all_reduce(x, dist.ReduceOp.MAX, group=ctl)
+                return float(x)
+            te = t(step)
+            torch.cuda.empty_cache()
+            gstep = graphed(model, opt, cfg, lambda: sharded(seq, counts_all, labels),
+                            (lambda: sync.sync(static=True)) if world > 1 else None)
+            tg = t(gstep)
+            trial_ms = {"graph_ms": round(tg * 1e3, 3), "eager_ms": round(te * 1e3, 3)}
+            if tg < te:
+                launch, step = "hip-graph", gstep
+            else:
+                gstep.close()
+                gstep = None
     rec = sub_record("c5 (BASELINE configs[4]): one sequence of %d snapshots (%d nodes, %d edges each), hidden %d, "
                      "%d heads, fp32, sharded by snapshot over %d ranks" % (T, N, E, H, heads, world),
                      step, world, ctl, steps, warmup, T,
-                     {"parallelism": "snapshot-shard%d" % world, "scaling": "strong", "launch": "eager",
+                     {"parallelism": "snapshot-shard%d" % world, "scaling": "strong", "launch": launch,
                       "dtype": "fp32", "n_ranks_rccl": world if backend == "nccl" else 0})
+    if trial_ms:
+        rec["launch_trial"] = trial_ms
     rec["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
+    if gstep is not None:
+        gstep.close()
     return rec
 
 
@@ -669,8 +713,9 @@ def main():
     # every form of the step is captured whole (the RCCL all-reduce inside the graph); only a gloo data plane
     # (the one-GPU rehearsal knob) cannot be captured and launches eagerly
     capturable = world == 1 or backend == "nccl"
-    # --shard launches eagerly: no test captures the sharded step (all-to-all + segment reduce + static grad sync)
-    launch = "eager" if (args.no_graph or not capturable or args.shard) else args.launch
+    # --shard captures too: the all-to-all, the pooling all-reduce and the static gradient sync are graph-safe
+    # (tests/test_gpu_rccl.py::test_rccl_world1_graph_step_sharded)
+    launch = "eager" if (args.no_graph or not capturable) else args.launch
     use_graph = launch != "eager"   # capturable optimizer whenever a graph may be captured
     torch.manual_seed(0)
     model = TAGAN(cfg, precision=args.precision).to(dev).train()
@@ -845,7 +890,10 @@ def main():
         torch.cuda.empty_cache()
         for name in subs:
             fn = {"c3_dp": c3_dp_record, "c5_shard": c5_shard_record}[name]
-            rec[name] = fn(dev, rank, world, ctl, backend)
+            kw = {}
+            if name == "c5_shard" and args.c5_shard_size:
+                kw = dict(zip(("nodes", "edges"), (int(x) for x in args.c5_shard_size.split(","))))
+            rec[name] = fn(dev, rank, world, ctl, backend, **kw)
             torch.cuda.empty_cache()
     if rank == 0 and not args.no_roofline:
         roof = roofline_c4(args.roofline_reps)

@@ -1700,14 +1700,17 @@ struct NtCfg {
 
 // MINB: waves per SIMD the register allocation must allow (4 = two 8-wave workgroups per CU: the LN epilogues
 // serialise each workgroup's memory and matrix phases, a second workgroup per CU overlaps them)
-// TAGAN_SG_PP: the three-plane 8-wave forms without a row-wide epilogue run on the ping-pong kernel (k_sgemm_nt_pp)
+// TAGAN_SG_PP: the three-plane 8-wave plain / split-K forms run on the ping-pong kernel (k_sgemm_nt_pp).  C2 QKV
+// input gradient 173.8 -> 163.1 us (profiles/r6k_pp_ab.txt).  The LN-prologue QKV forward stays on k_sgemm_nt: on
+// the ping-pong kernel it measured 175.8 -> 196.8 us; an L2 prefetch of the tile after next (TAGAN_SG_PF) slowed
+// both (dX 185.8, QKV 234.8 us).
 #ifndef TAGAN_SG_PP
-#define TAGAN_SG_PP 0
+#define TAGAN_SG_PP 1
 #endif
 template <int K, int NSUB, int NW, int BM, int P, bool ABF, bool CBF, int MODE, int MINB>
 constexpr nt_fn nt_kernel() {
     if constexpr (TAGAN_SG_PP && P == 3 && NW == 8 && MINB == 1 && (BM / 16) % 2 == 0 &&
-                  (MODE == MODE_PLAIN || MODE == MODE_ACC || MODE == MODE_LN_IN))
+                  (MODE == MODE_PLAIN || MODE == MODE_ACC))
         return k_sgemm_nt_pp<K, NSUB, BM, P, ABF, CBF, MODE>;
     else
         return k_sgemm_nt<K, NSUB, NW, BM, P, ABF, CBF, MODE, MINB>;

@@ -81,12 +81,12 @@ class _SnapshotsToRows(torch.autograd.Function):
     """[T_r, N, H] (this rank's snapshots, all rows) -> [T, n_r, H] (all snapshots, this rank's rows)."""
 
     @staticmethod
-    def forward(ctx, x_local, t_sizes, n_blocks, group):
+    def forward(ctx, x_local, t_sizes, n_blocks, group, force=False):
         P, r = _world(group)
         H = x_local.shape[2]
-        ctx.t_sizes, ctx.n_blocks, ctx.group = list(t_sizes), list(n_blocks), group
+        ctx.t_sizes, ctx.n_blocks, ctx.group, ctx.force = list(t_sizes), list(n_blocks), group, force
         n0, n1 = n_blocks[r]
-        if P == 1:
+        if P == 1 and not force:
             return x_local.clone()
         sends = [x_local[:, a:b] for a, b in n_blocks]
         recvs = _all_to_all(sends, [(t_sizes[p], n1 - n0, H) for p in range(P)], group)
@@ -95,54 +95,50 @@ class _SnapshotsToRows(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         P, r = _world(ctx.group)
-        if P == 1:
-            return g.clone(), None, None, None
+        if P == 1 and not ctx.force:
+            return g.clone(), None, None, None, None
         H = g.shape[2]
         t_r = ctx.t_sizes[r]
         sends = list(g.split(ctx.t_sizes, 0))
         recvs = _all_to_all(sends, [(t_r, b - a, H) for a, b in ctx.n_blocks], ctx.group)
-        return torch.cat(recvs, 1), None, None, None
+        return torch.cat(recvs, 1), None, None, None, None
 
 
 class _SumAcrossRanks(torch.autograd.Function):
     """all-reduce(SUM) whose consumer is replicated on every rank: the backward is the identity."""
 
     @staticmethod
-    def forward(ctx, x, group):
+    def forward(ctx, x, group, force=False):
         y = x.clone()
         P, _ = _world(group)
-        if P > 1:
+        if P > 1 or (force and dist.is_available() and dist.is_initialized()):
             _all_reduce_sum(y, group)
         return y
 
     @staticmethod
     def backward(ctx, g):
-        return g, None
+        return g, None, None
 
 
 def pool_partial(out_rows: torch.Tensor, n0: int, n_max: int) -> torch.Tensor:
     """[T, n_r, H] temporal output of rows [n0, n0+n_r) -> [T, H] partial sums of the reference's
-    pooling chunks (chunk t = node-major flat rows [t*N, (t+1)*N), flat row = n*T + t')."""
+    pooling chunks (chunk t = node-major flat rows [t*N, (t+1)*N), flat row = n*T + t').
+
+    The rank's flat rows meet a contiguous run of chunks, each in one contiguous stretch of them: one fixed-order
+    column sum per stretch (static Python bounds: no device-side length table, nothing a captured HIP graph cannot
+    replay -- torch.segment_reduce refused stream capture)."""
     T, n_r, H = out_rows.shape
     flat = out_rows.transpose(0, 1).reshape(n_r * T, H)
     f0, f1 = n0 * T, (n0 + n_r) * T
-    lengths = [max(0, min((t + 1) * n_max, f1) - max(t * n_max, f0)) for t in range(T)]
-    return torch.segment_reduce(flat, "sum", lengths=_lengths_table(lengths, flat.device), axis=0)
-
-
-_LENGTHS = {}
-
-
-def _lengths_table(lengths, dev):
-    """Device copy of the pooling segment lengths, made once per (lengths, device): no host-to-device copy inside
-    the step (a captured HIP graph would otherwise re-read a freed host buffer at every replay)."""
-    key = (tuple(lengths), str(dev))
-    t = _LENGTHS.get(key)
-    if t is None:
-        if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("pool_partial: segment-length table first needed inside a capture (warm up eagerly)")
-        t = _LENGTHS[key] = torch.tensor(lengths, device=dev)
-    return t
+    sums, first = [], None
+    for t in range(T):
+        a, b = max(t * n_max, f0), min((t + 1) * n_max, f1)
+        if b > a:
+            first = t if first is None else first
+            sums.append(flat[a - f0:b - f0].sum(0))
+    if not sums:
+        return flat.new_zeros(T, H)
+    return torch.cat([flat.new_zeros(first, H), torch.stack(sums), flat.new_zeros(T - first - len(sums), H)])
 
 
 class SnapshotShardedTAGAN:
@@ -154,14 +150,18 @@ class SnapshotShardedTAGAN:
     ``tagan_amd.TAGAN``; tests wire the CPU oracle to check the exchange logic.
     """
 
-    def __init__(self, encode: Callable, temporal: Callable, head: Callable, group=None, head_seed: int = 0x7A6A):
+    def __init__(self, encode: Callable, temporal: Callable, head: Callable, group=None, head_seed: int = 0x7A6A,
+                 force_collectives: bool = False):
         self.encode, self.temporal, self.head = encode, temporal, head
         self.group = group
         self.head_seed = head_seed
         self.step = 0
+        # run the all-to-all and the pooling all-reduce even at world size 1 (a live process group is required):
+        # the one-GPU RCCL tests exercise (and capture) the exchange path this way
+        self.force_collectives = force_collectives
 
     @classmethod
-    def for_model(cls, model, group=None):
+    def for_model(cls, model, group=None, force_collectives: bool = False):
         def encode(snaps):
             x_cat, counts, _ = model.encode_snapshots(snaps)
             return x_cat, counts
@@ -174,7 +174,7 @@ class SnapshotShardedTAGAN:
         def head(pooled, labels, step_seed):   # the fused head kernel's dropout mask: same on every rank
             return model.head(pooled, labels, dropout_seed=step_seed)
 
-        obj = cls(encode, temporal, head, group)
+        obj = cls(encode, temporal, head, group, force_collectives=force_collectives)
         obj.head_takes_seed = True
         return obj
 
@@ -194,9 +194,10 @@ class SnapshotShardedTAGAN:
             x_local = TAGAN._time_major(x_cat, list(counts), n_max)
         else:
             x_local = self._empty(n_max)
-        xt_rows = _SnapshotsToRows.apply(x_local, [b - a for a, b in t_blocks], n_blocks, self.group)
+        force = self.force_collectives and dist.is_available() and dist.is_initialized()
+        xt_rows = _SnapshotsToRows.apply(x_local, [b - a for a, b in t_blocks], n_blocks, self.group, force)
         out_rows = self.temporal(xt_rows) if n1 > n0 else xt_rows
-        pooled = _SumAcrossRanks.apply(pool_partial(out_rows, n0, n_max), self.group) / n_max
+        pooled = _SumAcrossRanks.apply(pool_partial(out_rows, n0, n_max), self.group, force) / n_max
         self.step += 1
         if getattr(self, "head_takes_seed", False):
             # the fused head kernel takes its dropout seed directly (the same on every rank; under a captured

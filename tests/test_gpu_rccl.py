@@ -134,6 +134,77 @@ def _graph_vs_eager(dev, seq, steps_eager=6, replays=3, seed=3):
         torch.testing.assert_close(p2, p1, atol=1e-5, rtol=1e-4, msg=k)
 
 
+def _case_graph_step_sharded():
+    """The snapshot-sharded step (sharded.py) captured as ONE HIP graph at world size 1 over RCCL, its exchanges
+    forced: the all-to-all (snapshots -> node rows and back), the pooling all-reduce and the static ShardGradSync
+    all-reduce all inside the graph; replays against the same step launched eagerly (the flagged ShardGradSync):
+    the same loss trajectory and weights."""
+    import tagan_amd  # noqa: F401
+    from tagan_amd import TAGAN, synthetic
+    from tagan_amd.graph_step import GraphedStep
+    from tagan_amd.sharded import ShardGradSync, SnapshotShardedTAGAN
+    dev = torch.device("cuda:0")
+    _init_nccl(dev, "gsh")
+    try:
+        cfg = synthetic.config_for("c5", dropout=0.0)
+        seq = synthetic.make_sequence("c5", dev, seed=11, snapshots=8, nodes=300, edges=2400)
+        counts = [int(x.shape[0]) for x, _, _, _ in seq]
+        labels = torch.tensor([1.0], device=dev)
+        steps_eager, replays = 6, 3
+
+        def setup():
+            torch.manual_seed(5)
+            m = TAGAN(cfg).to(dev).train()
+            o = torch.optim.Adam(m.parameters(), lr=1e-3, capturable=True)
+            return (m, o, SnapshotShardedTAGAN.for_model(m, force_collectives=True),
+                    ShardGradSync(list(m.named_parameters())))
+
+        m1, o1, sh1, sy1 = setup()
+        eager = []
+        print("sharded case: eager steps", flush=True)
+        for _ in range(steps_eager):
+            o1.zero_grad(set_to_none=True)
+            out = sh1(seq, counts, labels)
+            out["loss"].backward()
+            sy1.sync(force=True)
+            torch.nn.utils.clip_grad_norm_(m1.parameters(), 1.0)
+            o1.step()
+            eager.append(float(out["loss"]))
+        m2, o2, sh2, sy2 = setup()
+
+        def whole():
+            out = sh2(seq, counts, labels)
+            out["loss"].backward()
+            sy2.sync(force=True, static=True)
+            torch.nn.utils.clip_grad_norm_(m2.parameters(), 1.0)
+            o2.step()
+            return out["loss"]
+
+        print("sharded case: eager done %s; capture" % eager, flush=True)
+        g = GraphedStep(m2, whole, optimizer=o2, warmup=steps_eager - replays)
+        print("sharded case: captured; replays", flush=True)
+        try:
+            graphed = []
+            for _ in range(replays):
+                graphed.append(float(g()))
+                print("sharded case: replay", graphed[-1], flush=True)
+        finally:
+            g.close()
+        torch.cuda.synchronize()
+        for a, b in zip(eager[steps_eager - replays:], graphed):
+            assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (eager, graphed)
+        for (k, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+            torch.testing.assert_close(p2, p1, atol=1e-5, rtol=1e-4, msg=k)
+    except BaseException:
+        # a failed capture can leave the group unable to shut down: report and leave without destroying it
+        import traceback
+        traceback.print_exc()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(3)
+    dist.destroy_process_group()
+
+
 def _init_nccl(dev, tag):
     import tempfile
     torch.cuda.set_device(dev)
@@ -207,7 +278,7 @@ def _case_capture_race_unfixed():
 
 CASES = {"shard_and_buckets": _case_shard_and_buckets, "graph_step_small": _case_graph_step_small,
          "graph_step_c2": _case_graph_step_c2, "capture_after_eager_collective": _capture_after_eager_collective,
-         "capture_race_unfixed": _case_capture_race_unfixed}
+         "capture_race_unfixed": _case_capture_race_unfixed, "graph_step_sharded": _case_graph_step_sharded}
 OK = "RCCL_CASE_OK"
 
 
@@ -233,6 +304,11 @@ def test_rccl_world1_graph_step_c2():
     _run_case("graph_step_c2", timeout=280)
 
 
+def test_rccl_world1_graph_step_sharded():
+    """The snapshot-sharded step (all-to-all, pooling all-reduce, static gradient sync over RCCL) captured whole."""
+    _run_case("graph_step_sharded", timeout=100)
+
+
 def test_rccl_capture_after_eager_collective():
     """The capture-time watchdog race forced open: eager collectives on the capture stream right
     before a capture that holds the host across several watchdog polls.  Passes only because GraphedStep waits for the
@@ -241,6 +317,9 @@ def test_rccl_capture_after_eager_collective():
 
 
 if __name__ == "__main__":
+    if os.environ.get("TAGAN_CASE_STACK_AFTER"):   # diagnostics: dump every thread's stack, then exit, after N s
+        import faulthandler
+        faulthandler.dump_traceback_later(int(os.environ["TAGAN_CASE_STACK_AFTER"]), exit=True)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     CASES[sys.argv[1]]()
     torch.cuda.synchronize()
