@@ -328,7 +328,7 @@ int tagan_layernorm_bwd(int dtype, int64_t M, int32_t H, const float* s, const f
                         const float* rstd, const float* gamma, const float* dy, const float* dres,
                         float p_drop, uint64_t seed, float* ds, float* da, float* dgamma, float* dbeta,
                         float* dsum_a, void* workspace, size_t workspace_bytes, void* stream);
-/* The backward of the skip form y = LN(s) + LN_s(b) (model.py:258-262) in one pass (H = 128): ds = dL/ds of LN plus
+/* The backward of the skip form y = LN(s) + LN_s(b) (model.py:258-262) in one pass (H = 128 or 256): ds = dL/ds of LN plus
  * LN_s's input gradient (the residual gradient of the block input b), da = dL/ds of LN masked / scaled by the
  * dropout, dgamma/dbeta/dsum_a as tagan_layernorm_bwd, dgamma_s/dbeta_s of LN_s; equal, to fp32 rounding (the same
  * dropout decisions), to tagan_layernorm_bwd on (s, LN) followed by tagan_layernorm_bwd on (b, LN_s) with that ds

@@ -340,14 +340,21 @@ int ln_bwd_blocks() { return TAGAN_LN_BWD_BLOCKS; }
 static_assert(TAGAN_LN_ROWS == 1 || TAGAN_LN_ROWS == 2 || TAGAN_LN_ROWS == 4, "TAGAN_LN_ROWS: 1, 2 or 4 (instantiated)");
 int ln_rows(int nv) { return nv == 2 && TAGAN_LN_ROWS > 2 ? 2 : TAGAN_LN_ROWS; }
 
-// the fused LN2 + skip-LN backward (H = 128: LPR 32, NV 1; any U)
-// Both launchers run exactly the U the caller sized the grid for, or launch nothing and return false.
+// the fused LN2 + skip-LN backward (one float4 per lane and row: H = 128 (LPR 32) and, round 6, H = 256 (LPR 64);
+// any U).  Both launchers run exactly the U the caller sized the grid for, or launch nothing and return false.
 template <typename S>
-bool launch_ln_skip_bwd(int u, dim3 g, hipStream_t s, const LnArgs& A) {
-    if (u == 1) k_ln_bwd<32, 1, 1, S, true><<<g, BLK, 0, s>>>(A);
-    else if (u == 2) k_ln_bwd<32, 1, 2, S, true><<<g, BLK, 0, s>>>(A);
-    else if (u == 4) k_ln_bwd<32, 1, 4, S, true><<<g, BLK, 0, s>>>(A);
+bool launch_ln_skip_bwd(int lpr, int u, dim3 g, hipStream_t s, const LnArgs& A) {
+#define TAGAN_LN_SK(L)                                                       \
+    do {                                                                     \
+        if (u == 1) k_ln_bwd<L, 1, 1, S, true><<<g, BLK, 0, s>>>(A);         \
+        else if (u == 2) k_ln_bwd<L, 1, 2, S, true><<<g, BLK, 0, s>>>(A);    \
+        else if (u == 4) k_ln_bwd<L, 1, 4, S, true><<<g, BLK, 0, s>>>(A);    \
+        else return false;                                                   \
+    } while (0)
+    if (lpr == 32) TAGAN_LN_SK(32);
+    else if (lpr == 64) TAGAN_LN_SK(64);
     else return false;
+#undef TAGAN_LN_SK
     return true;
 }
 
@@ -489,7 +496,9 @@ int tagan_layernorm_skip_bwd(int dtype, int64_t M, int32_t H, const float* s_in,
                              void* workspace, size_t workspace_bytes, void* stream) {
     using namespace tagan;
     TAGAN_REQUIRE(dtype == TAGAN_F32 || dtype == TAGAN_BF16, TAGAN_ERR_UNSUPPORTED, "layernorm: dtype %d", dtype);
-    TAGAN_REQUIRE(H == 128, TAGAN_ERR_UNSUPPORTED, "layernorm_skip_bwd: H=%d (H = 128 only)", H);
+    int lpr, nv;
+    TAGAN_REQUIRE(geometry(H, lpr, nv) && nv == 1 && (lpr == 32 || lpr == 64), TAGAN_ERR_UNSUPPORTED,
+                  "layernorm_skip_bwd: H=%d (H = 128 or 256)", H);
     TAGAN_REQUIRE(M > 0 && s_in && mean && rstd && gamma && b && mean_s && rstd_s && gamma_s && dy && ds && da &&
                       dgamma && dbeta && dsum_a && dgamma_s && dbeta_s,
                   TAGAN_ERR_ARG, "layernorm_skip_bwd: bad args");
@@ -503,12 +512,12 @@ int tagan_layernorm_skip_bwd(int dtype, int64_t M, int32_t H, const float* s_in,
     A.part = (float*)workspace;
     A.want_dsa = 1;
     const int u = ln_rows(1);
-    const int64_t rpw = (WAVE / 32) * u;
+    const int64_t rpw = (WAVE / lpr) * u;
     const int64_t need = ((M + rpw - 1) / rpw + (BLK / WAVE) - 1) / (BLK / WAVE);
     const int nblk = (int)std::min<int64_t>(need, ln_bwd_blocks());
     hipStream_t s = as_stream(stream);
-    const bool ok = dtype == TAGAN_BF16 ? launch_ln_skip_bwd<bf16s>(u, dim3(nblk), s, A)
-                                        : launch_ln_skip_bwd<float>(u, dim3(nblk), s, A);
+    const bool ok = dtype == TAGAN_BF16 ? launch_ln_skip_bwd<bf16s>(lpr, u, dim3(nblk), s, A)
+                                        : launch_ln_skip_bwd<float>(lpr, u, dim3(nblk), s, A);
     TAGAN_REQUIRE(ok, TAGAN_ERR_UNSUPPORTED, "layernorm_skip_bwd: no kernel with %d row groups per wave", u);
     TAGAN_CHECK_LAUNCH("layernorm_skip_bwd");
     launch_colsum(A.part, nblk, 2 * H, dgamma, dbeta, H, s, 1.f, 5 * H);

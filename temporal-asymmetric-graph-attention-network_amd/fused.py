@@ -98,7 +98,7 @@ def ln_skip_bwd(s, mean, rstd, gamma, b, mean_s, rstd_s, gamma_s, dy2, p_drop, s
 def _ln2_bwd(s2, mean2, rstd2, ln2_w, dy2, skip, x2, lns_w, p_out, seed_out, da_dtype):
     """LN2's backward of a block (and, for the skip block, LN_s's): dres, do, dg2, db2, dbo, dgs, dbs."""
     M, H = dy2.shape
-    if skip is not None and H == 128:   # one pass for both LayerNorms (150 vs 2 x 118 us at C2)
+    if skip is not None and H in (128, 256):   # one pass for both LayerNorms (150 vs 2 x 118 us at C2)
         return ln_skip_bwd(s2, mean2, rstd2, ln2_w, x2, skip[0], skip[1], lns_w, dy2, p_out, seed_out,
                            da_dtype=da_dtype)
     dres, do, dg2, db2, dbo = ln_bwd(s2, mean2, rstd2, ln2_w, dy2, None, p_out, seed_out, True, True, True,

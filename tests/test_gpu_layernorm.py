@@ -89,15 +89,15 @@ def test_layernorm_dropout_mask_shared(dev, M):
     torch.testing.assert_close(da[~drop], ds[~drop] / (1 - p), atol=1e-6, rtol=1e-5)
 
 
+@pytest.mark.parametrize("H", [128, 256])
 @pytest.mark.parametrize("M", MS + (320000,))
 @pytest.mark.parametrize("da_bf16", [False, True])
-def test_skip_bwd_fused_equals_two_passes(dev, M, da_bf16):
+def test_skip_bwd_fused_equals_two_passes(dev, M, da_bf16, H):
     """tagan_layernorm_skip_bwd (the skip block's LN2 + LN_s backward in one pass) against the two-pass chain it
     replaces (LN2's backward, then LN_s's with that ds as dres), with dropout: the same dropout decisions (da zero
     exactly where the chain's is) and the same values to fp32 rounding -- the compiler contracts the fused pass's
     multiply-adds differently (observed 1 ulp), so the bound is 4 ulp of the tensor's scale, not bit equality."""
     from tagan_amd.fused import ln_bwd, ln_skip_bwd, ln_skip_fwd
-    H = 128
     a, b, ab, g2, b2, _, dy = _inputs(dev, M, H, seed=11)
     gs, bs = 1.0 + 0.1 * torch.randn(H, device=dev), 0.1 * torch.randn(H, device=dev)
     y, s, mean, rstd, (ms, rss) = ln_skip_fwd(a, b, 0.1, 99, g2, b2, 1e-5, gs, bs, 1e-5, a_bias=ab)
