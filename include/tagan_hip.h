@@ -403,7 +403,8 @@ int tagan_sgemm_nt_ln_bwd(int32_t a_dtype, int64_t M, int32_t H, int32_t K, cons
                           const float* gamma, const float* dres, float* dx, float* dgamma, float* dbeta,
                           void* workspace, size_t workspace_bytes, void* stream);
 
-/* tagan_ln2_bwd_out: the start of an attention block's backward in one pass over the rows (H = 128):
+/* tagan_ln2_bwd_out: the start of an attention block's backward in one pass over the rows (H = 128; H = 256 with
+ * planes = 1, as two column groups over the same rows):
  *   LN2 backward of y = LN(s) [+ LN_s(xs)]:  ds = rstd (g dy - mean(g dy x̂) x̂ - mean(g dy)) [+ LN_s's input gradient]
  *     -> dres [M, H] fp32; do = dropout(ds) with the forward's mask (p_drop, seed; stream = row, counter = column);
  *     dgamma, dbeta [, dgamma_s, dbeta_s] = column sums;

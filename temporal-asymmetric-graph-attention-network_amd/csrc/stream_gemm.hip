@@ -1675,6 +1675,254 @@ __global__ void __launch_bounds__(512, 1) k_ln2_bwd_out(L2Args g) {
     }
 }
 
+// ------------------------------------------------------------------------------------------- LN2 backward + out-projection, H = 256
+#ifndef TAGAN_SG_LN2_256
+#define TAGAN_SG_LN2_256 1
+#endif
+// k_ln2_bwd_out at H = 256 with one plane (the bf16 activation mode, C5; round 6).  A whole 256-wide W_o^T panel and
+// dW_o's 256 x 256 accumulators do not fit one 8-wave workgroup's registers, so the work is split over TWO column
+// groups cg (grid = 2 G, adjacent on one XCD: block b -> cg = (b / 8) % 2, row range (b / 16) * 8 + b % 8): both run
+// the LN2 row math over whole rows (the row sums need all 256 columns; the second group's reads of dy / s / x hit
+// the L2 the first one just filled), and group cg then owns
+//   dW_o rows n in [128 cg, 128 cg + 128) (wave w: 16 rows x all 256 k: 16 accumulator tiles), db_o of those rows,
+//   dc columns in [128 cg, 128 cg + 128) (wave w: 16 columns, K = 256: 8 W_o^T fragments in registers),
+//   dres columns of its half; group 0 also accumulates the LN column sums (dgamma | dbeta [| dgamma_s | dbeta_s]).
+// Thread = (row, 8 columns), 32 lanes per row (two DPP rows: lane_sum<32>), 16 rows per pass, two passes per
+// 32-row tile (the MFMA K of dW_o); the operands of the next pass are loaded while this one's planes are built.
+template <bool ABF, bool SK>
+__global__ void __launch_bounds__(512, 1) k_ln2_bwd_out256(L2Args g) {
+    constexpr int H = 256, BM = 32, NW = 8, KK = H / 32, S = H + 16, PL = BM * S;
+    extern __shared__ uint4 sg_lds[];
+    uint16_t* ldo = reinterpret_cast<uint16_t*>(sg_lds);   // do plane [BM][S]
+    uint16_t* lcp = ldo + PL;                              // c plane
+    float* red = reinterpret_cast<float*>(lcp + PL);       // [NW][NPL * H] wave partials of the LN sums (end)
+    float* lgm = red + NW * (SK ? 4 : 2) * H;              // gamma | gamma_s (read per row: 16 VGPRs fewer)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int grp = lane >> 4, li = lane & 15;
+    const int rr = threadIdx.x >> 5, q = threadIdx.x & 31;   // row math: pass row, 8-column group
+    const int cg = (blockIdx.x >> 3) & 1;
+    const int64_t rb = ((int64_t)(blockIdx.x >> 4) << 3) | (blockIdx.x & 7);
+    TAGAN_LIVE_SEED(g);
+
+    for (int i = threadIdx.x; i < (SK ? 2 : 1) * H; i += NW * 64) lgm[i] = i < H ? g.gamma[i] : g.gamma_s[i - H];
+    __syncthreads();
+    bf16x8 wr[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) wr[kk] = __builtin_bit_cast(bf16x8, g.wp[((int64_t)((8 * cg + w) * KK + kk)) * 64 + lane]);
+    // column sums over the rows, fp32: group 0 the LN ones (dg: dgamma, db: dbeta [, dgs, dbs]), group 1 db_o
+    // (in dg: the exact sum of the fp32 do, not of its bf16 plane)
+    // (dbeta_s = Σ dy = dbeta: one array serves both)
+    float dg[8], db[8], dgs[SK ? 8 : 1];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        dg[e] = db[e] = 0.f;
+        if constexpr (SK) dgs[e] = 0.f;
+    }
+    f32x4 accw[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) accw[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int64_t t0 = rb * g.tiles_per_wg;
+    const int64_t t1 = min(t0 + g.tiles_per_wg, (g.M + BM - 1) / BM);
+
+    // one pass-row's operands (row r = 32 t + 16 pass + rr, columns 8 q..)
+    float4 vdy[2], vs[2], vx[SK ? 2 : 1], vc[ABF ? 1 : 2];
+    uint4 vcb;
+    float mrow = 0.f, rrow = 0.f, mrs = 0.f, rrs = 0.f;
+    auto load = [&](int64_t row0) {
+        const int64_t r = row0 < g.M ? row0 : g.M - 1;
+        const float* pdy = g.dy + r * H + 8 * q;
+        const float* ps = g.s + r * H + 8 * q;
+        vdy[0] = *reinterpret_cast<const float4*>(pdy);
+        vdy[1] = *reinterpret_cast<const float4*>(pdy + 4);
+        vs[0] = *reinterpret_cast<const float4*>(ps);
+        vs[1] = *reinterpret_cast<const float4*>(ps + 4);
+        if constexpr (ABF) {
+            vcb = *reinterpret_cast<const uint4*>((const uint16_t*)g.c + r * H + 8 * q);
+        } else {
+            const float* pc = (const float*)g.c + r * H + 8 * q;
+            vc[0] = *reinterpret_cast<const float4*>(pc);
+            vc[1] = *reinterpret_cast<const float4*>(pc + 4);
+        }
+        mrow = g.mean[r];
+        rrow = g.rstd[r];
+        if constexpr (SK) {
+            const float* px = g.xs + r * H + 8 * q;
+            vx[0] = *reinterpret_cast<const float4*>(px);
+            vx[1] = *reinterpret_cast<const float4*>(px + 4);
+            mrs = g.mean_s[r];
+            rrs = g.rstd_s[r];
+        }
+    };
+    auto frag = [&](const uint16_t* plane, int c0) {
+        const int qq = li >> 2, p4 = li & 3;
+        const uint16_t* a0 = plane + (4 * grp + qq) * S + c0 + 4 * p4;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 16 * S));
+        const short __attribute__((ext_vector_type(8))) v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, v);
+    };
+    // the LN2 backward of this thread's 8 columns of one row -> its do and c plane words (4 + 4 packed bf16 pairs)
+    auto rowmath = [&](int64_t row, uint32_t (&pd)[4], uint32_t (&pc)[4]) {
+        const bool live = row < g.M;
+        const float d[8] = {vdy[0].x, vdy[0].y, vdy[0].z, vdy[0].w, vdy[1].x, vdy[1].y, vdy[1].z, vdy[1].w};
+        const float sv[8] = {vs[0].x, vs[0].y, vs[0].z, vs[0].w, vs[1].x, vs[1].y, vs[1].z, vs[1].w};
+        float xh[8], gd[8];
+        const float4 g0 = *reinterpret_cast<const float4*>(lgm + 8 * q), g1 = *reinterpret_cast<const float4*>(lgm + 8 * q + 4);
+        const float gm[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            xh[e] = (sv[e] - mrow) * rrow;
+            gd[e] = d[e] * gm[e];
+        }
+        float c1 = ((gd[0] * xh[0] + gd[1] * xh[1]) + (gd[2] * xh[2] + gd[3] * xh[3])) +
+                   ((gd[4] * xh[4] + gd[5] * xh[5]) + (gd[6] * xh[6] + gd[7] * xh[7]));
+        float c2 = ((gd[0] + gd[1]) + (gd[2] + gd[3])) + ((gd[4] + gd[5]) + (gd[6] + gd[7]));
+        c1 = xsum<32>(c1) / (float)H;
+        c2 = xsum<32>(c2) / (float)H;
+        float xsk[SK ? 8 : 1], gsk[SK ? 8 : 1], c1s = 0.f, c2s = 0.f;
+        if constexpr (SK) {
+            const float xv[8] = {vx[0].x, vx[0].y, vx[0].z, vx[0].w, vx[1].x, vx[1].y, vx[1].z, vx[1].w};
+            const float4 h0 = *reinterpret_cast<const float4*>(lgm + H + 8 * q);
+            const float4 h1 = *reinterpret_cast<const float4*>(lgm + H + 8 * q + 4);
+            const float gms[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                xsk[e] = (xv[e] - mrs) * rrs;
+                gsk[e] = d[e] * gms[e];
+            }
+            c1s = ((gsk[0] * xsk[0] + gsk[1] * xsk[1]) + (gsk[2] * xsk[2] + gsk[3] * xsk[3])) +
+                  ((gsk[4] * xsk[4] + gsk[5] * xsk[5]) + (gsk[6] * xsk[6] + gsk[7] * xsk[7]));
+            c2s = ((gsk[0] + gsk[1]) + (gsk[2] + gsk[3])) + ((gsk[4] + gsk[5]) + (gsk[6] + gsk[7]));
+            c1s = xsum<32>(c1s) / (float)H;
+            c2s = xsum<32>(c2s) / (float)H;
+        }
+        const uint32_t key = drop_key(g.seed, (uint64_t)row);
+        float dov[8], dsv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float o = rrow * (gd[e] - c1 * xh[e] - c2);
+            float a = o;
+            if (g.p_drop > 0.f) a = drop_u(key, (uint32_t)(8 * q + e)) >= g.p_drop ? o * g.inv_keep : 0.f;
+            dov[e] = live ? a : 0.f;
+            float sres = o;
+            if constexpr (SK) sres += rrs * (gsk[e] - c1s * xsk[e] - c2s);
+            dsv[e] = sres;
+            // the column sums, branch-free (a branch here sent the arrays to scratch): group 0 the LN ones (dead
+            // rows add exact zeros), group 1 db_o
+            const float dl = (live && cg == 0) ? d[e] : 0.f;
+            dg[e] += cg == 0 ? dl * xh[e] : dov[e];
+            db[e] += dl;
+            if constexpr (SK) dgs[e] += dl * xsk[e];
+        }
+        if (live && (q >> 4) == cg) {   // dres: each group its half of the columns
+            float* pr = g.dres + row * H + 8 * q;
+            *reinterpret_cast<float4*>(pr) = make_float4(dsv[0], dsv[1], dsv[2], dsv[3]);
+            *reinterpret_cast<float4*>(pr + 4) = make_float4(dsv[4], dsv[5], dsv[6], dsv[7]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pd[e] = pk_bf16(dov[2 * e], dov[2 * e + 1]);
+        if constexpr (ABF) {
+            pc[0] = vcb.x; pc[1] = vcb.y; pc[2] = vcb.z; pc[3] = vcb.w;
+        } else {
+            pc[0] = pk_bf16(vc[0].x, vc[0].y);
+            pc[1] = pk_bf16(vc[0].z, vc[0].w);
+            pc[2] = pk_bf16(vc[1].x, vc[1].y);
+            pc[3] = pk_bf16(vc[1].z, vc[1].w);
+        }
+    };
+
+    if (t0 < t1) load(t0 * BM + rr);
+    for (int64_t t = t0; t < t1; ++t) {
+        uint32_t pd[2][4], pc[2][4];
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+            rowmath(t * BM + 16 * pass + rr, pd[pass], pc[pass]);
+            // next pass-row: row rr + 16 of this tile, then row rr of the next one (t1 - 1's second pass reloads
+            // itself: unconditional loads)
+            const int64_t nrow = pass == 0 ? t * BM + 16 + rr : (t + 1 < t1 ? (t + 1) * BM + rr : t * BM + rr);
+            load(nrow);
+        }
+        lds_barrier();   // the previous tile's fragments are read
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+            *reinterpret_cast<uint4*>(ldo + (16 * pass + rr) * S + 8 * q) = make_uint4(pd[pass][0], pd[pass][1], pd[pass][2], pd[pass][3]);
+            *reinterpret_cast<uint4*>(lcp + (16 * pass + rr) * S + 8 * q) = make_uint4(pc[pass][0], pc[pass][1], pc[pass][2], pc[pass][3]);
+        }
+        lds_barrier();
+        // ---- dW_o rows 128 cg + 16 w.. (all 256 k)
+        {
+            const bf16x8 ya = frag(ldo, 128 * cg + 16 * w);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) accw[k] = mfma(ya, frag(lcp, 16 * k), accw[k]);
+        }
+        // ---- dc columns 128 cg + 16 w.. for the tile's two 16-row halves
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) {
+                const bf16x8 a = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+                                                                ldo + (16 * j + li) * S + 32 * kk + 8 * grp));
+                acc = mfma(wr[kk], a, acc);
+            }
+            const int64_t orow = t * BM + 16 * j + li;
+            if (orow < g.M) {
+                const int64_t off = orow * H + 128 * cg + 16 * w + 4 * grp;
+                if constexpr (ABF) {
+                    *reinterpret_cast<uint2*>((uint16_t*)g.dc + off) = make_uint2(pk_bf16(acc[0], acc[1]),
+                                                                                  pk_bf16(acc[2], acc[3]));
+                } else {
+                    *reinterpret_cast<f32x4*>((float*)g.dc + off) = acc;
+                }
+            }
+        }
+    }
+    // ---- partials of row range rb: dW_o rows of this group (k_sgemm_tn_reduce layout)
+    float* pw = g.part_w + rb * (H * H + H);
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pw[(int64_t)(128 * cg + 16 * w + 4 * grp + r) * H + 16 * k + li] = accw[k][r];
+    // column sums: lanes l and l ^ 32 share columns (two rows per wave); then the 8 waves in order through LDS.
+    // Group 0: the LN sums -> part_ln; group 1: db_o -> the bias slot of part_w.
+    const int NPL = cg == 0 ? (SK ? 4 : 2) : 1;
+    auto sum2 = [](float x) {
+        float a, b;
+        swap32(x, a, b);
+        return a + b;
+    };
+    lds_barrier();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float a0 = sum2(dg[e]), a1 = sum2(db[e]);
+        float a2 = 0.f, a3 = 0.f;
+        if constexpr (SK) {
+            a2 = sum2(dgs[e]);
+            a3 = a1;
+        }
+        if (lane < 32) {
+            float* rw = red + w * NPL * H + 8 * q + e;
+            rw[0] = a0;
+            if (cg == 0) {
+                rw[H] = a1;
+                if constexpr (SK) {
+                    rw[2 * H] = a2;
+                    rw[3 * H] = a3;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NPL * H; i += NW * 64) {
+        float a = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) a += red[ww * NPL * H + i];
+        if (cg == 0) g.part_ln[rb * NPL * H + i] = a;
+        else pw[H * H + i] = a;
+    }
+}
+
 // ------------------------------------------------------------------------------------------- dispatch
 int g_num_cu = 0;
 int num_cu() {
@@ -2200,6 +2448,23 @@ static int tn_run(int32_t dtype, int64_t M, int32_t N, int32_t K, const void* dy
 namespace tagan {
 namespace {
 typedef void (*l2_fn)(L2Args);
+// H = 256: one plane only (k_ln2_bwd_out256; the three-plane panel would not fit)
+l2_fn l2_pick256(int planes, int abf, int skip) {
+    if (planes != 1) return nullptr;
+    if (abf) return skip ? k_ln2_bwd_out256<true, true> : k_ln2_bwd_out256<true, false>;
+    return skip ? k_ln2_bwd_out256<false, true> : k_ln2_bwd_out256<false, false>;
+}
+size_t l2_lds256(int skip) {
+    return (size_t)2 * 32 * (256 + 16) * 2 + (size_t)8 * (skip ? 4 : 2) * 256 * 4 + (size_t)(skip ? 2 : 1) * 256 * 4;
+}
+// row ranges of the H = 256 form: a multiple of 8 (the two column groups of a range share an XCD), 2 x <= the CUs
+int64_t l2_groups256(int64_t M) {
+    const int64_t tiles = (M + 31) / 32;
+    int64_t g = num_cu() / 2;
+    if (tiles < g) g = tiles;
+    g = (g + 7) / 8 * 8;
+    return g < 8 ? 8 : g;
+}
 l2_fn l2_pick(int planes, int abf, int skip) {
     if (planes == 3 && !abf) return skip ? k_ln2_bwd_out<3, false, true> : k_ln2_bwd_out<3, false, false>;
     if (planes == 1 && abf) return skip ? k_ln2_bwd_out<1, true, true> : k_ln2_bwd_out<1, true, false>;
@@ -2216,11 +2481,12 @@ int64_t l2_groups(int64_t M) {
 }  // namespace tagan
 
 extern "C" int tagan_ln2_bwd_out_supported(int32_t H, int32_t planes, int32_t act_dtype) {
+    if (H == 256) return TAGAN_SG_LN2_256 && l2_pick256(planes, act_dtype == TAGAN_BF16, 0) != nullptr;
     return H == 128 && l2_pick(planes, act_dtype == TAGAN_BF16, 0) != nullptr;
 }
 
 extern "C" size_t tagan_ln2_bwd_out_workspace(int64_t M, int32_t H, int32_t skip) {
-    const int64_t G = l2_groups(M);
+    const int64_t G = H == 256 ? l2_groups256(M) : l2_groups(M);
     return (size_t)G * ((size_t)H * H + H + (size_t)(skip ? 4 : 2) * H) * sizeof(float);
 }
 
@@ -2231,7 +2497,8 @@ extern "C" int tagan_ln2_bwd_out(int32_t act_dtype, int32_t planes, int64_t M, i
                                  float* dw_o, float* db_o, float* dgamma, float* dbeta, float* dgamma_s,
                                  float* dbeta_s, void* ws, size_t ws_bytes, void* stream) {
     const int abf = act_dtype == TAGAN_BF16, skip = xs != nullptr;
-    const l2_fn fn = H == 128 ? l2_pick(planes, abf, skip) : nullptr;
+    const bool w256 = H == 256 && TAGAN_SG_LN2_256;
+    const l2_fn fn = H == 128 ? l2_pick(planes, abf, skip) : w256 ? l2_pick256(planes, abf, skip) : nullptr;
     TAGAN_REQUIRE(fn, TAGAN_ERR_UNSUPPORTED, "tagan_ln2_bwd_out: no kernel for H=%d planes=%d act dtype %d", H, planes,
                   act_dtype);
     TAGAN_REQUIRE(M > 0 && dy && s && mean && rstd && gamma && c && wp_km && dres && dc && dgamma && dbeta &&
@@ -2244,9 +2511,9 @@ extern "C" int tagan_ln2_bwd_out(int32_t act_dtype, int32_t planes, int64_t M, i
                   TAGAN_ERR_ARG, "tagan_ln2_bwd_out: operands must be 16-byte aligned (dense [M, H] rows)");
     const size_t need = tagan_ln2_bwd_out_workspace(M, H, skip);
     TAGAN_REQUIRE(ws && ws_bytes >= need, TAGAN_ERR_ARG, "tagan_ln2_bwd_out: workspace %zu < %zu", ws_bytes, need);
-    const size_t lds = l2_lds(planes, skip);
+    const size_t lds = w256 ? l2_lds256(skip) : l2_lds(planes, skip);
     TAGAN_REQUIRE(lds_ok((const void*)fn, lds), TAGAN_ERR_LAUNCH, "tagan_ln2_bwd_out: LDS attribute");
-    const int64_t G = l2_groups(M), tiles = (M + 31) / 32;
+    const int64_t G = w256 ? l2_groups256(M) : l2_groups(M), tiles = (M + 31) / 32;
     L2Args g{};
     g.M = M; g.tiles_per_wg = (tiles + G - 1) / G;
     g.dy = dy; g.s = s; g.mean = mean; g.rstd = rstd; g.gamma = gamma;
@@ -2255,7 +2522,7 @@ extern "C" int tagan_ln2_bwd_out(int32_t act_dtype, int32_t planes, int64_t M, i
     g.c = c; g.wp = (const uint4*)wp_km; g.dres = dres; g.dc = dc;
     g.part_w = (float*)ws;
     g.part_ln = (float*)ws + (size_t)G * (H * H + H);
-    hipLaunchKernelGGL(fn, dim3((unsigned)G), dim3(512), lds, as_stream(stream), g);
+    hipLaunchKernelGGL(fn, dim3((unsigned)(w256 ? 2 * G : G)), dim3(512), lds, as_stream(stream), g);
     TAGAN_CHECK_LAUNCH("tagan_ln2_bwd_out");
     const int L = H * H + H;
     k_sgemm_tn_reduce<<<(L + TNR_COLS - 1) / TNR_COLS, TNR_COLS * TNR_SLICES, 0, as_stream(stream)>>>(

@@ -336,6 +336,109 @@ def test_ln2_bwd_out_matches_unfused_chain_with_dropout(skip):
         assert _merr(a, b.double()) <= 2e-5, (name, _merr(a, b.double()))
 
 
+@pytest.mark.parametrize("M", [5003, 40961])
+@pytest.mark.parametrize("store", ["bf16", "fp32"])
+@pytest.mark.parametrize("skip", [False, True])
+def test_ln2_bwd_out_256_matches_unfused_chain(skip, store, M):
+    """H = 256, one plane (k_ln2_bwd_out256: two column groups): the same values as the unfused chain -- LN2 backward
+    [+ skip] (tagan_layernorm_bwd / _skip_bwd), then tagan_sgemm_nt (dC) and tagan_sgemm_tn (dW_o) on its do -- with
+    dropout: the same do (bf16-rounded operand of both products), fp32 sums in another order (column sums: 1e-5
+    sqrt(M / 1000) of the tensor's scale; dres per element; dc per element to one bf16 ulp: do is a bf16 operand of
+    its product in both, and the two fp32 row maths may round it differently where they differ by an fp32 ulp)."""
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    from tagan_amd.fused import ln_bwd, ln_skip_bwd
+    W = 256
+    if not sg.ln2_bwd_out_supported(W, 1, store == "bf16"):
+        pytest.skip("no H = 256 fused LN2 backward")
+    g = torch.Generator(device=dev).manual_seed(256 + M)
+    ln_w = 1.0 + 0.1 * torch.randn(W, device=dev, generator=g)
+    dt = torch.bfloat16 if store == "bf16" else torch.float32
+    s = torch.randn(M, W, device=dev, generator=g)
+    dy = torch.randn(M, W, device=dev, generator=g)
+    c = torch.randn(M, W, device=dev, generator=g).to(dt)
+    w_o = torch.randn(W, W, device=dev, generator=g) / W ** 0.5
+    x = s.double()
+    m64 = x.mean(1)
+    rs64 = 1.0 / torch.sqrt(((x - m64[:, None]) ** 2).mean(1) + 1e-5)
+    mean, rstd = m64.float(), rs64.float()
+    wp = sg.wprep(w_o, True, 1)
+    if skip:
+        xs = torch.randn(M, W, device=dev, generator=g)
+        gs = 1.0 + 0.1 * torch.randn(W, device=dev, generator=g)
+        xx = xs.double()
+        ms = xx.mean(1)
+        rss = 1.0 / torch.sqrt(((xx - ms[:, None]) ** 2).mean(1) + 1e-5)
+        ms, rss = ms.float(), rss.float()
+        dres0, do0, dg0, db0, dbo0, dgs0, dbs0 = ln_skip_bwd(s, mean, rstd, ln_w, xs, ms, rss, gs, dy, 0.1, 4321,
+                                                             da_dtype=dt)
+        got = sg.ln2_bwd_out(dy, s, mean, rstd, ln_w, 0.1, 4321, c, wp, 1, skip=(xs, ms, rss, gs))
+    else:
+        dres0, do0, dg0, db0, dbo0 = ln_bwd(s, mean, rstd, ln_w, dy, None, 0.1, 4321, True, True, True, da_dtype=dt)
+        dgs0 = dbs0 = None
+        got = sg.ln2_bwd_out(dy, s, mean, rstd, ln_w, 0.1, 4321, c, wp, 1)
+    dc0 = sg.nt(do0, wp, W, 1, out_dtype=dt)
+    dw0 = sg.tn(do0, c, 1, want_db=False)[0]
+    want = [dres0, dc0, dw0, dbo0, dg0, db0, dgs0, dbs0]
+    assert 0.05 < float((do0 == 0).float().mean()) < 0.15
+    for name, a, b in zip(["dres", "dc", "dw_o", "db_o", "dgamma", "dbeta", "dgamma_s", "dbeta_s"], got, want):
+        if b is None:
+            assert a is None
+            continue
+        if name == "dres":           # per element, fp32
+            tol = 2e-5
+        elif name == "dc":           # per element: a 1-ulp fp32 difference in do can flip its bf16 operand rounding
+            tol = 2.0 ** -7
+        else:                        # column sums over M rows in another fp32 order: grows like sqrt(M)
+            tol = 1e-5 * (M / 1000) ** 0.5
+        assert a.dtype == b.dtype, name
+        assert _merr(a, b.double()) <= tol, (name, _merr(a, b.double()))
+    again = sg.ln2_bwd_out(dy, s, mean, rstd, ln_w, 0.1, 4321, c, wp, 1, skip=(xs, ms, rss, gs) if skip else None)
+    for a, b in zip(got, again):
+        assert (a is None and b is None) or torch.equal(a, b)
+
+
+@pytest.mark.timeout(300)
+def test_ln2_bwd_out_256_reproducible_at_scale():
+    """3.2M rows (a quarter of the C5 one-rank share), bf16 activations, skip form, dropout: three calls bitwise
+    equal (fixed-order partials in both column groups), dgamma within fp32 accuracy of fp64."""
+    dev = _dev()
+    from tagan_amd import stream_gemm as sg
+    W, M = 256, 3_200_000
+    if not sg.ln2_bwd_out_supported(W, 1, True):
+        pytest.skip("no H = 256 fused LN2 backward")
+    g = torch.Generator(device=dev).manual_seed(77)
+    ln_w = 1.0 + 0.1 * torch.randn(W, device=dev, generator=g)
+    gs = 1.0 + 0.1 * torch.randn(W, device=dev, generator=g)
+    s = 0.2 + torch.randn(M, W, device=dev, generator=g)
+    dy = torch.randn(M, W, device=dev, generator=g)
+    c = torch.randn(M, W, device=dev, generator=g).to(torch.bfloat16)
+    xs = torch.randn(M, W, device=dev, generator=g)
+    w_o = torch.randn(W, W, device=dev, generator=g) / W ** 0.5
+
+    def stats(t):
+        m = torch.empty(M, device=dev, dtype=torch.float64)
+        r = torch.empty(M, device=dev, dtype=torch.float64)
+        for a in range(0, M, 400_000):
+            x = t[a:a + 400_000].double()
+            m[a:a + 400_000] = x.mean(1)
+            r[a:a + 400_000] = 1.0 / torch.sqrt(((x - m[a:a + 400_000, None]) ** 2).mean(1) + 1e-5)
+        return m, r
+    m64, rs64 = stats(s)
+    ms, rss = stats(xs)
+    wp = sg.wprep(w_o, True, 1)
+    runs = [sg.ln2_bwd_out(dy, s, m64.float(), rs64.float(), ln_w, 0.1, 5, c, wp, 1,
+                           skip=(xs, ms.float(), rss.float(), gs)) for _ in range(3)]
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
+    ref = torch.zeros(W, device=dev, dtype=torch.float64)
+    for a in range(0, M, 400_000):
+        xh = (s[a:a + 400_000].double() - m64[a:a + 400_000, None]) * rs64[a:a + 400_000, None]
+        ref += (dy[a:a + 400_000].double() * xh).sum(0)
+    assert _merr(runs[0][4], ref) <= 2e-5
+
+
 def test_ln_supported_shapes():
     _dev()
     from tagan_amd import stream_gemm as sg
