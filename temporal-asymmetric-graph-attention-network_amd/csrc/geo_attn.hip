@@ -400,11 +400,24 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_chunk(GeoArgs A) {
 
 // Merge of multi-chunk segments (hub rows / columns).  A wave per segment, persistent over segments (the grid is
 // bounded: the partial capacity is a worst case, most of it unused).  A lane owns 4 features; the wave's
-// 64 / (width / 4) lane groups ("phases") take interleaved chunks, and each lane keeps MG independent partial states
-// over its chunks, so MG·phases partial loads are in flight instead of one dependent chain per chunk (a C2 hub row
+// 64 / (width / 4) lane groups ("phases") take interleaved chunks, and each lane keeps G independent partial states
+// over its chunks, so G·phases partial loads are in flight instead of one dependent chain per chunk (a C2 hub row
 // spans ~100 chunks).  The states combine in a fixed order (accumulators, then phases by xor-shuffle): the result
 // is deterministic (bitwise reproducible), in another summation order than a chunk-serial loop.
-constexpr int MG = 4;
+// Round 6: the accumulator count G is a template parameter (env TAGAN_GEO_MG = 4 / 8 / 16, see geo_mg()), and the
+// G chunk loads of an iteration are branch-free (index clamped into the segment, dead slots dropped by a select):
+// with a guarded load per accumulator each one sat in its own basic block behind a wait, so the G loads of an
+// iteration ran as a dependent chain (a C2 hub: k_geo_sum_parts 25 us, k_geo_fwd_merge 20 us per call).
+// fixed-order pairwise tree over the G accumulators (bitwise reproducible)
+template <int G, typename T, typename F>
+__device__ __forceinline__ T tree_combine(T (&v)[G], F f) {
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "G: a power of two <= 16");
+#pragma unroll
+    for (int w = 1; w < G; w <<= 1)
+#pragma unroll
+        for (int u = 0; u + w < G; u += 2 * w) v[u] = f(v[u], v[u + w]);
+    return v[0];
+}
 struct SoftState {
     float m, l;
     float4 a;
@@ -435,9 +448,36 @@ __device__ __forceinline__ float4 f4add(const float4& x, const float4& y) {
     return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
 }
 
+// component-wise select (a float4 ternary lowers to a select of stack addresses through scratch)
+__device__ __forceinline__ float4 f4live(bool live, const float4& x) {
+    return make_float4(live ? x.x : 0.f, live ? x.y : 0.f, live ? x.z : 0.f, live ? x.w : 0.f);
+}
+
 __device__ __forceinline__ float4 f4shfl_xor(const float4& x, int mask) {
     return make_float4(__shfl_xor(x.x, mask, WAVE), __shfl_xor(x.y, mask, WAVE), __shfl_xor(x.z, mask, WAVE),
                        __shfl_xor(x.w, mask, WAVE));
+}
+
+// accumulators per lane of the merge kernels, read once: TAGAN_GEO_MG for k_geo_sum_parts (default 16),
+// TAGAN_GEO_MG_FWD for k_geo_fwd_merge (default 8: its 6-float states take 243 VGPRs at 16); 4, 8 or 16.
+// C2 per call (profiles/r6q_*, r6r_*): sum_parts 25.0 -> 10.4 us, fwd_merge 19.5 -> 11.2 us at G = 8 (branch-free
+// loads); G = 16 takes the C2 backward another ~8 us lower and the forward ~5 us higher.
+int geo_mg_env(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    const int x = e ? std::atoi(e) : dflt;
+    return (x == 4 || x == 8 || x == 16) ? x : dflt;
+}
+int geo_mg(bool fwd) {
+    static const int vs = geo_mg_env("TAGAN_GEO_MG", 16), vf = geo_mg_env("TAGAN_GEO_MG_FWD", 8);
+    return fwd ? vf : vs;
+}
+template <typename F>
+void geo_mg_dispatch(bool fwd, F&& f) {
+    switch (geo_mg(fwd)) {
+        case 4: f(std::integral_constant<int, 4>{}); break;
+        case 16: f(std::integral_constant<int, 16>{}); break;
+        default: f(std::integral_constant<int, 8>{}); break;
+    }
 }
 
 unsigned merge_grid(int64_t part_cap) {
@@ -446,7 +486,7 @@ unsigned merge_grid(int64_t part_cap) {
 }
 
 // Merge the partial softmax states {m, l, acc} of multi-chunk rows (H <= 256).
-template <typename S>
+template <int G, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_fwd_merge(GeoArgs A) {
     TAGAN_LIVE_SEED(A);
     using IO = Io<S>;
@@ -461,25 +501,35 @@ __global__ void __launch_bounds__(BLK) k_geo_fwd_merge(GeoArgs A) {
     for (int64_t k = blockIdx.x * (int64_t)(BLK / WAVE) + (threadIdx.x >> 6); k < nmulti; k += stride) {
         const int row = A.g.row_multi[k];
         const int c0 = A.g.row_chunk_ptr[row], c1 = A.g.row_chunk_ptr[row + 1];
-        SoftState st[MG];
+        SoftState st[G];
 #pragma unroll
-        for (int u = 0; u < MG; ++u) st[u] = SoftState{-INFINITY, 0.f, make_float4(0.f, 0.f, 0.f, 0.f)};
-        for (int c = c0 + ph; c < c1; c += nph * MG) {
+        for (int u = 0; u < G; ++u) st[u] = SoftState{-INFINITY, 0.f, make_float4(0.f, 0.f, 0.f, 0.f)};
+        for (int c = c0 + ph; c < c1; c += nph * G) {
+            int part[G];
+            bool live[G];
 #pragma unroll
-            for (int u = 0; u < MG; ++u) {
+            for (int u = 0; u < G; ++u) {
                 const int cc = c + u * nph;
-                if (cc < c1) {
-                    const int part = A.g.row_chunk_part[cc];
-                    if (TAGAN_DBAD(part >= 0 && part < A.g.part_cap, part, A.g.part_cap)) continue;   // partial slot
-                    SoftState y;
-                    y.m = A.part_m[(int64_t)part * A.heads + h];
-                    y.l = A.part_l[(int64_t)part * A.heads + h];
-                    y.a = ld4(A.part_v + (int64_t)part * A.H + f0);
-                    st[u] = soft_merge(st[u], y);
-                }
+                part[u] = A.g.row_chunk_part[min(cc, c1 - 1)];
+                live[u] = cc < c1;
+                if (TAGAN_DBAD(part[u] >= 0 && part[u] < A.g.part_cap, part[u], A.g.part_cap)) live[u] = false, part[u] = 0;
+            }
+            SoftState y[G];
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                y[u].m = A.part_m[(int64_t)part[u] * A.heads + h];
+                y[u].l = A.part_l[(int64_t)part[u] * A.heads + h];
+                y[u].a = ld4(A.part_v + (int64_t)part[u] * A.H + f0);
+            }
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                y[u].m = live[u] ? y[u].m : -INFINITY;              // a dead slot merges as the empty state
+                y[u].l = live[u] ? y[u].l : 0.f;
+                y[u].a = f4live(live[u], y[u].a);
+                st[u] = soft_merge(st[u], y[u]);
             }
         }
-        SoftState r = soft_merge(soft_merge(st[0], st[1]), soft_merge(st[2], st[3]));
+        SoftState r = tree_combine<G>(st, [](const SoftState& x, const SoftState& y) { return soft_merge(x, y); });
         for (int m = lanes; m < WAVE; m <<= 1) r = soft_merge(r, soft_shfl_xor(r, m));   // phases, fixed order
         if (ph == 0) {
             const float inv = (r.l > 0.f) ? 1.f / r.l : NAN;
@@ -583,9 +633,9 @@ __global__ void __launch_bounds__(BLK) k_geo_bwd_row_chunk(GeoArgs A) {
     }
 }
 
-// Sum partial rows (bwd row: dq; bwd col: dk|dv) of multi-chunk segments; same lane / phase / MG-accumulator
+// Sum partial rows (bwd row: dq; bwd col: dk|dv) of multi-chunk segments; same lane / phase / G-accumulator
 // scheme and bounded persistent grid as k_geo_fwd_merge, fixed combination order.
-template <typename S>
+template <int G, typename S>
 __global__ void __launch_bounds__(BLK) k_geo_sum_parts(const int32_t* __restrict__ counts,
                                                        const int32_t* __restrict__ multi,
                                                        const int32_t* __restrict__ chunk_ptr,
@@ -604,18 +654,26 @@ __global__ void __launch_bounds__(BLK) k_geo_sum_parts(const int32_t* __restrict
         const int c0 = chunk_ptr[seg], c1 = chunk_ptr[seg + 1];
         for (int fb = 0; fb < width; fb += lanes * 4) {
             const int f0 = fb + (lane % lanes) * 4;
-            float4 acc[MG];
+            float4 acc[G];
 #pragma unroll
-            for (int u = 0; u < MG; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int c = c0 + ph; c < c1; c += nph * MG) {
+            for (int u = 0; u < G; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int c = c0 + ph; c < c1; c += nph * G) {
+                int pidx[G];
+                bool live[G];
 #pragma unroll
-                for (int u = 0; u < MG; ++u) {
+                for (int u = 0; u < G; ++u) {
                     const int cc = c + u * nph;
-                    if (cc < c1 && !TAGAN_DBAD(chunk_part[cc] >= 0, chunk_part[cc], cc))   // partial slot
-                        acc[u] = f4add(acc[u], ld4(part + (int64_t)chunk_part[cc] * width + f0));
+                    pidx[u] = chunk_part[min(cc, c1 - 1)];
+                    live[u] = cc < c1;
+                    if (TAGAN_DBAD(pidx[u] >= 0, pidx[u], cc)) live[u] = false, pidx[u] = 0;   // partial slot
                 }
+                float4 v[G];
+#pragma unroll
+                for (int u = 0; u < G; ++u) v[u] = ld4(part + (int64_t)pidx[u] * width + f0);
+#pragma unroll
+                for (int u = 0; u < G; ++u) acc[u] = f4add(acc[u], f4live(live[u], v[u]));
             }
-            float4 sum = f4add(f4add(acc[0], acc[1]), f4add(acc[2], acc[3]));
+            float4 sum = tree_combine<G>(acc, [](const float4& x, const float4& y) { return f4add(x, y); });
             for (int m = lanes; m < WAVE; m <<= 1) sum = f4add(sum, f4shfl_xor(sum, m));
             if (ph == 0) {
                 if (f0 < H) Io<S>::st(dst0, (int64_t)seg * ldd + f0, sum);
@@ -1294,8 +1352,11 @@ int tagan_geo_attn_fwd(int dtype, int metric, const tagan_graph* g, int32_t head
     TAGAN_CHECK_LAUNCH("geo_attn_fwd");
     if (lpr) {
         const unsigned gm = merge_grid(g->part_cap);
-        if (A.bf16) k_geo_fwd_merge<bf16s><<<gm, BLK, 0, s>>>(A);
-        else k_geo_fwd_merge<float><<<gm, BLK, 0, s>>>(A);
+        geo_mg_dispatch(true, [&](auto g) {
+            constexpr int G = decltype(g)::value;
+            if (A.bf16) k_geo_fwd_merge<G, bf16s><<<gm, BLK, 0, s>>>(A);
+            else k_geo_fwd_merge<G, float><<<gm, BLK, 0, s>>>(A);
+        });
         TAGAN_CHECK_LAUNCH("geo_attn_fwd_merge");
     }
     if (edge_alpha) {
@@ -1357,21 +1418,27 @@ int tagan_geo_attn_bwd(int dtype, int metric, const tagan_graph* g, int32_t head
     hipStream_t s = as_stream(stream);
     const unsigned gm = merge_grid(g->part_cap);
     auto sum_cols = [&]() {
-        if (A.bf16)
-            k_geo_sum_parts<bf16s><<<gm, BLK, 0, s>>>(g->col_counts, g->col_multi, g->col_chunk_ptr,
-                                                      g->col_chunk_part, A.part_v2, 2 * H, A.dk, A.dv, A.ldd, H);
-        else
-            k_geo_sum_parts<float><<<gm, BLK, 0, s>>>(g->col_counts, g->col_multi, g->col_chunk_ptr,
-                                                      g->col_chunk_part, A.part_v2, 2 * H, A.dk, A.dv, A.ldd, H);
+        geo_mg_dispatch(false, [&](auto gg) {
+            constexpr int G = decltype(gg)::value;
+            if (A.bf16)
+                k_geo_sum_parts<G, bf16s><<<gm, BLK, 0, s>>>(g->col_counts, g->col_multi, g->col_chunk_ptr,
+                                                             g->col_chunk_part, A.part_v2, 2 * H, A.dk, A.dv, A.ldd, H);
+            else
+                k_geo_sum_parts<G, float><<<gm, BLK, 0, s>>>(g->col_counts, g->col_multi, g->col_chunk_ptr,
+                                                             g->col_chunk_part, A.part_v2, 2 * H, A.dk, A.dv, A.ldd, H);
+        });
         return hipGetLastError();
     };
     auto sum_rows = [&]() {
-        if (A.bf16)
-            k_geo_sum_parts<bf16s><<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr,
-                                                      g->row_chunk_part, A.part_v, H, A.dq, A.dq, A.ldd, H);
-        else
-            k_geo_sum_parts<float><<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr,
-                                                      g->row_chunk_part, A.part_v, H, A.dq, A.dq, A.ldd, H);
+        geo_mg_dispatch(false, [&](auto gg) {
+            constexpr int G = decltype(gg)::value;
+            if (A.bf16)
+                k_geo_sum_parts<G, bf16s><<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr,
+                                                             g->row_chunk_part, A.part_v, H, A.dq, A.dq, A.ldd, H);
+            else
+                k_geo_sum_parts<G, float><<<gm, BLK, 0, s>>>(g->row_counts, g->row_multi, g->row_chunk_ptr,
+                                                             g->row_chunk_part, A.part_v, H, A.dq, A.dq, A.ldd, H);
+        });
         return hipGetLastError();
     };
     if (w.col_first) {
