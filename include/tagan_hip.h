@@ -572,6 +572,22 @@ int tagan_qkv_pack(int64_t H, const float* wq, const float* wk, const float* wv,
 int tagan_qkv_unpack(int64_t H, const float* dw, int64_t ld_dw, const float* db, int64_t db_stride, float* dwq,
                      float* dwk, float* dwv, float* dbq, float* dbk, float* dbv, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Narrow-input projection (the node embedding, model.py:233: nn.Linear(node_feature_dim, hidden_dim) on
+ * every snapshot's x).  y[M, N] = x[M, K] Wᵀ + b, W row-major [N, K], fp32, K <= 31, N in {64, 128, 256};
+ * x row stride ldx (>= K, any alignment), y / dY 16-byte aligned with row strides ldy / lddy % 4 == 0, b 16-byte
+ * aligned.  Backward: dW [N, K] = dYᵀ x and db [N] = Σ dY
+ * (either may be NULL) in one pass over dY, exact-f32 MFMA, ordered per-workgroup partials: deterministic.
+ * The input gradient is not produced (the caller's x is data).
+ * ------------------------------------------------------------------------- */
+int tagan_narrow_linear_supported(int32_t K, int32_t N);
+int tagan_narrow_linear_fwd(int64_t M, int32_t K, int32_t N, const float* x, int64_t ldx, const float* w,
+                            const float* b, float* y, int64_t ldy, void* stream);
+size_t tagan_narrow_linear_bwd_workspace(int64_t M, int32_t K, int32_t N);
+int tagan_narrow_linear_bwd(int64_t M, int32_t K, int32_t N, const float* x, int64_t ldx, const float* dy,
+                            int64_t lddy, float* dw, float* db, void* workspace, size_t workspace_bytes,
+                            void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -523,6 +523,63 @@ def linear(x, w, b=None):
     return LinearFn.apply(x, w, b)
 
 
+class NarrowLinearFn(torch.autograd.Function):
+    """y = x·Wᵀ + b for a narrow fp32 input (K <= 31 features): csrc/narrow.hip's exact-f32 MFMA kernels, the
+    weight and bias gradients in one pass over dy (the node embedding, model.py:233)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        require_hip(x)
+        M, K = x.shape
+        N = w.shape[0]
+        y = torch.empty(M, N, device=x.device, dtype=torch.float32)
+        wc = w.contiguous()
+        check(lib().tagan_narrow_linear_fwd(M, K, N, ptr(x), x.stride(0), ptr(wc), ptr(b), ptr(y), N,
+                                            stream_of(x)), "tagan_narrow_linear_fwd")
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        M, K = x.shape
+        N = w.shape[0]
+        dy = dy.float().contiguous()
+        if dy.data_ptr() % 16:
+            dy = dy.clone()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = dy @ w
+        want_w = ctx.needs_input_grad[1]
+        want_b = ctx.has_b and ctx.needs_input_grad[2]
+        if (want_w or want_b) and M > 0:
+            dw = torch.empty(N, K, device=x.device) if want_w else None
+            db = torch.empty(N, device=x.device) if want_b else None
+            L = lib()
+            wsb = L.tagan_narrow_linear_bwd_workspace(M, K, N)
+            ws = torch.empty(int(wsb), dtype=torch.uint8, device=x.device)
+            check(L.tagan_narrow_linear_bwd(M, K, N, ptr(x), x.stride(0), ptr(dy), N, ptr(dw), ptr(db), ptr(ws), wsb,
+                                            stream_of(x)), "tagan_narrow_linear_bwd")
+        elif want_w or want_b:
+            dw = torch.zeros_like(w) if want_w else None
+            db = torch.zeros(N, device=x.device) if want_b else None
+        return dx, dw, db
+
+
+_NARROW = os.environ.get("TAGAN_NARROW", "1") != "0"
+
+
+def embed_linear(x, w, b=None):
+    """The node embedding: the narrow-input HIP kernels when they apply (fp32 CUDA x with unit column stride,
+    K <= 31, N in 64 / 128 / 256, a 16-byte aligned bias), else ``linear``."""
+    if (_NARROW and x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and w.dtype == torch.float32
+            and x.stride(1) == 1 and (b is None or (b.is_contiguous() and b.data_ptr() % 16 == 0))
+            and lib().tagan_narrow_linear_supported(x.shape[1], w.shape[0])):
+        return NarrowLinearFn.apply(x, w, b)
+    return linear(x, w, b)
+
+
 def fused_qkv(x, q_lin, k_lin, v_lin):
     """One GEMM for the three projections (hipBLASLt via torch): [.., H] -> [.., 3H] = q | k | v."""
     w = torch.cat([q_lin.weight, k_lin.weight, v_lin.weight], 0)

@@ -27,7 +27,7 @@ import torch.nn.functional as F
 
 from .fused import precision as precision_ctx
 from .ingest import SnapshotBatch, unpack as _unpack
-from .kernels import build_graph, build_graph_cat, cat_adjacent, layer_norm, linear, pool_time_major
+from .kernels import build_graph, build_graph_cat, cat_adjacent, embed_linear, layer_norm, pool_time_major
 from .layers.classification import ClassificationModule, TemporalLossModule, fused_head
 from .layers.graph_attention import TAGANGraphAttention
 from .layers.temporal_attention import AsymmetricTemporalAttention, MaskBroadcastError
@@ -114,7 +114,7 @@ class TAGAN(nn.Module):
                 counts.append(int(x.shape[0]))
             x_cat = cat_adjacent(xs, 0)   # a view when the snapshots share one buffer
             graph = build_graph(eis, counts, validate=self.validate_edges)
-        h = linear(x_cat, self.node_embedding.weight, self.node_embedding.bias)
+        h = embed_linear(x_cat, self.node_embedding.weight, self.node_embedding.bias)
         skip = h
         for i, layer in enumerate(self.geometric_attention_layers):
             if i == 0 and self.skip_layer_norm is not None:
