@@ -842,7 +842,8 @@ def main():
                      "fp32 mode as three bf16 planes, six plane products, fp32 accumulate; the N = 128 products on "
                      "row-owner kernels; LN1 fused into the QKV projection's prologue, dropout + residual + LN2 into "
                      "the out-projection's epilogue, in bf16 mode also LN1's backward into the QKV input gradient's "
-                     "epilogue); node embedding, head and GRU GEMMs: " + lib_gemms)
+                     "epilogue); node embedding: exact-f32 matrix-core kernels (csrc/narrow.hip, weight and bias "
+                     "gradients in one pass); head and GRU GEMMs: " + lib_gemms)
     rec["config"]["gemms"] = lib_gemms
     rec["launch"] = (("hip-graph (one replay per step)" if world == 1 else
                       "hip-graph (one replay per step; the RCCL gradient all-reduce captured inside it)")
