@@ -572,6 +572,15 @@ int tagan_qkv_pack(int64_t H, const float* wq, const float* wk, const float* wv,
 int tagan_qkv_unpack(int64_t H, const float* dw, int64_t ld_dw, const float* db, int64_t db_stride, float* dwq,
                      float* dwk, float* dwv, float* dbq, float* dbk, float* dbv, void* stream);
 
+/* Temporal bias table (temporal_attention.py:732-790; the additive terms of :1010-1027): tab[h][d] (row length
+ * 2T-1, d = i - j + T - 1, delta = d - (T-1)) = R[clamp(delta + m, 0, 2m)][h] + K[delta + W][h]*[|delta| <= W];
+ * K = asymmetric_kernel [2W+1][heads], R = relative_pos_table [2m+1][heads] (NULL: no relative term).
+ * Backward: dK, dR (either may be NULL) from g [heads][2T-1]; ordered sums, deterministic. */
+int tagan_temporal_bias_table(int32_t T, int32_t heads, const float* K, int32_t W, const float* R, int32_t m,
+                              float* tab, void* stream);
+int tagan_temporal_bias_table_bwd(int32_t T, int32_t heads, const float* g, int32_t W, int32_t m, float* dK,
+                                  float* dR, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Narrow-input projection (the node embedding, model.py:233: nn.Linear(node_feature_dim, hidden_dim) on
  * every snapshot's x).  y[M, N] = x[M, K] Wᵀ + b, W row-major [N, K], fp32, K <= 31, N in {64, 128, 256};

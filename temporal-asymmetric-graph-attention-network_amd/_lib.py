@@ -44,6 +44,8 @@ _SIGNATURES = {
     "tagan_pool_workspace": (_sz, [_i32, _i32]),
     "tagan_colsum_workspace": (_sz, [_i64, _i32]),
     "tagan_colsum": (_c.c_int, [_c.c_int, _i64, _i32, _p, _i64, _p, _p, _sz, _p]),
+    "tagan_temporal_bias_table": (_c.c_int, [_i32, _i32, _p, _i32, _p, _i32, _p, _p]),
+    "tagan_temporal_bias_table_bwd": (_c.c_int, [_i32, _i32, _p, _i32, _i32, _p, _p, _p]),
     "tagan_narrow_linear_supported": (_c.c_int, [_i32, _i32]),
     "tagan_narrow_linear_fwd": (_c.c_int, [_i64, _i32, _i32, _p, _i64, _p, _p, _p, _i64, _p]),
     "tagan_narrow_linear_bwd_workspace": (_sz, [_i64, _i32, _i32]),

@@ -47,6 +47,38 @@ __global__ void __launch_bounds__(BLK) k_qkv_unpack(int64_t H, const float* __re
     if (db && dstb && threadIdx.x == 0) dstb[rr] = db[(int64_t)r * db_stride];
 }
 
+// Temporal bias table (temporal_attention.py:732-790, the additive terms of :1010-1027): tab[h][d], d = i - j + T - 1,
+// = R[clamp(δ + m, 0, 2m)][h] + K[δ + W][h]·[|δ| <= W] with δ = d - (T - 1) -- the gathers the layer used to run as
+// two one-hot GEMMs, an add and a transpose copy (forward) and two GEMMs (backward).  Forward: the same fp32 add as
+// before (bitwise).  Backward: dK[k][h] = g[h][k - W + T - 1] (one diagonal each), dR[k][h] = Σ over the diagonals
+// clamped onto k, in ascending d (deterministic).
+__global__ void __launch_bounds__(BLK) k_bias_table_fwd(int T, int heads, const float* __restrict__ K, int W,
+                                                        const float* __restrict__ R, int m, float* __restrict__ tab) {
+    const int D = 2 * T - 1;
+    for (int i = blockIdx.x * BLK + threadIdx.x; i < heads * D; i += gridDim.x * BLK) {
+        const int h = i / D, d = i % D, dl = d - (T - 1);
+        const float kv = (dl >= -W && dl <= W) ? K[(dl + W) * heads + h] : 0.f;
+        tab[i] = R ? R[min(max(dl + m, 0), 2 * m) * heads + h] + kv : kv;
+    }
+}
+
+__global__ void __launch_bounds__(BLK) k_bias_table_bwd(int T, int heads, const float* __restrict__ g, int W, int m,
+                                                        float* __restrict__ dK, float* __restrict__ dR) {
+    const int D = 2 * T - 1, nk = (2 * W + 1) * heads, nr = dR ? (2 * m + 1) * heads : 0;
+    for (int i = blockIdx.x * BLK + threadIdx.x; i < nk + nr; i += gridDim.x * BLK) {
+        if (i < nk) {
+            const int k = i / heads, h = i % heads, d = k - W + T - 1;
+            if (dK) dK[i] = (d >= 0 && d < D) ? g[h * D + d] : 0.f;
+        } else {
+            const int j = i - nk, k = j / heads, h = j % heads;
+            float acc = 0.f;
+            for (int d = 0; d < D; ++d)
+                if (min(max(d - (T - 1) + m, 0), 2 * m) == k) acc += g[h * D + d];
+            dR[j] = acc;
+        }
+    }
+}
+
 }  // namespace
 }  // namespace tagan
 
@@ -72,6 +104,27 @@ int tagan_qkv_unpack(int64_t H, const float* dw, int64_t ld_dw, const float* db,
     k_qkv_unpack<<<(unsigned)(3 * H), BLK, 0, as_stream(stream)>>>(H, dw, ld_dw, db, db_stride, dwq, dwk, dwv, dbq, dbk,
                                                                  dbv);
     TAGAN_CHECK_LAUNCH("qkv_unpack");
+    return TAGAN_OK;
+}
+
+int tagan_temporal_bias_table(int32_t T, int32_t heads, const float* K, int32_t W, const float* R, int32_t m,
+                              float* tab, void* stream) {
+    using namespace tagan;
+    TAGAN_REQUIRE(T > 0 && heads > 0 && W >= 0 && m >= 0 && K && tab, TAGAN_ERR_ARG, "temporal_bias_table: bad args");
+    const int n = heads * (2 * T - 1);
+    k_bias_table_fwd<<<(unsigned)((n + BLK - 1) / BLK), BLK, 0, as_stream(stream)>>>(T, heads, K, W, R, m, tab);
+    TAGAN_CHECK_LAUNCH("temporal_bias_table");
+    return TAGAN_OK;
+}
+
+int tagan_temporal_bias_table_bwd(int32_t T, int32_t heads, const float* g, int32_t W, int32_t m, float* dK,
+                                  float* dR, void* stream) {
+    using namespace tagan;
+    TAGAN_REQUIRE(T > 0 && heads > 0 && W >= 0 && m >= 0 && g && (dK || dR), TAGAN_ERR_ARG,
+                  "temporal_bias_table_bwd: bad args");
+    const int n = (2 * W + 1) * heads + (dR ? (2 * m + 1) * heads : 0);
+    k_bias_table_bwd<<<(unsigned)((n + BLK - 1) / BLK), BLK, 0, as_stream(stream)>>>(T, heads, g, W, m, dK, dR);
+    TAGAN_CHECK_LAUNCH("temporal_bias_table_bwd");
     return TAGAN_OK;
 }
 

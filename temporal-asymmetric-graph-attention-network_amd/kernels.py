@@ -567,6 +567,34 @@ class NarrowLinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+class BiasTableFn(torch.autograd.Function):
+    """The temporal layer's [heads, 2T-1] bias table from its asymmetric-kernel and relative-position tables
+    (csrc/params.hip: one launch each way; temporal_attention.py:732-790)."""
+
+    @staticmethod
+    def forward(ctx, K, R, T: int, W: int, m: int):
+        require_hip(K)
+        heads = K.shape[1]
+        Kc = K.contiguous()
+        Rc = R.contiguous() if R is not None else None
+        tab = torch.empty(heads, 2 * T - 1, device=K.device, dtype=torch.float32)
+        check(lib().tagan_temporal_bias_table(T, heads, ptr(Kc), W, ptr(Rc), m, ptr(tab), stream_of(K)),
+              "tagan_temporal_bias_table")
+        ctx.cfg = (T, W, m, heads, R is not None)
+        return tab
+
+    @staticmethod
+    def backward(ctx, g):
+        T, W, m, heads, has_r = ctx.cfg
+        g = g.float().contiguous()
+        dK = torch.empty(2 * W + 1, heads, device=g.device) if ctx.needs_input_grad[0] else None
+        dR = torch.empty(2 * m + 1, heads, device=g.device) if (has_r and ctx.needs_input_grad[1]) else None
+        if dK is not None or dR is not None:
+            check(lib().tagan_temporal_bias_table_bwd(T, heads, ptr(g), W, m, ptr(dK), ptr(dR), stream_of(g)),
+                  "tagan_temporal_bias_table_bwd")
+        return dK, dR, None, None, None
+
+
 _NARROW = os.environ.get("TAGAN_NARROW", "1") != "0"
 
 

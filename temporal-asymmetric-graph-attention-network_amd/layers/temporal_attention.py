@@ -25,8 +25,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..fused import TemporalCore, attention_block, fusable
-from ..kernels import (TemporalAttnFn, TemporalMask, dropout_add_layer_norm, fused_qkv, layer_norm, linear,
-                       new_seed)
+from ..kernels import (BiasTableFn, TemporalAttnFn, TemporalMask, dropout_add_layer_norm, fused_qkv, layer_norm,
+                       linear, new_seed)
 
 
 class MaskBroadcastError(RuntimeError):
@@ -318,6 +318,11 @@ class AsymmetricTemporalAttention(TemporalAttention):
 
     def _bias_table(self, T, device):
         """[heads, 2T-1] table, entry [h][i-j+T-1] = R[clamp(i-j+32)] + K[clamp(i-j+W)]·[|i-j|<=W] (:1010-1027)."""
+        if (self.asymmetric_kernel.is_cuda and self.asymmetric_kernel.dtype == torch.float32
+                and (not self.relative_position_bias or self.relative_pos_table.dtype == torch.float32)):
+            return BiasTableFn.apply(self.asymmetric_kernel,
+                                     self.relative_pos_table if self.relative_position_bias else None, T,
+                                     self.asymmetric_window_size, self.max_relative_position)
         a, r = self._selectors(T, device, self.asymmetric_kernel.dtype)
         tab = a @ self.asymmetric_kernel                   # exact: one nonzero (1.0) term per row
         if r is not None:
