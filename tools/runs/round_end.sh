@@ -12,7 +12,8 @@ tail -1 $OUT/gpu_tests.log
 TAGAN_LIB=$GRAFT_REPO_ROOT/temporal-asymmetric-graph-attention-network_amd/libtagan_hip_debug.so timeout -k 10 600 \
     python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_membank.py tests/test_gpu_ingest.py \
     tests/test_gpu_temporal_v4.py tests/test_gpu_temporal_v5.py tests/test_gpu_temporal_v6.py tests/test_gpu_sgemm.py \
-    tests/test_gpu_sgemm_ln.py tests/test_gpu_debug.py tests/test_gpu_head.py -m gpu \
+    tests/test_gpu_sgemm_ln.py tests/test_gpu_debug.py tests/test_gpu_head.py tests/test_gpu_narrow.py \
+    tests/test_gpu_bias_table.py -m gpu \
     -q --timeout 300 --timeout-method thread > $OUT/debug_tests.log 2>&1 || { tail -40 $OUT/debug_tests.log; exit 1; }
 tail -1 $OUT/debug_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
