@@ -203,12 +203,15 @@ int tagan_narrow_linear_fwd(int64_t M, int32_t K, int32_t N, const float* x, int
     // tiles re-read it 4096 times and spent its life in the staging: 69 us at C2)
     const unsigned grid = (unsigned)std::min<int64_t>((tiles + 3) / 4, 512);
     hipStream_t s = as_stream(stream);
-#define TAGAN_NF(NB, KS) k_narrow_fwd<NB, KS><<<grid, NBLK, 0, s>>>(M, K, x, ldx, w, b, y, ldy)
+#define TAGAN_NF(NB, KS) k_narrow_fwd<NB, KS><<<grid, NBLK, 0, s>>>(M, K, x, ldx, wc, bc, yc, ldy)
 #define TAGAN_NFK(NB) if (K <= 16) TAGAN_NF(NB, 4); else if (K <= 28) TAGAN_NF(NB, 7); else TAGAN_NF(NB, 8)
-    switch (N / 64) {
-        case 1: TAGAN_NFK(1); break;
-        case 2: TAGAN_NFK(2); break;
-        default: TAGAN_NFK(4); break;
+    // N = 256 as two 128-column launches (a four-block kernel takes 308 registers: one wave per SIMD)
+    for (int c0 = 0; c0 < N; c0 += 128) {
+        const float* wc = w + (int64_t)c0 * K;
+        const float* bc = b ? b + c0 : nullptr;
+        float* yc = y + c0;
+        if (N == 64) TAGAN_NFK(1);
+        else TAGAN_NFK(2);
     }
 #undef TAGAN_NFK
 #undef TAGAN_NF
@@ -217,7 +220,8 @@ int tagan_narrow_linear_fwd(int64_t M, int32_t K, int32_t N, const float* x, int
 }
 
 size_t tagan_narrow_linear_bwd_workspace(int64_t M, int32_t K, int32_t N) {
-    return (size_t)tagan::narrow_groups(M) * (size_t)(N * K + N) * sizeof(float);
+    const int NC = N <= 128 ? N : 128;   // per column pass
+    return (size_t)tagan::narrow_groups(M) * (size_t)(NC * K + NC) * sizeof(float);
 }
 
 int tagan_narrow_linear_bwd(int64_t M, int32_t K, int32_t N, const float* x, int64_t ldx, const float* dy,
@@ -234,16 +238,16 @@ int tagan_narrow_linear_bwd(int64_t M, int32_t K, int32_t N, const float* x, int
     const int64_t per = ((M + G - 1) / G + 3) / 4 * 4;
     hipStream_t s = as_stream(stream);
     float* part = (float*)workspace;
-#define TAGAN_NB(NB) k_narrow_bwd<NB><<<G, NBLK, 0, s>>>(M, K, x, ldx, dy, lddy, per, part)
-    switch (N / 64) {
-        case 1: TAGAN_NB(1); break;
-        case 2: TAGAN_NB(2); break;
-        default: TAGAN_NB(4); break;
+    // N = 256 as two 128-column passes, each with its own partials and ordered column sum
+    const int NC = N == 64 ? 64 : 128;
+    for (int c0 = 0; c0 < N; c0 += NC) {
+        const float* dyc = dy + c0;
+        if (NC == 64) k_narrow_bwd<1><<<G, NBLK, 0, s>>>(M, K, x, ldx, dyc, lddy, per, part);
+        else k_narrow_bwd<2><<<G, NBLK, 0, s>>>(M, K, x, ldx, dyc, lddy, per, part);
+        TAGAN_CHECK_LAUNCH("narrow_linear_bwd");
+        launch_colsum(part, G, NC * K + NC, dw ? dw + (int64_t)c0 * K : nullptr, db ? db + c0 : nullptr, NC * K, s);
+        TAGAN_CHECK_LAUNCH("narrow_linear_bwd_sum");
     }
-#undef TAGAN_NB
-    TAGAN_CHECK_LAUNCH("narrow_linear_bwd");
-    launch_colsum(part, G, N * K + N, dw, db, N * K, s);
-    TAGAN_CHECK_LAUNCH("narrow_linear_bwd_sum");
     return TAGAN_OK;
 }
 
