@@ -18,6 +18,8 @@ FAMILIES = [
     ("proj (fused MFMA)", r"k_proj"),
     ("csr", r"rocprim|k_scatter|k_fill_tail|k_keys|k_chunk|k_tri|csr|csc|k_count|k_part_|k_refine|k_big_list|k_init\(|scan::k_|Tri"),
     ("colsum/pool", r"k_colsum|k_pool"),
+    ("embedding (narrow)", r"k_narrow"),
+    ("head / bias table / params", r"k_head_|k_bias_table|k_qkv_|k_sgemm_wprep"),
     ("torch elementwise", r"elementwise|CatArray|index|gather|scatter"),
     ("torch reduce", r"reduce_kernel"),
     ("fill/copy", r"__amd_rocclr"),
