@@ -2023,7 +2023,8 @@ constexpr NtCfg nt_cfg(int N, int wg_per_cu) {
 // bf16 activation mode), dropout + residual + LN2 [+ skip LN] epilogue of the out-projection (y fp32), LN1 backward
 // epilogue of the QKV input gradient (dx fp32).  At H = 256 (C3, C5) the LN1 prologue (32 lanes per row) with its
 // LN-recomputing weight gradient, and in the one-plane (bf16 activation) mode the LN2 epilogue of the out-projection
-// (MODE_LN_OUT row-owner kernels with N = 256); LN1's and LN2's backward stay standalone there.
+// (MODE_LN_OUT row-owner kernels with N = 256); LN1's backward stays standalone there, LN2's backward is fused with the
+// out-projection's gradients in one plane (k_ln2_bwd_out256) and standalone in three.
 // (The LN2 epilogue and the one-plane LN1-backward epilogue run on the row-owner kernels, RG_TABLE; the three-plane
 // LN1-backward epilogue lost its A/B -- fp32 step 6.99 vs 6.75 ms, profiles/r3d_ab_step.txt -- and is not built.)
 #ifndef TAGAN_SG_LN256
