@@ -17,8 +17,11 @@
 namespace tagan {
 namespace {
 
-constexpr int HB = 1024;     // threads: NG = HB / H groups of H feature threads
-constexpr int HU = 8;        // max steps per thread in the [T, H] products (ceil(T / NG); T·H <= 8192)
+#ifndef TAGAN_HEAD_HB
+#define TAGAN_HEAD_HB 1024
+#endif
+constexpr int HB = TAGAN_HEAD_HB;   // threads: NG = HB / H groups of H feature threads
+constexpr int HU = 8192 / HB;   // max steps per thread in the [T, H] products (ceil(T / NG); T·H <= 8192)
 constexpr int HC = 16;       // max classes
 constexpr int KC = 64;       // weight rows / columns staged per LDS chunk (H > 128; the whole matrix at H <= 128):
                              // 64 (H + 1) floats next to both [T, H] tiles stay under 141 KB at T·H = 8192
@@ -476,7 +479,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 // steps per thread in the [T, H] products (ceil(T / NG)) rounded up to the kernels' template argument 1, 2, 4 or 8
 int head_nu(int T, int H) {
     const int ng = HB / H, n = (T + ng - 1) / ng;
-    return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : 8;
+    return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : n <= 8 ? 8 : 16;
 }
 
 template <int NU>
@@ -494,7 +497,8 @@ int head_optin_nu() {
 
 int head_lds_optin(size_t bytes, int nu) {
     if (bytes <= 64 * 1024) return TAGAN_OK;
-    return nu == 1 ? head_optin_nu<1>() : nu == 2 ? head_optin_nu<2>() : nu == 4 ? head_optin_nu<4>() : head_optin_nu<8>();
+    return nu == 1 ? head_optin_nu<1>() : nu == 2 ? head_optin_nu<2>() : nu == 4 ? head_optin_nu<4>()
+           : nu == 8 ? head_optin_nu<8>() : head_optin_nu<HU>();
 }
 
 #define TAGAN_HEAD_LAUNCH(KERN, NU, LDS, STREAM, ARGS)                                       \
@@ -502,7 +506,8 @@ int head_lds_optin(size_t bytes, int nu) {
         if ((NU) == 1) KERN<1><<<1, HB, LDS, STREAM>>>(ARGS);                             \
         else if ((NU) == 2) KERN<2><<<1, HB, LDS, STREAM>>>(ARGS);                        \
         else if ((NU) == 4) KERN<4><<<1, HB, LDS, STREAM>>>(ARGS);                        \
-        else KERN<8><<<1, HB, LDS, STREAM>>>(ARGS);                                       \
+        else if ((NU) == 8) KERN<8><<<1, HB, LDS, STREAM>>>(ARGS);                        \
+        else KERN<HU><<<1, HB, LDS, STREAM>>>(ARGS);                                      \
     } while (0)
 
 }  // namespace
