@@ -15,6 +15,7 @@
 // Replaces the library GEMM + split-K batched GEMM + sum + bias column sum of the projection (4 launches, ~150 us
 // per C2 step; profiles/r6r_c2_kernel_stats.csv) with 1 + 2 launches over y / dY once each.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.cuh"
 
@@ -201,7 +202,11 @@ int tagan_narrow_linear_fwd(int64_t M, int32_t K, int32_t N, const float* x, int
     const int64_t tiles = (M + 15) / 16;
     // persistent: two workgroups per CU (the register-bound occupancy), each stages Wᵀ once (a workgroup per 4
     // tiles re-read it 4096 times and spent its life in the staging: 69 us at C2)
-    const unsigned grid = (unsigned)std::min<int64_t>((tiles + 3) / 4, 512);
+    static const int64_t gmax = [] {
+        const char* e = std::getenv("TAGAN_NARROW_GRID");   // A/B knob (workgroups, default 512)
+        return (int64_t)(e && std::atoi(e) > 0 ? std::atoi(e) : 512);
+    }();
+    const unsigned grid = (unsigned)std::min<int64_t>((tiles + 3) / 4, gmax);
     hipStream_t s = as_stream(stream);
 #define TAGAN_NF(NB, KS) k_narrow_fwd<NB, KS><<<grid, NBLK, 0, s>>>(M, K, x, ldx, wc, bc, yc, ldy)
 #define TAGAN_NFK(NB) if (K <= 16) TAGAN_NF(NB, 4); else if (K <= 28) TAGAN_NF(NB, 7); else TAGAN_NF(NB, 8)
