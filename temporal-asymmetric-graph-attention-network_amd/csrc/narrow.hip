@@ -200,11 +200,12 @@ int tagan_narrow_linear_fwd(int64_t M, int32_t K, int32_t N, const float* x, int
                   "narrow_linear_fwd: bad args");
     if (M == 0) return TAGAN_OK;
     const int64_t tiles = (M + 15) / 16;
-    // persistent: two workgroups per CU (the register-bound occupancy), each stages Wᵀ once (a workgroup per 4
+    // persistent: one workgroup per CU (256 / 512 / 768 / 1024: 43.8 / 47.3 / 54.9 / 48.2 us at C2,
+    // profiles/r6ac_narrow_grid.txt), each stages Wᵀ once (a workgroup per 4
     // tiles re-read it 4096 times and spent its life in the staging: 69 us at C2)
     static const int64_t gmax = [] {
-        const char* e = std::getenv("TAGAN_NARROW_GRID");   // A/B knob (workgroups, default 512)
-        return (int64_t)(e && std::atoi(e) > 0 ? std::atoi(e) : 512);
+        const char* e = std::getenv("TAGAN_NARROW_GRID");   // A/B knob (workgroups, default 256)
+        return (int64_t)(e && std::atoi(e) > 0 ? std::atoi(e) : 256);
     }();
     const unsigned grid = (unsigned)std::min<int64_t>((tiles + 3) / 4, gmax);
     hipStream_t s = as_stream(stream);
