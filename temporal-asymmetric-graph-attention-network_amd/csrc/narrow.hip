@@ -177,9 +177,14 @@ __global__ void __launch_bounds__(NBLK) k_narrow_bwd(int64_t M, int K, const flo
     }
 }
 
+// backward workgroups (row ranges): at most TAGAN_NARROW_BWD_GROUPS (A/B knob, default 512), >= 256 rows each
 int narrow_groups(int64_t M) {
+    static const int64_t gmax = [] {
+        const char* e = std::getenv("TAGAN_NARROW_BWD_GROUPS");
+        return (int64_t)(e && std::atoi(e) > 0 ? std::atoi(e) : 512);
+    }();
     const int64_t g = (M + 255) / 256;
-    return (int)(g < 512 ? (g > 0 ? g : 1) : 512);
+    return (int)(g < gmax ? (g > 0 ? g : 1) : gmax);
 }
 
 }  // namespace
